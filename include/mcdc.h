@@ -1,0 +1,171 @@
+/*
+ * mcdc.h — C ABI of the MI355X-native FastCDC v2020 chunker (libmcdc.so).
+ *
+ * This is the drop-in boundary for mapache's Archiver chunker.  The reference
+ * has no in-tree FFI for this path: it calls the Rust crate `fastcdc` 3.2.1
+ * directly at
+ *     /root/reference/src/archiver/processor.rs:173-179
+ *         StreamCDC::with_level(reader, MIN_CHUNK_SIZE as u32,
+ *                               AVG_CHUNK_SIZE as u32, MAX_CHUNK_SIZE as u32,
+ *                               Normalization::Level1)
+ *     /root/reference/src/archiver/processor.rs:181-202  (`for result in chunker`)
+ * with parameters from /root/reference/src/global/defaults.rs:35-40.  Each
+ * entry point below states which piece of that interface it replaces; the
+ * Rust-side binding a maintainer would add is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every function returns an int status: MCDC_OK (0) or a negative code.
+ *     No exception, panic or abort crosses this boundary; the message of the
+ *     last failure on the calling thread is returned by mcdc_last_error().
+ *   - The caller owns every buffer.  Output arrays are caller-allocated with a
+ *     capacity; MCDC_E_CAPACITY reports the required count in *n_out.
+ *   - A context (mcdc_ctx) owns one HIP device, one stream and its device
+ *     workspace.  Contexts are independent (the library is re-entrant across
+ *     contexts); one context must not be used by two threads at once.
+ *   - Chunk boundaries are bit-identical to fastcdc::v2020 (the crate's
+ *     cut_gear loop restated in oracle/), including ChunkData.hash.
+ */
+#ifndef MCDC_H
+#define MCDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCDC_ABI_VERSION 1
+
+/* status codes */
+#define MCDC_OK 0
+#define MCDC_E_INVALID (-1)  /* null pointer / bad argument                         */
+#define MCDC_E_PARAMS (-2)   /* min/avg/max/level outside the crate's asserts       */
+#define MCDC_E_CAPACITY (-3) /* output array too small; *n_out = required count      */
+#define MCDC_E_DEVICE (-4)   /* HIP runtime error (message in mcdc_last_error)      */
+#define MCDC_E_NOMEM (-5)    /* device or pinned host allocation failed              */
+#define MCDC_E_TOOBIG (-6)   /* input larger than the context was created for       */
+#define MCDC_E_INTERNAL (-7) /* internal consistency check failed                  */
+
+/* fastcdc::v2020::Normalization (crate enum; Level1 is what mapache uses,
+ * processor.rs:178). */
+typedef enum {
+  MCDC_LEVEL0 = 0,
+  MCDC_LEVEL1 = 1,
+  MCDC_LEVEL2 = 2,
+  MCDC_LEVEL3 = 3
+} mcdc_normalization;
+
+/* The arguments of StreamCDC::with_level(source, min_size, avg_size,
+ * max_size, level) — processor.rs:173-179. */
+typedef struct {
+  uint32_t min_size;
+  uint32_t avg_size;
+  uint32_t max_size;
+  uint32_t level; /* mcdc_normalization */
+} mcdc_params;
+
+/* One yielded chunk: the crate's ChunkData{hash, offset, length, data} minus
+ * the owned `data` Vec (the caller slices its own buffer).  `offset` is
+ * relative to the start of the buffer/file it belongs to. */
+typedef struct {
+  uint64_t offset;
+  uint64_t length;
+  uint64_t hash;
+} mcdc_chunk;
+
+/* Device time of the last call on a context (HIP events on the context
+ * stream).  device_ms covers the first scan kernel to the last boundary
+ * written (the device-resident metric); the copies are timed separately. */
+typedef struct {
+  double scan_ms;      /* candidate scan kernel(s) only                  */
+  double resolve_ms;   /* chain resolution + boundary emission kernels   */
+  double device_ms;    /* scan_ms + resolve_ms, one event pair           */
+  double h2d_ms;       /* host->device input copies (host entry points)  */
+  double d2h_ms;       /* boundary list device->host                     */
+  double total_ms;     /* host wall time of the whole call               */
+  uint64_t bytes;      /* input bytes chunked                            */
+  uint64_t chunks;     /* chunks produced                                */
+  uint64_t scan_launches; /* number of scan kernel launches             */
+  uint64_t fallback_files; /* files resolved by the serial fallback     */
+} mcdc_timing;
+
+/* ------------------------------------------------------------------ API -- */
+
+/* Validate params exactly as the crate's with_level asserts do
+ * (MINIMUM_MIN 64 <= min <= 1 MiB, 256 <= avg <= 4 MiB, 1 KiB <= max <=
+ * 16 MiB, level <= 3).  Where the crate panics this returns MCDC_E_PARAMS.
+ * Optionally returns the normalised masks mask_s = MASKS[bits+level],
+ * mask_l = MASKS[bits-level] (either pointer may be NULL). */
+int mcdc_params_check(const mcdc_params *params, uint64_t *mask_s, uint64_t *mask_l);
+
+/* Create a context on HIP device `device` able to chunk inputs up to
+ * max_bytes per call (workspace is sized lazily up to that bound). */
+int mcdc_ctx_create(int device, size_t max_bytes, struct mcdc_ctx **out);
+void mcdc_ctx_destroy(struct mcdc_ctx *ctx);
+
+/* Chunk one device-resident buffer (the device-resident GiB/s metric).
+ * Replaces one StreamCDC::with_level(..) + its full iteration over a file
+ * whose bytes already sit in HBM (processor.rs:173-202).  d_data is a device
+ * pointer on the context's device (any alignment). */
+int mcdc_chunk_device(struct mcdc_ctx *ctx, const mcdc_params *params, const void *d_data,
+                      size_t n, mcdc_chunk *out, size_t cap, size_t *n_out);
+
+/* Chunk one host buffer (end-to-end: H2D copy, kernels, D2H of boundaries).
+ * This is what the Archiver adapter calls per file (processor.rs:165-202):
+ * the file's bytes are read into host memory, chunked here, and each
+ * ChunkData is the caller's slice [offset, offset+length). */
+int mcdc_chunk_host(struct mcdc_ctx *ctx, const mcdc_params *params, const void *h_data,
+                    size_t n, mcdc_chunk *out, size_t cap, size_t *n_out);
+
+/* Chunk many independent host buffers in one batch (the many-buffer path:
+ * one StreamCDC per file, processor.rs:173; chains restart at every buffer).
+ * Chunks of buffer i are written contiguously in buffer order; counts[i]
+ * receives buffer i's chunk count (may be NULL).  Offsets are relative to
+ * each buffer. */
+int mcdc_chunk_batch(struct mcdc_ctx *ctx, const mcdc_params *params,
+                     const uint8_t *const *bufs, const size_t *lens, size_t nbufs,
+                     mcdc_chunk *out, size_t cap, size_t *counts, size_t *n_out);
+
+/* Same, but the buffers already sit back to back in one device arena:
+ * buffer i is d_arena[offsets[i], offsets[i] + lens[i]).  offsets/lens are
+ * host arrays; the ranges must not overlap. */
+int mcdc_chunk_batch_device(struct mcdc_ctx *ctx, const mcdc_params *params,
+                            const void *d_arena, const uint64_t *offsets, const uint64_t *lens,
+                            size_t nbufs, mcdc_chunk *out, size_t cap, size_t *counts,
+                            size_t *n_out);
+
+/* Timing of the last call on ctx. */
+int mcdc_ctx_timing(const struct mcdc_ctx *ctx, mcdc_timing *out);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *mcdc_last_error(void);
+
+/* ---------------------------------------------- utilities (not reference
+ * interface: benchmark / test plumbing) -- */
+
+/* Device / pinned-host allocation on the context's device. */
+int mcdc_device_alloc(struct mcdc_ctx *ctx, size_t bytes, void **d_ptr);
+int mcdc_device_free(struct mcdc_ctx *ctx, void *d_ptr);
+int mcdc_host_alloc(struct mcdc_ctx *ctx, size_t bytes, void **h_ptr);
+int mcdc_host_free(struct mcdc_ctx *ctx, void *h_ptr);
+int mcdc_memcpy_h2d(struct mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+
+/* Fill d_dst[0, n) with the counter-based synthetic stream used by the bench
+ * and tests: byte at stream position p = pos + i is
+ *   (mix64(seed + (p/8 + 1) * 0x9e3779b97f4a7c15) >> 8*(p%8)) & 0xff
+ * where mix64 is the SplitMix64 finaliser (also in oracle/). */
+int mcdc_fill_random_device(struct mcdc_ctx *ctx, void *d_dst, uint64_t pos, size_t n,
+                            uint64_t seed);
+
+/* Order-sensitive digest of a boundary list (offset, length pairs), the same
+ * function as the oracle's; used to compare full-size runs cheaply. */
+uint64_t mcdc_digest(const mcdc_chunk *chunks, size_t n);
+
+/* Library/ABI version. */
+int mcdc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCDC_H */

@@ -1,0 +1,218 @@
+"""ctypes binding of libmcdc.so (the C ABI in include/mcdc.h).
+
+The library is built in-tree by ``mapache_amd.build`` (hipcc, gfx950).  There
+is no CPU fallback: if the shared object or a HIP device is missing, every
+entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmcdc.so")
+
+MCDC_OK = 0
+MCDC_E_INVALID = -1
+MCDC_E_PARAMS = -2
+MCDC_E_CAPACITY = -3
+MCDC_E_DEVICE = -4
+MCDC_E_NOMEM = -5
+MCDC_E_TOOBIG = -6
+MCDC_E_INTERNAL = -7
+
+# every symbol include/mcdc.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "mcdc_params_check", "mcdc_ctx_create", "mcdc_ctx_destroy", "mcdc_chunk_device",
+    "mcdc_chunk_host", "mcdc_chunk_batch", "mcdc_chunk_batch_device", "mcdc_ctx_timing",
+    "mcdc_last_error", "mcdc_device_alloc", "mcdc_device_free", "mcdc_host_alloc",
+    "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_fill_random_device", "mcdc_digest",
+    "mcdc_abi_version",
+)
+
+
+class McdcParams(ctypes.Structure):
+    _fields_ = [("min_size", ctypes.c_uint32), ("avg_size", ctypes.c_uint32),
+                ("max_size", ctypes.c_uint32), ("level", ctypes.c_uint32)]
+
+
+class McdcChunk(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint64), ("hash", ctypes.c_uint64)]
+
+
+class McdcTiming(ctypes.Structure):
+    _fields_ = [("scan_ms", ctypes.c_double), ("resolve_ms", ctypes.c_double),
+                ("device_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
+                ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64)]
+
+
+CHUNK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("hash", "<u8")])
+
+_lib = None
+
+
+class McdcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mcdc error {code}: {msg}")
+        self.code = code
+
+
+def load():
+    """Load libmcdc.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python -m mapache_amd.build` (hipcc gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u64, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
+    P = ctypes.POINTER
+    L.mcdc_params_check.argtypes = [P(McdcParams), P(u64), P(u64)]
+    L.mcdc_ctx_create.argtypes = [i32, sz, P(vp)]
+    L.mcdc_ctx_destroy.argtypes = [vp]
+    L.mcdc_ctx_destroy.restype = None
+    L.mcdc_chunk_device.argtypes = [vp, P(McdcParams), vp, sz, vp, sz, P(sz)]
+    L.mcdc_chunk_host.argtypes = [vp, P(McdcParams), vp, sz, vp, sz, P(sz)]
+    L.mcdc_chunk_batch.argtypes = [vp, P(McdcParams), vp, vp, sz, vp, sz, vp, P(sz)]
+    L.mcdc_chunk_batch_device.argtypes = [vp, P(McdcParams), vp, vp, vp, sz, vp, sz, vp, P(sz)]
+    L.mcdc_ctx_timing.argtypes = [vp, P(McdcTiming)]
+    L.mcdc_last_error.argtypes = []
+    L.mcdc_last_error.restype = ctypes.c_char_p
+    L.mcdc_device_alloc.argtypes = [vp, sz, P(vp)]
+    L.mcdc_device_free.argtypes = [vp, vp]
+    L.mcdc_host_alloc.argtypes = [vp, sz, P(vp)]
+    L.mcdc_host_free.argtypes = [vp, vp]
+    L.mcdc_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.mcdc_fill_random_device.argtypes = [vp, vp, u64, sz, u64]
+    L.mcdc_digest.argtypes = [vp, sz]
+    L.mcdc_digest.restype = u64
+    L.mcdc_abi_version.argtypes = []
+    for name in EXPORTS:  # fail loudly if the build is stale
+        getattr(L, name)
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != MCDC_OK:
+        raise McdcError(rc, load().mcdc_last_error().decode(errors="replace"))
+
+
+def params(min_size: int, avg_size: int, max_size: int, level: int = 1) -> McdcParams:
+    return McdcParams(min_size, avg_size, max_size, level)
+
+
+class Context:
+    """One mcdc_ctx: a HIP device, a stream and its workspace."""
+
+    def __init__(self, device: int = 0, max_bytes: int = 1 << 30):
+        L = load()
+        h = ctypes.c_void_p()
+        check(L.mcdc_ctx_create(device, max_bytes, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.max_bytes = max_bytes
+
+    def close(self):
+        if self._h:
+            load().mcdc_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------- chunking --
+    @staticmethod
+    def _bound(n: int, p: McdcParams) -> int:
+        return n // max(p.min_size - 1, 1) + 2
+
+    def _run(self, fn, p: McdcParams, *args, cap: int):
+        out = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
+        n_out = ctypes.c_size_t()
+        rc = fn(self._h, ctypes.byref(p), *args, out.ctypes.data, cap, ctypes.byref(n_out))
+        check(rc)
+        return out[: n_out.value].copy()
+
+    def chunk_device(self, p: McdcParams, d_ptr: int, n: int) -> np.ndarray:
+        return self._run(load().mcdc_chunk_device, p, ctypes.c_void_p(d_ptr), n, cap=self._bound(n, p))
+
+    def chunk_host(self, p: McdcParams, data) -> np.ndarray:
+        a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                 else data.view(np.uint8).reshape(-1))
+        return self._run(load().mcdc_chunk_host, p, ctypes.c_void_p(a.ctypes.data), a.size,
+                         cap=self._bound(a.size, p))
+
+    def chunk_batch(self, p: McdcParams, bufs):
+        arrs = [np.ascontiguousarray(np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray)
+                                     else b.view(np.uint8).reshape(-1)) for b in bufs]
+        n = len(arrs)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
+        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        cap = sum(self._bound(a.size, p) for a in arrs) + 1
+        out = np.zeros(cap, dtype=CHUNK_DTYPE)
+        n_out = ctypes.c_size_t()
+        check(load().mcdc_chunk_batch(self._h, ctypes.byref(p), ptrs, lens, n, out.ctypes.data, cap,
+                                      counts.ctypes.data, ctypes.byref(n_out)))
+        return out[: n_out.value].copy(), counts[:n].astype(np.int64)
+
+    def chunk_batch_device(self, p: McdcParams, d_arena: int, offsets, lens):
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ls = np.ascontiguousarray(lens, dtype=np.uint64)
+        n = offs.size
+        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        cap = int(sum(self._bound(int(x), p) for x in ls)) + 1
+        out = np.zeros(cap, dtype=CHUNK_DTYPE)
+        n_out = ctypes.c_size_t()
+        check(load().mcdc_chunk_batch_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_arena),
+                                             offs.ctypes.data, ls.ctypes.data, n, out.ctypes.data, cap,
+                                             counts.ctypes.data, ctypes.byref(n_out)))
+        return out[: n_out.value].copy(), counts[:n].astype(np.int64)
+
+    def timing(self) -> dict:
+        t = McdcTiming()
+        check(load().mcdc_ctx_timing(self._h, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in McdcTiming._fields_}
+
+    # ---------------------------------------------------------- plumbing --
+    def device_alloc(self, n: int) -> int:
+        p = ctypes.c_void_p()
+        check(load().mcdc_device_alloc(self._h, n, ctypes.byref(p)))
+        return p.value
+
+    def device_free(self, ptr: int) -> None:
+        check(load().mcdc_device_free(self._h, ctypes.c_void_p(ptr)))
+
+    def host_alloc(self, n: int) -> int:
+        p = ctypes.c_void_p()
+        check(load().mcdc_host_alloc(self._h, n, ctypes.byref(p)))
+        return p.value
+
+    def host_free(self, ptr: int) -> None:
+        check(load().mcdc_host_free(self._h, ctypes.c_void_p(ptr)))
+
+    def h2d(self, d_dst: int, data) -> None:
+        a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                 else data.view(np.uint8).reshape(-1))
+        check(load().mcdc_memcpy_h2d(self._h, ctypes.c_void_p(d_dst), ctypes.c_void_p(a.ctypes.data), a.size))
+
+    def fill_random(self, d_dst: int, n: int, seed: int, pos: int = 0) -> None:
+        check(load().mcdc_fill_random_device(self._h, ctypes.c_void_p(d_dst), pos, n, seed))
+
+
+def digest(chunks: np.ndarray) -> int:
+    a = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+    return int(load().mcdc_digest(ctypes.c_void_p(a.ctypes.data), a.size))

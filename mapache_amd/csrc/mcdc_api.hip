@@ -1,0 +1,592 @@
+// mcdc_api.hip — host side of libmcdc.so: the C ABI declared in include/mcdc.h.
+//
+// Replaces, for mapache's Archiver, the construction and iteration of
+// fastcdc::v2020::StreamCDC at /root/reference/src/archiver/processor.rs:173-202
+// (see INTEGRATION.md for the Rust binding).  Device work is delegated to the
+// kernels in mcdc_kernels.hip; nothing here computes chunk boundaries.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mcdc.h"
+#include "gear_table.h"
+#include "mcdc_internal.h"
+
+using namespace mcdc;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(MCDC_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                  __FILE__, __LINE__);                                                    \
+  } while (0)
+
+constexpr uint32_t MINIMUM_MIN = 64, MINIMUM_MAX = 1048576;
+constexpr uint32_t AVERAGE_MIN = 256, AVERAGE_MAX = 4194304;
+constexpr uint32_t MAXIMUM_MIN = 1024, MAXIMUM_MAX = 16777216;
+
+// crate: fn logarithm2(value: u32) -> u32 { f64::from(value).log2().round() as u32 }
+uint32_t logarithm2(uint32_t v) { return (uint32_t)std::lround(std::log2((double)v)); }
+
+int check_params(const mcdc_params *p, uint64_t *ms, uint64_t *ml) {
+  if (!p) return fail(MCDC_E_INVALID, "params is NULL");
+  if (p->min_size < MINIMUM_MIN || p->min_size > MINIMUM_MAX)
+    return fail(MCDC_E_PARAMS, "min_size %u outside [%u, %u]", p->min_size, MINIMUM_MIN, MINIMUM_MAX);
+  if (p->avg_size < AVERAGE_MIN || p->avg_size > AVERAGE_MAX)
+    return fail(MCDC_E_PARAMS, "avg_size %u outside [%u, %u]", p->avg_size, AVERAGE_MIN, AVERAGE_MAX);
+  if (p->max_size < MAXIMUM_MIN || p->max_size > MAXIMUM_MAX)
+    return fail(MCDC_E_PARAMS, "max_size %u outside [%u, %u]", p->max_size, MAXIMUM_MIN, MAXIMUM_MAX);
+  if (p->level > 3) return fail(MCDC_E_PARAMS, "level %u not a Normalization", p->level);
+  const uint32_t bits = logarithm2(p->avg_size);
+  if (ms) *ms = kMasks[bits + p->level];
+  if (ml) *ml = kMasks[bits - p->level];
+  return MCDC_OK;
+}
+
+uint32_t next_pow2(uint32_t v) {
+  uint32_t r = 1;
+  while (r < v) r <<= 1;
+  return r;
+}
+
+DevParams make_dev_params(const mcdc_params *p, uint64_t ms, uint64_t ml) {
+  DevParams d{};
+  d.min = p->min_size;
+  d.avg = p->avg_size;
+  d.max = p->max_size;
+  d.ms = ms;
+  d.ml = ml;
+  d.ms16 = ms << 16;
+  d.ml16 = ml << 16;
+  d.pf_hi = (uint32_t)((ms & ml) >> 16);
+  // candidate slots per run: ~4x the expected S|L count, at least 8
+  const double dens = std::ldexp(1.0, -__builtin_popcountll(ms)) + std::ldexp(1.0, -__builtin_popcountll(ml));
+  const uint32_t want = (uint32_t)std::ceil(4.0 * kRun * dens) + 4;
+  d.cap = std::min<uint32_t>(128, std::max<uint32_t>(8, next_pow2(want)));
+  return d;
+}
+
+// Segment length: ~16 expected chunks per speculative chain, >= 2 * max.
+uint64_t segment_bytes(const mcdc_params *p) {
+  uint64_t z = std::max<uint64_t>(2ull * p->max_size, 16ull * ((uint64_t)p->min_size + p->avg_size));
+  return (z + kRun - 1) / kRun * kRun;
+}
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct mcdc_ctx {
+  int device = 0;
+  int num_cus = 256;
+  size_t max_bytes = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_start = nullptr, ev_scan = nullptr, ev_end = nullptr, ev_h2d0 = nullptr,
+             ev_h2d1 = nullptr;
+  uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
+  // workspace
+  DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
+      link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
+      scan_tmp;
+  // pinned host staging
+  void *h_stage = nullptr;
+  size_t h_stage_cap = 0;
+  std::vector<Seg> h_segs;
+  std::vector<File> h_files;
+  std::vector<uint64_t> h_node_off;
+  mcdc_timing timing{};
+};
+
+namespace {
+
+int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return MCDC_OK;
+  if (b.p) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t alloc = (bytes + bytes / 8 + 255) / 256 * 256;  // headroom against regrowth
+  if (hipMalloc(&b.p, alloc) != hipSuccess) {
+    b.p = nullptr;
+    (void)hipGetLastError();
+    return fail(MCDC_E_NOMEM, "hipMalloc(%zu) failed", alloc);
+  }
+  b.cap = alloc;
+  return MCDC_OK;
+}
+
+int ensure_stage(mcdc_ctx *ctx, size_t bytes) {
+  if (ctx->h_stage_cap >= bytes) return MCDC_OK;
+  if (ctx->h_stage) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipHostFree(ctx->h_stage));
+    ctx->h_stage = nullptr;
+    ctx->h_stage_cap = 0;
+  }
+  if (hipHostMalloc(&ctx->h_stage, bytes, hipHostMallocDefault) != hipSuccess) {
+    ctx->h_stage = nullptr;
+    (void)hipGetLastError();
+    return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+  }
+  ctx->h_stage_cap = bytes;
+  return MCDC_OK;
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Core: files are [fstart[i], fend[i]) in an arena at `base` (16-aligned),
+// arena length n_al (multiple of 16, all reads stay below it).
+int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, uint64_t n_al,
+                 const uint64_t *fstart, const uint64_t *fend, size_t nfiles, mcdc_chunk *out,
+                 size_t cap, size_t *counts, size_t *n_out) {
+  uint64_t ms = 0, ml = 0;
+  int rc = check_params(params, &ms, &ml);
+  if (rc) return rc;
+  const DevParams P = make_dev_params(params, ms, ml);
+  const uint64_t Z = segment_bytes(params);
+
+  // ---- plan segments (host) ----
+  ctx->h_files.resize(nfiles);
+  ctx->h_segs.clear();
+  ctx->h_node_off.clear();
+  ctx->h_node_off.push_back(0);
+  uint64_t total_bytes = 0, out_bound = 0;
+  for (size_t i = 0; i < nfiles; ++i) {
+    const uint64_t len = fend[i] - fstart[i];
+    total_bytes += len;
+    const uint32_t nseg = (uint32_t)((len + Z - 1) / Z);
+    File F{fstart[i], fend[i], (uint32_t)ctx->h_segs.size(), nseg};
+    ctx->h_files[i] = F;
+    for (uint32_t k = 0; k < nseg; ++k) {
+      Seg S;
+      S.start = fstart[i] + (uint64_t)k * Z;
+      S.end = std::min<uint64_t>(S.start + Z, fend[i]);
+      S.file = (uint32_t)i;
+      S.flags = (k == 0 ? kSegFirst : 0) | (k + 1 == nseg ? kSegLast : 0);
+      ctx->h_segs.push_back(S);
+      const uint64_t ncap = (S.end - S.start) / (params->min_size - 1) + 2;
+      ctx->h_node_off.push_back(ctx->h_node_off.back() + ncap);
+    }
+    out_bound += len / (params->min_size - 1) + 2;
+  }
+  const uint32_t nsegs = (uint32_t)ctx->h_segs.size();
+  const uint64_t nruns = (n_al + kRun - 1) / kRun;
+
+  // ---- workspace ----
+  if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
+  if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
+  if ((rc = ensure(ctx, ctx->files, nfiles * sizeof(File)))) return rc;
+  if ((rc = ensure(ctx, ctx->nodes, ctx->h_node_off.back() * sizeof(uint64_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->node_off, ctx->h_node_off.size() * sizeof(uint64_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->node_cnt, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->seg_exit, nsegs * 8))) return rc;
+  if ((rc = ensure(ctx, ctx->cont, (size_t)nsegs * kContMax * 8))) return rc;
+  if ((rc = ensure(ctx, ctx->cont_cnt, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->link_seg, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->link_idx, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->link_pos, nsegs * 8))) return rc;
+  if ((rc = ensure(ctx, ctx->file_flags, nfiles * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->seg_true, nsegs))) return rc;
+  if ((rc = ensure(ctx, ctx->entry_idx, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->seg_count, (nsegs + 1) * 8))) return rc;
+  if ((rc = ensure(ctx, ctx->seg_off, (nsegs + 1) * 8))) return rc;
+  if ((rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
+  if ((rc = ensure(ctx, ctx->err, 16))) return rc;
+  const size_t tmpb = scan_tmp_bytes(nsegs);
+  if ((rc = ensure(ctx, ctx->scan_tmp, tmpb))) return rc;
+
+  hipStream_t st = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->segs.p, ctx->h_segs.data(), nsegs * sizeof(Seg), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->files.p, ctx->h_files.data(), nfiles * sizeof(File), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->node_off.p, ctx->h_node_off.data(), ctx->h_node_off.size() * 8,
+                         hipMemcpyHostToDevice, st));
+  if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st));
+  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st));
+  HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st));
+
+  Work W{};
+  W.base = base;
+  W.n_al = n_al;
+  W.nruns = nruns;
+  W.gear = ctx->d_gear;
+  W.gear16 = ctx->d_gear16;
+  W.run_cnt = (uint8_t *)ctx->run_cnt.p;
+  W.run_ent = (uint32_t *)ctx->run_ent.p;
+  W.segs = (const Seg *)ctx->segs.p;
+  W.nsegs = nsegs;
+  W.nfiles = (uint32_t)nfiles;
+  W.files = (const File *)ctx->files.p;
+  W.zseg = Z;
+  W.nodes = (uint64_t *)ctx->nodes.p;
+  W.node_off = (const uint64_t *)ctx->node_off.p;
+  W.node_cnt = (uint32_t *)ctx->node_cnt.p;
+  W.seg_exit = (uint64_t *)ctx->seg_exit.p;
+  W.cont = (uint64_t *)ctx->cont.p;
+  W.cont_cnt = (uint32_t *)ctx->cont_cnt.p;
+  W.link_seg = (uint32_t *)ctx->link_seg.p;
+  W.link_idx = (uint32_t *)ctx->link_idx.p;
+  W.link_pos = (uint64_t *)ctx->link_pos.p;
+  W.file_flags = (uint32_t *)ctx->file_flags.p;
+  W.seg_true = (uint8_t *)ctx->seg_true.p;
+  W.entry_idx = (uint32_t *)ctx->entry_idx.p;
+  W.seg_count = (uint64_t *)ctx->seg_count.p;
+  W.seg_off = (uint64_t *)ctx->seg_off.p;
+  W.out = (DevChunk *)ctx->out.p;
+  W.out_cap = out_bound;
+  W.err = (uint32_t *)ctx->err.p;
+
+  HIP_TRY(hipEventRecord(ctx->ev_start, st));
+  if (n_al > 0) launch_scan(W, P, ctx->num_cus, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev_scan, st));
+  launch_resolve(W, P, ctx->scan_tmp.p, tmpb, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev_end, st));
+
+  // ---- results ----
+  uint64_t total = 0;
+  uint32_t err = 0;
+  const double t_d2h0 = now_ms();
+  if (nsegs) HIP_TRY(hipMemcpyAsync(&total, (uint64_t *)ctx->seg_off.p + nsegs, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&err, ctx->err.p, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (err) return fail(MCDC_E_INTERNAL, "device consistency error 0x%x", err);
+  if (n_out) *n_out = (size_t)total;
+  if (total > cap || (total && !out))
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu chunks", cap, (unsigned long long)total);
+  if (total)
+    HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st));
+  std::vector<uint64_t> seg_off;
+  if (counts && nfiles) {
+    seg_off.resize(nsegs + 1);
+    if (nsegs) HIP_TRY(hipMemcpyAsync(seg_off.data(), ctx->seg_off.p, (nsegs + 1) * 8, hipMemcpyDeviceToHost, st));
+  }
+  std::vector<uint32_t> fflags(nfiles);
+  if (nfiles) HIP_TRY(hipMemcpyAsync(fflags.data(), ctx->file_flags.p, nfiles * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const double t_d2h1 = now_ms();
+  if (counts) {
+    for (size_t i = 0; i < nfiles; ++i) {
+      const File &F = ctx->h_files[i];
+      counts[i] = F.nsegs ? (size_t)(seg_off[F.first_seg + F.nsegs] - seg_off[F.first_seg]) : 0;
+    }
+  }
+  float scan_ms = 0, dev_ms = 0;
+  HIP_TRY(hipEventElapsedTime(&scan_ms, ctx->ev_start, ctx->ev_scan));
+  HIP_TRY(hipEventElapsedTime(&dev_ms, ctx->ev_start, ctx->ev_end));
+  ctx->timing.scan_ms = scan_ms;
+  ctx->timing.device_ms = dev_ms;
+  ctx->timing.resolve_ms = dev_ms - scan_ms;
+  ctx->timing.d2h_ms = t_d2h1 - t_d2h0;
+  ctx->timing.bytes = total_bytes;
+  ctx->timing.chunks = total;
+  ctx->timing.scan_launches = n_al > 0 ? 1 : 0;
+  uint64_t fb = 0;
+  for (uint32_t f : fflags) fb += (f & kFileFallbackDone) ? 1 : 0;
+  ctx->timing.fallback_files = fb;
+  return MCDC_OK;
+}
+
+int check_ctx(mcdc_ctx *ctx) {
+  if (!ctx) return fail(MCDC_E_INVALID, "ctx is NULL");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return fail(MCDC_E_DEVICE, "hipSetDevice: %s", hipGetErrorString(e));
+  return MCDC_OK;
+}
+
+}  // namespace
+
+// ================================================================= C ABI ==
+extern "C" {
+
+int mcdc_abi_version(void) { return MCDC_ABI_VERSION; }
+
+const char *mcdc_last_error(void) { return g_last_error.c_str(); }
+
+int mcdc_params_check(const mcdc_params *params, uint64_t *mask_s, uint64_t *mask_l) {
+  return check_params(params, mask_s, mask_l);
+}
+
+int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
+  if (!out) return fail(MCDC_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    (void)hipGetLastError();
+    return fail(MCDC_E_DEVICE, "no HIP device available");
+  }
+  if (device < 0 || device >= ndev) return fail(MCDC_E_INVALID, "device %d out of range (%d)", device, ndev);
+  mcdc_ctx *ctx = new (std::nothrow) mcdc_ctx();
+  if (!ctx) return fail(MCDC_E_NOMEM, "host allocation failed");
+  ctx->device = device;
+  ctx->max_bytes = max_bytes;
+  auto bail = [&](int rc) {
+    mcdc_ctx_destroy(ctx);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return bail(fail(MCDC_E_DEVICE, "hipSetDevice(%d)", device));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(MCDC_E_DEVICE, "hipStreamCreate failed"));
+  hipEvent_t *evs[] = {&ctx->ev_start, &ctx->ev_scan, &ctx->ev_end, &ctx->ev_h2d0, &ctx->ev_h2d1};
+  for (hipEvent_t *e : evs)
+    if (hipEventCreate(e) != hipSuccess) return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
+  uint64_t g16[256];
+  for (int i = 0; i < 256; ++i) g16[i] = kGear[i] << 16;
+  if (hipMalloc(&ctx->d_gear, 2048) != hipSuccess || hipMalloc(&ctx->d_gear16, 2048) != hipSuccess)
+    return bail(fail(MCDC_E_NOMEM, "hipMalloc(tables) failed"));
+  if (hipMemcpy(ctx->d_gear, kGear, 2048, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(ctx->d_gear16, g16, 2048, hipMemcpyHostToDevice) != hipSuccess)
+    return bail(fail(MCDC_E_DEVICE, "table upload failed"));
+  *out = ctx;
+  return MCDC_OK;
+}
+
+void mcdc_ctx_destroy(mcdc_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
+                    &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
+                    &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
+                    &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
+                    &ctx->err, &ctx->scan_tmp};
+  for (DevBuf *b : bufs)
+    if (b->p) (void)hipFree(b->p);
+  if (ctx->d_gear) (void)hipFree(ctx->d_gear);
+  if (ctx->d_gear16) (void)hipFree(ctx->d_gear16);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  hipEvent_t evs[] = {ctx->ev_start, ctx->ev_scan, ctx->ev_end, ctx->ev_h2d0, ctx->ev_h2d1};
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int mcdc_ctx_timing(const mcdc_ctx *ctx, mcdc_timing *out) {
+  if (!ctx || !out) return fail(MCDC_E_INVALID, "NULL argument");
+  *out = ctx->timing;
+  return MCDC_OK;
+}
+
+int mcdc_chunk_device(mcdc_ctx *ctx, const mcdc_params *params, const void *d_data, size_t n,
+                      mcdc_chunk *out, size_t cap, size_t *n_out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!d_data && n) return fail(MCDC_E_INVALID, "d_data is NULL");
+  if (n > ctx->max_bytes) return fail(MCDC_E_TOOBIG, "n=%zu > max_bytes=%zu", n, ctx->max_bytes);
+  const double t0 = now_ms();
+  const uintptr_t addr = (uintptr_t)d_data;
+  const uint8_t *base = (const uint8_t *)(addr & ~(uintptr_t)15);
+  const uint64_t delta = addr & 15;
+  const uint64_t n_al = n ? (delta + n + 15) / 16 * 16 : 0;
+  const uint64_t fs = delta, fe = delta + n;
+  rc = run_pipeline(ctx, params, base, n_al, &fs, &fe, 1, out, cap, nullptr, n_out);
+  ctx->timing.h2d_ms = 0;
+  ctx->timing.total_ms = now_ms() - t0;
+  return rc;
+}
+
+int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void *d_arena,
+                            const uint64_t *offsets, const uint64_t *lens, size_t nbufs,
+                            mcdc_chunk *out, size_t cap, size_t *counts, size_t *n_out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (nbufs && (!d_arena || !offsets || !lens)) return fail(MCDC_E_INVALID, "NULL argument");
+  const double t0 = now_ms();
+  const uintptr_t addr = (uintptr_t)d_arena;
+  const uint8_t *base = (const uint8_t *)(addr & ~(uintptr_t)15);
+  const uint64_t delta = addr & 15;
+  std::vector<uint64_t> fs(nbufs), fe(nbufs);
+  uint64_t hi = 0, total = 0;
+  for (size_t i = 0; i < nbufs; ++i) {
+    fs[i] = delta + offsets[i];
+    fe[i] = fs[i] + lens[i];
+    hi = std::max(hi, fe[i]);
+    total += lens[i];
+  }
+  if (total > ctx->max_bytes) return fail(MCDC_E_TOOBIG, "batch bytes %llu > max_bytes", (unsigned long long)total);
+  const uint64_t n_al = (hi + 15) / 16 * 16;
+  rc = run_pipeline(ctx, params, base, n_al, fs.data(), fe.data(), nbufs, out, cap, counts, n_out);
+  ctx->timing.h2d_ms = 0;
+  ctx->timing.total_ms = now_ms() - t0;
+  return rc;
+}
+
+// Host buffers are packed back to back into the context's device arena
+// through a pinned staging buffer (slab by slab), then chunked as a batch.
+static int stage_to_arena(mcdc_ctx *ctx, const uint8_t *const *bufs, const size_t *lens, size_t nbufs,
+                          uint64_t total) {
+  int rc = ensure(ctx, ctx->arena, total + 16);
+  if (rc) return rc;
+  const size_t slab = (size_t)std::min<uint64_t>(total ? total : 1, 256ull << 20);
+  if ((rc = ensure_stage(ctx, 2 * slab))) return rc;
+  uint8_t *stage[2] = {(uint8_t *)ctx->h_stage, (uint8_t *)ctx->h_stage + slab};
+  hipEvent_t done[2] = {ctx->ev_h2d0, ctx->ev_h2d1};
+  bool inflight[2] = {false, false};
+  uint64_t dst = 0;
+  size_t bi = 0, boff = 0;
+  int k = 0;
+  while (dst < total) {
+    if (inflight[k]) HIP_TRY(hipEventSynchronize(done[k]));
+    size_t fill = 0;
+    while (fill < slab && bi < nbufs) {
+      const size_t take = std::min(slab - fill, lens[bi] - boff);
+      if (take) memcpy(stage[k] + fill, bufs[bi] + boff, take);
+      fill += take;
+      boff += take;
+      if (boff == lens[bi]) { ++bi; boff = 0; }
+    }
+    HIP_TRY(hipMemcpyAsync((uint8_t *)ctx->arena.p + dst, stage[k], fill, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipEventRecord(done[k], ctx->stream));
+    inflight[k] = true;
+    dst += fill;
+    k ^= 1;
+  }
+  return MCDC_OK;
+}
+
+int mcdc_chunk_batch(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *const *bufs,
+                     const size_t *lens, size_t nbufs, mcdc_chunk *out, size_t cap, size_t *counts,
+                     size_t *n_out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (nbufs && (!bufs || !lens)) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((rc = check_params(params, nullptr, nullptr))) return rc;
+  const double t0 = now_ms();
+  uint64_t total = 0;
+  std::vector<uint64_t> offs(nbufs), ls(nbufs);
+  for (size_t i = 0; i < nbufs; ++i) {
+    if (lens[i] && !bufs[i]) return fail(MCDC_E_INVALID, "bufs[%zu] is NULL", i);
+    offs[i] = total;
+    ls[i] = lens[i];
+    total += lens[i];
+  }
+  if (total > ctx->max_bytes) return fail(MCDC_E_TOOBIG, "batch bytes %llu > max_bytes", (unsigned long long)total);
+  const double th0 = now_ms();
+  if ((rc = stage_to_arena(ctx, bufs, lens, nbufs, total))) return rc;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  const double th1 = now_ms();
+  std::vector<uint64_t> fs(nbufs), fe(nbufs);
+  for (size_t i = 0; i < nbufs; ++i) { fs[i] = offs[i]; fe[i] = offs[i] + ls[i]; }
+  const uint64_t n_al = (total + 15) / 16 * 16;
+  rc = run_pipeline(ctx, params, (const uint8_t *)ctx->arena.p, n_al, fs.data(), fe.data(), nbufs,
+                    out, cap, counts, n_out);
+  ctx->timing.h2d_ms = th1 - th0;
+  ctx->timing.total_ms = now_ms() - t0;
+  return rc;
+}
+
+int mcdc_chunk_host(mcdc_ctx *ctx, const mcdc_params *params, const void *h_data, size_t n,
+                    mcdc_chunk *out, size_t cap, size_t *n_out) {
+  const uint8_t *b = (const uint8_t *)h_data;
+  if (!h_data && n) return fail(MCDC_E_INVALID, "h_data is NULL");
+  return mcdc_chunk_batch(ctx, params, &b, &n, 1, out, cap, nullptr, n_out);
+}
+
+int mcdc_device_alloc(mcdc_ctx *ctx, size_t bytes, void **d_ptr) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!d_ptr) return fail(MCDC_E_INVALID, "d_ptr is NULL");
+  if (hipMalloc(d_ptr, bytes ? bytes : 16) != hipSuccess) {
+    (void)hipGetLastError();
+    *d_ptr = nullptr;
+    return fail(MCDC_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+  }
+  return MCDC_OK;
+}
+
+int mcdc_device_free(mcdc_ctx *ctx, void *d_ptr) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (d_ptr) HIP_TRY(hipFree(d_ptr));
+  return MCDC_OK;
+}
+
+int mcdc_host_alloc(mcdc_ctx *ctx, size_t bytes, void **h_ptr) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!h_ptr) return fail(MCDC_E_INVALID, "h_ptr is NULL");
+  if (hipHostMalloc(h_ptr, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *h_ptr = nullptr;
+    return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+  }
+  return MCDC_OK;
+}
+
+int mcdc_host_free(mcdc_ctx *ctx, void *h_ptr) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (h_ptr) HIP_TRY(hipHostFree(h_ptr));
+  return MCDC_OK;
+}
+
+int mcdc_memcpy_h2d(mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return MCDC_OK;
+}
+
+int mcdc_fill_random_device(mcdc_ctx *ctx, void *d_dst, uint64_t pos, size_t n, uint64_t seed) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!d_dst && n) return fail(MCDC_E_INVALID, "d_dst is NULL");
+  launch_fill_random(d_dst, pos, n, seed, ctx->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return MCDC_OK;
+}
+
+static uint64_t mix64h(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+uint64_t mcdc_digest(const mcdc_chunk *chunks, size_t n) {
+  uint64_t d = 0;
+  for (size_t i = 0; i < n; ++i) {
+    d = mix64h(d ^ (chunks[i].offset + 0x9e3779b97f4a7c15ull + (d << 6) + (d >> 2)));
+    d = mix64h(d ^ (chunks[i].length + 0x9e3779b97f4a7c15ull + (d << 6) + (d >> 2)));
+  }
+  return d;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+// mcdc_internal.h — device data layout shared by the HIP kernels
+// (mcdc_kernels.hip) and the C-ABI host code (mcdc_api.hip).
+//
+// Pipeline:
+//   k_scan      streaming, HBM-bound: per-position windowed Gear hash, exact
+//               S/L flags for every position whose 48-byte window passes the
+//               prefilter -> per-run candidate lists (run = kRun bytes/lane)
+//   k_spec      one wave per segment: speculative cut chain from the segment
+//               start (wave-level `next` = exact fastcdc cut_gear semantics)
+//   k_link      one wave per segment: continue past the segment end until
+//               the chain merges with a later segment's speculative chain
+//   k_fallback  one wave per file whose continuation never merged: serial walk
+//   k_walk      one wave per file: mark the segments on the true chain
+//   k_count / hipcub exclusive scan / k_emit: (offset, length, hash) per chunk
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mcdc {
+
+constexpr int kRun = 2048;            // bytes hashed per lane per scan run
+constexpr int kWin = 48;              // bits 0..47 of the Gear hash = last 48 bytes
+constexpr int kContMax = 64;          // continuation steps before serial fallback
+constexpr uint8_t kRunOverflow = 255; // run_cnt marker: candidates exceed cap
+constexpr uint32_t kSegNone = 0xffffffffu;
+constexpr uint32_t kSegFail = 0xfffffffeu;
+
+// per-segment flags
+constexpr uint32_t kSegFirst = 1u, kSegLast = 2u;
+// per-file flags (set with atomicOr by k_link)
+constexpr uint32_t kFileSkip = 1u, kFileFail = 2u, kFileFallbackDone = 4u;
+// error word bits
+constexpr uint32_t kErrNodeCap = 1u, kErrOutCap = 2u;
+
+struct Seg {
+  uint64_t start, end;  // arena positions [start, end)
+  uint32_t file, flags;
+};
+
+struct File {
+  uint64_t start, end;  // arena positions
+  uint32_t first_seg, nsegs;
+};
+
+struct DevChunk {       // == mcdc_chunk
+  uint64_t offset, length, hash;
+};
+
+struct DevParams {
+  uint32_t min, avg, max, cap;  // cap = candidate slots per run
+  uint64_t ms, ml;              // mask_s, mask_l
+  uint64_t ms16, ml16;          // masks << 16 (scan keeps h << 16)
+  uint32_t pf_hi;               // prefilter on the high dword of h << 16
+  uint32_t pad;
+};
+
+struct Work {
+  const uint8_t *base;   // 16-byte aligned arena base
+  uint64_t n_al;         // arena length (multiple of 16)
+  uint64_t nruns;        // ceil(n_al / kRun)
+  const uint64_t *gear;  // GEAR[256]
+  const uint64_t *gear16;// GEAR[256] << 16
+  uint8_t *run_cnt;      // [nruns]
+  uint32_t *run_ent;     // [nruns * cap]: off | S<<31 | L<<30
+
+  const Seg *segs;
+  uint32_t nsegs, nfiles;
+  const File *files;
+  uint64_t zseg;         // segment length (bytes)
+
+  uint64_t *nodes;       // speculative chain nodes, per segment at node_off[s]
+  const uint64_t *node_off;
+  uint32_t *node_cnt;
+  uint64_t *seg_exit;    // first chain position >= segment end
+  uint64_t *cont;        // [nsegs * kContMax] continuation nodes
+  uint32_t *cont_cnt;
+  uint32_t *link_seg;    // segment the continuation merged into (or None/Fail)
+  uint32_t *link_idx;    // index of the merge node in that segment's list
+  uint64_t *link_pos;    // merge position (= next true chunk start) or file end
+  uint32_t *file_flags;
+  uint8_t *seg_true;
+  uint32_t *entry_idx;
+  uint64_t *seg_count;   // chunks emitted per segment
+  uint64_t *seg_off;     // exclusive prefix of seg_count
+  DevChunk *out;
+  uint64_t out_cap;
+  uint32_t *err;
+};
+
+// launch wrappers (mcdc_kernels.hip); all enqueue on `stream`.
+void launch_fill_random(void *dst, uint64_t pos, uint64_t n, uint64_t seed, hipStream_t stream);
+void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream);
+void launch_resolve(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
+                    hipStream_t stream);
+size_t scan_tmp_bytes(uint32_t nsegs);
+
+}  // namespace mcdc

@@ -1,0 +1,244 @@
+"""ctypes front-end of the FastCDC v2020 CPU restatement (oracle/fastcdc_oracle.c).
+
+TEST INFRASTRUCTURE ONLY — the parity checker and the timed CPU baseline.
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module.  The product path
+(``mapache_amd``) never does.
+
+Provenance: see ``fastcdc_oracle.h``.  The reference's chunker is the
+un-vendored crate ``fastcdc`` 3.2.1 (``/root/reference/Cargo.lock:449-452``)
+called at ``/root/reference/src/archiver/processor.rs:173-179``; parity is
+"vs this restatement" (pinned by the GEAR derivation, the MASKS popcounts and
+the crate's recalled ``test_all_zeros`` KAT).  Also holds a pure-Python loop
+(``cut_gear_py``) used as a third, independent statement on small inputs.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import math
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+MINIMUM_MIN, MINIMUM_MAX = 64, 1_048_576
+AVERAGE_MIN, AVERAGE_MAX = 256, 4_194_304
+MAXIMUM_MIN, MAXIMUM_MAX = 1024, 16_777_216
+
+
+class OcParams(ctypes.Structure):
+    _fields_ = [
+        ("min_size", ctypes.c_uint32), ("avg_size", ctypes.c_uint32),
+        ("max_size", ctypes.c_uint32), ("level", ctypes.c_uint32),
+        ("mask_s", ctypes.c_uint64), ("mask_l", ctypes.c_uint64),
+        ("mask_s_ls", ctypes.c_uint64), ("mask_l_ls", ctypes.c_uint64),
+    ]
+
+
+CHUNK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("hash", "<u8")])
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.oc_params_init.argtypes = [ctypes.POINTER(OcParams), ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32]
+        L.oc_params_init.restype = ctypes.c_int
+        for name in ("oc_gear", "oc_gear_ls", "oc_masks"):
+            getattr(L, name).argtypes = [u64p]
+            getattr(L, name).restype = None
+        L.oc_logarithm2.argtypes = [ctypes.c_uint32]
+        L.oc_logarithm2.restype = ctypes.c_uint32
+        for name in ("oc_cut_gear", "oc_cut_gear_1byte"):
+            getattr(L, name).argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_size_t,
+                                         u64p, ctypes.POINTER(ctypes.c_size_t)]
+            getattr(L, name).restype = None
+        for name in ("oc_chunk_slice", "oc_chunk_slice_1byte"):
+            getattr(L, name).argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_size_t]
+            getattr(L, name).restype = ctypes.c_size_t
+        L.oc_chunk_stream.argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        L.oc_chunk_stream.restype = ctypes.c_size_t
+        L.oc_chunk_files.argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p]
+        L.oc_chunk_files.restype = ctypes.c_size_t
+        L.oc_chunk_digest.argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_size_t, u64p]
+        L.oc_chunk_digest.restype = ctypes.c_size_t
+        L.oc_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint64]
+        L.oc_fill_random.restype = None
+        L.oc_file_seed.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.oc_file_seed.restype = ctypes.c_uint64
+        L.oc_digest_step.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        L.oc_digest_step.restype = ctypes.c_uint64
+        _lib = L
+    return _lib
+
+
+# ----------------------------------------------------------------- params --
+@dataclass(frozen=True)
+class Params:
+    min_size: int
+    avg_size: int
+    max_size: int
+    level: int = 1
+
+    def c(self) -> OcParams:
+        p = OcParams()
+        if lib().oc_params_init(ctypes.byref(p), self.min_size, self.avg_size, self.max_size, self.level) != 0:
+            raise ValueError(f"invalid FastCDC params {self}")
+        return p
+
+
+P16 = Params(16 * 1024, 64 * 1024, 256 * 1024, 1)      # BASELINE.json configs
+P512 = Params(512 * 1024, 1024 * 1024, 8 * 1024 * 1024, 1)  # reference defaults.rs:35-40
+
+
+def tables():
+    g = (ctypes.c_uint64 * 256)()
+    gl = (ctypes.c_uint64 * 256)()
+    m = (ctypes.c_uint64 * 26)()
+    lib().oc_gear(g)
+    lib().oc_gear_ls(gl)
+    lib().oc_masks(m)
+    return list(g), list(gl), list(m)
+
+
+def gear_md5() -> list[int]:
+    """Independent derivation with Python's hashlib."""
+    return [int.from_bytes(hashlib.md5(bytes([i]) * 64).digest()[:8], "big") for i in range(256)]
+
+
+# -------------------------------------------------------------- chunking --
+def _buf(data):
+    a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data,
+                             dtype=np.uint8)
+    return a, a.ctypes.data
+
+
+def cut_gear(params: Params, data, one_byte: bool = False):
+    a, ptr = _buf(data)
+    h = ctypes.c_uint64()
+    c = ctypes.c_size_t()
+    fn = lib().oc_cut_gear_1byte if one_byte else lib().oc_cut_gear
+    fn(ctypes.byref(params.c()), ptr, a.size, ctypes.byref(h), ctypes.byref(c))
+    return h.value, c.value
+
+
+def chunk(params: Params, data, one_byte: bool = False) -> np.ndarray:
+    """FastCDC over a whole slice -> structured array (offset, length, hash)."""
+    a, ptr = _buf(data)
+    cap = a.size // max(params.min_size - 1, 1) + 2
+    out = np.zeros(cap, dtype=CHUNK_DTYPE)
+    fn = lib().oc_chunk_slice_1byte if one_byte else lib().oc_chunk_slice
+    k = fn(ctypes.byref(params.c()), ptr, a.size, out.ctypes.data, cap)
+    assert k <= cap
+    return out[:k].copy()
+
+
+def chunk_stream(params: Params, data, read_quantum: int) -> np.ndarray:
+    a, ptr = _buf(data)
+    cap = a.size // max(params.min_size - 1, 1) + 2
+    out = np.zeros(cap, dtype=CHUNK_DTYPE)
+    k = lib().oc_chunk_stream(ctypes.byref(params.c()), ptr, a.size, read_quantum, out.ctypes.data, cap)
+    return out[:k].copy()
+
+
+def chunk_files(params: Params, files, threads: int = 1):
+    arrs = [np.ascontiguousarray(np.frombuffer(f, dtype=np.uint8) if not isinstance(f, np.ndarray) else f,
+                                 dtype=np.uint8) for f in files]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[x.ctypes.data for x in arrs])
+    lens = (ctypes.c_size_t * max(n, 1))(*[x.size for x in arrs])
+    cap = sum(x.size // max(params.min_size - 1, 1) + 2 for x in arrs)
+    out = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
+    counts = np.zeros(max(n, 1), dtype=np.uint64)
+    k = lib().oc_chunk_files(ctypes.byref(params.c()), ptrs, lens, n, threads, out.ctypes.data, cap,
+                             counts.ctypes.data)
+    if k == ctypes.c_size_t(-1).value:
+        raise RuntimeError("oc_chunk_files failed")
+    return out[:k].copy(), counts[:n].astype(np.int64)
+
+
+def chunk_digest(params: Params, data):
+    a, ptr = _buf(data)
+    d = ctypes.c_uint64()
+    k = lib().oc_chunk_digest(ctypes.byref(params.c()), ptr, a.size, ctypes.byref(d))
+    return k, d.value
+
+
+def digest_of(chunks: np.ndarray) -> int:
+    d = 0
+    step = lib().oc_digest_step
+    for off, ln in zip(chunks["offset"].tolist(), chunks["length"].tolist()):
+        d = step(d, off, ln)
+    return d
+
+
+def random_bytes(n: int, seed: int, pos: int = 0) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint8)
+    lib().oc_fill_random(out.ctypes.data, pos, n, seed)
+    return out
+
+
+def file_seed(seed: int, index: int) -> int:
+    return lib().oc_file_seed(seed, index)
+
+
+# ------------------------------------------------- pure-Python statement --
+_M64 = (1 << 64) - 1
+
+
+def cut_gear_py(params: Params, src: bytes):
+    """Third statement of crate cut_gear (2-byte loop), pure Python, small inputs only."""
+    g = gear_md5()
+    gls = [(x << 1) & _M64 for x in g]
+    _, _, masks = tables()
+    bits = round(math.log2(params.avg_size))
+    ms, ml = masks[bits + params.level], masks[bits - params.level]
+    msl, mll = (ms << 1) & _M64, (ml << 1) & _M64
+    remaining = len(src)
+    if remaining <= params.min_size:
+        return 0, remaining
+    center = params.avg_size
+    if remaining > params.max_size:
+        remaining = params.max_size
+    elif remaining < center:
+        center = remaining
+    index, h = params.min_size // 2, 0
+    while index < center // 2:
+        a = 2 * index
+        h = ((h << 2) + gls[src[a]]) & _M64
+        if h & msl == 0:
+            return h, a
+        h = (h + g[src[a + 1]]) & _M64
+        if h & ms == 0:
+            return h, a + 1
+        index += 1
+    while index < remaining // 2:
+        a = 2 * index
+        h = ((h << 2) + gls[src[a]]) & _M64
+        if h & mll == 0:
+            return h, a
+        h = (h + g[src[a + 1]]) & _M64
+        if h & ml == 0:
+            return h, a + 1
+        index += 1
+    return h, remaining
