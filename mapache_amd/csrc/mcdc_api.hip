@@ -454,13 +454,34 @@ static int stage_to_arena(mcdc_ctx *ctx, const uint8_t *const *bufs, const size_
   int rc = ensure(ctx, ctx->arena, total + 16);
   if (rc) return rc;
   const size_t slab = (size_t)std::min<uint64_t>(total ? total : 1, 256ull << 20);
-  if ((rc = ensure_stage(ctx, 2 * slab))) return rc;
-  uint8_t *stage[2] = {(uint8_t *)ctx->h_stage, (uint8_t *)ctx->h_stage + slab};
+  uint8_t *stage[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {ctx->ev_h2d0, ctx->ev_h2d1};
   bool inflight[2] = {false, false};
   uint64_t dst = 0;
   size_t bi = 0, boff = 0;
   int k = 0;
+  // Buffers that already live in pinned (or device) memory are DMA'd directly.
+  auto direct = [&](const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice;
+  };
+  bool all_direct = nbufs > 0;
+  for (size_t i = 0; i < nbufs && all_direct; ++i) all_direct = lens[i] == 0 || direct(bufs[i]);
+  if (all_direct) {
+    for (size_t i = 0; i < nbufs; ++i) {
+      if (lens[i])
+        HIP_TRY(hipMemcpyAsync((uint8_t *)ctx->arena.p + dst, bufs[i], lens[i], hipMemcpyDefault, ctx->stream));
+      dst += lens[i];
+    }
+    return MCDC_OK;
+  }
+  if ((rc = ensure_stage(ctx, 2 * slab))) return rc;
+  stage[0] = (uint8_t *)ctx->h_stage;
+  stage[1] = (uint8_t *)ctx->h_stage + slab;
   while (dst < total) {
     if (inflight[k]) HIP_TRY(hipEventSynchronize(done[k]));
     size_t fill = 0;

@@ -18,7 +18,7 @@
 
 namespace mcdc {
 
-constexpr int kRun = 2048;            // bytes hashed per lane per scan run
+constexpr int kRun = 4096;            // bytes hashed per lane per scan run
 constexpr int kWin = 48;              // bits 0..47 of the Gear hash = last 48 bytes
 constexpr int kContMax = 64;          // continuation steps before serial fallback
 constexpr uint8_t kRunOverflow = 255; // run_cnt marker: candidates exceed cap

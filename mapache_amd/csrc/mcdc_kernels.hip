@@ -21,6 +21,7 @@
 
 #include "mcdc_internal.h"
 
+
 namespace mcdc {
 
 // ======================================================== wave helpers ====
@@ -146,11 +147,15 @@ __device__ __forceinline__ void scan16(const uint64_t *tab, uint32_t lo, const u
   }
 }
 
+// One full run of RUN bytes.  PF = 64-byte groups kept in flight ahead of the
+// group being hashed (register ring of 4*PF uint4 per lane).
+template <int RUN, int PF>
 __device__ __forceinline__ void scan_run_full(const uint64_t *tab, uint32_t lo, const Work &W,
-                                              const DevParams &P, uint64_t run) {
-  const uint4 *p = reinterpret_cast<const uint4 *>(W.base + run * (uint64_t)kRun);
+                                              const DevParams &P, uint64_t run, uint64_t addr_run) {
+  static_assert(RUN % 64 == 0 && RUN / 64 > PF, "run too short");
+  const uint4 *p = reinterpret_cast<const uint4 *>(W.base + addr_run * (uint64_t)RUN);
   uint64_t h = 0;
-  if (run > 0) {  // warm-up: the 48 bytes before the run complete every window
+  if (addr_run > 0) {  // warm-up: the 48 bytes before the run complete every window
     const uint4 w0 = p[-3], w1 = p[-2], w2 = p[-1];
     hash16(tab, lo, w0, h);
     hash16(tab, lo, w1, h);
@@ -160,31 +165,39 @@ __device__ __forceinline__ void scan_run_full(const uint64_t *tab, uint32_t lo, 
   const uint64_t ms16 = P.ms16, ml16 = P.ml16;
   uint32_t *ent = W.run_ent + run * (uint64_t)cap;
   uint32_t cnt = 0;
-  uint4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+  constexpr int G = RUN / 64;
+  uint4 ring[PF + 1][4];
+#pragma unroll
+  for (int k = 0; k < PF; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ring[k][j] = p[4 * k + j];
 #pragma unroll 1
-  for (int g = 0; g < kRun / 64 - 1; ++g) {
-    const uint4 b0 = p[4 * g + 4], b1 = p[4 * g + 5], b2 = p[4 * g + 6], b3 = p[4 * g + 7];
-    const uint32_t off = 64u * g;
-    scan16(tab, lo, a0, h, pf, ms16, ml16, off, cnt, ent, cap);
-    scan16(tab, lo, a1, h, pf, ms16, ml16, off + 16, cnt, ent, cap);
-    scan16(tab, lo, a2, h, pf, ms16, ml16, off + 32, cnt, ent, cap);
-    scan16(tab, lo, a3, h, pf, ms16, ml16, off + 48, cnt, ent, cap);
-    a0 = b0; a1 = b1; a2 = b2; a3 = b3;
-  }
-  {
-    const uint32_t off = 64u * (kRun / 64 - 1);
-    scan16(tab, lo, a0, h, pf, ms16, ml16, off, cnt, ent, cap);
-    scan16(tab, lo, a1, h, pf, ms16, ml16, off + 16, cnt, ent, cap);
-    scan16(tab, lo, a2, h, pf, ms16, ml16, off + 32, cnt, ent, cap);
-    scan16(tab, lo, a3, h, pf, ms16, ml16, off + 48, cnt, ent, cap);
+  for (int g = 0; g < G; g += PF + 1) {
+    // PF+1 groups per iteration so that ring slots are compile-time indices
+#pragma unroll
+    for (int u = 0; u <= PF; ++u) {
+      const int gg = g + u;
+      if (gg < G) {
+        {  // unconditional (clamped) prefetch keeps vmcnt waits counted
+          const int src = gg + PF < G ? gg + PF : G - 1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ring[(u + PF) % (PF + 1)][j] = p[4 * src + j];
+        }
+        const uint32_t off = 64u * gg;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          scan16(tab, lo, ring[u][j], h, pf, ms16, ml16, off + 16 * j, cnt, ent, cap);
+      }
+    }
   }
   W.run_cnt[run] = cnt > cap ? kRunOverflow : (uint8_t)cnt;
 }
 
 // Last, partial run: byte loop with exact tests (one lane in the whole grid).
+template <int RUN>
 __device__ void scan_run_tail(const uint64_t *tab, uint32_t lo, const Work &W, const DevParams &P,
                               uint64_t run) {
-  const uint64_t start = run * (uint64_t)kRun, end = W.n_al;
+  const uint64_t start = run * (uint64_t)RUN, end = W.n_al;
   const uint64_t w0 = start >= (uint64_t)kWin ? start - kWin : 0;
   uint64_t h = 0;
   uint32_t cnt = 0;
@@ -202,29 +215,132 @@ __device__ void scan_run_tail(const uint64_t *tab, uint32_t lo, const Work &W, c
   W.run_cnt[run] = cnt > P.cap ? kRunOverflow : (uint8_t)cnt;
 }
 
-__global__ __launch_bounds__(512) void k_scan(Work W, DevParams P) {
+template <int RUN, int WPE, int PF, int CH = 1, int BLOCK = 512>
+__global__ __launch_bounds__(BLOCK, WPE) void k_scan_t(Work W, DevParams P) {
   __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
   for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) tab[i] = W.gear16[i >> 5];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, lo = (lane & 31) << 3;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const uint64_t nfull = W.n_al / kRun;
-  const uint64_t ntiles = (W.nruns + 63) / 64;
+  const uint64_t nfull = W.n_al / RUN;
+  const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
+  const uint64_t ntiles = (nruns + 63) / 64;
   for (uint64_t t = wid; t < ntiles; t += nwaves) {
     const uint64_t run = t * 64 + lane;
-    if (run < nfull) scan_run_full(tab, lo, W, P, run);
-    else if (run < W.nruns) scan_run_tail(tab, lo, W, P, run);
+    if (run < nfull) {
+      scan_run_full<RUN, PF>(tab, lo, W, P, run, run);
+    }
+    else if (run < nruns) scan_run_tail<RUN>(tab, lo, W, P, run);
   }
 }
 
+// ---- Quad-coalesced scan: lane quad i loads one whole 64-byte line of run
+// (4i+k) per load instruction k (16 lines per wave-instruction instead of 64),
+// then the wave transposes through a private 5 KiB LDS pad (run stride 80 B:
+// conflict-free ds_write_b128 / ds_read_b128) so each lane again hashes its
+// own contiguous run.  LDS = 64 KiB table + 16 waves x 5 KiB = 144 KiB.
+constexpr int kQPad = 80;                 // run stride in the transpose pad
+constexpr int kQWaveBytes = 64 * kQPad;   // 5 KiB
+constexpr int kSTab = 65536;              // GEAR<<16 x 32 copies
+
+template <int RUN>
+__global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
+  __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8];
+  const uint64_t *tab = smem;
+  for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) smem[i] = W.gear16[i >> 5];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, lo = (lane & 31) << 3;
+  const uint32_t wv = threadIdx.x >> 6;
+  char *pad = reinterpret_cast<char *>(smem) + kSTab + wv * kQWaveBytes;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  const uint64_t nfull = W.n_al / RUN;
+  const uint64_t ntiles_full = nfull / 64;
+  constexpr int G = RUN / 64;
+  static_assert(G % 2 == 0, "even group count");
+  const uint32_t qi = lane >> 2, qj = lane & 3;
+  // load k: lane (4i+j) fetches piece j of run 4i+k; it lands in the pad at run*80 + 16j
+  char *wr0 = pad + (4 * qi + 0) * kQPad + 16 * qj;
+  char *wr1 = pad + (4 * qi + 1) * kQPad + 16 * qj;
+  char *wr2 = pad + (4 * qi + 2) * kQPad + 16 * qj;
+  char *wr3 = pad + (4 * qi + 3) * kQPad + 16 * qj;
+  const char *rd = pad + lane * kQPad;
+  const uint32_t pf = P.pf_hi, cap = P.cap;
+  const uint64_t ms16 = P.ms16, ml16 = P.ml16;
+  for (uint64_t t = wid; t < ntiles_full; t += nwaves) {
+    const uint64_t run = t * 64 + lane;
+    uint64_t h = 0;
+    if (run > 0) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(W.base + run * (uint64_t)RUN);
+      const uint4 w0 = p[-3], w1 = p[-2], w2 = p[-1];
+      hash16(tab, lo, w0, h);
+      hash16(tab, lo, w1, h);
+      hash16(tab, lo, w2, h);
+    }
+    uint32_t *ent = W.run_ent + run * (uint64_t)cap;
+    uint32_t cnt = 0;
+    // quad-coalesced sources: run (4i+k), piece j
+    const uint8_t *tb = W.base + t * 64 * (uint64_t)RUN + 16 * qj;
+    const uint4 *s0 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 0) * (uint64_t)RUN);
+    const uint4 *s1 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 1) * (uint64_t)RUN);
+    const uint4 *s2 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 2) * (uint64_t)RUN);
+    const uint4 *s3 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 3) * (uint64_t)RUN);
+    uint4 a0 = s0[0], a1 = s1[0], a2 = s2[0], a3 = s3[0];
+    uint4 b0 = s0[4], b1 = s1[4], b2 = s2[4], b3 = s3[4];
+#pragma unroll 1
+    for (int g = 0; g < G; g += 2) {
+      {
+        *reinterpret_cast<uint4 *>(wr0) = a0; *reinterpret_cast<uint4 *>(wr1) = a1;
+        *reinterpret_cast<uint4 *>(wr2) = a2; *reinterpret_cast<uint4 *>(wr3) = a3;
+        const uint4 c0 = *reinterpret_cast<const uint4 *>(rd);
+        const uint4 c1 = *reinterpret_cast<const uint4 *>(rd + 16);
+        const uint4 c2 = *reinterpret_cast<const uint4 *>(rd + 32);
+        const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
+        const int gn = g + 2 < G ? g + 2 : G - 1;  // clamped, unconditional
+        a0 = s0[4 * gn]; a1 = s1[4 * gn]; a2 = s2[4 * gn]; a3 = s3[4 * gn];
+        const uint32_t off = 64u * g;
+        scan16(tab, lo, c0, h, pf, ms16, ml16, off, cnt, ent, cap);
+        scan16(tab, lo, c1, h, pf, ms16, ml16, off + 16, cnt, ent, cap);
+        scan16(tab, lo, c2, h, pf, ms16, ml16, off + 32, cnt, ent, cap);
+        scan16(tab, lo, c3, h, pf, ms16, ml16, off + 48, cnt, ent, cap);
+      }
+      {
+        *reinterpret_cast<uint4 *>(wr0) = b0; *reinterpret_cast<uint4 *>(wr1) = b1;
+        *reinterpret_cast<uint4 *>(wr2) = b2; *reinterpret_cast<uint4 *>(wr3) = b3;
+        const uint4 c0 = *reinterpret_cast<const uint4 *>(rd);
+        const uint4 c1 = *reinterpret_cast<const uint4 *>(rd + 16);
+        const uint4 c2 = *reinterpret_cast<const uint4 *>(rd + 32);
+        const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
+        const int gn = g + 3 < G ? g + 3 : G - 1;
+        b0 = s0[4 * gn]; b1 = s1[4 * gn]; b2 = s2[4 * gn]; b3 = s3[4 * gn];
+        const uint32_t off = 64u * (g + 1);
+        scan16(tab, lo, c0, h, pf, ms16, ml16, off, cnt, ent, cap);
+        scan16(tab, lo, c1, h, pf, ms16, ml16, off + 16, cnt, ent, cap);
+        scan16(tab, lo, c2, h, pf, ms16, ml16, off + 32, cnt, ent, cap);
+        scan16(tab, lo, c3, h, pf, ms16, ml16, off + 48, cnt, ent, cap);
+      }
+    }
+    W.run_cnt[run] = cnt > cap ? kRunOverflow : (uint8_t)cnt;
+  }
+  const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
+  for (uint64_t t = ntiles_full + wid; t * 64 < nruns; t += nwaves) {
+    const uint64_t run = t * 64 + lane;
+    if (run < nfull) scan_run_full<RUN, 1>(tab, lo, W, P, run, run);
+    else if (run < nruns) scan_run_tail<RUN>(tab, lo, W, P, run);
+  }
+}
+
+// Product configuration: quad-coalesced scan, 16 waves (one 1024-thread
+// block) per CU; tools/scanbench.hip keeps the lane-strided k_scan_t variants
+// for comparison.
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream) {
   const uint64_t ntiles = (w.nruns + 63) / 64;
-  uint64_t blocks = (ntiles + 7) / 8;  // 8 waves per 512-thread block
-  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * 2;  // 2 blocks/CU (64 KiB LDS each)
+  uint64_t blocks = (ntiles + 15) / 16;
+  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);  // 144 KiB LDS -> 1 block/CU
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return;
-  hipLaunchKernelGGL(k_scan, dim3((unsigned)blocks), dim3(512), 0, stream, w, p);
+  hipLaunchKernelGGL(k_scan_q<kRun>, dim3((unsigned)blocks), dim3(1024), 0, stream, w, p);
 }
 
 // ===================================================== chain walking =====
@@ -283,12 +399,12 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uin
             found = run_first_hit(W, P, r, lo, hi, cce);
           } else {
             const uint32_t *ent = W.run_ent + r * (uint64_t)P.cap;
-            for (uint32_t i = 0; i < cnt; ++i) {
+            for (uint32_t i = 0; i < cnt; ++i) {  // entries are not position-sorted
               const uint32_t e = ent[i];
               const uint64_t pos = r * (uint64_t)kRun + (e & 0x00ffffffu);
-              if (pos >= lo && pos < hi) {
+              if (pos >= lo && pos < hi && pos < found) {
                 const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
-                if (ok) { found = pos; break; }
+                if (ok) found = pos;
               }
             }
           }

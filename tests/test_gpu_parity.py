@@ -1,0 +1,189 @@
+"""GPU parity: the MI355X path (libmcdc.so through the C ABI) against the
+oracle restatement, bit for bit (offsets, lengths, ChunkData.hash).
+
+Covers the edge cases the reference's call semantics imply
+(/root/reference/src/archiver/processor.rs:160-205: per-file restart, tail
+chunk, empty input) and every internal path of the GPU pipeline: the
+windowed-candidate scan, run overflow (dense candidates -> on-the-fly
+rescans), speculative segment chains that merge, skip a segment, or never
+merge (serial fallback), unaligned device pointers and batches.
+"""
+import numpy as np
+import pytest
+
+from mapache_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x6d61706163686521
+PARAMS = [(16384, 65536, 262144, 1), (524288, 1048576, 8388608, 1), (64, 256, 1024, 1),
+          (4096, 16384, 65536, 2), (65, 300, 1111, 3), (1024, 4096, 16384, 0), (4095, 8191, 65535, 1)]
+
+
+def _same(g, r):
+    assert len(g) == len(r), (len(g), len(r))
+    if len(g):
+        bad = np.nonzero((g["offset"] != r["offset"]) | (g["length"] != r["length"]) | (g["hash"] != r["hash"]))[0]
+        assert bad.size == 0, f"first mismatch at {bad[0]}: gpu {g[bad[0]]} ref {r[bad[0]]}"
+
+
+@pytest.mark.parametrize("p", PARAMS, ids=lambda p: "/".join(map(str, p)))
+def test_random_sizes(ctx, p):
+    for n in [0, 1, 2, 47, 48, 4095, 4096, 4097, 65535, 65536, 262145, (1 << 20) + 3, (7 << 20) + 1,
+              2 * p[2] + 1, 3 * p[2]]:
+        d = O.random_bytes(n, SEED + n)
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+
+
+def test_large_random_host(ctx):
+    d = O.random_bytes(300 << 20, SEED)
+    for p in PARAMS[:2]:
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+
+
+@pytest.mark.parametrize("misalign", [0, 1, 3, 7, 8, 13, 15])
+def test_device_pointer_any_alignment(ctx, misalign):
+    n = (64 << 20) + 12345
+    dp = ctx.device_alloc(n + 64)
+    try:
+        ctx.fill_random(dp, n + 64, SEED)
+        h = O.random_bytes(n, SEED, pos=misalign)
+        p = PARAMS[0]
+        _same(ctx.chunk_device(_lib.params(*p), dp + misalign, n), O.chunk(O.Params(*p), h))
+    finally:
+        ctx.device_free(dp)
+
+
+def test_batch_many_files(ctx):
+    rng = np.random.default_rng(3)
+    sizes = [0, 1, 5, 16383, 16384, 16385, 100_000, 262_144, 262_145, 1 << 20, (3 << 20) + 7, 9 << 20]
+    sizes += rng.integers(0, 2 << 20, 200).tolist()
+    files = [O.random_bytes(int(s), 1000 + i) for i, s in enumerate(sizes)]
+    for p in PARAMS[:4]:
+        g, gc = ctx.chunk_batch(_lib.params(*p), files)
+        r, rc = O.chunk_files(O.Params(*p), files, threads=4)
+        assert (gc == rc).all()
+        _same(g, r)
+
+
+def test_batch_device_arena(ctx):
+    sizes = [70_000, 0, 5 << 20, 123, (2 << 20) + 1, 262_144]
+    gaps = [0, 16, 1, 4095, 0, 7]
+    offs, pos = [], 0
+    for s, gp in zip(sizes, gaps):
+        pos += gp
+        offs.append(pos)
+        pos += s
+    dp = ctx.device_alloc(pos + 64)
+    try:
+        ctx.fill_random(dp, pos + 64, SEED)
+        p = PARAMS[0]
+        g, gc = ctx.chunk_batch_device(_lib.params(*p), dp, offs, sizes)
+        files = [O.random_bytes(s, SEED, pos=o) for o, s in zip(offs, sizes)]
+        r, rc = O.chunk_files(O.Params(*p), files)
+        assert (gc == rc).all()
+        _same(g, r)
+    finally:
+        ctx.device_free(dp)
+
+
+def _find_dense_byte(p):
+    """A constant byte whose windowed hash passes mask_l: every position becomes a candidate."""
+    _, _, masks = O.tables()
+    g = O.gear_md5()
+    import math
+    ml = masks[round(math.log2(p[1])) - p[3]]
+    for b in range(256):
+        w = sum(g[b] << k for k in range(48)) & ((1 << 48) - 1)
+        if w & ml == 0:
+            return b
+    return None
+
+
+@pytest.mark.parametrize("p", PARAMS, ids=lambda p: "/".join(map(str, p)))
+def test_adversarial_patterns(ctx, p):
+    rng = np.random.default_rng(7)
+    pats = [np.zeros(6 << 20, np.uint8),                                     # forced cuts only
+            np.full(3 << 20, 0xa5, np.uint8),
+            np.tile(rng.integers(0, 256, 13, dtype=np.uint8), 300_000),     # periodic, dense or empty
+            np.tile(rng.integers(0, 256, 5000, dtype=np.uint8), 900),
+            np.frombuffer(b"all work and no play makes jack a dull boy\n" * 90_000, np.uint8)]
+    b = _find_dense_byte(p)
+    if b is not None:  # every position a candidate -> every run overflows -> on-the-fly rescans
+        pats.append(np.full(2 << 20, b, np.uint8))
+    for d in pats:
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+
+
+def test_non_merging_chains_take_the_serial_fallback(ctx):
+    """Random prefix sets a forced-cut phase the segment-start speculation never
+    matches; long zero runs then keep every continuation from merging."""
+    p = PARAMS[0]
+    d = np.concatenate([O.random_bytes(100_003, 9), np.zeros(48 << 20, np.uint8), O.random_bytes(3 << 20, 10)])
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    assert ctx.timing()["fallback_files"] == 1
+
+
+def test_skipped_segment_walk(ctx):
+    """A zero run about one segment long: the continuation crosses a whole
+    segment before merging (k_walk's serial link-following)."""
+    p = PARAMS[0]
+    for zlen in [1_310_720 - 5000, 1_310_720 + 70_000, 2 * 1_310_720 + 1]:
+        d = np.concatenate([O.random_bytes(1_000_001, 11), np.zeros(zlen, np.uint8), O.random_bytes(5 << 20, 12)])
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+
+
+def test_full_size_digest_and_invariants(ctx):
+    """8 GiB device-resident stream: digest of (offset, length) equals the
+    oracle's over the regenerated bytes; every chunk within [min, max] except
+    the tail; lengths sum to n."""
+    n = 8 << 30
+    dp = ctx.device_alloc(n)
+    try:
+        ctx.fill_random(dp, n, SEED)
+        p = PARAMS[0]
+        g = ctx.chunk_device(_lib.params(*p), dp, n)
+    finally:
+        ctx.device_free(dp)
+    assert int(g["length"].sum()) == n
+    assert (g["offset"][1:] == np.cumsum(g["length"])[:-1]).all()
+    assert g["length"][:-1].min() >= p[0] and g["length"].max() <= p[2]
+    h = O.random_bytes(n, SEED)
+    k, dig = O.chunk_digest(O.Params(*p), h)
+    assert k == len(g)
+    assert _lib.digest(g) == dig
+    # spot-check hashes on a sample of chunks against cut_gear restarted at the chunk
+    for i in np.linspace(0, len(g) - 2, 64).astype(int):
+        o = int(g["offset"][i])
+        hh, cc = O.cut_gear(O.Params(*p), h[o:o + p[2] + 1])
+        assert (hh, cc) == (int(g["hash"][i]), int(g["length"][i]))
+
+
+def test_python_mirror_fastcdc_and_streamcdc(ctx):
+    import io
+    from mapache_amd import FastCDC, StreamCDC
+    d = O.random_bytes(50 << 20, 21)
+    ref = O.chunk(O.P512, d)
+    got = list(FastCDC(d, 524288, 1048576, 8388608, ctx=ctx))
+    assert [(c.offset, c.length, c.hash) for c in got] == list(zip(ref["offset"].tolist(), ref["length"].tolist(),
+                                                                  ref["hash"].tolist()))
+    stream = list(StreamCDC(io.BytesIO(d.tobytes()), 524288, 1048576, 8388608, window=20 << 20, ctx=ctx))
+    assert [(c.offset, c.length, c.hash) for c in stream] == [(c.offset, c.length, c.hash) for c in got]
+    assert b"".join(c.data for c in stream) == d.tobytes()
+
+
+def test_cpp_host_api_gpu():
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "test_host_api")
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_timing_reported(ctx):
+    d = O.random_bytes(64 << 20, 5)
+    ctx.chunk_host(_lib.params(*PARAMS[0]), d)
+    t = ctx.timing()
+    assert t["bytes"] == d.size and t["chunks"] > 0
+    assert 0 < t["scan_ms"] <= t["device_ms"] and t["h2d_ms"] > 0
