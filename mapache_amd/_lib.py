@@ -116,11 +116,28 @@ class Context:
         self._h = h
         self.device = device
         self.max_bytes = max_bytes
+        self._out = None      # reusable pinned output buffer (np view) and its pointer
+        self._out_ptr = None
 
     def close(self):
         if self._h:
+            if self._out_ptr:
+                load().mcdc_host_free(self._h, ctypes.c_void_p(self._out_ptr))
+                self._out, self._out_ptr = None, None
             load().mcdc_ctx_destroy(self._h)
             self._h = None
+
+    def pinned_out(self, cap: int) -> np.ndarray:
+        """A reusable pinned-host chunk array of at least `cap` entries (grown on demand).
+        Results written into it are only valid until the next call that reuses it."""
+        if self._out is None or self._out.size < cap:
+            if self._out_ptr:
+                check(load().mcdc_host_free(self._h, ctypes.c_void_p(self._out_ptr)))
+            ptr = self.host_alloc(cap * CHUNK_DTYPE.itemsize)
+            buf = (ctypes.c_uint8 * (cap * CHUNK_DTYPE.itemsize)).from_address(ptr)
+            self._out = np.frombuffer(buf, dtype=CHUNK_DTYPE)
+            self._out_ptr = ptr
+        return self._out
 
     def __enter__(self):
         return self
@@ -139,15 +156,23 @@ class Context:
     def _bound(n: int, p: McdcParams) -> int:
         return n // max(p.min_size - 1, 1) + 2
 
-    def _run(self, fn, p: McdcParams, *args, cap: int):
-        out = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
+    def _run(self, fn, p: McdcParams, *args, cap: int, out: np.ndarray | None = None):
+        if out is None:
+            out = np.empty(max(cap, 1), dtype=CHUNK_DTYPE)
+            copy = True
+        else:
+            copy = False
+            cap = min(cap, out.size)
         n_out = ctypes.c_size_t()
         rc = fn(self._h, ctypes.byref(p), *args, out.ctypes.data, cap, ctypes.byref(n_out))
         check(rc)
-        return out[: n_out.value].copy()
+        return out[: n_out.value].copy() if copy else out[: n_out.value]
 
-    def chunk_device(self, p: McdcParams, d_ptr: int, n: int) -> np.ndarray:
-        return self._run(load().mcdc_chunk_device, p, ctypes.c_void_p(d_ptr), n, cap=self._bound(n, p))
+    def chunk_device(self, p: McdcParams, d_ptr: int, n: int, out: np.ndarray | None = None) -> np.ndarray:
+        """Chunks of a device-resident buffer.  With `out` (e.g. ``pinned_out``) the
+        result is a view into it (no allocation, pinned D2H)."""
+        return self._run(load().mcdc_chunk_device, p, ctypes.c_void_p(d_ptr), n, cap=self._bound(n, p),
+                         out=out)
 
     def chunk_host(self, p: McdcParams, data) -> np.ndarray:
         a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)

@@ -10,7 +10,8 @@
 //   k_link      one wave per segment: continue past the segment end until
 //               the chain merges with a later segment's speculative chain
 //   k_fallback  one wave per file whose continuation never merged: serial walk
-//   k_walk      one wave per file: mark the segments on the true chain
+//   k_walk_*    mark the segments on the true chain (parallel common case,
+//               serial link-following for files whose chains skipped a segment)
 //   k_count / hipcub exclusive scan / k_emit: (offset, length, hash) per chunk
 #pragma once
 #include <hip/hip_runtime.h>

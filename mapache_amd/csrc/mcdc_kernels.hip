@@ -361,9 +361,31 @@ __device__ uint64_t run_first_hit(const Work &W, const DevParams &P, uint64_t r,
   return ~0ull;
 }
 
+// First candidate of one run in [lo, hi) from its (up to 8, cap == 8) entries;
+// entries are not position-sorted, so take the minimum.  ~0 if none.
+__device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, const uint4 ea,
+                                                    const uint4 eb, uint64_t lo, uint64_t hi,
+                                                    uint64_t cce) {
+  uint64_t found = ~0ull;
+  const uint64_t rb = r * (uint64_t)kRun;
+  const uint32_t e8[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t e = e8[i];
+    const uint64_t pos = rb + (e & 0x00ffffffu);
+    if ((uint32_t)i < cnt && pos >= lo && pos < hi && pos < found) {
+      const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
+      if (ok) found = pos;
+    }
+  }
+  return found;
+}
+
 // next(c): the chunk starting at arena position c (file ends at fend) ends
 // where fastcdc's cut_gear(&file[c..], min, avg, max, masks) says.  Called by
 // a full wave with wave-uniform c, fend; returns the next chunk start.
+// Latency shape: the restart-window bytes, the first 64 runs' candidate counts
+// and (speculatively) their first 8 entries are all requested at once.
 __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uint64_t fend) {
   const uint32_t lane = lane_id();
   const uint64_t rem = fend - c;
@@ -372,47 +394,81 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uin
   if (rem > P.max) remaining = P.max;
   else if (rem < center) center = rem;
   const uint64_t t0 = (uint64_t)(P.min / 2) * 2, ce = (center / 2) * 2, re = (remaining / 2) * 2;
-  if (re > t0) {
-    // (1) exact restarted hash for the first <= 47 tested positions
-    const uint64_t t = c + t0;
-    const uint32_t wlen = (uint32_t)((re - t0) < (uint64_t)(kWin - 1) ? (re - t0) : (uint64_t)(kWin - 1));
-    uint64_t h = lane < wlen ? W.gear[W.base[t + lane]] : 0;
-#pragma unroll
-    for (unsigned d = 1; d < 64; d <<= 1) {
-      const uint64_t v = shfl_up64(h, d);
-      if (lane >= d) h += v << d;
+  if (re <= t0) return c + remaining;             // loop never runs: forced
+  const uint64_t t = c + t0;
+  const uint32_t wlen = (uint32_t)((re - t0) < (uint64_t)(kWin - 1) ? (re - t0) : (uint64_t)(kWin - 1));
+  const uint64_t lo = t + (kWin - 1), hi = c + re, cce = c + ce;
+  const bool cand = lo < hi;
+  const uint64_t r0 = lo / kRun, r1 = cand ? (hi - 1) / kRun : 0;
+  // ---- level-1 loads, all independent
+  const uint32_t byte = lane < wlen ? W.base[t + lane] : 0;
+  const uint64_t r = r0 + lane;
+  const bool rl = cand && r <= r1;
+  uint32_t cnt = 0;
+  uint4 ea = make_uint4(0, 0, 0, 0), eb = make_uint4(0, 0, 0, 0);
+  if (rl) {
+    cnt = W.run_cnt[r];
+    if (P.cap == 8) {
+      const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
+      ea = ep[0];
+      eb = ep[1];
     }
-    bool pass = false;
-    if (lane < wlen) pass = (h & ((t0 + lane < ce) ? P.ms : P.ml)) == 0;
-    const uint64_t b = __ballot(pass);
-    if (b) return t + (uint64_t)(__ffsll((unsigned long long)b) - 1);
-    // (2) windowed candidates for [t + 47, c + re)
-    const uint64_t lo = t + (kWin - 1), hi = c + re, cce = c + ce;
-    if (lo < hi) {
-      const uint64_t r0 = lo / kRun, r1 = (hi - 1) / kRun;
-      for (uint64_t rb = r0; rb <= r1; rb += 64) {
-        const uint64_t r = rb + lane;
-        uint64_t found = ~0ull;
-        if (r <= r1) {
-          const uint32_t cnt = W.run_cnt[r];
-          if (cnt > P.cap) {
-            found = run_first_hit(W, P, r, lo, hi, cce);
-          } else {
-            const uint32_t *ent = W.run_ent + r * (uint64_t)P.cap;
-            for (uint32_t i = 0; i < cnt; ++i) {  // entries are not position-sorted
-              const uint32_t e = ent[i];
-              const uint64_t pos = r * (uint64_t)kRun + (e & 0x00ffffffu);
-              if (pos >= lo && pos < hi && pos < found) {
-                const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
-                if (ok) found = pos;
-              }
-            }
+  }
+  // ---- (1) exact restarted hash for the first <= 47 tested positions
+  uint64_t h = lane < wlen ? W.gear[byte] : 0;
+#pragma unroll
+  for (unsigned d = 1; d < 64; d <<= 1) {
+    const uint64_t v = shfl_up64(h, d);
+    if (lane >= d) h += v << d;
+  }
+  bool pass = false;
+  if (lane < wlen) pass = (h & ((t0 + lane < ce) ? P.ms : P.ml)) == 0;
+  const uint64_t b = __ballot(pass);
+  if (b) return t + (uint64_t)(__ffsll((unsigned long long)b) - 1);
+  if (!cand) return c + remaining;
+  // ---- (2) windowed candidates for [t + 47, c + re), first 64 runs
+  {
+    uint64_t found = ~0ull;
+    if (rl) {
+      if (cnt > P.cap) {
+        found = run_first_hit(W, P, r, lo, hi, cce);
+      } else if (P.cap == 8) {
+        found = run_first_entry(r, cnt, ea, eb, lo, hi, cce);
+      } else {
+        for (uint32_t i = 0; i < cnt; ++i) {
+          const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
+          const uint64_t pos = r * (uint64_t)kRun + (e & 0x00ffffffu);
+          if (pos >= lo && pos < hi && pos < found) {
+            const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
+            if (ok) found = pos;
           }
         }
-        const uint64_t fb = __ballot(found != ~0ull);
-        if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
       }
     }
+    const uint64_t fb = __ballot(found != ~0ull);
+    if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
+  }
+  // ---- later batches (only when max spans more than 64 runs)
+  for (uint64_t rb = r0 + 64; rb <= r1; rb += 64) {
+    const uint64_t rr = rb + lane;
+    uint64_t found = ~0ull;
+    if (rr <= r1) {
+      const uint32_t cn = W.run_cnt[rr];
+      if (cn > P.cap) {
+        found = run_first_hit(W, P, rr, lo, hi, cce);
+      } else {
+        for (uint32_t i = 0; i < cn; ++i) {
+          const uint32_t e = W.run_ent[rr * (uint64_t)P.cap + i];
+          const uint64_t pos = rr * (uint64_t)kRun + (e & 0x00ffffffu);
+          if (pos >= lo && pos < hi && pos < found) {
+            const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
+            if (ok) found = pos;
+          }
+        }
+      }
+    }
+    const uint64_t fb = __ballot(found != ~0ull);
+    if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
   }
   return c + remaining;  // forced cut (e.g. all zeros)
 }
@@ -527,22 +583,27 @@ __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
 }
 
 // ============================================================ walk =======
-__global__ __launch_bounds__(64) void k_walk(Work W) {
+// Common case (every continuation merged into the next segment, or the file
+// was resolved serially): every segment is on the true chain; entry = the
+// merge index handed over by the previous segment.  One thread per segment.
+__global__ void k_walk_fast(Work W) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= W.nsegs) return;
+  const Seg S = W.segs[s];
+  const uint32_t fl = W.file_flags[S.file];
+  if (fl != 0 && !(fl & kFileFallbackDone)) return;  // k_walk_seq owns this file
+  W.seg_true[s] = 1;
+  W.entry_idx[s] = ((S.flags & kSegFirst) || (fl & kFileFallbackDone)) ? 0 : W.link_idx[s - 1];
+}
+
+// Files whose chain skipped a segment: follow the links serially (one wave).
+__global__ __launch_bounds__(64) void k_walk_seq(Work W) {
   const uint32_t f = blockIdx.x;
   if (f >= W.nfiles) return;
+  const uint32_t fl = W.file_flags[f];
+  if (fl == 0 || (fl & kFileFallbackDone)) return;
   const uint32_t lane = lane_id();
   const File F = W.files[f];
-  const uint32_t fl = W.file_flags[f];
-  if (fl == 0 || (fl & kFileFallbackDone)) {
-    const bool fb = (fl & kFileFallbackDone) != 0;
-    for (uint32_t i = lane; i < F.nsegs; i += 64) {
-      const uint32_t s = F.first_seg + i;
-      W.seg_true[s] = 1;
-      W.entry_idx[s] = (i == 0 || fb) ? 0 : W.link_idx[s - 1];
-    }
-    return;
-  }
-  // chains skipped a segment: follow the links serially
   for (uint32_t i = lane; i < F.nsegs; i += 64) W.seg_true[F.first_seg + i] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
@@ -639,7 +700,8 @@ void launch_resolve(const Work &w, const DevParams &p, void *scan_tmp, size_t sc
   hipLaunchKernelGGL(k_spec, dim3(wave_blocks), dim3(256), 0, stream, w, p);
   hipLaunchKernelGGL(k_link, dim3(wave_blocks), dim3(256), 0, stream, w, p);
   hipLaunchKernelGGL(k_fallback, dim3(w.nfiles), dim3(64), 0, stream, w, p);
-  hipLaunchKernelGGL(k_walk, dim3(w.nfiles), dim3(64), 0, stream, w);
+  hipLaunchKernelGGL(k_walk_fast, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
+  hipLaunchKernelGGL(k_walk_seq, dim3(w.nfiles), dim3(64), 0, stream, w);
   hipLaunchKernelGGL(k_count, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
   size_t bytes = scan_tmp_bytes_;
   // seg_count has nsegs + 1 entries (last = 0) so seg_off[nsegs] = total
