@@ -6,7 +6,7 @@ Host-side Python mirror of the chunker interface mapache uses
 ``include/mcdc.h`` (``libmcdc.so``: HIP kernels for gfx950).  There is no CPU
 fallback: without the built library or a HIP device every call raises.
 """
-from . import _lib  # noqa: F401
+from . import _lib, shard  # noqa: F401
 from .fastcdc import (  # noqa: F401
     AVERAGE_MAX, AVERAGE_MIN, MAXIMUM_MAX, MAXIMUM_MIN, MINIMUM_MAX, MINIMUM_MIN,
     Chunk, ChunkData, Chunker, Error, FastCDC, Normalization, StreamCDC,
