@@ -235,24 +235,152 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan_t(Work W, DevParams P) {
   }
 }
 
-// ---- Quad-coalesced scan: lane quad i loads one whole 64-byte line of run
-// (4i+k) per load instruction k (16 lines per wave-instruction instead of 64),
-// then the wave transposes through a private 5 KiB LDS pad (run stride 80 B:
-// conflict-free ds_write_b128 / ds_read_b128) so each lane again hashes its
-// own contiguous run.  LDS = 64 KiB table + 16 waves x 5 KiB = 144 KiB.
-constexpr int kQPad = 80;                 // run stride in the transpose pad
-constexpr int kQWaveBytes = 64 * kQPad;   // 5 KiB
-constexpr int kSTab = 65536;              // GEAR<<16 x 32 copies
+// ---- Product scan (k_scan_q).  One wave = one tile of 64 runs (one per
+// lane).  Loads are quad-coalesced: lane quad i fetches one whole 64-byte line
+// of run (4i+k) per load instruction k (16 lines per wave-instruction instead
+// of 64), then the wave transposes through a private LDS pad (run stride 80 B:
+// conflict-free ds_write_b128 / ds_read_b128) so each lane hashes its own
+// contiguous run.  Per byte the loop issues one v_perm_b32 (LDS address), one
+// ds_read_b64 (GEAR<<16), one v_lshl_add_u64 (hash), one v_and_b32 with the
+// prefilter mask held in a VGPR (VOP2 with an SGPR operand issues at half rate
+// on gfx950, tools/ubench2.hip) and half a v_min3_u32; the LDS lookups of the
+// next dword are issued before the hash chain of the current one.
+//
+// Rare path, deferred: a 16-byte block whose prefilter fires (2^-14 per byte
+// at 16/64/256 KiB; ~6 % of wave-steps have at least one such lane) is only
+// queued — hash before the block, run lane, offset — in the 16 spare bytes of
+// the pad rows.  The queue is drained by all lanes at once (one entry per
+// lane) at the end of the tile or when it would overflow; candidates are
+// counted per run with LDS atomics, so a run's entries are unordered (the chain
+// walk takes the minimum).  Measured (tools/scanbench, 16 GiB): the deferred
+// queue alone +7-13 % over re-walking the block under an exec mask.
+//
+// LDS = 64 KiB table + 16 waves x (5 KiB pad + 256 B run counters) = 148 KiB.
+constexpr int kQPad = 80;                        // run stride in the transpose pad
+constexpr int kQPadBytes = 64 * kQPad;           // 5 KiB
+constexpr int kQWaveBytes = kQPadBytes + 64 * 4; // + per-run candidate counters
+constexpr int kSTab = 65536;                     // GEAR<<16 x 32 copies
+
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
+  uint32_t v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+  return v;
+}
+
+__device__ __forceinline__ void lookup4(const uint64_t *tab, uint32_t lo, uint32_t w, uint64_t *g) {
+  g[0] = lds_gear(tab, gaddr<0>(w, lo));
+  g[1] = lds_gear(tab, gaddr<1>(w, lo));
+  g[2] = lds_gear(tab, gaddr<2>(w, lo));
+  g[3] = lds_gear(tab, gaddr<3>(w, lo));
+}
+
+__device__ __forceinline__ void chain4(const uint64_t *g, uint64_t &h, uint32_t &acc, uint32_t pf) {
+  h = (h << 1) + g[0];
+  const uint32_t m0 = (uint32_t)(h >> 32) & pf;
+  h = (h << 1) + g[1];
+  const uint32_t m1 = (uint32_t)(h >> 32) & pf;
+  h = (h << 1) + g[2];
+  const uint32_t m2 = (uint32_t)(h >> 32) & pf;
+  h = (h << 1) + g[3];
+  const uint32_t m3 = (uint32_t)(h >> 32) & pf;
+  acc = min(acc, min(m0, m1));
+  acc = min(acc, min(m2, m3));
+}
+
+// Drain the wave's queue: lane i re-walks entry i's 16 bytes exactly.
+template <int RUN>
+__device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t lo, const uint8_t *base,
+                                                  uint32_t *run_ent, uint64_t ms16, uint64_t ml16, uint32_t cap,
+                                                  const char *pad, uint32_t *lcnt, uint32_t qn, uint64_t run0,
+                                                  uint32_t lane) {
+  if (lane < qn) {
+    const char *slot = pad + lane * kQPad + 64;
+    uint64_t x = *reinterpret_cast<const uint64_t *>(slot);
+    const uint32_t meta = *reinterpret_cast<const uint32_t *>(slot + 8);
+    const uint32_t rl = meta >> 16, off = meta & 0xffffu;
+    const uint64_t run = run0 + rl;
+    const uint4 d = *reinterpret_cast<const uint4 *>(base + run * (uint64_t)RUN + off);
+    uint32_t *ent = run_ent + run * (uint64_t)cap;
+    const uint32_t wd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      x = (x << 1) + lds_gear(tab, ((wd[i >> 2] >> (8 * (i & 3))) & 0xffu) << 8 | lo);
+      const uint32_t s_ = (x & ms16) == 0, l_ = (x & ml16) == 0;
+      if (s_ | l_) {
+        const uint32_t k = atomicAdd(&lcnt[rl], 1u);
+        if (k < cap) ent[k] = (off + i) | (s_ << 31) | (l_ << 30);
+      }
+    }
+  }
+}
+
+struct QScan {  // per-wave state of k_scan_q
+  const uint64_t *tab;
+  uint32_t lo, lane, pf, cap;
+  uint64_t ms16, ml16;
+  char *pad;
+  uint32_t *lcnt;
+  const uint8_t *base;
+  uint32_t *run_ent;
+};
+
+// 64 bytes (16 dwords) of one run: lookups one dword ahead of the chain;
+// every 16 bytes a wave-uniform test queues the blocks whose prefilter fired.
+template <int RUN>
+__device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint64_t &h, uint32_t off,
+                                        uint32_t &qn, uint64_t run0) {
+  uint64_t g[2][4];
+  lookup4(q.tab, q.lo, w[0], g[0]);
+  uint32_t acc = 0xffffffffu;
+  uint64_t hb = h;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    if (d + 1 < 16) lookup4(q.tab, q.lo, w[d + 1], g[(d + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    chain4(g[d & 1], h, acc, q.pf);
+    if (d % 4 == 3) {
+      const uint64_t m = __ballot(acc == 0);
+      if (__builtin_expect(m != 0, 0)) {
+        const uint32_t n = (uint32_t)__popcll(m);
+        if (qn + n > 64) {
+          q_drain<RUN>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, q.lane);
+          qn = 0;
+        }
+        if (acc == 0) {
+          const uint32_t slot =
+              qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          char *sp = q.pad + slot * kQPad + 64;
+          *reinterpret_cast<uint64_t *>(sp) = hb;
+          *reinterpret_cast<uint32_t *>(sp + 8) = (q.lane << 16) | (off + 4 * (d - 3));
+        }
+        qn += n;
+      }
+      acc = 0xffffffffu;
+      hb = h;
+    }
+  }
+}
 
 template <int RUN>
 __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
   __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8];
-  const uint64_t *tab = smem;
   for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) smem[i] = W.gear16[i >> 5];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
+  QScan q;
+  q.tab = smem;
+  q.lo = (lane & 31) << 3;
+  q.lane = lane;
+  q.pf = to_vgpr(P.pf_hi);
+  q.cap = P.cap;
+  q.ms16 = P.ms16;
+  q.ml16 = P.ml16;
+  q.pad = reinterpret_cast<char *>(smem) + kSTab + wv * kQWaveBytes;
+  q.lcnt = reinterpret_cast<uint32_t *>(q.pad + kQPadBytes);
+  q.base = W.base;
+  q.run_ent = W.run_ent;
+  q.lcnt[lane] = 0;
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, lo = (lane & 31) << 3;
-  const uint32_t wv = threadIdx.x >> 6;
-  char *pad = reinterpret_cast<char *>(smem) + kSTab + wv * kQWaveBytes;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   const uint64_t nfull = W.n_al / RUN;
@@ -261,73 +389,69 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
   static_assert(G % 2 == 0, "even group count");
   const uint32_t qi = lane >> 2, qj = lane & 3;
   // load k: lane (4i+j) fetches piece j of run 4i+k; it lands in the pad at run*80 + 16j
-  char *wr0 = pad + (4 * qi + 0) * kQPad + 16 * qj;
-  char *wr1 = pad + (4 * qi + 1) * kQPad + 16 * qj;
-  char *wr2 = pad + (4 * qi + 2) * kQPad + 16 * qj;
-  char *wr3 = pad + (4 * qi + 3) * kQPad + 16 * qj;
-  const char *rd = pad + lane * kQPad;
-  const uint32_t pf = P.pf_hi, cap = P.cap;
-  const uint64_t ms16 = P.ms16, ml16 = P.ml16;
+  char *wr = q.pad + 4 * qi * kQPad + 16 * qj;
+  const char *rd = q.pad + lane * kQPad;
+  const uint32_t o0 = 4 * qi * RUN + 16 * qj;  // lane's byte offset in the tile for load 0, group 0
   for (uint64_t t = wid; t < ntiles_full; t += nwaves) {
-    const uint64_t run = t * 64 + lane;
+    const uint64_t run0 = t * 64, run = run0 + lane;
     uint64_t h = 0;
-    if (run > 0) {
+    if (run > 0) {  // warm-up: the 48 bytes before the run complete every window
       const uint4 *p = reinterpret_cast<const uint4 *>(W.base + run * (uint64_t)RUN);
       const uint4 w0 = p[-3], w1 = p[-2], w2 = p[-1];
-      hash16(tab, lo, w0, h);
-      hash16(tab, lo, w1, h);
-      hash16(tab, lo, w2, h);
+      hash16(q.tab, q.lo, w0, h);
+      hash16(q.tab, q.lo, w1, h);
+      hash16(q.tab, q.lo, w2, h);
     }
-    uint32_t *ent = W.run_ent + run * (uint64_t)cap;
-    uint32_t cnt = 0;
-    // quad-coalesced sources: run (4i+k), piece j
-    const uint8_t *tb = W.base + t * 64 * (uint64_t)RUN + 16 * qj;
-    const uint4 *s0 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 0) * (uint64_t)RUN);
-    const uint4 *s1 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 1) * (uint64_t)RUN);
-    const uint4 *s2 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 2) * (uint64_t)RUN);
-    const uint4 *s3 = reinterpret_cast<const uint4 *>(tb + (4 * qi + 3) * (uint64_t)RUN);
-    uint4 a0 = s0[0], a1 = s1[0], a2 = s2[0], a3 = s3[0];
-    uint4 b0 = s0[4], b1 = s1[4], b2 = s2[4], b3 = s3[4];
+    uint32_t qn = 0;  // wave-uniform queue length
+    const uint8_t *tb = W.base + run0 * (uint64_t)RUN;  // wave-uniform tile base (SGPR)
+#define MCDC_LDQ(k, gg) (*reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * RUN + 64 * (gg))))
+    uint4 a0 = MCDC_LDQ(0, 0), a1 = MCDC_LDQ(1, 0), a2 = MCDC_LDQ(2, 0), a3 = MCDC_LDQ(3, 0);
+    uint4 b0 = MCDC_LDQ(0, 1), b1 = MCDC_LDQ(1, 1), b2 = MCDC_LDQ(2, 1), b3 = MCDC_LDQ(3, 1);
 #pragma unroll 1
     for (int g = 0; g < G; g += 2) {
       {
-        *reinterpret_cast<uint4 *>(wr0) = a0; *reinterpret_cast<uint4 *>(wr1) = a1;
-        *reinterpret_cast<uint4 *>(wr2) = a2; *reinterpret_cast<uint4 *>(wr3) = a3;
+        *reinterpret_cast<uint4 *>(wr) = a0;
+        *reinterpret_cast<uint4 *>(wr + kQPad) = a1;
+        *reinterpret_cast<uint4 *>(wr + 2 * kQPad) = a2;
+        *reinterpret_cast<uint4 *>(wr + 3 * kQPad) = a3;
         const uint4 c0 = *reinterpret_cast<const uint4 *>(rd);
         const uint4 c1 = *reinterpret_cast<const uint4 *>(rd + 16);
         const uint4 c2 = *reinterpret_cast<const uint4 *>(rd + 32);
         const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
         const int gn = g + 2 < G ? g + 2 : G - 1;  // clamped, unconditional
-        a0 = s0[4 * gn]; a1 = s1[4 * gn]; a2 = s2[4 * gn]; a3 = s3[4 * gn];
-        const uint32_t off = 64u * g;
-        scan16(tab, lo, c0, h, pf, ms16, ml16, off, cnt, ent, cap);
-        scan16(tab, lo, c1, h, pf, ms16, ml16, off + 16, cnt, ent, cap);
-        scan16(tab, lo, c2, h, pf, ms16, ml16, off + 32, cnt, ent, cap);
-        scan16(tab, lo, c3, h, pf, ms16, ml16, off + 48, cnt, ent, cap);
+        a0 = MCDC_LDQ(0, gn); a1 = MCDC_LDQ(1, gn); a2 = MCDC_LDQ(2, gn); a3 = MCDC_LDQ(3, gn);
+        const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        scan64q<RUN>(q, w, h, 64u * g, qn, run0);
       }
       {
-        *reinterpret_cast<uint4 *>(wr0) = b0; *reinterpret_cast<uint4 *>(wr1) = b1;
-        *reinterpret_cast<uint4 *>(wr2) = b2; *reinterpret_cast<uint4 *>(wr3) = b3;
+        *reinterpret_cast<uint4 *>(wr) = b0;
+        *reinterpret_cast<uint4 *>(wr + kQPad) = b1;
+        *reinterpret_cast<uint4 *>(wr + 2 * kQPad) = b2;
+        *reinterpret_cast<uint4 *>(wr + 3 * kQPad) = b3;
         const uint4 c0 = *reinterpret_cast<const uint4 *>(rd);
         const uint4 c1 = *reinterpret_cast<const uint4 *>(rd + 16);
         const uint4 c2 = *reinterpret_cast<const uint4 *>(rd + 32);
         const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
         const int gn = g + 3 < G ? g + 3 : G - 1;
-        b0 = s0[4 * gn]; b1 = s1[4 * gn]; b2 = s2[4 * gn]; b3 = s3[4 * gn];
-        const uint32_t off = 64u * (g + 1);
-        scan16(tab, lo, c0, h, pf, ms16, ml16, off, cnt, ent, cap);
-        scan16(tab, lo, c1, h, pf, ms16, ml16, off + 16, cnt, ent, cap);
-        scan16(tab, lo, c2, h, pf, ms16, ml16, off + 32, cnt, ent, cap);
-        scan16(tab, lo, c3, h, pf, ms16, ml16, off + 48, cnt, ent, cap);
+        b0 = MCDC_LDQ(0, gn); b1 = MCDC_LDQ(1, gn); b2 = MCDC_LDQ(2, gn); b3 = MCDC_LDQ(3, gn);
+        const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        scan64q<RUN>(q, w, h, 64u * (g + 1), qn, run0);
       }
     }
-    W.run_cnt[run] = cnt > cap ? kRunOverflow : (uint8_t)cnt;
+#undef MCDC_LDQ
+    if (qn) q_drain<RUN>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
+    const uint32_t cnt = q.lcnt[lane];
+    q.lcnt[lane] = 0;
+    W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
   }
+  // partial last tile: lane-strided runs, exact per-lane path
   const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
   for (uint64_t t = ntiles_full + wid; t * 64 < nruns; t += nwaves) {
     const uint64_t run = t * 64 + lane;
-    if (run < nfull) scan_run_full<RUN, 1>(tab, lo, W, P, run, run);
-    else if (run < nruns) scan_run_tail<RUN>(tab, lo, W, P, run);
+    if (run < nfull) scan_run_full<RUN, 1>(q.tab, q.lo, W, P, run, run);
+    else if (run < nruns) scan_run_tail<RUN>(q.tab, q.lo, W, P, run);
   }
 }
 

@@ -22,6 +22,7 @@ for step in "$@"; do
     test)  run pytest_gpu 1200 python -m pytest tests -q -m gpu -x --timeout=900 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
+    scanvar) run scanvar 300 ./tools/scanbench 16 var ;;
     benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --cpu-sample-gib 4 --e2e-gib 4 ;;
     prof)  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu --e2e-gib 0 \

@@ -195,6 +195,41 @@ int main(int argc, char **argv) {
     report("scan product (quad-coalesced)", med, best);
     return 0;
   }
+  if (mode == "var") {
+    const uint64_t nr = W.nruns;
+    auto snap = [&](std::vector<uint8_t> &cv, std::vector<uint32_t> &ev) {
+      cv.resize(nr); ev.resize(nr * 8);
+      CK(hipMemcpy(cv.data(), cnt, nr, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(ev.data(), ent, nr * 8 * 4, hipMemcpyDeviceToHost));
+    };
+    std::vector<uint8_t> c0, c1; std::vector<uint32_t> e0, e1;
+    CK(hipMemset(ent, 0, nr * 8 * 4));
+    {
+      const uint64_t blocks = std::min<uint64_t>((W.nruns / 64 + 7) / 8, (uint64_t)cus * 2);
+      hipLaunchKernelGGL((k_scan_t<kRun, 2, 1, 1, 512>), dim3(blocks), dim3(512), 0, st, W, P);
+    }
+    CK(hipStreamSynchronize(st)); snap(c0, e0);
+    auto check = [&](const char *name, const std::function<void()> &f) {
+      CK(hipMemset(ent, 0, nr * 8 * 4)); CK(hipMemset(cnt, 0, nr));
+      f(); CK(hipStreamSynchronize(st)); snap(c1, e1);
+      bool ok = c0 == c1;
+      for (uint64_t r = 0; ok && r < nr; ++r) {
+        if (c0[r] > 8) continue;
+        std::vector<uint32_t> x(e0.begin() + 8 * r, e0.begin() + 8 * r + c0[r]), y(e1.begin() + 8 * r, e1.begin() + 8 * r + c0[r]);
+        std::sort(x.begin(), x.end()); std::sort(y.begin(), y.end());
+        ok = x == y;
+      }
+      med = time_it(st, 5, f, &best);
+      char nm[96]; snprintf(nm, sizeof nm, "%s %s", name, ok ? "[ok]" : "[MISMATCH]");
+      report(nm, med, best);
+    };
+    check("product k_scan_q", prod);
+    check("lane-strided k_scan_t (reference)", [&] {
+      const uint64_t blocks = std::min<uint64_t>((W.nruns / 64 + 7) / 8, (uint64_t)cus * 2);
+      hipLaunchKernelGGL((k_scan_t<kRun, 2, 1, 1, 512>), dim3(blocks), dim3(512), 0, st, W, P);
+    });
+    return 0;
+  }
   if (mode == "sweep") {
     for (uint64_t sz = 32ull << 20; sz <= n; sz *= 2) {
       Work Ws = W; Ws.n_al = sz; Ws.nruns = (sz + kRun - 1) / kRun;
