@@ -120,6 +120,8 @@ struct mcdc_ctx {
   std::vector<Seg> h_segs;
   std::vector<File> h_files;
   std::vector<uint64_t> h_node_off;
+  void *h_tab = nullptr;  // pinned copy of the segment tables (async H2D)
+  size_t h_tab_cap = 0;
   mcdc_timing timing{};
 };
 
@@ -159,6 +161,38 @@ int ensure_stage(mcdc_ctx *ctx, size_t bytes) {
   }
   ctx->h_stage_cap = bytes;
   return MCDC_OK;
+}
+
+int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
+  if (ctx->h_tab_cap >= bytes) return MCDC_OK;
+  if (ctx->h_tab) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipHostFree(ctx->h_tab));
+    ctx->h_tab = nullptr;
+    ctx->h_tab_cap = 0;
+  }
+  const size_t alloc = (bytes + bytes / 4 + 4095) / 4096 * 4096;
+  if (hipHostMalloc(&ctx->h_tab, alloc, hipHostMallocDefault) != hipSuccess) {
+    ctx->h_tab = nullptr;
+    (void)hipGetLastError();
+    return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", alloc);
+  }
+  ctx->h_tab_cap = alloc;
+  return MCDC_OK;
+}
+
+// Device-visible alias of a caller's output array when it is pinned host
+// memory (hipHostMalloc / registered): k_emit then writes the boundary list
+// straight over PCIe and no separate copy is needed.  nullptr otherwise.
+void *host_out_alias(void *out) {
+  if (!out) return nullptr;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, out) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  return a.devicePointer;
 }
 
 double now_ms() {
@@ -223,16 +257,26 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if ((rc = ensure(ctx, ctx->entry_idx, nsegs * 4))) return rc;
   if ((rc = ensure(ctx, ctx->seg_count, (nsegs + 1) * 8))) return rc;
   if ((rc = ensure(ctx, ctx->seg_off, (nsegs + 1) * 8))) return rc;
-  if ((rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
+  if (!host_out_alias(out) && (rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
   if ((rc = ensure(ctx, ctx->err, 16))) return rc;
   const size_t tmpb = scan_tmp_bytes(nsegs);
   if ((rc = ensure(ctx, ctx->scan_tmp, tmpb))) return rc;
 
   hipStream_t st = ctx->stream;
-  HIP_TRY(hipMemcpyAsync(ctx->segs.p, ctx->h_segs.data(), nsegs * sizeof(Seg), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->files.p, ctx->h_files.data(), nfiles * sizeof(File), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->node_off.p, ctx->h_node_off.data(), ctx->h_node_off.size() * 8,
-                         hipMemcpyHostToDevice, st));
+  {  // tables -> pinned stage -> one async copy each
+    const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
+                 b_noff = ctx->h_node_off.size() * 8;
+    const size_t o_files = (b_segs + 255) / 256 * 256, o_noff = o_files + (b_files + 255) / 256 * 256;
+    if ((rc = ensure_tab(ctx, o_noff + b_noff))) return rc;
+    char *tb = (char *)ctx->h_tab;
+    if (b_segs) std::memcpy(tb, ctx->h_segs.data(), b_segs);
+    if (b_files) std::memcpy(tb + o_files, ctx->h_files.data(), b_files);
+    std::memcpy(tb + o_noff, ctx->h_node_off.data(), b_noff);
+    if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tb, b_segs, hipMemcpyHostToDevice, st));
+    if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tb + o_files, b_files, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tb + o_noff, b_noff, hipMemcpyHostToDevice, st));
+  }
+  void *out_dev = host_out_alias(out);  // pinned caller array: emit writes it directly
   if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st));
   HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st));
   HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st));
@@ -264,8 +308,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.entry_idx = (uint32_t *)ctx->entry_idx.p;
   W.seg_count = (uint64_t *)ctx->seg_count.p;
   W.seg_off = (uint64_t *)ctx->seg_off.p;
-  W.out = (DevChunk *)ctx->out.p;
-  W.out_cap = out_bound;
+  W.out = out_dev ? (DevChunk *)out_dev : (DevChunk *)ctx->out.p;
+  W.out_cap = out_dev ? std::min<uint64_t>(out_bound, cap) : out_bound;
   W.err = (uint32_t *)ctx->err.p;
 
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
@@ -283,11 +327,11 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if (nsegs) HIP_TRY(hipMemcpyAsync(&total, (uint64_t *)ctx->seg_off.p + nsegs, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(&err, ctx->err.p, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (err) return fail(MCDC_E_INTERNAL, "device consistency error 0x%x", err);
   if (n_out) *n_out = (size_t)total;
   if (total > cap || (total && !out))
     return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu chunks", cap, (unsigned long long)total);
-  if (total)
+  if (err) return fail(MCDC_E_INTERNAL, "device consistency error 0x%x", err);
+  if (total && !out_dev)
     HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st));
   std::vector<uint64_t> seg_off;
   if (counts && nfiles) {
@@ -380,6 +424,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,

@@ -469,14 +469,14 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
 
 // ===================================================== chain walking =====
 // First candidate of run r in [lo, hi) recomputed from bytes (overflowed run).
-__device__ uint64_t run_first_hit(const Work &W, const DevParams &P, uint64_t r, uint64_t lo,
-                                  uint64_t hi, uint64_t cce) {
+__device__ uint64_t run_first_hit(const Work &W, const DevParams &P, const uint64_t *gt, uint64_t r,
+                                  uint64_t lo, uint64_t hi, uint64_t cce) {
   const uint64_t rs = r * (uint64_t)kRun, rend = rs + kRun;
   const uint64_t s = rs > lo ? rs : lo, e = rend < hi ? rend : hi;
   if (s >= e) return ~0ull;
   uint64_t h = 0;
   for (uint64_t q = s - (kWin - 1); q < e; ++q) {  // s >= lo = t + 47
-    h = (h << 1) + W.gear[W.base[q]];
+    h = (h << 1) + gt[W.base[q]];
     if (q >= s) {
       const uint64_t m = q < cce ? P.ms : P.ml;
       if ((h & m) == 0) return q;
@@ -508,9 +508,10 @@ __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, co
 // next(c): the chunk starting at arena position c (file ends at fend) ends
 // where fastcdc's cut_gear(&file[c..], min, avg, max, masks) says.  Called by
 // a full wave with wave-uniform c, fend; returns the next chunk start.
-// Latency shape: the restart-window bytes, the first 64 runs' candidate counts
-// and (speculatively) their first 8 entries are all requested at once.
-__device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uint64_t fend) {
+// Latency shape: two dependent global levels per step — {restart-window bytes,
+// the first 64 runs' candidate counts}, then {entries of the non-empty runs};
+// GEAR comes from the block's LDS copy `gt`.
+__device__ uint64_t wave_next(const Work &W, const DevParams &P, const uint64_t *gt, uint64_t c, uint64_t fend) {
   const uint32_t lane = lane_id();
   const uint64_t rem = fend - c;
   if (rem <= P.min) return fend;                  // remaining <= min_size: whole tail
@@ -528,18 +529,16 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uin
   const uint32_t byte = lane < wlen ? W.base[t + lane] : 0;
   const uint64_t r = r0 + lane;
   const bool rl = cand && r <= r1;
-  uint32_t cnt = 0;
+  const uint32_t cnt = rl ? W.run_cnt[r] : 0;
+  // ---- level 2: entries of non-empty runs (~15 % of runs on random data)
   uint4 ea = make_uint4(0, 0, 0, 0), eb = make_uint4(0, 0, 0, 0);
-  if (rl) {
-    cnt = W.run_cnt[r];
-    if (P.cap == 8) {
-      const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
-      ea = ep[0];
-      eb = ep[1];
-    }
+  if (P.cap == 8 && cnt > 0 && cnt <= 8) {
+    const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
+    ea = ep[0];
+    if (cnt > 4) eb = ep[1];
   }
   // ---- (1) exact restarted hash for the first <= 47 tested positions
-  uint64_t h = lane < wlen ? W.gear[byte] : 0;
+  uint64_t h = lane < wlen ? gt[byte] : 0;
 #pragma unroll
   for (unsigned d = 1; d < 64; d <<= 1) {
     const uint64_t v = shfl_up64(h, d);
@@ -555,7 +554,7 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uin
     uint64_t found = ~0ull;
     if (rl) {
       if (cnt > P.cap) {
-        found = run_first_hit(W, P, r, lo, hi, cce);
+        found = run_first_hit(W, P, gt, r, lo, hi, cce);
       } else if (P.cap == 8) {
         found = run_first_entry(r, cnt, ea, eb, lo, hi, cce);
       } else {
@@ -579,7 +578,7 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uin
     if (rr <= r1) {
       const uint32_t cn = W.run_cnt[rr];
       if (cn > P.cap) {
-        found = run_first_hit(W, P, rr, lo, hi, cce);
+        found = run_first_hit(W, P, gt, rr, lo, hi, cce);
       } else {
         for (uint32_t i = 0; i < cn; ++i) {
           const uint32_t e = W.run_ent[rr * (uint64_t)P.cap + i];
@@ -598,7 +597,14 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, uint64_t c, uin
 }
 
 // ============================================================ spec =======
+__device__ __forceinline__ void load_gear_lds(uint64_t *gt, const Work &W) {
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) gt[i] = W.gear[i];
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_spec(Work W, DevParams P) {
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
   const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (s >= W.nsegs) return;
   const uint32_t lane = lane_id();
@@ -611,7 +617,7 @@ __global__ __launch_bounds__(256) void k_spec(Work W, DevParams P) {
     if (k >= cap) { if (lane == 0) atomicOr(W.err, kErrNodeCap); break; }
     if (lane == 0) out[k] = c;
     ++k;
-    const uint64_t nc = wave_next(W, P, c, fend);
+    const uint64_t nc = wave_next(W, P, gt, c, fend);
     if (nc >= S.end) { exitp = nc; break; }
     c = nc;
   }
@@ -638,6 +644,8 @@ __device__ int find_node(const Work &W, uint32_t j, uint64_t c) {
 
 // ============================================================ link =======
 __global__ __launch_bounds__(256) void k_link(Work W, DevParams P) {
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
   const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (s >= W.nsegs) return;
   const uint32_t lane = lane_id();
@@ -660,7 +668,7 @@ __global__ __launch_bounds__(256) void k_link(Work W, DevParams P) {
     if (steps == (uint32_t)kContMax) break;  // give up: serial fallback
     if (lane == 0) W.cont[(uint64_t)s * kContMax + steps] = c;
     ++steps;
-    c = wave_next(W, P, c, F.end);
+    c = wave_next(W, P, gt, c, F.end);
   }
   if (lane == 0) {
     W.link_seg[s] = ls; W.link_idx[s] = li; W.link_pos[s] = lp; W.cont_cnt[s] = steps;
@@ -672,6 +680,8 @@ __global__ __launch_bounds__(256) void k_link(Work W, DevParams P) {
 // ======================================================== fallback =======
 // One wave walks a whole file serially and rewrites its segments' node lists.
 __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
   const uint32_t f = blockIdx.x;
   if (f >= W.nfiles) return;
   if (!(W.file_flags[f] & kFileFail)) return;
@@ -693,7 +703,7 @@ __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
     if (k >= cap) { if (lane == 0) atomicOr(W.err, kErrNodeCap); break; }
     if (lane == 0) W.nodes[W.node_off[j] + k] = c;
     ++k;
-    c = wave_next(W, P, c, F.end);
+    c = wave_next(W, P, gt, c, F.end);
     if (c >= F.end) break;
   }
   const uint32_t last = F.first_seg + F.nsegs - 1;
@@ -756,30 +766,57 @@ __global__ void k_count(Work W) {
 }
 
 // ChunkData.hash as fastcdc returns it: the 2-byte loop's state at the cut.
-__device__ uint64_t chunk_hash(const Work &W, const DevParams &P, uint64_t c, uint64_t len,
-                               uint64_t fend) {
+// ChunkData.hash of the chunk [c, c + len) (file ends at fend): the 2-byte
+// loop's state at its return.  A hit at even index i returns (h << 2) +
+// GEAR_LS = 2 * (the 1-byte state), at odd index the 1-byte state; a forced
+// cut returns the state after position re - 1; a tail <= min returns 0.  The
+// state is sum_{j=from..q} GEAR[x_j] << (q - j) mod 2^64 with from = max(q-63,
+// restart): k_emit evaluates it as a 64-lane wave sum (lane k holds x_{q-k}).
+struct ChunkQ {
+  uint64_t q, from;  // last byte, first byte of the window (q < from: hash 0)
+  bool dbl;
+};
+
+__device__ __forceinline__ ChunkQ chunk_q(const DevParams &P, uint64_t c, uint64_t len, uint64_t fend) {
+  ChunkQ r{0, 1, false};
   const uint64_t rem = fend - c;
-  if (rem <= P.min) return 0;
+  if (rem <= P.min) return r;
   const uint64_t remaining = rem > P.max ? (uint64_t)P.max : rem;
   const uint64_t t0 = (uint64_t)(P.min / 2) * 2, re = (remaining / 2) * 2;
-  uint64_t q;
-  bool dbl;
   if (len < remaining) {  // cut by a mask hit at position c + len
-    q = c + len;
-    dbl = (len & 1) == 0;  // even index: state is (h << 2) + GEAR_LS
-  } else {                 // forced cut: state after position re - 1
-    if (re <= t0) return 0;
-    q = c + re - 1;
-    dbl = false;
+    r.q = c + len;
+    r.dbl = (len & 1) == 0;  // even index: state is (h << 2) + GEAR_LS
+  } else {                   // forced cut: state after position re - 1
+    if (re <= t0) return r;
+    r.q = c + re - 1;
   }
   const uint64_t t = c + t0;
-  const uint64_t from = q >= t + 63 ? q - 63 : t;
-  uint64_t h = 0;
-  for (uint64_t j = from; j <= q; ++j) h = (h << 1) + W.gear[W.base[j]];
-  return dbl ? h << 1 : h;
+  r.from = r.q >= t + 63 ? r.q - 63 : t;
+  return r;
 }
 
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// One wave per segment: lane i owns chunk i (of each batch of 64); the
+// chunk hashes are computed 8 at a time by the whole wave (byte loads of all 8
+// windows issued together, GEAR from LDS, one wave sum each).
 __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P) {
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
   const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (s >= W.nsegs) return;
   const uint64_t n = W.seg_count[s];
@@ -793,19 +830,45 @@ __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P) {
   const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
   const uint64_t after = W.link_pos[s];
   const uint64_t base_out = W.seg_off[s];
-  for (uint64_t i = lane; i < n; i += 64) {
-    const uint64_t pos = i < nn ? nd[i] : ct[i - nn];
-    const uint64_t j = i + 1;
-    const uint64_t nxt = j < n ? (j < nn ? nd[j] : ct[j - nn]) : after;
-    const uint64_t o = base_out + i;
-    if (o < W.out_cap) {
-      DevChunk ch;
-      ch.offset = pos - F.start;
-      ch.length = nxt - pos;
-      ch.hash = chunk_hash(W, P, pos, nxt - pos, F.end);
-      W.out[o] = ch;
-    } else if (lane == 0) {
-      atomicOr(W.err, kErrOutCap);
+  for (uint64_t i0 = 0; i0 < n; i0 += 64) {
+    const uint64_t i = i0 + lane;
+    const bool act = i < n;
+    uint64_t pos = 0, nxt = 0;
+    if (act) {
+      pos = i < nn ? nd[i] : ct[i - nn];
+      const uint64_t j = i + 1;
+      nxt = j < n ? (j < nn ? nd[j] : ct[j - nn]) : after;
+    }
+    const ChunkQ cq = act ? chunk_q(P, pos, nxt - pos, F.end) : ChunkQ{0, 1, false};
+    uint64_t mine = 0;
+    const uint32_t m = (uint32_t)(n - i0 < 64 ? n - i0 : 64);
+    for (uint32_t b = 0; b < m; b += 8) {  // wave-uniform
+      uint32_t by[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t src = b + k < m ? b + k : m - 1;
+        const uint64_t q = readlane64(cq.q, src), fr = readlane64(cq.from, src);
+        const bool in = b + k < m && q >= fr + lane;  // position q - lane in [from, q]
+        by[k] = in ? (uint32_t)W.base[q - lane] : 256u;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t v = by[k] < 256u ? gt[by[k]] << lane : 0;
+        const uint64_t hsum = wave_sum64(v);
+        if (lane == b + k) mine = hsum;
+      }
+    }
+    if (act) {
+      const uint64_t o = base_out + i;
+      if (o < W.out_cap) {
+        DevChunk ch;
+        ch.offset = pos - F.start;
+        ch.length = nxt - pos;
+        ch.hash = cq.dbl ? mine << 1 : mine;
+        W.out[o] = ch;
+      } else {
+        atomicOr(W.err, kErrOutCap);
+      }
     }
   }
 }

@@ -187,3 +187,25 @@ def test_timing_reported(ctx):
     t = ctx.timing()
     assert t["bytes"] == d.size and t["chunks"] > 0
     assert 0 < t["scan_ms"] <= t["device_ms"] and t["h2d_ms"] > 0
+
+
+def test_pinned_output_written_directly(ctx):
+    """A pinned caller array is written by k_emit over PCIe (no staging copy):
+    same result as the pageable path; a too-small pinned array reports
+    MCDC_E_CAPACITY with the required count."""
+    n = (96 << 20) + 777
+    dp = ctx.device_alloc(n)
+    try:
+        ctx.fill_random(dp, n, SEED + 3)
+        p = _lib.params(*PARAMS[0])
+        ref = ctx.chunk_device(p, dp, n)
+        pin = ctx.pinned_out(len(ref) + 8)
+        got = ctx.chunk_device(p, dp, n, out=pin)
+        assert len(got) == len(ref) and (got == ref).all()
+        small = pin[: len(ref) - 1]
+        with pytest.raises(_lib.McdcError) as ei:
+            ctx.chunk_device(p, dp, n, out=small)
+        assert ei.value.code == -3
+        _same(ref, O.chunk(O.Params(*PARAMS[0]), O.random_bytes(n, SEED + 3)))
+    finally:
+        ctx.device_free(dp)
