@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmcdc.so")
+# MCDC_LIBRARY overrides the in-tree build (A/B comparisons of kernel variants)
+LIB_PATH = os.environ.get("MCDC_LIBRARY") or os.path.join(HERE, "libmcdc.so")
 
 MCDC_OK = 0
 MCDC_E_INVALID = -1
