@@ -111,7 +111,7 @@ struct mcdc_ctx {
              ev_h2d1 = nullptr;
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
-  DevBuf arena, run_cnt, run_ent, run_sum, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
+  DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp;
   // pinned host staging
@@ -241,7 +241,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // ---- workspace ----
   if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
   if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
-  if ((rc = ensure(ctx, ctx->run_sum, nruns * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
   if ((rc = ensure(ctx, ctx->files, nfiles * sizeof(File)))) return rc;
   if ((rc = ensure(ctx, ctx->nodes, ctx->h_node_off.back() * sizeof(uint64_t)))) return rc;
@@ -290,7 +289,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.gear16 = ctx->d_gear16;
   W.run_cnt = (uint8_t *)ctx->run_cnt.p;
   W.run_ent = (uint32_t *)ctx->run_ent.p;
-  W.run_sum = (uint32_t *)ctx->run_sum.p;
   W.segs = (const Seg *)ctx->segs.p;
   W.nsegs = nsegs;
   W.nfiles = (uint32_t)nfiles;
@@ -427,7 +425,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
-  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->run_sum, &ctx->segs, &ctx->files, &ctx->nodes,
+  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,

@@ -32,7 +32,6 @@ constexpr uint32_t kSegFirst = 1u, kSegLast = 2u;
 constexpr uint32_t kFileSkip = 1u, kFileFail = 2u, kFileFallbackDone = 4u;
 // error word bits
 constexpr uint32_t kErrNodeCap = 1u, kErrOutCap = 2u;
-constexpr uint32_t kSumNone = 0xffffu;  // run_sum half: no candidate of that kind
 
 struct Seg {
   uint64_t start, end;  // arena positions [start, end)
@@ -64,7 +63,6 @@ struct Work {
   const uint64_t *gear16;// GEAR[256] << 16
   uint8_t *run_cnt;      // [nruns]
   uint32_t *run_ent;     // [nruns * cap]: off | S<<31 | L<<30
-  uint32_t *run_sum;     // [nruns]: first S offset | first L offset << 16 (0xffff = none)
 
   const Seg *segs;
   uint32_t nsegs, nfiles;

@@ -115,8 +115,6 @@ __device__ __forceinline__ uint32_t gaddr(uint32_t w, uint32_t laneoff) {
     if (s_ | l_) {                                                                    \
       if (cnt < cap) ent[cnt] = (off + (I)) | (s_ << 31) | (l_ << 30);                \
       ++cnt;                                                                          \
-      if (s_ && fs == kSumNone) fs = off + (I);                                       \
-      if (l_ && fl == kSumNone) fl = off + (I);                                       \
     }                                                                                 \
   }
 
@@ -131,7 +129,7 @@ __device__ __forceinline__ void hash16(const uint64_t *tab, uint32_t lo, const u
 // the 16 bytes exactly and append S/L candidates.
 __device__ __forceinline__ void scan16(const uint64_t *tab, uint32_t lo, const uint4 d, uint64_t &h,
                                        uint32_t pf, uint64_t ms16, uint64_t ml16, uint32_t off,
-                                       uint32_t &cnt, uint32_t *ent, uint32_t cap, uint32_t &fs, uint32_t &fl) {
+                                       uint32_t &cnt, uint32_t *ent, uint32_t cap) {
   const uint64_t h0 = h;
   uint32_t acc = 0xffffffffu;
   MCDC_STEP_PF(d.x, 0) MCDC_STEP_PF(d.x, 1) MCDC_STEP_PF(d.x, 2) MCDC_STEP_PF(d.x, 3)
@@ -166,7 +164,7 @@ __device__ __forceinline__ void scan_run_full(const uint64_t *tab, uint32_t lo, 
   const uint32_t pf = P.pf_hi, cap = P.cap;
   const uint64_t ms16 = P.ms16, ml16 = P.ml16;
   uint32_t *ent = W.run_ent + run * (uint64_t)cap;
-  uint32_t cnt = 0, fs = kSumNone, fl = kSumNone;
+  uint32_t cnt = 0;
   constexpr int G = RUN / 64;
   uint4 ring[PF + 1][4];
 #pragma unroll
@@ -188,12 +186,11 @@ __device__ __forceinline__ void scan_run_full(const uint64_t *tab, uint32_t lo, 
         const uint32_t off = 64u * gg;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          scan16(tab, lo, ring[u][j], h, pf, ms16, ml16, off + 16 * j, cnt, ent, cap, fs, fl);
+          scan16(tab, lo, ring[u][j], h, pf, ms16, ml16, off + 16 * j, cnt, ent, cap);
       }
     }
   }
   W.run_cnt[run] = cnt > cap ? kRunOverflow : (uint8_t)cnt;
-  W.run_sum[run] = fs | (fl << 16);
 }
 
 // Last, partial run: byte loop with exact tests (one lane in the whole grid).
@@ -203,7 +200,7 @@ __device__ void scan_run_tail(const uint64_t *tab, uint32_t lo, const Work &W, c
   const uint64_t start = run * (uint64_t)RUN, end = W.n_al;
   const uint64_t w0 = start >= (uint64_t)kWin ? start - kWin : 0;
   uint64_t h = 0;
-  uint32_t cnt = 0, fs = kSumNone, fl = kSumNone;
+  uint32_t cnt = 0;
   uint32_t *ent = W.run_ent + run * (uint64_t)P.cap;
   for (uint64_t q = w0; q < end; ++q) {
     h = (h << 1) + lds_gear(tab, ((uint32_t)W.base[q] << 8) | lo);
@@ -212,13 +209,10 @@ __device__ void scan_run_tail(const uint64_t *tab, uint32_t lo, const Work &W, c
       if (s_ | l_) {
         if (cnt < P.cap) ent[cnt] = (uint32_t)(q - start) | (s_ << 31) | (l_ << 30);
         ++cnt;
-        if (s_ && fs == kSumNone) fs = (uint32_t)(q - start);
-        if (l_ && fl == kSumNone) fl = (uint32_t)(q - start);
       }
     }
   }
   W.run_cnt[run] = cnt > P.cap ? kRunOverflow : (uint8_t)cnt;
-  W.run_sum[run] = fs | (fl << 16);
 }
 
 template <int RUN, int WPE, int PF, int CH = 1, int BLOCK = 512>
@@ -261,11 +255,16 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan_t(Work W, DevParams P) {
 // walk takes the minimum).  Measured (tools/scanbench, 16 GiB): the deferred
 // queue alone +7-13 % over re-walking the block under an exec mask.
 //
-// LDS = 64 KiB table + 16 waves x (5 KiB pad + 768 B per-run counters) = 156 KiB.
+// LDS = 64 KiB table + 16 waves x (5 KiB pad + 256 B run counters) = 148 KiB.
 constexpr int kQPad = 80;                        // run stride in the transpose pad
 constexpr int kQPadBytes = 64 * kQPad;           // 5 KiB
-constexpr int kQWaveBytes = kQPadBytes + 3 * 64 * 4; // + per-run counters, first S, first L
+constexpr int kQWaveBytes = kQPadBytes + 64 * 4; // + per-run candidate counters
 constexpr int kSTab = 65536;                     // GEAR<<16 x 32 copies
+
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4],
+// lgkmcnt [11:8]); vmcnt/expcnt left at their maxima (no wait).
+constexpr int kWaitLgkm4 = 0xC07F | (4 << 8);
+constexpr int kWaitLgkm0 = 0xC07F;
 
 __device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
   uint32_t v;
@@ -289,8 +288,8 @@ __device__ __forceinline__ void chain4(const uint64_t *g, uint64_t &h, uint32_t 
   const uint32_t m2 = (uint32_t)(h >> 32) & pf;
   h = (h << 1) + g[3];
   const uint32_t m3 = (uint32_t)(h >> 32) & pf;
-  acc = min(acc, min(m0, m1));
-  acc = min(acc, min(m2, m3));
+  acc = min(min(acc, m0), m1);  // -> v_min3_u32 x2
+  acc = min(min(acc, m2), m3);
 }
 
 // Drain the wave's queue: lane i re-walks entry i's 16 bytes exactly.
@@ -315,8 +314,6 @@ __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t 
       if (s_ | l_) {
         const uint32_t k = atomicAdd(&lcnt[rl], 1u);
         if (k < cap) ent[k] = (off + i) | (s_ << 31) | (l_ << 30);
-        if (s_) atomicMin(&lcnt[64 + rl], off + i);
-        if (l_) atomicMin(&lcnt[128 + rl], off + i);
       }
     }
   }
@@ -344,6 +341,11 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
 #pragma unroll
   for (int d = 0; d < 16; ++d) {
     if (d + 1 < 16) lookup4(q.tab, q.lo, w[d + 1], g[(d + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    // one wait per dword for its 4 lookups (the next dword's 4 stay in flight)
+    // instead of the compiler's one wait per lookup
+    if (d + 1 < 16) __builtin_amdgcn_s_waitcnt(kWaitLgkm4);
+    else __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     chain4(g[d & 1], h, acc, q.pf);
     if (d % 4 == 3) {
@@ -388,8 +390,6 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
   q.base = W.base;
   q.run_ent = W.run_ent;
   q.lcnt[lane] = 0;
-  q.lcnt[64 + lane] = kSumNone;
-  q.lcnt[128 + lane] = kSumNone;
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
@@ -452,12 +452,9 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
     }
 #undef MCDC_LDQ
     if (qn) q_drain<RUN>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
-    const uint32_t cnt = q.lcnt[lane], fs = q.lcnt[64 + lane], fl = q.lcnt[128 + lane];
+    const uint32_t cnt = q.lcnt[lane];
     q.lcnt[lane] = 0;
-    q.lcnt[64 + lane] = kSumNone;
-    q.lcnt[128 + lane] = kSumNone;
     W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
-    W.run_sum[run] = fs | (fl << 16);
   }
   // partial last tile: lane-strided runs, exact per-lane path
   const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
@@ -518,66 +515,12 @@ __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, co
   return found;
 }
 
-// Candidate lookup for one run r (positions [rb, rb + kRun)): the first
-// position p in [lo, hi) with S(p) if p < cce or L(p) if p >= cce; ~0 if none.
-// A run wholly inside [lo, cce) or [cce, hi) is answered by its summary word
-// (first S / first L offset, written by the scan); only the <= 3 runs that
-// straddle lo, cce or hi need their entries (or, if they overflowed, a rescan).
-struct RunLoad {
-  uint32_t kind;  // 0 none, 1 wholly S, 2 wholly L, 3 boundary
-  uint32_t sum, cnt;
-  uint4 ea, eb;
-};
-
-__device__ __forceinline__ RunLoad run_load(const Work &W, const DevParams &P, uint64_t r, bool valid,
-                                            uint64_t lo, uint64_t hi, uint64_t cce) {
-  RunLoad L{0, kSumNone | (kSumNone << 16), 0, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-  if (!valid) return L;
-  const uint64_t rb = r * (uint64_t)kRun, re = rb + kRun;
-  if (rb >= lo && re <= cce) L.kind = 1;
-  else if (rb >= cce && re <= hi) L.kind = 2;
-  else L.kind = 3;
-  if (L.kind < 3) {
-    L.sum = W.run_sum[r];
-  } else {
-    L.cnt = W.run_cnt[r];
-    if (P.cap == 8) {  // speculative: the 8 slots of this run (one 32-byte line)
-      const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
-      L.ea = ep[0];
-      L.eb = ep[1];
-    }
-  }
-  return L;
-}
-
-__device__ __forceinline__ uint64_t run_candidate(const Work &W, const DevParams &P, const uint64_t *gt,
-                                                  uint64_t r, const RunLoad &L, uint64_t lo, uint64_t hi,
-                                                  uint64_t cce) {
-  const uint64_t rb = r * (uint64_t)kRun;
-  if (L.kind == 0) return ~0ull;
-  if (L.kind == 1) return (L.sum & 0xffffu) != kSumNone ? rb + (L.sum & 0xffffu) : ~0ull;
-  if (L.kind == 2) return (L.sum >> 16) != kSumNone ? rb + (L.sum >> 16) : ~0ull;
-  if (L.cnt > P.cap) return run_first_hit(W, P, gt, r, lo, hi, cce);
-  if (P.cap == 8) return run_first_entry(r, L.cnt, L.ea, L.eb, lo, hi, cce);
-  uint64_t found = ~0ull;
-  for (uint32_t i = 0; i < L.cnt; ++i) {
-    const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
-    const uint64_t pos = rb + (e & 0x00ffffffu);
-    if (pos >= lo && pos < hi && pos < found) {
-      const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
-      if (ok) found = pos;
-    }
-  }
-  return found;
-}
-
 // next(c): the chunk starting at arena position c (file ends at fend) ends
 // where fastcdc's cut_gear(&file[c..], min, avg, max, masks) says.  Called by
 // a full wave with wave-uniform c, fend; returns the next chunk start.
-// Latency shape: one dependent global level per step — the restart-window
-// bytes and, for the first 64 runs, their summary words (or, for the <= 3
-// boundary runs, counts and entries) are all requested at once; GEAR comes
-// from the block's LDS copy `gt`.
+// Latency shape: two dependent global levels per step — {restart-window bytes,
+// the first 64 runs' candidate counts}, then {entries of the non-empty runs};
+// GEAR comes from the block's LDS copy `gt`.
 __device__ uint64_t wave_next(const Work &W, const DevParams &P, const uint64_t *gt, uint64_t c, uint64_t fend) {
   const uint32_t lane = lane_id();
   const uint64_t rem = fend - c;
@@ -592,10 +535,18 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, const uint64_t 
   const uint64_t lo = t + (kWin - 1), hi = c + re, cce = c + ce;
   const bool cand = lo < hi;
   const uint64_t r0 = lo / kRun, r1 = cand ? (hi - 1) / kRun : 0;
-  // ---- one level of independent loads
+  // ---- level-1 loads, all independent
   const uint32_t byte = lane < wlen ? W.base[t + lane] : 0;
   const uint64_t r = r0 + lane;
-  const RunLoad L = run_load(W, P, r, cand && r <= r1, lo, hi, cce);
+  const bool rl = cand && r <= r1;
+  const uint32_t cnt = rl ? W.run_cnt[r] : 0;
+  // ---- level 2: entries of non-empty runs (~15 % of runs on random data)
+  uint4 ea = make_uint4(0, 0, 0, 0), eb = make_uint4(0, 0, 0, 0);
+  if (P.cap == 8 && cnt > 0 && cnt <= 8) {
+    const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
+    ea = ep[0];
+    if (cnt > 4) eb = ep[1];
+  }
   // ---- (1) exact restarted hash for the first <= 47 tested positions
   uint64_t h = lane < wlen ? gt[byte] : 0;
 #pragma unroll
@@ -608,16 +559,47 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, const uint64_t 
   const uint64_t b = __ballot(pass);
   if (b) return t + (uint64_t)(__ffsll((unsigned long long)b) - 1);
   if (!cand) return c + remaining;
-  // ---- (2) windowed candidates for [t + 47, c + re), 64 runs at a time
+  // ---- (2) windowed candidates for [t + 47, c + re), first 64 runs
   {
-    const uint64_t found = run_candidate(W, P, gt, r, L, lo, hi, cce);
+    uint64_t found = ~0ull;
+    if (rl) {
+      if (cnt > P.cap) {
+        found = run_first_hit(W, P, gt, r, lo, hi, cce);
+      } else if (P.cap == 8) {
+        found = run_first_entry(r, cnt, ea, eb, lo, hi, cce);
+      } else {
+        for (uint32_t i = 0; i < cnt; ++i) {
+          const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
+          const uint64_t pos = r * (uint64_t)kRun + (e & 0x00ffffffu);
+          if (pos >= lo && pos < hi && pos < found) {
+            const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
+            if (ok) found = pos;
+          }
+        }
+      }
+    }
     const uint64_t fb = __ballot(found != ~0ull);
     if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
   }
+  // ---- later batches (only when max spans more than 64 runs)
   for (uint64_t rb = r0 + 64; rb <= r1; rb += 64) {
     const uint64_t rr = rb + lane;
-    const RunLoad LL = run_load(W, P, rr, rr <= r1, lo, hi, cce);
-    const uint64_t found = run_candidate(W, P, gt, rr, LL, lo, hi, cce);
+    uint64_t found = ~0ull;
+    if (rr <= r1) {
+      const uint32_t cn = W.run_cnt[rr];
+      if (cn > P.cap) {
+        found = run_first_hit(W, P, gt, rr, lo, hi, cce);
+      } else {
+        for (uint32_t i = 0; i < cn; ++i) {
+          const uint32_t e = W.run_ent[rr * (uint64_t)P.cap + i];
+          const uint64_t pos = rr * (uint64_t)kRun + (e & 0x00ffffffu);
+          if (pos >= lo && pos < hi && pos < found) {
+            const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
+            if (ok) found = pos;
+          }
+        }
+      }
+    }
     const uint64_t fb = __ballot(found != ~0ull);
     if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
   }

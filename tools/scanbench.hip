@@ -67,6 +67,63 @@ __global__ __launch_bounds__(512, 2) void k_scan_l2(Work W, DevParams P) {
   }
 }
 
+// Diagnostic: s_memtime stamps split each group into load-wait and compute.
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+template <int RUN, int L2>
+__global__ __launch_bounds__(512, 2) void k_scan_diag(Work W, DevParams P, uint64_t *dbg) {
+  __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
+  for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) tab[i] = W.gear16[i >> 5];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, lo = (lane & 31) << 3;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t ntiles = W.n_al / RUN / 64;
+  uint64_t twait = 0, tcomp = 0, tall0 = stamp();
+  const uint32_t pf = P.pf_hi, cap = P.cap;
+  for (uint64_t t = wid; t < ntiles; t += nwaves) {
+    const uint64_t run = t * 64 + lane;
+    const uint64_t ar = L2 ? 1 + (run & 1023) : run;
+    const uint4 *p = reinterpret_cast<const uint4 *>(W.base + ar * (uint64_t)RUN);
+    uint64_t h = 0;
+    uint32_t *ent = W.run_ent + run * (uint64_t)cap;
+    uint32_t cnt = 0;
+    constexpr int G = RUN / 64;
+    uint4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], b0, b1, b2, b3;
+    for (int g = 0; g < G; g += 2) {
+      const uint4 *qb = p + 4 * (g + 1);
+      const uint4 *qa = p + 4 * (g + 2 < G ? g + 2 : g + 1);
+      b0 = qb[0]; b1 = qb[1]; b2 = qb[2]; b3 = qb[3];
+      uint64_t t0 = stamp();
+      __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): group g landed
+      asm volatile("" ::: "memory");
+      uint64_t t1 = stamp();
+      scan16(tab, lo, a0, h, pf, P.ms16, P.ml16, 64 * g, cnt, ent, cap);
+      scan16(tab, lo, a1, h, pf, P.ms16, P.ml16, 64 * g + 16, cnt, ent, cap);
+      scan16(tab, lo, a2, h, pf, P.ms16, P.ml16, 64 * g + 32, cnt, ent, cap);
+      scan16(tab, lo, a3, h, pf, P.ms16, P.ml16, 64 * g + 48, cnt, ent, cap);
+      a0 = qa[0]; a1 = qa[1]; a2 = qa[2]; a3 = qa[3];
+      uint64_t t2 = stamp();
+      __builtin_amdgcn_s_waitcnt(0x0F74);
+      asm volatile("" ::: "memory");
+      uint64_t t3 = stamp();
+      scan16(tab, lo, b0, h, pf, P.ms16, P.ml16, 64 * g + 64, cnt, ent, cap);
+      scan16(tab, lo, b1, h, pf, P.ms16, P.ml16, 64 * g + 80, cnt, ent, cap);
+      scan16(tab, lo, b2, h, pf, P.ms16, P.ml16, 64 * g + 96, cnt, ent, cap);
+      scan16(tab, lo, b3, h, pf, P.ms16, P.ml16, 64 * g + 112, cnt, ent, cap);
+      uint64_t t4 = stamp();
+      twait += (t1 - t0) + (t3 - t2);
+      tcomp += (t2 - t1) + (t4 - t3);
+    }
+    W.run_cnt[run] = cnt > cap ? kRunOverflow : (uint8_t)cnt;
+  }
+  uint64_t tall = stamp() - tall0;
+  if (lane == 0) { dbg[wid * 4 + 0] = twait; dbg[wid * 4 + 1] = tcomp; dbg[wid * 4 + 2] = tall; }
+}
+
 static float time_it(hipStream_t st, int iters, const std::function<void()> &f, float *best) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -109,8 +166,6 @@ int main(int argc, char **argv) {
   uint32_t *ent, *sink;
   CK(hipMalloc(&cnt, nruns_max));
   CK(hipMalloc(&ent, nruns_max * 8 * 4));
-  uint32_t *sum;
-  CK(hipMalloc(&sum, nruns_max * 4));
   CK(hipMalloc(&sink, 64));
   DevParams P{};
   P.min = 16384; P.avg = 65536; P.max = 262144; P.cap = 8;
@@ -118,7 +173,7 @@ int main(int argc, char **argv) {
   P.ms16 = P.ms << 16; P.ml16 = P.ml << 16;
   P.pf_hi = (uint32_t)((P.ms & P.ml) >> 16);
   Work W{};
-  W.base = d; W.n_al = n; W.gear16 = dg16; W.run_cnt = cnt; W.run_ent = ent; W.run_sum = sum;
+  W.base = d; W.n_al = n; W.gear16 = dg16; W.run_cnt = cnt; W.run_ent = ent;
   W.nruns = (n + kRun - 1) / kRun;
   CK(hipStreamSynchronize(st));
   auto report = [&](const char *name, float med, float best) {
@@ -142,13 +197,10 @@ int main(int argc, char **argv) {
   }
   if (mode == "var") {
     const uint64_t nr = W.nruns;
-    std::vector<uint32_t> sv0, sv1;
     auto snap = [&](std::vector<uint8_t> &cv, std::vector<uint32_t> &ev) {
       cv.resize(nr); ev.resize(nr * 8);
       CK(hipMemcpy(cv.data(), cnt, nr, hipMemcpyDeviceToHost));
       CK(hipMemcpy(ev.data(), ent, nr * 8 * 4, hipMemcpyDeviceToHost));
-      sv1.resize(nr);
-      CK(hipMemcpy(sv1.data(), sum, nr * 4, hipMemcpyDeviceToHost));
     };
     std::vector<uint8_t> c0, c1; std::vector<uint32_t> e0, e1;
     CK(hipMemset(ent, 0, nr * 8 * 4));
@@ -156,11 +208,11 @@ int main(int argc, char **argv) {
       const uint64_t blocks = std::min<uint64_t>((W.nruns / 64 + 7) / 8, (uint64_t)cus * 2);
       hipLaunchKernelGGL((k_scan_t<kRun, 2, 1, 1, 512>), dim3(blocks), dim3(512), 0, st, W, P);
     }
-    CK(hipStreamSynchronize(st)); snap(c0, e0); sv0 = sv1;
+    CK(hipStreamSynchronize(st)); snap(c0, e0);
     auto check = [&](const char *name, const std::function<void()> &f) {
       CK(hipMemset(ent, 0, nr * 8 * 4)); CK(hipMemset(cnt, 0, nr));
       f(); CK(hipStreamSynchronize(st)); snap(c1, e1);
-      bool ok = c0 == c1 && sv0 == sv1;
+      bool ok = c0 == c1;
       for (uint64_t r = 0; ok && r < nr; ++r) {
         if (c0[r] > 8) continue;
         std::vector<uint32_t> x(e0.begin() + 8 * r, e0.begin() + 8 * r + c0[r]), y(e1.begin() + 8 * r, e1.begin() + 8 * r + c0[r]);
@@ -186,6 +238,25 @@ int main(int argc, char **argv) {
       printf("sweep %8.1f MiB x%3d: %7.3f TB/s (best %7.3f)\n", sz / 1048576.0, reps,
              sz * (double)reps / (med * 1e9), sz * (double)reps / (best * 1e9));
       fflush(stdout);
+    }
+    return 0;
+  }
+  if (mode == "diag") {
+    uint64_t *dbg; CK(hipMalloc(&dbg, 8 * 4 * 8192)); CK(hipMemset(dbg, 0, 8 * 4 * 8192));
+    const uint64_t nr = n / 2048;
+    const uint64_t blocks = std::min<uint64_t>((nr / 64 + 7) / 8, (uint64_t)cus * 2);
+    for (int l2 = 0; l2 < 2; ++l2) {
+      med = time_it(st, 3, [&] {
+        if (l2) hipLaunchKernelGGL((k_scan_diag<2048, 1>), dim3(blocks), dim3(512), 0, st, W, P, dbg);
+        else hipLaunchKernelGGL((k_scan_diag<2048, 0>), dim3(blocks), dim3(512), 0, st, W, P, dbg);
+      }, &best);
+      std::vector<uint64_t> h(4 * blocks * 8);
+      CK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+      double w = 0, c = 0, a = 0;
+      for (uint64_t i = 0; i < blocks * 8; ++i) { w += h[4 * i]; c += h[4 * i + 1]; a += h[4 * i + 2]; }
+      printf("diag %s: %.3f TB/s  per-wave cycles: wait %.3g compute %.3g all %.3g  (wait %.1f%%)  clk %.2f GHz\n",
+             l2 ? "L2 " : "HBM", n / (med * 1e9), w / (blocks * 8), c / (blocks * 8), a / (blocks * 8),
+             100.0 * w / (w + c), a / (blocks * 8) / (med * 1e-3) / 1e9);
     }
     return 0;
   }
