@@ -497,22 +497,28 @@ __device__ uint64_t run_first_hit(const Work &W, const DevParams &P, const uint6
 
 // First candidate of one run in [lo, hi) from its (up to 8, cap == 8) entries;
 // entries are not position-sorted, so take the minimum.  ~0 if none.
+__device__ __forceinline__ uint32_t rel_clamp(uint64_t x, uint64_t rb) {
+  return x <= rb ? 0u : (x - rb >= (uint64_t)kRun ? (uint32_t)kRun : (uint32_t)(x - rb));
+}
+
+// In run-relative 32-bit coordinates: entries 0-3 always, 4-7 only when some
+// lane of the wave has more than 4 (wave-uniform branch, rare on real data).
 __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, const uint4 ea,
                                                     const uint4 eb, uint64_t lo, uint64_t hi,
                                                     uint64_t cce) {
-  uint64_t found = ~0ull;
   const uint64_t rb = r * (uint64_t)kRun;
-  const uint32_t e8[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t e = e8[i];
-    const uint64_t pos = rb + (e & 0x00ffffffu);
-    if ((uint32_t)i < cnt && pos >= lo && pos < hi && pos < found) {
-      const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
-      if (ok) found = pos;
-    }
+  const uint32_t l = rel_clamp(lo, rb), h = rel_clamp(hi, rb), m = rel_clamp(cce, rb);
+  uint32_t best = 0xffffffffu;
+  auto take = [&](uint32_t i, uint32_t e) {
+    const uint32_t off = e & 0x00ffffffu;
+    const uint32_t kind = off < m ? (e >> 31) : (e >> 30) & 1u;
+    if (i < cnt && off >= l && off < h && kind) best = min(best, off);
+  };
+  take(0, ea.x); take(1, ea.y); take(2, ea.z); take(3, ea.w);
+  if (__any(cnt > 4)) {
+    take(4, eb.x); take(5, eb.y); take(6, eb.z); take(7, eb.w);
   }
-  return found;
+  return best == 0xffffffffu ? ~0ull : rb + best;
 }
 
 // next(c): the chunk starting at arena position c (file ends at fend) ends
