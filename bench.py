@@ -44,6 +44,18 @@ def _dist():
     return world, rank, local
 
 
+def _pmc_traffic():
+    """Calibrated PMC read traffic of the scan (profiles/r01/pmc_traffic.json, written from a
+    separate rocprofv3 --pmc FETCH_SIZE pass by tools/pmc_calib.sh): HBM bytes per input byte."""
+    path = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return float(d["traffic_per_input_byte"]), os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -175,6 +187,7 @@ def main() -> int:
     value = total_bytes / elapsed / (1 << 30)
     scan_avg = float(np.mean(scan_ms))
     achieved = n / (scan_avg * 1e-3) / 1e9
+    tpb, tsrc = _pmc_traffic()
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": n_gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
@@ -185,7 +198,8 @@ def main() -> int:
                    "parallelism": f"{n_gpus} independent streams, no collectives"},
         "roofline": {"bound": "hbm", "kernel": "k_scan_q", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "bytes_per_launch": n, "avg_launch_ms": round(scan_avg, 3)},
+                     "traffic": int(round(tpb * n)) if tpb else None, "traffic_unit": "bytes per launch",
+                     "traffic_source": tsrc, "bytes_per_launch": n, "avg_launch_ms": round(scan_avg, 3)},
         "device_only": {"scan_ms": round(scan_avg, 3), "device_ms": round(float(np.mean(dev_ms)), 3),
                         "gib_s": round(n / (float(np.mean(dev_ms)) * 1e-3) / (1 << 30), 2),
                         "call_ms": round(float(np.mean(total_ms)), 3)},

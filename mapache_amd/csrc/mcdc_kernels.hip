@@ -428,8 +428,6 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
         const uint4 c1 = *reinterpret_cast<const uint4 *>(rd + 16);
         const uint4 c2 = *reinterpret_cast<const uint4 *>(rd + 32);
         const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
-        const int gn = g + 2 < G ? g + 2 : G - 1;  // clamped, unconditional
-        a0 = MCDC_LDQ(0, gn); a1 = MCDC_LDQ(1, gn); a2 = MCDC_LDQ(2, gn); a3 = MCDC_LDQ(3, gn);
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
         scan64q<RUN>(q, w, h, 64u * g, qn, run0);
@@ -443,8 +441,13 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
         const uint4 c1 = *reinterpret_cast<const uint4 *>(rd + 16);
         const uint4 c2 = *reinterpret_cast<const uint4 *>(rd + 32);
         const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
-        const int gn = g + 3 < G ? g + 3 : G - 1;
-        b0 = MCDC_LDQ(0, gn); b1 = MCDC_LDQ(1, gn); b2 = MCDC_LDQ(2, gn); b3 = MCDC_LDQ(3, gn);
+        // both 64-byte halves of the next 128-byte lines are requested back
+        // to back (groups g+2, g+3): requesting them a step apart let L2 evict
+        // the line in between (+12 % fabric reads, FETCH_SIZE calibrated
+        // against the bare load pattern in tools/scanbench quadread)
+        const int ga = g + 2 < G ? g + 2 : G - 1, gb = g + 3 < G ? g + 3 : G - 1;  // clamped
+        a0 = MCDC_LDQ(0, ga); b0 = MCDC_LDQ(0, gb); a1 = MCDC_LDQ(1, ga); b1 = MCDC_LDQ(1, gb);
+        a2 = MCDC_LDQ(2, ga); b2 = MCDC_LDQ(2, gb); a3 = MCDC_LDQ(3, ga); b3 = MCDC_LDQ(3, gb);
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
         scan64q<RUN>(q, w, h, 64u * (g + 1), qn, run0);

@@ -124,6 +124,36 @@ __global__ __launch_bounds__(512, 2) void k_scan_diag(Work W, DevParams P, uint6
   if (lane == 0) { dbg[wid * 4 + 0] = twait; dbg[wid * 4 + 1] = tcomp; dbg[wid * 4 + 2] = tall; }
 }
 
+// Calibration: the product's quad-coalesced ping-pong load pattern with no
+// hashing (known byte count for FETCH_SIZE calibration).
+template <int RUN>
+__global__ __launch_bounds__(1024) void k_read_quad(const uint8_t *base, uint64_t n, uint32_t *sink) {
+  const uint32_t lane = threadIdx.x & 63, qi = lane >> 2, qj = lane & 3;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t ntiles = n / RUN / 64;
+  constexpr int G = RUN / 64;
+  uint32_t acc = 0;
+  for (uint64_t t = wid; t < ntiles; t += nwaves) {
+    const uint8_t *tb = base + t * 64 * (uint64_t)RUN;
+    const uint32_t o0 = 4 * qi * RUN + 16 * qj;
+#define LQ(k, gg) (*reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * RUN + 64 * (gg))))
+    uint4 a0 = LQ(0, 0), a1 = LQ(1, 0), a2 = LQ(2, 0), a3 = LQ(3, 0);
+    uint4 b0 = LQ(0, 1), b1 = LQ(1, 1), b2 = LQ(2, 1), b3 = LQ(3, 1);
+#pragma unroll 1
+    for (int g = 0; g < G; g += 2) {
+      acc ^= (a0.x ^ a0.y ^ a0.z ^ a0.w) + (a1.x ^ a1.y ^ a1.z ^ a1.w) + (a2.x ^ a2.y ^ a2.z ^ a2.w) + (a3.x ^ a3.y ^ a3.z ^ a3.w);
+      const int gn = g + 2 < G ? g + 2 : G - 1;
+      a0 = LQ(0, gn); a1 = LQ(1, gn); a2 = LQ(2, gn); a3 = LQ(3, gn);
+      acc ^= (b0.x ^ b0.y ^ b0.z ^ b0.w) + (b1.x ^ b1.y ^ b1.z ^ b1.w) + (b2.x ^ b2.y ^ b2.z ^ b2.w) + (b3.x ^ b3.y ^ b3.z ^ b3.w);
+      const int gm = g + 3 < G ? g + 3 : G - 1;
+      b0 = LQ(0, gm); b1 = LQ(1, gm); b2 = LQ(2, gm); b3 = LQ(3, gm);
+    }
+#undef LQ
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 static float time_it(hipStream_t st, int iters, const std::function<void()> &f, float *best) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -190,6 +220,13 @@ int main(int argc, char **argv) {
   float best, med;
   const int it = 7;
   auto prod = [&] { launch_scan(W, P, cus, st); };
+  if (mode == "quadread") {
+    med = time_it(st, 3, [&] {
+      hipLaunchKernelGGL(k_read_quad<kRun>, dim3(cus), dim3(1024), 0, st, (const uint8_t *)d, n, sink);
+    }, &best);
+    report("quad-coalesced reads only (calibration)", med, best);
+    return 0;
+  }
   if (mode == "prod") {
     med = time_it(st, 3, prod, &best);
     report("scan product (quad-coalesced)", med, best);
