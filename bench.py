@@ -5,17 +5,24 @@ Workload (BASELINE.json configs[1]): per GPU one 64 GiB uniform-random byte
 buffer resident in HBM (counter-based PRNG generated on the device, seed per
 rank), FastCDC v2020 at min/avg/max = 16/64/256 KiB, Normalization::Level1.
 A step = one full chunking pass over that buffer through the C ABI
-(mcdc_chunk_device: scan + chain resolution + boundary emission + boundary
-list copied to host).  N GPUs = N independent streams (weak scaling, no
-collectives on the data path; torch.distributed is used only for the barrier
-and the max-over-ranks timing).
+(mcdc_chunk_device: scan + chain resolution + boundary emission), with the
+boundary list written to a device-resident output array (device-resident in,
+device-resident out: the next pipeline stage consumes it in HBM).  The same
+call with the list written to pinned host memory is reported beside it
+("host_out").  N GPUs = N independent streams (weak scaling, no collectives on
+the data path; torch.distributed is used only for the barrier and the
+max-over-ranks timing).
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline     - the scan kernel (dominant) vs HBM peak: algorithmic bytes per
-                 launch (1 byte read per input byte) / average launch time from
-                 HIP events recorded on the library's stream.
-  cpu_baseline - oracle/ C restatement of the crate, 1 thread, bounded sample
-                 of the same stream (rank 0, N=1 only).
+  roofline      - the scan kernel (dominant) vs HBM peak: algorithmic bytes per
+                  launch (1 byte read per input byte) / average launch time from
+                  HIP events recorded on the library's stream.
+  cpu_baseline  - oracle/ C restatement of the crate, 1 thread, bounded sample
+                  of the same stream (rank 0, N=1 only).
+  host_out      - same step, boundary list to pinned host memory (PCIe-inclusive)
+  e2e_host      - pinned host input -> H2D -> kernels -> boundaries to host
+  batch_files   - BASELINE configs[2]: 10 000 independent 8 MiB files, one call
+  small_files   - BASELINE configs[3] stand-in: synthetic kernel-tree-like mix
 """
 from __future__ import annotations
 
@@ -35,6 +42,7 @@ METRIC = "device-resident GiB/s chunked, FastCDC 16/64/256 KiB, 1 & 8 MI355X"
 SEED = 0x6d61706163686521
 PARAMS = (16384, 65536, 262144, 1)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+GIB = 1 << 30
 
 
 def _dist():
@@ -66,12 +74,17 @@ def _cpu_model():
     return platform.processor()
 
 
+def _same(a: np.ndarray, b: np.ndarray) -> bool:
+    return bool(len(a) == len(b) and (a["offset"] == b["offset"]).all() and (a["length"] == b["length"]).all()
+                and (a["hash"] == b["hash"]).all())
+
+
 def cpu_baseline(sample_gib: float, gpu_chunks: np.ndarray) -> dict:
     """Oracle (C restatement of fastcdc v2020), single thread, on the first
     `sample_gib` GiB of rank 0's stream.  Also cross-checks the GPU boundaries
     that lie wholly inside the sample (a size-independent parity probe)."""
     from oracle import oracle as O
-    n = int(sample_gib * (1 << 30))
+    n = int(sample_gib * GIB)
     d = O.random_bytes(n, SEED)  # generation is not timed
     t0 = time.perf_counter()
     c = O.chunk(O.Params(*PARAMS), d)
@@ -79,27 +92,25 @@ def cpu_baseline(sample_gib: float, gpu_chunks: np.ndarray) -> dict:
     # GPU chunks that end before the sample's last max-window are final in both
     lim = n - PARAMS[2]
     g = gpu_chunks[gpu_chunks["offset"] + PARAMS[2] <= lim]
-    r = c[: len(g)]
-    ok = bool(len(g) > 0 and (g["offset"] == r["offset"]).all() and (g["length"] == r["length"]).all()
-              and (g["hash"] == r["hash"]).all())
-    return {"value": round(n / dt / (1 << 30), 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+    ok = len(g) > 0 and _same(g, c[: len(g)])
+    return {"value": round(n / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {sample_gib:g} GiB of the rank-0 stream (seed 0x{SEED:x}), 16/64/256 KiB L1, "
                       f"oracle/fastcdc_oracle.c cut_gear loop, 1 thread, input pre-generated in RAM",
             "cpu": _cpu_model(), "seconds": round(dt, 3), "parity_probe_chunks": int(len(g)),
-            "parity_probe_ok": ok}
+            "parity_probe_ok": bool(ok)}
 
 
 def e2e_host(ctx, p, gib: float) -> dict:
     """End-to-end host path: pinned host buffer -> H2D -> kernels -> boundaries to host."""
     import ctypes
     from mapache_amd import _lib
-    n = int(gib * (1 << 30))
+    n = int(gib * GIB)
     hp = ctx.host_alloc(n)
     dp = ctx.device_alloc(n)
     try:
         ctx.fill_random(dp, n, SEED ^ 0x55)
-        _copy_d2h(dp, hp, n)  # synthetic bytes into pinned host memory (untimed)
         lib = _lib.load()
+        _lib.check(lib.mcdc_memcpy_d2h(ctx._h, ctypes.c_void_p(hp), ctypes.c_void_p(dp), n))
         out = np.zeros(n // (p.min_size - 1) + 2, dtype=_lib.CHUNK_DTYPE)
         n_out = ctypes.c_size_t()
         best, bt = None, None
@@ -110,7 +121,7 @@ def e2e_host(ctx, p, gib: float) -> dict:
             dt = time.perf_counter() - t0
             if best is None or dt < best:
                 best, bt = dt, ctx.timing()
-        return {"bytes": n, "gib_s": round(n / best / (1 << 30), 2), "h2d_ms": round(bt["h2d_ms"], 3),
+        return {"bytes": n, "gib_s": round(n / best / GIB, 2), "h2d_ms": round(bt["h2d_ms"], 3),
                 "device_ms": round(bt["device_ms"], 3), "d2h_ms": round(bt["d2h_ms"], 3),
                 "total_ms": round(bt["total_ms"], 3), "source": "pinned host buffer (hipHostMalloc)"}
     finally:
@@ -118,13 +129,78 @@ def e2e_host(ctx, p, gib: float) -> dict:
         ctx.device_free(dp)
 
 
-def _copy_d2h(dp: int, hp: int, n: int) -> None:
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    rc = hip.hipMemcpy(ctypes.c_void_p(hp), ctypes.c_void_p(dp), n, 2)  # hipMemcpyDeviceToHost
-    if rc != 0:
-        raise RuntimeError(f"hipMemcpy D2H failed: {rc}")
+def _timed(fn, steps: int, warmup: int):
+    for _ in range(warmup):
+        fn()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = fn()
+    return (time.perf_counter() - t0) / steps, r
+
+
+def batch_files(ctx, p, nfiles: int, size: int, steps: int) -> dict:
+    """BASELINE configs[2]: `nfiles` independent files of `size` bytes back to back
+    in one device arena (each file's chain restarts at 0), one batched call."""
+    from mapache_amd import _lib
+    n = nfiles * size
+    arena = ctx.device_alloc(n)
+    cap = nfiles * (size // (p.min_size - 1) + 2)
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        ctx.fill_random(arena, n, SEED ^ 0xB0)
+        offs = np.arange(nfiles, dtype=np.uint64) * size
+        lens = np.full(nfiles, size, dtype=np.uint64)
+        dt, (total, counts) = _timed(lambda: ctx.chunk_batch_device_to_device(p, arena, offs, lens, d_out, cap),
+                                     steps, 1)
+        t = ctx.timing()
+        # parity probe: three files against the oracle
+        from oracle import oracle as O
+        chunks = ctx.d2h_chunks(d_out, total)
+        starts = np.concatenate([[0], np.cumsum(counts)])
+        ok = int(counts.sum()) == total
+        for i in (0, nfiles // 2, nfiles - 1):
+            host = O.random_bytes(size, SEED ^ 0xB0, pos=i * size)
+            ok &= _same(chunks[starts[i]:starts[i + 1]], O.chunk(O.Params(*PARAMS), host))
+        return {"files": nfiles, "file_bytes": size, "bytes": n, "steps": steps,
+                "ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
+                "files_per_s": round(nfiles / dt, 1), "chunks": int(total),
+                "scan_ms": round(t["scan_ms"], 3), "device_ms": round(t["device_ms"], 3),
+                "parity_probe_files": 3, "parity_probe_ok": bool(ok),
+                "data": "synthetic uniform-random (device PRNG), per-file counts returned"}
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(arena)
+
+
+def small_files(ctx, p, nfiles: int, steps: int) -> dict:
+    """Stand-in for BASELINE configs[3] (no kernel tree here or on the box):
+    `nfiles` files with a log-normal size mix (median 8 KiB, sigma 1.2, capped at
+    64 MiB), random bytes, packed back to back in one device arena."""
+    from mapache_amd import _lib
+    rng = np.random.default_rng(20251016)
+    sizes = np.minimum(np.exp(rng.normal(np.log(8192), 1.2, nfiles)).astype(np.uint64) + 1, 64 << 20)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    n = int(sizes.sum())
+    arena = ctx.device_alloc(n + 16)
+    cap = int(sum(int(s) // (p.min_size - 1) + 2 for s in sizes))
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        ctx.fill_random(arena, n, SEED ^ 0x5F)
+        dt, (total, counts) = _timed(lambda: ctx.chunk_batch_device_to_device(p, arena, offs, sizes, d_out, cap),
+                                     steps, 1)
+        from oracle import oracle as O
+        chunks = ctx.d2h_chunks(d_out, total)
+        host = O.random_bytes(n, SEED ^ 0x5F)
+        ref, rc = O.chunk_files(O.Params(*PARAMS), [host[int(o):int(o) + int(s)] for o, s in zip(offs, sizes)],
+                                threads=8)
+        ok = _same(chunks, ref) and bool((counts == rc).all())
+        return {"files": nfiles, "bytes": n, "median_file_bytes": int(np.median(sizes)),
+                "ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
+                "files_per_s": round(nfiles / dt, 1), "chunks": int(total), "parity_ok": bool(ok),
+                "data": "synthetic log-normal size mix (median 8 KiB), uniform-random bytes"}
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(arena)
 
 
 def main() -> int:
@@ -135,6 +211,8 @@ def main() -> int:
     ap.add_argument("--gib", type=float, default=64.0, help="bytes per GPU (GiB)")
     ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
     ap.add_argument("--e2e-gib", type=float, default=8.0)
+    ap.add_argument("--batch-files", type=int, default=10000, help="configs[2] file count (0: skip)")
+    ap.add_argument("--small-files", type=int, default=80000, help="configs[3] file count (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
 
@@ -150,10 +228,14 @@ def main() -> int:
 
     from mapache_amd import _lib
     p = _lib.params(*PARAMS)
-    n = int(a.gib * (1 << 30))
-    ctx = _lib.Context(local, n)
+    n = int(a.gib * GIB)
+    extras = rank == 0 and world == 1
+    max_bytes = max(n, a.batch_files * (8 << 20) if extras else 0)
+    ctx = _lib.Context(local, max_bytes)
     dp = ctx.device_alloc(n)
     ctx.fill_random(dp, n, SEED ^ rank)  # rank 0 uses SEED itself
+    cap = n // (p.min_size - 1) + 2
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
 
     def barrier():
         if dist is not None:
@@ -161,15 +243,14 @@ def main() -> int:
             torch.cuda.synchronize()
             dist.barrier()
 
-    out = ctx.pinned_out(n // (p.min_size - 1) + 2)  # reused pinned boundary list
     for _ in range(a.warmup):
-        ctx.chunk_device(p, dp, n, out=out)
+        ctx.chunk_device_to_device(p, dp, n, d_out, cap)
     scan_ms, dev_ms, total_ms = [], [], []
     barrier()
     t0 = time.perf_counter()
-    chunks = None
+    count = 0
     for _ in range(a.steps):
-        chunks = ctx.chunk_device(p, dp, n, out=out)
+        count = ctx.chunk_device_to_device(p, dp, n, d_out, cap)
         t = ctx.timing()
         scan_ms.append(t["scan_ms"])
         dev_ms.append(t["device_ms"])
@@ -184,7 +265,7 @@ def main() -> int:
 
     n_gpus = world if world > 1 else 1
     total_bytes = n_gpus * n * a.steps
-    value = total_bytes / elapsed / (1 << 30)
+    value = total_bytes / elapsed / GIB
     scan_avg = float(np.mean(scan_ms))
     achieved = n / (scan_avg * 1e-3) / 1e9
     tpb, tsrc = _pmc_traffic()
@@ -192,27 +273,39 @@ def main() -> int:
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": n_gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"one {a.gib:g} GiB uniform-random buffer per GPU, device-resident "
+        "config": {"workload": f"one {a.gib:g} GiB uniform-random buffer per GPU, device-resident in and out "
                                f"(BASELINE configs[1])", "params": "FastCDC v2020 16/64/256 KiB Level1",
-                   "bytes_per_gpu": n, "chunks_per_step": int(len(chunks)),
+                   "bytes_per_gpu": n, "chunks_per_step": int(count),
                    "parallelism": f"{n_gpus} independent streams, no collectives"},
         "roofline": {"bound": "hbm", "kernel": "k_scan_q", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": int(round(tpb * n)) if tpb else None, "traffic_unit": "bytes per launch",
                      "traffic_source": tsrc, "bytes_per_launch": n, "avg_launch_ms": round(scan_avg, 3)},
         "device_only": {"scan_ms": round(scan_avg, 3), "device_ms": round(float(np.mean(dev_ms)), 3),
-                        "gib_s": round(n / (float(np.mean(dev_ms)) * 1e-3) / (1 << 30), 2),
+                        "gib_s": round(n / (float(np.mean(dev_ms)) * 1e-3) / GIB, 2),
                         "call_ms": round(float(np.mean(total_ms)), 3)},
     }
-    chunks = chunks.copy()
-    if rank == 0 and n_gpus == 1:
-        try:
-            result["e2e_host"] = e2e_host(ctx, p, a.e2e_gib) if a.e2e_gib > 0 else None
-        except Exception as e:  # reported, never silently dropped
-            result["e2e_host"] = {"error": str(e)}
+    chunks = ctx.d2h_chunks(d_out, count)
+    if extras:
+        # same step, boundary list to pinned host memory (crosses PCIe inside the call)
+        out = ctx.pinned_out(cap)
+        dt, hc = _timed(lambda: ctx.chunk_device(p, dp, n, out=out), max(3, a.steps // 2), 1)
+        result["host_out"] = {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
+                              "identical_to_device_out": _same(hc, chunks),
+                              "output": "pinned host array (hipHostMalloc), written by k_emit over PCIe"}
+    ctx.device_free(d_out)
+    ctx.device_free(dp)
+    if extras:
+        for key, fn in (("e2e_host", lambda: e2e_host(ctx, p, a.e2e_gib) if a.e2e_gib > 0 else None),
+                        ("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3)
+                         if a.batch_files > 0 else None),
+                        ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None)):
+            try:
+                result[key] = fn()
+            except Exception as e:  # reported, never silently dropped
+                result[key] = {"error": f"{type(e).__name__}: {e}"}
         if not a.no_cpu:
             result["cpu_baseline"] = cpu_baseline(a.cpu_sample_gib, chunks)
-    ctx.device_free(dp)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

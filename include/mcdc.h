@@ -107,7 +107,12 @@ void mcdc_ctx_destroy(struct mcdc_ctx *ctx);
 /* Chunk one device-resident buffer (the device-resident GiB/s metric).
  * Replaces one StreamCDC::with_level(..) + its full iteration over a file
  * whose bytes already sit in HBM (processor.rs:173-202).  d_data is a device
- * pointer on the context's device (any alignment). */
+ * pointer on the context's device (any alignment).
+ * `out` may be host memory (pageable: one D2H copy; pinned: written directly
+ * over PCIe) or a device pointer on the context's device, in which case the
+ * boundary list stays in HBM for a device-side consumer (the next pipeline
+ * stage, chunk IDs) and nothing crosses PCIe but the count.  The same holds
+ * for `out` of every entry point below. */
 int mcdc_chunk_device(struct mcdc_ctx *ctx, const mcdc_params *params, const void *d_data,
                       size_t n, mcdc_chunk *out, size_t cap, size_t *n_out);
 
@@ -150,6 +155,7 @@ int mcdc_device_free(struct mcdc_ctx *ctx, void *d_ptr);
 int mcdc_host_alloc(struct mcdc_ctx *ctx, size_t bytes, void **h_ptr);
 int mcdc_host_free(struct mcdc_ctx *ctx, void *h_ptr);
 int mcdc_memcpy_h2d(struct mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int mcdc_memcpy_d2h(struct mcdc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
 
 /* Fill d_dst[0, n) with the counter-based synthetic stream used by the bench
  * and tests: byte at stream position p = pos + i is

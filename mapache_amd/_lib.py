@@ -29,7 +29,7 @@ EXPORTS = (
     "mcdc_params_check", "mcdc_ctx_create", "mcdc_ctx_destroy", "mcdc_chunk_device",
     "mcdc_chunk_host", "mcdc_chunk_batch", "mcdc_chunk_batch_device", "mcdc_ctx_timing",
     "mcdc_last_error", "mcdc_device_alloc", "mcdc_device_free", "mcdc_host_alloc",
-    "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_fill_random_device", "mcdc_digest",
+    "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_memcpy_d2h", "mcdc_fill_random_device", "mcdc_digest",
     "mcdc_abi_version",
 )
 
@@ -88,6 +88,7 @@ def load():
     L.mcdc_host_alloc.argtypes = [vp, sz, P(vp)]
     L.mcdc_host_free.argtypes = [vp, vp]
     L.mcdc_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.mcdc_memcpy_d2h.argtypes = [vp, vp, vp, sz]
     L.mcdc_fill_random_device.argtypes = [vp, vp, u64, sz, u64]
     L.mcdc_digest.argtypes = [vp, sz]
     L.mcdc_digest.restype = u64
@@ -207,6 +208,34 @@ class Context:
                                              offs.ctypes.data, ls.ctypes.data, n, out.ctypes.data, cap,
                                              counts.ctypes.data, ctypes.byref(n_out)))
         return out[: n_out.value].copy(), counts[:n].astype(np.int64)
+
+    def chunk_device_to_device(self, p: McdcParams, d_ptr: int, n: int, d_out: int, cap: int) -> int:
+        """Chunk a device-resident buffer into a device-resident boundary list
+        (`cap` mcdc_chunk records at device pointer `d_out`); returns the count."""
+        n_out = ctypes.c_size_t()
+        check(load().mcdc_chunk_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_ptr), n,
+                                       ctypes.c_void_p(d_out), cap, ctypes.byref(n_out)))
+        return n_out.value
+
+    def chunk_batch_device_to_device(self, p: McdcParams, d_arena: int, offsets, lens, d_out: int, cap: int):
+        """Many device-resident files -> device-resident boundary list; returns
+        (total chunks, per-file counts)."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ls = np.ascontiguousarray(lens, dtype=np.uint64)
+        n = offs.size
+        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        n_out = ctypes.c_size_t()
+        check(load().mcdc_chunk_batch_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_arena),
+                                             offs.ctypes.data, ls.ctypes.data, n, ctypes.c_void_p(d_out), cap,
+                                             counts.ctypes.data, ctypes.byref(n_out)))
+        return n_out.value, counts[:n].astype(np.int64)
+
+    def d2h_chunks(self, d_out: int, count: int) -> np.ndarray:
+        out = np.empty(max(count, 1), dtype=CHUNK_DTYPE)
+        if count:
+            check(load().mcdc_memcpy_d2h(self._h, out.ctypes.data, ctypes.c_void_p(d_out),
+                                         count * CHUNK_DTYPE.itemsize))
+        return out[:count]
 
     def timing(self) -> dict:
         t = McdcTiming()

@@ -122,6 +122,13 @@ struct mcdc_ctx {
   std::vector<uint64_t> h_node_off;
   void *h_tab = nullptr;  // pinned copy of the segment tables (async H2D)
   size_t h_tab_cap = 0;
+  // Plan cache: the segment tables depend only on the file ranges and the
+  // parameters (never on the bytes), so a call with the same layout as the
+  // previous one reuses the uploaded tables.
+  std::vector<uint64_t> plan_key;
+  bool plan_valid = false;
+  uint64_t *h_res = nullptr;  // pinned call summary written by k_finish
+  uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
 
@@ -181,18 +188,31 @@ int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
   return MCDC_OK;
 }
 
-// Device-visible alias of a caller's output array when it is pinned host
-// memory (hipHostMalloc / registered): k_emit then writes the boundary list
-// straight over PCIe and no separate copy is needed.  nullptr otherwise.
-void *host_out_alias(void *out) {
+// Where k_emit can write the caller's output array directly: a device
+// pointer on the context's device (the boundary list stays in HBM for a
+// device-side consumer), or the device alias of pinned host memory
+// (hipHostMalloc / registered: written straight over PCIe, no separate copy).
+// nullptr for pageable host memory (staged through ctx->out + one D2H copy).
+void *direct_out(const mcdc_ctx *ctx, void *out) {
   if (!out) return nullptr;
   hipPointerAttribute_t a{};
   if (hipPointerGetAttributes(&a, out) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
+  if (a.type == hipMemoryTypeDevice) return a.device == ctx->device ? out : nullptr;
   if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
   return a.devicePointer;
+}
+
+bool is_device_ptr(const void *p) {
+  if (!p) return false;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
 }
 
 double now_ms() {
@@ -210,41 +230,62 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if (rc) return rc;
   const DevParams P = make_dev_params(params, ms, ml);
   const uint64_t Z = segment_bytes(params);
+  void *out_dev = direct_out(ctx, out);
+  if (!out_dev && is_device_ptr(out))
+    return fail(MCDC_E_INVALID, "out is a device pointer of another device");
 
-  // ---- plan segments (host) ----
-  ctx->h_files.resize(nfiles);
-  ctx->h_segs.clear();
-  ctx->h_node_off.clear();
-  ctx->h_node_off.push_back(0);
+  // ---- plan segments (host; reused when the layout repeats) ----
   uint64_t total_bytes = 0, out_bound = 0;
   for (size_t i = 0; i < nfiles; ++i) {
     const uint64_t len = fend[i] - fstart[i];
     total_bytes += len;
-    const uint32_t nseg = (uint32_t)((len + Z - 1) / Z);
-    File F{fstart[i], fend[i], (uint32_t)ctx->h_segs.size(), nseg};
-    ctx->h_files[i] = F;
-    for (uint32_t k = 0; k < nseg; ++k) {
-      Seg S;
-      S.start = fstart[i] + (uint64_t)k * Z;
-      S.end = std::min<uint64_t>(S.start + Z, fend[i]);
-      S.file = (uint32_t)i;
-      S.flags = (k == 0 ? kSegFirst : 0) | (k + 1 == nseg ? kSegLast : 0);
-      ctx->h_segs.push_back(S);
-      const uint64_t ncap = (S.end - S.start) / (params->min_size - 1) + 2;
-      ctx->h_node_off.push_back(ctx->h_node_off.back() + ncap);
-    }
     out_bound += len / (params->min_size - 1) + 2;
+  }
+  bool same_plan = ctx->plan_valid && ctx->plan_key.size() == 2 * nfiles + 2 &&
+                   ctx->plan_key[0] == Z && ctx->plan_key[1] == params->min_size;
+  for (size_t i = 0; same_plan && i < nfiles; ++i)
+    same_plan = ctx->plan_key[2 + 2 * i] == fstart[i] && ctx->plan_key[3 + 2 * i] == fend[i];
+  if (!same_plan) {
+    ctx->plan_valid = false;
+    ctx->plan_key.assign(2 * nfiles + 2, 0);
+    ctx->plan_key[0] = Z;
+    ctx->plan_key[1] = params->min_size;
+    ctx->h_files.resize(nfiles);
+    ctx->h_segs.clear();
+    ctx->h_node_off.clear();
+    ctx->h_node_off.push_back(0);
+    for (size_t i = 0; i < nfiles; ++i) {
+      ctx->plan_key[2 + 2 * i] = fstart[i];
+      ctx->plan_key[3 + 2 * i] = fend[i];
+      const uint64_t len = fend[i] - fstart[i];
+      const uint32_t nseg = (uint32_t)((len + Z - 1) / Z);
+      File F{fstart[i], fend[i], (uint32_t)ctx->h_segs.size(), nseg};
+      ctx->h_files[i] = F;
+      for (uint32_t k = 0; k < nseg; ++k) {
+        Seg S;
+        S.start = fstart[i] + (uint64_t)k * Z;
+        S.end = std::min<uint64_t>(S.start + Z, fend[i]);
+        S.file = (uint32_t)i;
+        S.flags = (k == 0 ? kSegFirst : 0) | (k + 1 == nseg ? kSegLast : 0);
+        ctx->h_segs.push_back(S);
+        const uint64_t ncap = (S.end - S.start) / (params->min_size - 1) + 2;
+        ctx->h_node_off.push_back(ctx->h_node_off.back() + ncap);
+      }
+    }
   }
   const uint32_t nsegs = (uint32_t)ctx->h_segs.size();
   const uint64_t nruns = (n_al + kRun - 1) / kRun;
 
   // ---- workspace ----
+  const void *tabs_before[3] = {ctx->segs.p, ctx->files.p, ctx->node_off.p};
   if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
   if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
   if ((rc = ensure(ctx, ctx->files, nfiles * sizeof(File)))) return rc;
   if ((rc = ensure(ctx, ctx->nodes, ctx->h_node_off.back() * sizeof(uint64_t)))) return rc;
   if ((rc = ensure(ctx, ctx->node_off, ctx->h_node_off.size() * sizeof(uint64_t)))) return rc;
+  if (tabs_before[0] != ctx->segs.p || tabs_before[1] != ctx->files.p || tabs_before[2] != ctx->node_off.p)
+    ctx->plan_valid = false;  // reallocated: the uploaded tables are gone
   if ((rc = ensure(ctx, ctx->node_cnt, nsegs * 4))) return rc;
   if ((rc = ensure(ctx, ctx->seg_exit, nsegs * 8))) return rc;
   if ((rc = ensure(ctx, ctx->cont, (size_t)nsegs * kContMax * 8))) return rc;
@@ -257,29 +298,11 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if ((rc = ensure(ctx, ctx->entry_idx, nsegs * 4))) return rc;
   if ((rc = ensure(ctx, ctx->seg_count, (nsegs + 1) * 8))) return rc;
   if ((rc = ensure(ctx, ctx->seg_off, (nsegs + 1) * 8))) return rc;
-  if (!host_out_alias(out) && (rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
+  if (!out_dev && (rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
   if ((rc = ensure(ctx, ctx->err, 16))) return rc;
   const size_t tmpb = scan_tmp_bytes(nsegs);
   if ((rc = ensure(ctx, ctx->scan_tmp, tmpb))) return rc;
-
   hipStream_t st = ctx->stream;
-  {  // tables -> pinned stage -> one async copy each
-    const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
-                 b_noff = ctx->h_node_off.size() * 8;
-    const size_t o_files = (b_segs + 255) / 256 * 256, o_noff = o_files + (b_files + 255) / 256 * 256;
-    if ((rc = ensure_tab(ctx, o_noff + b_noff))) return rc;
-    char *tb = (char *)ctx->h_tab;
-    if (b_segs) std::memcpy(tb, ctx->h_segs.data(), b_segs);
-    if (b_files) std::memcpy(tb + o_files, ctx->h_files.data(), b_files);
-    std::memcpy(tb + o_noff, ctx->h_node_off.data(), b_noff);
-    if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tb, b_segs, hipMemcpyHostToDevice, st));
-    if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tb + o_files, b_files, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tb + o_noff, b_noff, hipMemcpyHostToDevice, st));
-  }
-  void *out_dev = host_out_alias(out);  // pinned caller array: emit writes it directly
-  if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st));
-  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st));
-  HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st));
 
   Work W{};
   W.base = base;
@@ -312,35 +335,62 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.out_cap = out_dev ? std::min<uint64_t>(out_bound, cap) : out_bound;
   W.err = (uint32_t *)ctx->err.p;
 
+  // The scan needs none of the segment tables: it is enqueued first, and the
+  // table uploads / workspace resets queue behind it (they are only read by
+  // the resolution kernels).
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
   if (n_al > 0) launch_scan(W, P, ctx->num_cus, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_scan, st));
+  if (!ctx->plan_valid) {  // tables -> pinned stage -> one async copy each
+    const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
+                 b_noff = ctx->h_node_off.size() * 8;
+    const size_t o_files = (b_segs + 255) / 256 * 256, o_noff = o_files + (b_files + 255) / 256 * 256;
+    // (the previous call synchronised before returning, so the pinned stage
+    // is idle; staging on the host overlaps the scan just enqueued)
+    if ((rc = ensure_tab(ctx, o_noff + b_noff))) return rc;
+    char *tb = (char *)ctx->h_tab;
+    if (b_segs) std::memcpy(tb, ctx->h_segs.data(), b_segs);
+    if (b_files) std::memcpy(tb + o_files, ctx->h_files.data(), b_files);
+    std::memcpy(tb + o_noff, ctx->h_node_off.data(), b_noff);
+    if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tb, b_segs, hipMemcpyHostToDevice, st));
+    if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tb + o_files, b_files, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tb + o_noff, b_noff, hipMemcpyHostToDevice, st));
+    ctx->plan_valid = true;
+  }
+  if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st));
+  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st));
+  HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st));
   launch_resolve(W, P, ctx->scan_tmp.p, tmpb, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
+  launch_finish(W, ctx->d_res, st);
+  HIP_TRY(hipGetLastError());
 
-  // ---- results ----
-  uint64_t total = 0;
-  uint32_t err = 0;
+  // ---- results: one synchronisation in the common case ----
   const double t_d2h0 = now_ms();
-  if (nsegs) HIP_TRY(hipMemcpyAsync(&total, (uint64_t *)ctx->seg_off.p + nsegs, 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(&err, ctx->err.p, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t total = ((volatile uint64_t *)ctx->h_res)[0];
+  const uint32_t err = (uint32_t)((volatile uint64_t *)ctx->h_res)[1];
+  const uint64_t nfallback = ((volatile uint64_t *)ctx->h_res)[2];
   if (n_out) *n_out = (size_t)total;
   if (total > cap || (total && !out))
     return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu chunks", cap, (unsigned long long)total);
   if (err) return fail(MCDC_E_INTERNAL, "device consistency error 0x%x", err);
-  if (total && !out_dev)
+  bool copies = false;
+  if (total && !out_dev) {
     HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st));
+    copies = true;
+  }
   std::vector<uint64_t> seg_off;
   if (counts && nfiles) {
     seg_off.resize(nsegs + 1);
-    if (nsegs) HIP_TRY(hipMemcpyAsync(seg_off.data(), ctx->seg_off.p, (nsegs + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (nsegs) {
+      HIP_TRY(hipMemcpyAsync(seg_off.data(), ctx->seg_off.p, (nsegs + 1) * 8, hipMemcpyDeviceToHost, st));
+      copies = true;
+    }
   }
-  std::vector<uint32_t> fflags(nfiles);
-  if (nfiles) HIP_TRY(hipMemcpyAsync(fflags.data(), ctx->file_flags.p, nfiles * 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  if (copies) HIP_TRY(hipStreamSynchronize(st));
   const double t_d2h1 = now_ms();
   if (counts) {
     for (size_t i = 0; i < nfiles; ++i) {
@@ -358,9 +408,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->timing.bytes = total_bytes;
   ctx->timing.chunks = total;
   ctx->timing.scan_launches = n_al > 0 ? 1 : 0;
-  uint64_t fb = 0;
-  for (uint32_t f : fflags) fb += (f & kFileFallbackDone) ? 1 : 0;
-  ctx->timing.fallback_files = fb;
+  ctx->timing.fallback_files = nfallback;
   return MCDC_OK;
 }
 
@@ -416,6 +464,9 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
   if (hipMemcpy(ctx->d_gear, kGear, 2048, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(ctx->d_gear16, g16, 2048, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(MCDC_E_DEVICE, "table upload failed"));
+  if (hipHostMalloc((void **)&ctx->h_res, 64, hipHostMallocDefault) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&ctx->d_res, ctx->h_res, 0) != hipSuccess)
+    return bail(fail(MCDC_E_NOMEM, "pinned result word allocation failed"));
   *out = ctx;
   return MCDC_OK;
 }
@@ -425,6 +476,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
+  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
@@ -626,6 +678,14 @@ int mcdc_memcpy_h2d(mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes)
   int rc = check_ctx(ctx);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return MCDC_OK;
+}
+
+int mcdc_memcpy_d2h(mcdc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return MCDC_OK;
 }

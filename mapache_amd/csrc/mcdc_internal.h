@@ -85,7 +85,7 @@ struct Work {
   uint64_t *seg_off;     // exclusive prefix of seg_count
   DevChunk *out;
   uint64_t out_cap;
-  uint32_t *err;
+  uint32_t *err;         // [0] error bits, [1] files resolved by k_fallback
 };
 
 // launch wrappers (mcdc_kernels.hip); all enqueue on `stream`.
@@ -94,5 +94,6 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
 void launch_resolve(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
                     hipStream_t stream);
 size_t scan_tmp_bytes(uint32_t nsegs);
+void launch_finish(const Work &w, uint64_t *res, hipStream_t stream);
 
 }  // namespace mcdc

@@ -732,7 +732,10 @@ __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
     }
     k = 0; ++j;
   }
-  if (lane == 0) W.file_flags[f] = kFileFallbackDone;
+  if (lane == 0) {
+    W.file_flags[f] = kFileFallbackDone;
+    atomicAdd(W.err + 1, 1u);  // fallback file count (reported in mcdc_timing)
+  }
 }
 
 // ============================================================ walk =======
@@ -890,6 +893,20 @@ __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P) {
       }
     }
   }
+}
+
+// Call summary for the host in one small write (pinned host memory): chunk
+// total, error bits, fallback file count.
+__global__ void k_finish(Work W, uint64_t *res) {
+  if (threadIdx.x == 0) {
+    res[0] = W.nsegs ? W.seg_off[W.nsegs] : 0;
+    res[1] = W.err[0];
+    res[2] = W.err[1];
+  }
+}
+
+void launch_finish(const Work &w, uint64_t *res, hipStream_t stream) {
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, stream, w, res);
 }
 
 size_t scan_tmp_bytes(uint32_t nsegs) {

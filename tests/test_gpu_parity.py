@@ -209,3 +209,61 @@ def test_pinned_output_written_directly(ctx):
         _same(ref, O.chunk(O.Params(*PARAMS[0]), O.random_bytes(n, SEED + 3)))
     finally:
         ctx.device_free(dp)
+
+
+def test_device_output_stays_in_hbm(ctx):
+    """A device `out` array: k_emit writes the boundary list in HBM (the
+    bench's headline configuration); identical to the host-output path and the
+    oracle; a too-small device array reports MCDC_E_CAPACITY with the count."""
+    n = (80 << 20) + 4321
+    p = _lib.params(*PARAMS[0])
+    dp = ctx.device_alloc(n)
+    cap = n // (p.min_size - 1) + 2
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        ctx.fill_random(dp, n, SEED + 4)
+        k = ctx.chunk_device_to_device(p, dp, n, d_out, cap)
+        got = ctx.d2h_chunks(d_out, k)
+        ref = O.chunk(O.Params(*PARAMS[0]), O.random_bytes(n, SEED + 4))
+        _same(got, ref)
+        _same(ctx.chunk_device(p, dp, n), ref)
+        with pytest.raises(_lib.McdcError) as ei:
+            ctx.chunk_device_to_device(p, dp, n, d_out, k - 1)
+        assert ei.value.code == -3
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(dp)
+
+
+def test_batch_device_to_device(ctx):
+    sizes = [0, 17, 16385, 300_000, 5 << 20, 1, (2 << 20) + 9]
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64) + 3
+    n = int(sum(sizes)) + 64
+    p = _lib.params(*PARAMS[0])
+    arena = ctx.device_alloc(n)
+    cap = sum(s // (p.min_size - 1) + 2 for s in sizes)
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        ctx.fill_random(arena, n, SEED + 5)
+        total, counts = ctx.chunk_batch_device_to_device(p, arena, offs, sizes, d_out, cap)
+        host = O.random_bytes(n, SEED + 5)
+        ref, rc = O.chunk_files(O.Params(*PARAMS[0]), [host[int(o):int(o) + s] for o, s in zip(offs, sizes)])
+        _same(ctx.d2h_chunks(d_out, total), ref)
+        assert (counts == rc).all()
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(arena)
+
+
+def test_plan_reuse_across_layouts(ctx):
+    """The segment plan is cached per (file ranges, params): alternating
+    lengths and parameter sets must re-plan, repeats must reuse it."""
+    n = 40 << 20
+    dp = ctx.device_alloc(n)
+    try:
+        ctx.fill_random(dp, n, SEED + 6)
+        h = O.random_bytes(n, SEED + 6)
+        for ln, pi in [(n, 0), (n, 0), (n - 999, 0), (n, 1), (n, 0), (n - 999, 3), (n - 999, 3), (n, 2)]:
+            _same(ctx.chunk_device(_lib.params(*PARAMS[pi]), dp, ln), O.chunk(O.Params(*PARAMS[pi]), h[:ln]))
+    finally:
+        ctx.device_free(dp)
