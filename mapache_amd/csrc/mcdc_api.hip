@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -100,20 +101,35 @@ struct DevBuf {
   size_t cap = 0;
 };
 
+constexpr int kMaxParts = 4;
+
+// Scan parts (DESIGN.md §3 "Staged pipeline"): the scan is split into
+// consecutive tile ranges; the resolution of every segment whose inputs lie in
+// the parts already scanned runs on a second stream while the next part is
+// scanned.  Parts after the first are whole rounds (one tile per scan wave)
+// so no launch ends with a ragged last round.  MCDC_PARTS (1..4) overrides the
+// part count, MCDC_TAIL_ROUNDS the size of the last part.
+int env_int(const char *name, int dflt) {
+  const char *v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
 }  // namespace
 
 struct mcdc_ctx {
   int device = 0;
   int num_cus = 256;
   size_t max_bytes = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // scan (and input copies)
+  hipStream_t stream2 = nullptr;  // chain resolution, overlapping the scan's later parts
   hipEvent_t ev_start = nullptr, ev_scan = nullptr, ev_end = nullptr, ev_h2d0 = nullptr,
              ev_h2d1 = nullptr;
+  hipEvent_t ev_part[kMaxParts] = {};
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
   DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp;
+      scan_tmp, seg_incl;
   // pinned host staging
   void *h_stage = nullptr;
   size_t h_stage_cap = 0;
@@ -139,6 +155,7 @@ int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
   if (b.cap >= bytes) return MCDC_OK;
   if (b.p) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -157,6 +174,7 @@ int ensure_stage(mcdc_ctx *ctx, size_t bytes) {
   if (ctx->h_stage_cap >= bytes) return MCDC_OK;
   if (ctx->h_stage) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipHostFree(ctx->h_stage));
     ctx->h_stage = nullptr;
     ctx->h_stage_cap = 0;
@@ -174,6 +192,7 @@ int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
   if (ctx->h_tab_cap >= bytes) return MCDC_OK;
   if (ctx->h_tab) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipHostFree(ctx->h_tab));
     ctx->h_tab = nullptr;
     ctx->h_tab_cap = 0;
@@ -335,12 +354,72 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.out_cap = out_dev ? std::min<uint64_t>(out_bound, cap) : out_bound;
   W.err = (uint32_t *)ctx->err.p;
 
-  // The scan needs none of the segment tables: it is enqueued first, and the
-  // table uploads / workspace resets queue behind it (they are only read by
-  // the resolution kernels).
+  if ((rc = ensure(ctx, ctx->seg_incl, (size_t)nsegs * 8))) return rc;
+
+  // ---- staged pipeline plan ----
+  // parts: full tiles [tb[i], tb[i+1]); the last part also scans the partial tile
+  const uint64_t tile_bytes = 64ull * kRun;
+  const uint64_t ntiles_full = (n_al / kRun) / 64;
+  // (MCDC_PART_TILES / MCDC_MIN_ROUNDS shrink the round unit and the size
+  // threshold so that tests exercise the staged path on small inputs)
+  const uint64_t waves = (uint64_t)std::max(
+      env_int("MCDC_PART_TILES", (int)std::max<uint64_t>(1, scan_waves(ntiles_full, ctx->num_cus))), 1);
+  int K = std::min(std::max(env_int("MCDC_PARTS", 1), 1), kMaxParts);
+  const uint64_t tail_rounds = (uint64_t)std::max(env_int("MCDC_TAIL_ROUNDS", 2), 1);
+  const uint64_t min_rounds = (uint64_t)std::max(env_int("MCDC_MIN_ROUNDS", 8), 0);
+  uint64_t tb[kMaxParts + 1];
+  {
+    uint64_t rounds_needed = 0, r = tail_rounds;
+    for (int k = 1; k < K; ++k, r *= 3) rounds_needed += r;
+    if (nsegs == 0 || ntiles_full < (rounds_needed + min_rounds) * waves || ntiles_full <= rounds_needed * waves)
+      K = 1;
+    tb[0] = 0;
+    tb[K] = ntiles_full;
+    r = tail_rounds;
+    for (int k = K - 1; k >= 1; --k, r *= 3) tb[k] = tb[k + 1] - r * waves;
+  }
+  // resolution batches: spec/link/emit of segments [hi[i-1], hi[i]) after part i
+  uint32_t spec_hi[kMaxParts], link_hi[kMaxParts];
+  {
+    const uint64_t mx = params->max_size;
+    auto ceil_run = [](uint64_t x) { return (x + kRun - 1) / kRun * kRun; };
+    uint32_t sp = 0, lk = 0;
+    for (int i = 0; i < K; ++i) {
+      if (i == K - 1) {
+        sp = lk = nsegs;
+      } else {
+        const uint64_t B = tb[i + 1] * tile_bytes;
+        while (sp < nsegs) {  // k_spec reads candidates up to S.end + max
+          const Seg &S = ctx->h_segs[sp];
+          if (ceil_run(std::min<uint64_t>(S.end + mx, ctx->h_files[S.file].end)) > B) break;
+          ++sp;
+        }
+        while (lk < sp) {  // k_link: <= kContMax steps past S.end, merging into segments < sp
+          const Seg &S = ctx->h_segs[lk];
+          if (!(S.flags & kSegLast)) {
+            const File &F = ctx->h_files[S.file];
+            const uint64_t x = std::min<uint64_t>(S.end + (kContMax + 1) * mx, F.end);
+            const uint64_t j = F.first_seg + (std::min<uint64_t>(x, F.end - 1) - F.start) / Z;
+            if (ceil_run(x) > B || j >= sp) break;
+          }
+          ++lk;
+        }
+      }
+      spec_hi[i] = sp;
+      link_hi[i] = lk;
+    }
+  }
+
+  // ---- launches: scan parts on `stream`, resolution on `stream2` ----
+  // The scan needs none of the segment tables, so it is enqueued first; the
+  // table uploads and workspace resets run on stream2 beside it.
+  hipStream_t st2 = ctx->stream2;
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
-  if (n_al > 0) launch_scan(W, P, ctx->num_cus, st);
-  HIP_TRY(hipGetLastError());
+  for (int i = 0; i < K; ++i) {
+    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
+  }
   HIP_TRY(hipEventRecord(ctx->ev_scan, st));
   if (!ctx->plan_valid) {  // tables -> pinned stage -> one async copy each
     const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
@@ -349,27 +428,46 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     // (the previous call synchronised before returning, so the pinned stage
     // is idle; staging on the host overlaps the scan just enqueued)
     if ((rc = ensure_tab(ctx, o_noff + b_noff))) return rc;
-    char *tb = (char *)ctx->h_tab;
-    if (b_segs) std::memcpy(tb, ctx->h_segs.data(), b_segs);
-    if (b_files) std::memcpy(tb + o_files, ctx->h_files.data(), b_files);
-    std::memcpy(tb + o_noff, ctx->h_node_off.data(), b_noff);
-    if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tb, b_segs, hipMemcpyHostToDevice, st));
-    if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tb + o_files, b_files, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tb + o_noff, b_noff, hipMemcpyHostToDevice, st));
+    char *tbuf = (char *)ctx->h_tab;
+    if (b_segs) std::memcpy(tbuf, ctx->h_segs.data(), b_segs);
+    if (b_files) std::memcpy(tbuf + o_files, ctx->h_files.data(), b_files);
+    std::memcpy(tbuf + o_noff, ctx->h_node_off.data(), b_noff);
+    if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tbuf, b_segs, hipMemcpyHostToDevice, st2));
+    if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tbuf + o_files, b_files, hipMemcpyHostToDevice, st2));
+    HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tbuf + o_noff, b_noff, hipMemcpyHostToDevice, st2));
     ctx->plan_valid = true;
   }
-  if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st));
-  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st));
-  HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st));
-  launch_resolve(W, P, ctx->scan_tmp.p, tmpb, st);
+  if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st2));
+  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st2));
+  HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
+  HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, st2));
+  for (int i = 0; i < K; ++i) {
+    HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[i], 0));
+    const uint32_t a_s = i ? spec_hi[i - 1] : 0, a_l = i ? link_hi[i - 1] : 0;
+    launch_spec(W, P, a_s, spec_hi[i], st2);
+    launch_link(W, P, a_l, link_hi[i], st2);
+    launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(ctx->ev_end, st2));
+  launch_finish(W, ctx->d_res, st2);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ctx->ev_end, st));
-  launch_finish(W, ctx->d_res, st);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st2));
+  if (((volatile uint64_t *)ctx->h_res)[3]) {
+    // some continuation did not merge into the next segment: resolve the whole
+    // call with the general path (serial fallback / serial walk), which
+    // rewrites every count, offset and boundary of the incremental pass
+    HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 4, st2));  // incremental capacity bits are void
+    launch_resolve_general(W, P, ctx->scan_tmp.p, tmpb, st2);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev_end, st2));
+    launch_finish(W, ctx->d_res, st2);
+    HIP_TRY(hipGetLastError());
+  }
 
   // ---- results: one synchronisation in the common case ----
   const double t_d2h0 = now_ms();
-  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(hipStreamSynchronize(st2));
   const uint64_t total = ((volatile uint64_t *)ctx->h_res)[0];
   const uint32_t err = (uint32_t)((volatile uint64_t *)ctx->h_res)[1];
   const uint64_t nfallback = ((volatile uint64_t *)ctx->h_res)[2];
@@ -379,18 +477,18 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if (err) return fail(MCDC_E_INTERNAL, "device consistency error 0x%x", err);
   bool copies = false;
   if (total && !out_dev) {
-    HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st2));
     copies = true;
   }
   std::vector<uint64_t> seg_off;
   if (counts && nfiles) {
     seg_off.resize(nsegs + 1);
     if (nsegs) {
-      HIP_TRY(hipMemcpyAsync(seg_off.data(), ctx->seg_off.p, (nsegs + 1) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(seg_off.data(), ctx->seg_off.p, (nsegs + 1) * 8, hipMemcpyDeviceToHost, st2));
       copies = true;
     }
   }
-  if (copies) HIP_TRY(hipStreamSynchronize(st));
+  if (copies) HIP_TRY(hipStreamSynchronize(st2));
   const double t_d2h1 = now_ms();
   if (counts) {
     for (size_t i = 0; i < nfiles; ++i) {
@@ -407,7 +505,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->timing.d2h_ms = t_d2h1 - t_d2h0;
   ctx->timing.bytes = total_bytes;
   ctx->timing.chunks = total;
-  ctx->timing.scan_launches = n_al > 0 ? 1 : 0;
+  ctx->timing.scan_launches = n_al > 0 ? (uint64_t)K : 0;
   ctx->timing.fallback_files = nfallback;
   return MCDC_OK;
 }
@@ -452,11 +550,15 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return bail(fail(MCDC_E_DEVICE, "hipSetDevice(%d)", device));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(MCDC_E_DEVICE, "hipStreamCreate failed"));
   hipEvent_t *evs[] = {&ctx->ev_start, &ctx->ev_scan, &ctx->ev_end, &ctx->ev_h2d0, &ctx->ev_h2d1};
   for (hipEvent_t *e : evs)
     if (hipEventCreate(e) != hipSuccess) return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
+  for (hipEvent_t &e : ctx->ev_part)  // ordering only: no timestamps
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
   uint64_t g16[256];
   for (int i = 0; i < 256; ++i) g16[i] = kGear[i] << 16;
   if (hipMalloc(&ctx->d_gear, 2048) != hipSuccess || hipMalloc(&ctx->d_gear16, 2048) != hipSuccess)
@@ -475,13 +577,14 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
-                    &ctx->err, &ctx->scan_tmp};
+                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -490,7 +593,10 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   hipEvent_t evs[] = {ctx->ev_start, ctx->ev_scan, ctx->ev_end, ctx->ev_h2d0, ctx->ev_h2d1};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ev_part)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
 }
 

@@ -22,6 +22,7 @@ namespace mcdc {
 constexpr int kRun = 4096;            // bytes hashed per lane per scan run
 constexpr int kWin = 48;              // bits 0..47 of the Gear hash = last 48 bytes
 constexpr int kContMax = 64;          // continuation steps before serial fallback
+constexpr int kGroup = 16;            // lanes per chain in k_spec / k_link / k_emit
 constexpr uint8_t kRunOverflow = 255; // run_cnt marker: candidates exceed cap
 constexpr uint32_t kSegNone = 0xffffffffu;
 constexpr uint32_t kSegFail = 0xfffffffeu;
@@ -85,14 +86,21 @@ struct Work {
   uint64_t *seg_off;     // exclusive prefix of seg_count
   DevChunk *out;
   uint64_t out_cap;
-  uint32_t *err;         // [0] error bits, [1] files resolved by k_fallback
+  uint32_t *err;         // [0] error bits, [1] files resolved by k_fallback, [2] dirty
 };
 
 // launch wrappers (mcdc_kernels.hip); all enqueue on `stream`.
 void launch_fill_random(void *dst, uint64_t pos, uint64_t n, uint64_t seed, hipStream_t stream);
-void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream);
-void launch_resolve(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
-                    hipStream_t stream);
+// scan of full tiles [tile0, tile1) (+ the partial last tile when `tail`)
+void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
+                 uint64_t tile1, bool tail);
+uint64_t scan_waves(uint64_t ntiles, int num_cus);  // waves of a scan launch over ntiles
+void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream);
+void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream);
+void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
+                             void *scan_tmp, size_t scan_tmp_bytes, hipStream_t stream);
+void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
+                            hipStream_t stream);
 size_t scan_tmp_bytes(uint32_t nsegs);
 void launch_finish(const Work &w, uint64_t *res, hipStream_t stream);
 

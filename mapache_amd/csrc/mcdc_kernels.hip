@@ -372,7 +372,8 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
 }
 
 template <int RUN>
-__global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
+__global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_t tile0, uint64_t tile1,
+                                                   int do_tail) {
   __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8];
   for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) smem[i] = W.gear16[i >> 5];
   const uint32_t lane = threadIdx.x & 63;
@@ -395,6 +396,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
   const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   const uint64_t nfull = W.n_al / RUN;
   const uint64_t ntiles_full = nfull / 64;
+  if (tile1 > ntiles_full) tile1 = ntiles_full;
   constexpr int G = RUN / 64;
   static_assert(G % 2 == 0, "even group count");
   const uint32_t qi = lane >> 2, qj = lane & 3;
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
   char *wr = q.pad + 4 * qi * kQPad + 16 * qj;
   const char *rd = q.pad + lane * kQPad;
   const uint32_t o0 = 4 * qi * RUN + 16 * qj;  // lane's byte offset in the tile for load 0, group 0
-  for (uint64_t t = wid; t < ntiles_full; t += nwaves) {
+  for (uint64_t t = tile0 + wid; t < tile1; t += nwaves) {
     const uint64_t run0 = t * 64, run = run0 + lane;
     uint64_t h = 0;
     if (run > 0) {  // warm-up: the 48 bytes before the run complete every window
@@ -460,6 +462,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
     W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
   }
   // partial last tile: lane-strided runs, exact per-lane path
+  if (!do_tail) return;
   const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
   for (uint64_t t = ntiles_full + wid; t * 64 < nruns; t += nwaves) {
     const uint64_t run = t * 64 + lane;
@@ -471,13 +474,21 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P) {
 // Product configuration: quad-coalesced scan, 16 waves (one 1024-thread
 // block) per CU; tools/scanbench.hip keeps the lane-strided k_scan_t variants
 // for comparison.
-void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream) {
-  const uint64_t ntiles = (w.nruns + 63) / 64;
+void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
+                 uint64_t tile1, bool tail) {
+  const uint64_t ntiles = tail ? (w.nruns + 63) / 64 - tile0 : tile1 - tile0;
   uint64_t blocks = (ntiles + 15) / 16;
-  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);  // 144 KiB LDS -> 1 block/CU
+  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);  // 148 KiB LDS -> 1 block/CU
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return;
-  hipLaunchKernelGGL(k_scan_q<kRun>, dim3((unsigned)blocks), dim3(1024), 0, stream, w, p);
+  hipLaunchKernelGGL(k_scan_q<kRun>, dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1,
+                     tail ? 1 : 0);
+}
+
+uint64_t scan_waves(uint64_t ntiles, int num_cus) {
+  uint64_t blocks = (ntiles + 15) / 16;
+  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);
+  return 16 * (blocks > cap ? cap : blocks);
 }
 
 // ===================================================== chain walking =====
@@ -504,8 +515,8 @@ __device__ __forceinline__ uint32_t rel_clamp(uint64_t x, uint64_t rb) {
   return x <= rb ? 0u : (x - rb >= (uint64_t)kRun ? (uint32_t)kRun : (uint32_t)(x - rb));
 }
 
-// In run-relative 32-bit coordinates: entries 0-3 always, 4-7 only when some
-// lane of the wave has more than 4 (wave-uniform branch, rare on real data).
+// In run-relative 32-bit coordinates: entries 0-3 always, 4-7 only when the
+// run has more than 4 (rare on real data).
 __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, const uint4 ea,
                                                     const uint4 eb, uint64_t lo, uint64_t hi,
                                                     uint64_t cce) {
@@ -518,20 +529,68 @@ __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, co
     if (i < cnt && off >= l && off < h && kind) best = min(best, off);
   };
   take(0, ea.x); take(1, ea.y); take(2, ea.z); take(3, ea.w);
-  if (__any(cnt > 4)) {
+  if (cnt > 4) {
     take(4, eb.x); take(5, eb.y); take(6, eb.z); take(7, eb.w);
   }
   return best == 0xffffffffu ? ~0ull : rb + best;
 }
 
+// First candidate of run r in [lo, hi) whatever the run's state: recomputed
+// from bytes when it overflowed, from the preloaded entries when cap == 8,
+// else from its entry list.
+__device__ __forceinline__ uint64_t run_first(const Work &W, const DevParams &P, const uint64_t *gt, uint64_t r,
+                                              uint32_t cnt, const uint4 ea, const uint4 eb, uint64_t lo,
+                                              uint64_t hi, uint64_t cce) {
+  if (cnt == 0) return ~0ull;
+  if (cnt > P.cap) return run_first_hit(W, P, gt, r, lo, hi, cce);
+  if (P.cap == 8) return run_first_entry(r, cnt, ea, eb, lo, hi, cce);
+  uint64_t found = ~0ull;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
+    const uint64_t pos = r * (uint64_t)kRun + (e & 0x00ffffffu);
+    if (pos >= lo && pos < hi && pos < found) {
+      const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
+      if (ok) found = pos;
+    }
+  }
+  return found;
+}
+
+// A group of GS lanes (64: the whole wave; 16: a DPP row, four chains per
+// wave) walks one chain.  All control flow below is group-uniform.
+template <int GS>
+struct Group {
+  uint32_t gl, gb;  // lane within the group, first lane of the group
+  __device__ __forceinline__ Group() {
+    const uint32_t l = lane_id();
+    gl = l & (GS - 1);
+    gb = l & ~(uint32_t)(GS - 1);
+  }
+  __device__ __forceinline__ uint64_t ballot(bool p) const {
+    const uint64_t m = __ballot(p);
+    if constexpr (GS == 64) return m;
+    else return (m >> gb) & ((1ull << GS) - 1);
+  }
+  __device__ __forceinline__ uint64_t bcast(uint64_t v, uint32_t src) const { return shfl64(v, (int)(gb + src)); }
+  __device__ __forceinline__ uint64_t up(uint64_t v, unsigned d) const {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, GS);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, GS);
+    return ((uint64_t)hi << 32) | lo;
+  }
+};
+
 // next(c): the chunk starting at arena position c (file ends at fend) ends
 // where fastcdc's cut_gear(&file[c..], min, avg, max, masks) says.  Called by
-// a full wave with wave-uniform c, fend; returns the next chunk start.
-// Latency shape: two dependent global levels per step — {restart-window bytes,
-// the first 64 runs' candidate counts}, then {entries of the non-empty runs};
-// GEAR comes from the block's LDS copy `gt`.
-__device__ uint64_t wave_next(const Work &W, const DevParams &P, const uint64_t *gt, uint64_t c, uint64_t fend) {
-  const uint32_t lane = lane_id();
+// a whole group with group-uniform c, fend; returns the next chunk start.
+// Lane gl owns restart positions [PPL*gl, PPL*gl + PPL) and, per 64-run batch,
+// runs [RPL*gl, RPL*gl + RPL).  Latency shape: two dependent global levels per
+// step — {restart-window bytes, the first 64 runs' candidate counts}, then
+// {entries of the non-empty runs}; GEAR comes from the block's LDS copy `gt`.
+template <int GS>
+__device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParams &P, const uint64_t *gt,
+                               uint64_t c, uint64_t fend) {
+  constexpr int PPL = (kWin - 1 + GS - 1) / GS;  // 1 (GS 64), 2 (32), 3 (16)
+  constexpr int RPL = 64 / GS;
   const uint64_t rem = fend - c;
   if (rem <= P.min) return fend;                  // remaining <= min_size: whole tail
   uint64_t center = P.avg, remaining = rem;
@@ -544,73 +603,70 @@ __device__ uint64_t wave_next(const Work &W, const DevParams &P, const uint64_t 
   const uint64_t lo = t + (kWin - 1), hi = c + re, cce = c + ce;
   const bool cand = lo < hi;
   const uint64_t r0 = lo / kRun, r1 = cand ? (hi - 1) / kRun : 0;
-  // ---- level-1 loads, all independent
-  const uint32_t byte = lane < wlen ? W.base[t + lane] : 0;
-  const uint64_t r = r0 + lane;
-  const bool rl = cand && r <= r1;
-  const uint32_t cnt = rl ? W.run_cnt[r] : 0;
-  // ---- level 2: entries of non-empty runs (~15 % of runs on random data)
-  uint4 ea = make_uint4(0, 0, 0, 0), eb = make_uint4(0, 0, 0, 0);
-  if (P.cap == 8 && cnt > 0 && cnt <= 8) {
-    const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
-    ea = ep[0];
-    if (cnt > 4) eb = ep[1];
-  }
-  // ---- (1) exact restarted hash for the first <= 47 tested positions
-  uint64_t h = lane < wlen ? gt[byte] : 0;
+  uint32_t cn[RPL];
+  uint4 ea[RPL], eb[RPL];
+  auto load_batch = [&](uint64_t rb) {
 #pragma unroll
-  for (unsigned d = 1; d < 64; d <<= 1) {
-    const uint64_t v = shfl_up64(h, d);
-    if (lane >= d) h += v << d;
+    for (int k = 0; k < RPL; ++k) {
+      const uint64_t r = rb + RPL * G.gl + k;
+      cn[k] = (cand && r <= r1) ? W.run_cnt[r] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {  // level 2: entries of non-empty runs (~15 % on random data)
+      ea[k] = make_uint4(0, 0, 0, 0);
+      eb[k] = make_uint4(0, 0, 0, 0);
+      if (P.cap == 8 && cn[k] > 0 && cn[k] <= 8) {
+        const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + (rb + RPL * G.gl + k) * 8ull);
+        ea[k] = ep[0];
+        if (cn[k] > 4) eb[k] = ep[1];
+      }
+    }
+  };
+  // ---- level-1 loads, all independent
+  uint32_t by[PPL];
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const uint32_t idx = PPL * G.gl + k;
+    by[k] = idx < wlen ? W.base[t + idx] : 0;
   }
-  bool pass = false;
-  if (lane < wlen) pass = (h & ((t0 + lane < ce) ? P.ms : P.ml)) == 0;
-  const uint64_t b = __ballot(pass);
-  if (b) return t + (uint64_t)(__ffsll((unsigned long long)b) - 1);
+  load_batch(r0);
+  // ---- (1) exact restarted hash for the first <= 47 tested positions
+  uint64_t loc[PPL], acc = 0;
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const uint32_t idx = PPL * G.gl + k;
+    acc = (acc << 1) + (idx < wlen ? gt[by[k]] : 0);
+    loc[k] = acc;
+  }
+  uint64_t x = acc;  // hash at this lane's last position: shift-scan over the group
+#pragma unroll
+  for (unsigned d = 1; d < (unsigned)GS; d <<= 1) {
+    const uint64_t v = G.up(x, d);
+    if (G.gl >= d) x += v << (PPL * d);
+  }
+  uint64_t excl = G.up(x, 1);  // hash at the previous lane's last position
+  if (G.gl == 0) excl = 0;
+  uint32_t first = 0xffffffffu;
+#pragma unroll
+  for (int k = PPL - 1; k >= 0; --k) {
+    const uint32_t idx = PPL * G.gl + k;
+    const uint64_t h = (excl << (k + 1)) + loc[k];
+    if (idx < wlen && (h & ((t0 + idx < ce) ? P.ms : P.ml)) == 0) first = idx;
+  }
+  const uint64_t b = G.ballot(first != 0xffffffffu);
+  if (b) return t + G.bcast(first, (uint32_t)(__ffsll((unsigned long long)b) - 1));
   if (!cand) return c + remaining;
-  // ---- (2) windowed candidates for [t + 47, c + re), first 64 runs
-  {
+  // ---- (2) windowed candidates for [t + 47, c + re), 64 runs per batch
+  for (uint64_t rb = r0; rb <= r1; rb += 64) {
+    if (rb != r0) load_batch(rb);
     uint64_t found = ~0ull;
-    if (rl) {
-      if (cnt > P.cap) {
-        found = run_first_hit(W, P, gt, r, lo, hi, cce);
-      } else if (P.cap == 8) {
-        found = run_first_entry(r, cnt, ea, eb, lo, hi, cce);
-      } else {
-        for (uint32_t i = 0; i < cnt; ++i) {
-          const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
-          const uint64_t pos = r * (uint64_t)kRun + (e & 0x00ffffffu);
-          if (pos >= lo && pos < hi && pos < found) {
-            const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
-            if (ok) found = pos;
-          }
-        }
-      }
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const uint64_t r = rb + RPL * G.gl + k;
+      if (found == ~0ull && r <= r1) found = run_first(W, P, gt, r, cn[k], ea[k], eb[k], lo, hi, cce);
     }
-    const uint64_t fb = __ballot(found != ~0ull);
-    if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
-  }
-  // ---- later batches (only when max spans more than 64 runs)
-  for (uint64_t rb = r0 + 64; rb <= r1; rb += 64) {
-    const uint64_t rr = rb + lane;
-    uint64_t found = ~0ull;
-    if (rr <= r1) {
-      const uint32_t cn = W.run_cnt[rr];
-      if (cn > P.cap) {
-        found = run_first_hit(W, P, gt, rr, lo, hi, cce);
-      } else {
-        for (uint32_t i = 0; i < cn; ++i) {
-          const uint32_t e = W.run_ent[rr * (uint64_t)P.cap + i];
-          const uint64_t pos = rr * (uint64_t)kRun + (e & 0x00ffffffu);
-          if (pos >= lo && pos < hi && pos < found) {
-            const bool ok = pos < cce ? (e >> 31) & 1 : (e >> 30) & 1;
-            if (ok) found = pos;
-          }
-        }
-      }
-    }
-    const uint64_t fb = __ballot(found != ~0ull);
-    if (fb) return shfl64(found, __ffsll((unsigned long long)fb) - 1);
+    const uint64_t fb = G.ballot(found != ~0ull);
+    if (fb) return G.bcast(found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
   }
   return c + remaining;  // forced cut (e.g. all zeros)
 }
@@ -621,57 +677,62 @@ __device__ __forceinline__ void load_gear_lds(uint64_t *gt, const Work &W) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_spec(Work W, DevParams P) {
+// One group per segment.
+template <int GS>
+__global__ __launch_bounds__(256) void k_spec(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
-  const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (s >= W.nsegs) return;
-  const uint32_t lane = lane_id();
+  const Group<GS> G;
+  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+  if (s >= s1) return;
   const Seg S = W.segs[s];
   const uint64_t fend = W.files[S.file].end;
   uint64_t *out = W.nodes + W.node_off[s];
   const uint64_t cap = W.node_off[s + 1] - W.node_off[s];
   uint64_t c = S.start, k = 0, exitp = fend;
   for (;;) {
-    if (k >= cap) { if (lane == 0) atomicOr(W.err, kErrNodeCap); break; }
-    if (lane == 0) out[k] = c;
+    if (k >= cap) { if (G.gl == 0) atomicOr(W.err, kErrNodeCap); break; }
+    if (G.gl == 0) out[k] = c;
     ++k;
-    const uint64_t nc = wave_next(W, P, gt, c, fend);
+    const uint64_t nc = group_next<GS>(G, W, P, gt, c, fend);
     if (nc >= S.end) { exitp = nc; break; }
     c = nc;
   }
-  if (lane == 0) {
+  if (G.gl == 0) {
     W.node_cnt[s] = (uint32_t)k;
     W.seg_exit[s] = exitp;
   }
 }
 
-// index of c in nodes(j) (sorted), or -1; wave-cooperative
-__device__ int find_node(const Work &W, uint32_t j, uint64_t c) {
-  const uint32_t lane = lane_id();
+// index of c in nodes(j) (sorted), or -1; group-cooperative
+template <int GS>
+__device__ int find_node(const Group<GS> &G, const Work &W, uint32_t j, uint64_t c) {
   const uint64_t *nd = W.nodes + W.node_off[j];
   const uint32_t n = W.node_cnt[j];
-  for (uint32_t b = 0; b < n; b += 64) {
-    const uint32_t i = b + lane;
+  for (uint32_t b = 0; b < n; b += GS) {
+    const uint32_t i = b + G.gl;
     const uint64_t v = i < n ? nd[i] : ~0ull;
-    const uint64_t eq = __ballot(v == c);
+    const uint64_t eq = G.ballot(v == c);
     if (eq) return (int)(b + __ffsll((unsigned long long)eq) - 1);
-    if (__ballot(v > c)) return -1;
+    if (G.ballot(v > c)) return -1;
   }
   return -1;
 }
 
 // ============================================================ link =======
-__global__ __launch_bounds__(256) void k_link(Work W, DevParams P) {
+template <int GS>
+__global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
-  const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (s >= W.nsegs) return;
-  const uint32_t lane = lane_id();
+  const Group<GS> G;
+  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+  if (s >= s1) return;
   const Seg S = W.segs[s];
   const File F = W.files[S.file];
   if (S.flags & kSegLast) {
-    if (lane == 0) {
+    if (G.gl == 0) {
       W.link_seg[s] = kSegNone; W.link_idx[s] = 0; W.link_pos[s] = F.end; W.cont_cnt[s] = 0;
     }
     return;
@@ -682,14 +743,14 @@ __global__ __launch_bounds__(256) void k_link(Work W, DevParams P) {
   for (;;) {
     if (c >= F.end) { ls = kSegNone; lp = F.end; break; }
     const uint32_t j = F.first_seg + (uint32_t)((c - F.start) / W.zseg);
-    const int idx = find_node(W, j, c);
+    const int idx = find_node<GS>(G, W, j, c);
     if (idx >= 0) { ls = j; li = (uint32_t)idx; lp = c; break; }
     if (steps == (uint32_t)kContMax) break;  // give up: serial fallback
-    if (lane == 0) W.cont[(uint64_t)s * kContMax + steps] = c;
+    if (G.gl == 0) W.cont[(uint64_t)s * kContMax + steps] = c;
     ++steps;
-    c = wave_next(W, P, gt, c, F.end);
+    c = group_next<GS>(G, W, P, gt, c, F.end);
   }
-  if (lane == 0) {
+  if (G.gl == 0) {
     W.link_seg[s] = ls; W.link_idx[s] = li; W.link_pos[s] = lp; W.cont_cnt[s] = steps;
     if (ls == kSegFail) atomicOr(&W.file_flags[S.file], kFileFail);
     else if (ls != s + 1) atomicOr(&W.file_flags[S.file], kFileSkip);
@@ -722,7 +783,7 @@ __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
     if (k >= cap) { if (lane == 0) atomicOr(W.err, kErrNodeCap); break; }
     if (lane == 0) W.nodes[W.node_off[j] + k] = c;
     ++k;
-    c = wave_next(W, P, gt, c, F.end);
+    c = group_next<64>(Group<64>(), W, P, gt, c, F.end);
     if (c >= F.end) break;
   }
   const uint32_t last = F.first_seg + F.nsegs - 1;
@@ -817,33 +878,43 @@ __device__ __forceinline__ ChunkQ chunk_q(const DevParams &P, uint64_t c, uint64
   return r;
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+// ChunkData.hash of one chunk, computed by one lane: the <= 64 bytes [from, q]
+// arrive as five aligned 16-byte loads (blocks past q are not read, so no
+// load leaves the arena), and the state is summed from 80 independent LDS
+// lookups (no dependency chain through the hash).
+__device__ __forceinline__ uint64_t chunk_hash(const Work &W, const uint64_t *gt, const ChunkQ &cq) {
+  if (cq.q < cq.from) return 0;
+  const uint64_t A = cq.from & ~15ull;
+  uint4 blk[5];
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d);
-    v += ((uint64_t)hi << 32) | lo;
+  for (int k = 0; k < 5; ++k)
+    blk[k] = A + 16 * k <= cq.q ? *reinterpret_cast<const uint4 *>(W.base + A + 16 * k) : make_uint4(0, 0, 0, 0);
+  const uint32_t lo = (uint32_t)(cq.from - A), hi = (uint32_t)(cq.q - A);  // window [lo, hi] in blk bytes
+  uint64_t h = 0;
+#pragma unroll
+  for (int i = 0; i < 80; ++i) {
+    const uint4 b = blk[i / 16];
+    const uint32_t w = (i % 16) < 4 ? b.x : (i % 16) < 8 ? b.y : (i % 16) < 12 ? b.z : b.w;
+    const uint32_t x = (w >> (8 * (i % 4))) & 0xffu;
+    const uint64_t g = gt[x] << ((hi - (uint32_t)i) & 63u);
+    h += ((uint32_t)i >= lo && (uint32_t)i <= hi) ? g : 0;
   }
-  return v;
+  return cq.dbl ? h << 1 : h;
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// One wave per segment: lane i owns chunk i (of each batch of 64); the
-// chunk hashes are computed 8 at a time by the whole wave (byte loads of all 8
-// windows issued together, GEAR from LDS, one wave sum each).
-__global__ __launch_bounds__(256) void k_emit(Work W, DevParams P) {
+// One group of GS lanes per segment, lane i owns chunk i (of each batch of
+// GS) and computes its hash itself.  Resolution kernels raise their wave priority:
+// they run beside the scan's later parts and are latency-bound.
+template <int GS>
+__global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
-  const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (s >= W.nsegs) return;
+  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+  if (s >= s1) return;
   const uint64_t n = W.seg_count[s];
   if (n == 0) return;
-  const uint32_t lane = lane_id();
+  const uint32_t lane = lane_id() & (GS - 1);
   const Seg S = W.segs[s];
   const File F = W.files[S.file];
   const uint32_t e = W.entry_idx[s];
@@ -852,45 +923,23 @@ __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P) {
   const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
   const uint64_t after = W.link_pos[s];
   const uint64_t base_out = W.seg_off[s];
-  for (uint64_t i0 = 0; i0 < n; i0 += 64) {
+  for (uint64_t i0 = 0; i0 < n; i0 += GS) {
     const uint64_t i = i0 + lane;
-    const bool act = i < n;
-    uint64_t pos = 0, nxt = 0;
-    if (act) {
-      pos = i < nn ? nd[i] : ct[i - nn];
-      const uint64_t j = i + 1;
-      nxt = j < n ? (j < nn ? nd[j] : ct[j - nn]) : after;
-    }
-    const ChunkQ cq = act ? chunk_q(P, pos, nxt - pos, F.end) : ChunkQ{0, 1, false};
-    uint64_t mine = 0;
-    const uint32_t m = (uint32_t)(n - i0 < 64 ? n - i0 : 64);
-    for (uint32_t b = 0; b < m; b += 8) {  // wave-uniform
-      uint32_t by[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t src = b + k < m ? b + k : m - 1;
-        const uint64_t q = readlane64(cq.q, src), fr = readlane64(cq.from, src);
-        const bool in = b + k < m && q >= fr + lane;  // position q - lane in [from, q]
-        by[k] = in ? (uint32_t)W.base[q - lane] : 256u;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint64_t v = by[k] < 256u ? gt[by[k]] << lane : 0;
-        const uint64_t hsum = wave_sum64(v);
-        if (lane == b + k) mine = hsum;
-      }
-    }
-    if (act) {
-      const uint64_t o = base_out + i;
-      if (o < W.out_cap) {
-        DevChunk ch;
-        ch.offset = pos - F.start;
-        ch.length = nxt - pos;
-        ch.hash = cq.dbl ? mine << 1 : mine;
-        W.out[o] = ch;
-      } else {
-        atomicOr(W.err, kErrOutCap);
-      }
+    if (i >= n) break;
+    const uint64_t pos = i < nn ? nd[i] : ct[i - nn];
+    const uint64_t j = i + 1;
+    const uint64_t nxt = j < n ? (j < nn ? nd[j] : ct[j - nn]) : after;
+    const ChunkQ cq = chunk_q(P, pos, nxt - pos, F.end);
+    const uint64_t hash = chunk_hash(W, gt, cq);
+    const uint64_t o = base_out + i;
+    if (o < W.out_cap) {
+      DevChunk ch;
+      ch.offset = pos - F.start;
+      ch.length = nxt - pos;
+      ch.hash = hash;
+      W.out[o] = ch;
+    } else {
+      atomicOr(W.err, kErrOutCap);
     }
   }
 }
@@ -902,6 +951,7 @@ __global__ void k_finish(Work W, uint64_t *res) {
     res[0] = W.nsegs ? W.seg_off[W.nsegs] : 0;
     res[1] = W.err[0];
     res[2] = W.err[1];
+    res[3] = W.err[2];
   }
 }
 
@@ -909,27 +959,143 @@ void launch_finish(const Work &w, uint64_t *res, hipStream_t stream) {
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, stream, w, res);
 }
 
-size_t scan_tmp_bytes(uint32_t nsegs) {
-  size_t bytes = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                   (int)nsegs + 1);
-  return bytes;
+// ============================================= incremental resolution ====
+// The resolution of a prefix of segments runs while the scan of the rest of
+// the arena is still in flight (mcdc_api.hip: staged pipeline).  In the
+// common case every segment's continuation merged into the next segment
+// (link_seg[s] == s + 1), so the true chain enters segment s at link_idx[s-1]
+// and the per-segment counts / offsets / boundaries follow locally.  A segment
+// whose continuation did anything else sets err[2] ("dirty"); the host then
+// re-resolves the whole call with the general path (fallback, serial walk).
+__global__ void k_incr_count(Work W, uint32_t s0, uint32_t s1) {
+  const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= s1) return;
+  const uint32_t fl = W.segs[s].flags;
+  const uint32_t entry = (fl & kSegFirst) ? 0u : W.link_idx[s - 1];
+  const uint32_t nc = W.node_cnt[s];
+  const bool bad = (!(fl & kSegLast) && W.link_seg[s] != s + 1) || entry > nc;
+  W.seg_true[s] = 1;
+  W.entry_idx[s] = entry;
+  W.seg_count[s] = bad ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
+  if (bad) atomicOr(W.err + 2, 1u);
 }
 
-void launch_resolve(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes_,
-                    hipStream_t stream) {
+// Same, fused with the offsets for one block: counts of [s0, s1) and
+// seg_off[s + 1] = seg_off[s0] + inclusive prefix, 1024 threads x 8 segments
+// per pass (one launch instead of count + device scan + add-base).
+__device__ __forceinline__ uint64_t incr_count_one(const Work &W, uint32_t s, uint32_t &dirty) {
+  const uint32_t fl = W.segs[s].flags;
+  const uint32_t entry = (fl & kSegFirst) ? 0u : W.link_idx[s - 1];
+  const uint32_t nc = W.node_cnt[s];
+  const bool bad = (!(fl & kSegLast) && W.link_seg[s] != s + 1) || entry > nc;
+  const uint64_t c = bad ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
+  W.seg_true[s] = 1;
+  W.entry_idx[s] = entry;
+  W.seg_count[s] = c;
+  dirty |= bad ? 1u : 0u;
+  return c;
+}
+
+__global__ __launch_bounds__(1024) void k_incr_scan(Work W, uint32_t s0, uint32_t s1) {
+  __builtin_amdgcn_s_setprio(3);
+  constexpr int IT = 8;
+  __shared__ uint64_t wsum[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t carry = W.seg_off[s0];
+  uint32_t dirty = 0;
+  for (uint64_t base = s0; base < s1; base += 1024 * IT) {
+    uint64_t c[IT], tsum = 0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const uint64_t s = base + (uint64_t)tid * IT + k;
+      c[k] = s < s1 ? incr_count_one(W, (uint32_t)s, dirty) : 0;
+      tsum += c[k];
+    }
+    uint64_t x = tsum;  // inclusive wave scan
+#pragma unroll
+    for (unsigned d = 1; d < 64; d <<= 1) {
+      const uint64_t v = shfl_up64(x, d);
+      if (lane >= d) x += v;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t wpre = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t v = wsum[k];
+      wpre += (uint32_t)k < wv ? v : 0;
+      total += v;
+    }
+    uint64_t run = carry + wpre + x - tsum;  // exclusive prefix of this thread's first segment
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const uint64_t s = base + (uint64_t)tid * IT + k;
+      run += c[k];
+      if (s < s1) W.seg_off[s + 1] = run;
+    }
+    carry += total;
+    __syncthreads();
+  }
+  if (dirty) atomicOr(W.err + 2, 1u);
+}
+
+// seg_off[s + 1] = seg_off[s0] + inclusive prefix of seg_count over [s0, s].
+__global__ void k_add_base(Work W, const uint64_t *incl, uint32_t s0, uint32_t s1) {
+  const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= s1) return;
+  W.seg_off[s + 1] = W.seg_off[s0] + incl[s - s0];
+}
+
+size_t scan_tmp_bytes(uint32_t nsegs) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nsegs + 1);
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nsegs + 1);
+  return a > b ? a : b;
+}
+
+static unsigned group_blocks(uint32_t n) { return (n + 256 / kGroup - 1) / (256 / kGroup); }
+
+void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream) {
+  if (s1 > s0)
+    hipLaunchKernelGGL(k_spec<kGroup>, dim3(group_blocks(s1 - s0)), dim3(256), 0, stream, w, p, s0, s1);
+}
+
+void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream) {
+  if (s1 > s0)
+    hipLaunchKernelGGL(k_link<kGroup>, dim3(group_blocks(s1 - s0)), dim3(256), 0, stream, w, p, s0, s1);
+}
+
+// counts, offsets and boundaries of segments [s0, s1) assuming the clean case
+void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
+                             void *scan_tmp, size_t scan_tmp_bytes_, hipStream_t stream) {
+  if (s1 <= s0) return;
+  const uint32_t n = s1 - s0;
+  if (n <= 8192) {  // one block, one pass: a single launch for small batches
+    hipLaunchKernelGGL(k_incr_scan, dim3(1), dim3(1024), 0, stream, w, s0, s1);
+  } else {
+    hipLaunchKernelGGL(k_incr_count, dim3((n + 255) / 256), dim3(256), 0, stream, w, s0, s1);
+    size_t bytes = scan_tmp_bytes_;
+    (void)hipcub::DeviceScan::InclusiveSum(scan_tmp, bytes, w.seg_count + s0, incl, (int)n, stream);
+    hipLaunchKernelGGL(k_add_base, dim3((n + 255) / 256), dim3(256), 0, stream, w, (const uint64_t *)incl, s0,
+                       s1);
+  }
+  hipLaunchKernelGGL(k_emit<kGroup>, dim3(group_blocks(n)), dim3(256), 0, stream, w, p, s0, s1);
+}
+
+// General resolution after k_spec / k_link of every segment: serial fallback
+// for files whose chains never merged, chain walk (parallel or serial),
+// counts, offsets, boundaries.
+void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes_,
+                            hipStream_t stream) {
   if (w.nsegs == 0) return;
-  const unsigned wave_blocks = (w.nsegs + 3) / 4;
-  hipLaunchKernelGGL(k_spec, dim3(wave_blocks), dim3(256), 0, stream, w, p);
-  hipLaunchKernelGGL(k_link, dim3(wave_blocks), dim3(256), 0, stream, w, p);
   hipLaunchKernelGGL(k_fallback, dim3(w.nfiles), dim3(64), 0, stream, w, p);
   hipLaunchKernelGGL(k_walk_fast, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
   hipLaunchKernelGGL(k_walk_seq, dim3(w.nfiles), dim3(64), 0, stream, w);
   hipLaunchKernelGGL(k_count, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
   size_t bytes = scan_tmp_bytes_;
   // seg_count has nsegs + 1 entries (last = 0) so seg_off[nsegs] = total
-  hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, w.seg_count, w.seg_off, (int)w.nsegs + 1, stream);
-  hipLaunchKernelGGL(k_emit, dim3(wave_blocks), dim3(256), 0, stream, w, p);
+  (void)hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, w.seg_count, w.seg_off, (int)w.nsegs + 1, stream);
+  hipLaunchKernelGGL(k_emit<kGroup>, dim3(group_blocks(w.nsegs)), dim3(256), 0, stream, w, p, 0u, w.nsegs);
 }
 
 }  // namespace mcdc

@@ -267,3 +267,45 @@ def test_plan_reuse_across_layouts(ctx):
             _same(ctx.chunk_device(_lib.params(*PARAMS[pi]), dp, ln), O.chunk(O.Params(*PARAMS[pi]), h[:ln]))
     finally:
         ctx.device_free(dp)
+
+
+@pytest.fixture
+def staged(monkeypatch):
+    """Force the staged pipeline (scan in 4 parts, resolution of the scanned
+    prefix overlapping the next part) on small inputs: a round = 16 tiles
+    (4 MiB), parts of 1, 3 and 9 rounds at the end."""
+    monkeypatch.setenv("MCDC_PARTS", "4")
+    monkeypatch.setenv("MCDC_TAIL_ROUNDS", "1")
+    monkeypatch.setenv("MCDC_PART_TILES", "16")
+    monkeypatch.setenv("MCDC_MIN_ROUNDS", "0")
+    yield
+
+
+@pytest.mark.parametrize("p", PARAMS, ids=lambda p: "/".join(map(str, p)))
+def test_staged_pipeline_random(ctx, staged, p):
+    n = (200 << 20) + 12345
+    d = O.random_bytes(n, SEED + 7)
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    assert ctx.timing()["scan_launches"] == 4
+
+
+def test_staged_pipeline_dirty_paths(ctx, staged):
+    """Skipped segments and never-merging chains inside a staged call: the
+    incremental pass flags them and the general resolution redoes the call."""
+    p = PARAMS[0]
+    d = np.concatenate([O.random_bytes(100_003, 9), np.zeros(48 << 20, np.uint8), O.random_bytes(90 << 20, 10)])
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    assert ctx.timing()["fallback_files"] == 1
+    for zlen in [1_310_720 - 5000, 1_310_720 + 70_000, 2 * 1_310_720 + 1]:
+        d = np.concatenate([O.random_bytes(150 << 20, 11), np.zeros(zlen, np.uint8), O.random_bytes(60 << 20, 12)])
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+
+
+def test_staged_pipeline_batch(ctx, staged):
+    rng = np.random.default_rng(8)
+    sizes = [int(x) for x in rng.integers(0, 3 << 20, 150)] + [0, 1, 16384, 40 << 20]
+    files = [O.random_bytes(s, 500 + i) for i, s in enumerate(sizes)]
+    out, counts = ctx.chunk_batch(_lib.params(*PARAMS[0]), files)
+    ref, rc = O.chunk_files(O.Params(*PARAMS[0]), files)
+    _same(out, ref)
+    assert (counts == rc).all()
