@@ -23,6 +23,9 @@ Prints ONE JSON line (rank 0).  Extra objects:
   e2e_host      - pinned host input -> H2D -> kernels -> boundaries to host
   batch_files   - BASELINE configs[2]: 10 000 independent 8 MiB files, one call
   small_files   - BASELINE configs[3] stand-in: synthetic kernel-tree-like mix
+  chunk_ids     - SURVEY.md §8(f) next stage: BLAKE3 chunk IDs of the same 64 GiB
+                  boundary list in HBM (ID::from_content, processor.rs:184), and
+                  the chunk + ID pipeline
 """
 from __future__ import annotations
 
@@ -203,6 +206,48 @@ def small_files(ctx, p, nfiles: int, steps: int) -> dict:
         ctx.device_free(arena)
 
 
+def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_sample_gib: float,
+              no_cpu: bool) -> dict:
+    """BLAKE3 of every chunk of the headline boundary list (device in, device out),
+    timed per step; then chunk + IDs back to back.  Parity probe: the IDs of the
+    chunks inside the first GiB against the oracle."""
+    d_ids = ctx.device_alloc(32 * count)
+    try:
+        dt, _ = _timed(lambda: ctx.chunk_ids(dp, n, (d_out, count), ids=d_ids), steps, 1)
+        ids_ms = ctx.timing()["ids_ms"]
+        cap = n // (p.min_size - 1) + 2
+
+        def both():
+            k = ctx.chunk_device_to_device(p, dp, n, d_out, cap)
+            ctx.chunk_ids(dp, n, (d_out, k), ids=d_ids)
+        dt2, _ = _timed(both, steps, 1)
+        from oracle import oracle as O
+        probe_bytes = 1 << 30
+        chunks = ctx.d2h_chunks(d_out, count)
+        sel = chunks[chunks["offset"] + chunks["length"] <= probe_bytes]
+        host = O.random_bytes(probe_bytes, SEED)
+        got = ctx.d2h_bytes(d_ids, 32 * len(sel)).reshape(len(sel), 32)
+        ok = bool(len(sel) > 0 and (got == O.chunk_ids(host, sel, threads=16)).all())
+        r = {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2), "device_ms": round(ids_ms, 3),
+             "bound": "valu (32-bit add/xor/rotate of the BLAKE3 compression, ~11 ops per byte)",
+             "chunk_plus_ids_ms": round(dt2 * 1e3, 3), "chunk_plus_ids_gib_s": round(n / dt2 / GIB, 2),
+             "parity_probe_chunks": int(len(sel)), "parity_probe_ok": ok}
+        if not no_cpu:
+            m = int(cpu_sample_gib * GIB)
+            sample = chunks[chunks["offset"] + chunks["length"] <= m]
+            hs = host if m == probe_bytes else O.random_bytes(m, SEED)
+            t0 = time.perf_counter()
+            O.chunk_ids(hs, sample, threads=1)
+            cdt = time.perf_counter() - t0
+            r["cpu_baseline"] = {"value": round(int(sample["length"].sum()) / cdt / GIB, 3), "unit": "GiB/s",
+                                 "cores": 1, "kind": "port",
+                                 "sample": f"chunks of the first {cpu_sample_gib:g} GiB, oracle/blake3_oracle.c "
+                                           f"(portable scalar C, no SIMD), 1 thread"}
+        return r
+    finally:
+        ctx.device_free(d_ids)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,6 +259,7 @@ def main() -> int:
     ap.add_argument("--batch-files", type=int, default=10000, help="configs[2] file count (0: skip)")
     ap.add_argument("--small-files", type=int, default=80000, help="configs[3] file count (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ids", action="store_true", help="skip the chunk-ID (BLAKE3) stage")
     a = ap.parse_args()
 
     world, rank, local = _dist()
@@ -293,6 +339,11 @@ def main() -> int:
         result["host_out"] = {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
                               "identical_to_device_out": _same(hc, chunks),
                               "output": "pinned host array (hipHostMalloc), written by k_emit over PCIe"}
+        if not a.no_ids:
+            try:
+                result["chunk_ids"] = chunk_ids(ctx, p, dp, n, d_out, int(count), 3, 1.0, a.no_cpu)
+            except Exception as e:  # reported, never silently dropped
+                result["chunk_ids"] = {"error": f"{type(e).__name__}: {e}"}
     ctx.device_free(d_out)
     ctx.device_free(dp)
     if extras:

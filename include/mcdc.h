@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MCDC_ABI_VERSION 1
+#define MCDC_ABI_VERSION 2
 
 /* status codes */
 #define MCDC_OK 0
@@ -88,6 +88,7 @@ typedef struct {
   uint64_t chunks;     /* chunks produced                                */
   uint64_t scan_launches; /* number of scan kernel launches             */
   uint64_t fallback_files; /* files resolved by the serial fallback     */
+  double ids_ms;       /* chunk-ID (BLAKE3) kernels of mcdc_chunk_ids_device */
 } mcdc_timing;
 
 /* ------------------------------------------------------------------ API -- */
@@ -139,6 +140,19 @@ int mcdc_chunk_batch_device(struct mcdc_ctx *ctx, const mcdc_params *params,
                             const void *d_arena, const uint64_t *offsets, const uint64_t *lens,
                             size_t nbufs, mcdc_chunk *out, size_t cap, size_t *counts,
                             size_t *n_out);
+
+/* Chunk IDs of a boundary list: ids[32*i .. 32*i+32) = BLAKE3 (unkeyed,
+ * 32-byte output) of the chunk's bytes.  Replaces the per-chunk
+ * ID::from_content(&chunk.data) of chunk_and_save_blobs
+ * (/root/reference/src/archiver/processor.rs:184 -> src/global/mod.rs:86-88
+ * -> src/utils/mod.rs:62-68, crate blake3 1.8.2).  d_data: the device buffer
+ * the chunks index (n bytes, any alignment); chunks: nchunks records as
+ * produced by mcdc_chunk_device (offset/length relative to d_data; the hash
+ * field is ignored), either a device pointer on the context's device (the
+ * boundary list stays in HBM) or host memory; ids: 32 * nchunks bytes,
+ * device pointer or host memory.  A chunk outside [0, n) -> MCDC_E_INVALID. */
+int mcdc_chunk_ids_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
+                          size_t nchunks, uint8_t *ids);
 
 /* Timing of the last call on ctx. */
 int mcdc_ctx_timing(const struct mcdc_ctx *ctx, mcdc_timing *out);

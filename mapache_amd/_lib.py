@@ -30,7 +30,7 @@ EXPORTS = (
     "mcdc_chunk_host", "mcdc_chunk_batch", "mcdc_chunk_batch_device", "mcdc_ctx_timing",
     "mcdc_last_error", "mcdc_device_alloc", "mcdc_device_free", "mcdc_host_alloc",
     "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_memcpy_d2h", "mcdc_fill_random_device", "mcdc_digest",
-    "mcdc_abi_version",
+    "mcdc_abi_version", "mcdc_chunk_ids_device",
 )
 
 
@@ -48,7 +48,8 @@ class McdcTiming(ctypes.Structure):
                 ("device_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
                 ("d2h_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
-                ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64)]
+                ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64),
+                ("ids_ms", ctypes.c_double)]
 
 
 CHUNK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("hash", "<u8")])
@@ -93,6 +94,7 @@ def load():
     L.mcdc_digest.argtypes = [vp, sz]
     L.mcdc_digest.restype = u64
     L.mcdc_abi_version.argtypes = []
+    L.mcdc_chunk_ids_device.argtypes = [vp, vp, sz, vp, sz, vp]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -229,6 +231,32 @@ class Context:
                                              offs.ctypes.data, ls.ctypes.data, n, ctypes.c_void_p(d_out), cap,
                                              counts.ctypes.data, ctypes.byref(n_out)))
         return n_out.value, counts[:n].astype(np.int64)
+
+    def chunk_ids(self, d_data: int, n: int, chunks, ids=None) -> np.ndarray:
+        """BLAKE3 chunk IDs (ID::from_content) of a boundary list over the device
+        buffer d_data[0, n).  `chunks`: a CHUNK_DTYPE array (host) or an int
+        device pointer with `count` given as (ptr, count).  Returns (count, 32) uint8
+        unless `ids` (an int device pointer) is given, then returns None."""
+        if isinstance(chunks, tuple):
+            cptr, count = chunks
+        else:
+            arr = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+            cptr, count = arr.ctypes.data, arr.size
+            keep = arr  # noqa: F841  (alive across the call)
+        if ids is not None:
+            check(load().mcdc_chunk_ids_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(cptr), count,
+                                               ctypes.c_void_p(ids)))
+            return None
+        out = np.zeros((max(count, 1), 32), dtype=np.uint8)
+        check(load().mcdc_chunk_ids_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(cptr), count,
+                                           out.ctypes.data))
+        return out[:count]
+
+    def d2h_bytes(self, d_src: int, nbytes: int) -> np.ndarray:
+        out = np.empty(max(nbytes, 1), dtype=np.uint8)
+        if nbytes:
+            check(load().mcdc_memcpy_d2h(self._h, out.ctypes.data, ctypes.c_void_p(d_src), nbytes))
+        return out[:nbytes]
 
     def d2h_chunks(self, d_out: int, count: int) -> np.ndarray:
         out = np.empty(max(count, 1), dtype=CHUNK_DTYPE)

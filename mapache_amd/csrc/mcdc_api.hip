@@ -19,6 +19,7 @@
 
 #include "../../include/mcdc.h"
 #include "gear_table.h"
+#include "mcdc_blake3.h"
 #include "mcdc_internal.h"
 
 using namespace mcdc;
@@ -129,7 +130,7 @@ struct mcdc_ctx {
   // workspace
   DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl;
+      scan_tmp, seg_incl, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
   // pinned host staging
   void *h_stage = nullptr;
   size_t h_stage_cap = 0;
@@ -584,7 +585,8 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
-                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl};
+                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->b3_chunks, &ctx->b3_gcnt,
+                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -785,6 +787,66 @@ int mcdc_memcpy_h2d(mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes)
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return MCDC_OK;
+}
+
+int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks, size_t nchunks,
+                          uint8_t *ids) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if ((!d_data && n) || (nchunks && (!chunks || !ids))) return fail(MCDC_E_INVALID, "NULL argument");
+  const double t0 = now_ms();
+  hipStream_t st = ctx->stream;
+  ctx->timing = mcdc_timing{};
+  if (nchunks == 0) {
+    ctx->timing.total_ms = now_ms() - t0;
+    return MCDC_OK;
+  }
+  const DevChunk *dch = nullptr;
+  if (is_device_ptr(chunks)) {
+    if (!direct_out(ctx, (void *)chunks)) return fail(MCDC_E_INVALID, "chunks is a device pointer of another device");
+    dch = (const DevChunk *)chunks;
+  } else {
+    if ((rc = ensure(ctx, ctx->b3_chunks, nchunks * sizeof(DevChunk)))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->b3_chunks.p, chunks, nchunks * sizeof(DevChunk), hipMemcpyHostToDevice, st));
+    dch = (const DevChunk *)ctx->b3_chunks.p;
+  }
+  uint8_t *ids_dev = (uint8_t *)direct_out(ctx, ids);
+  if (!ids_dev && is_device_ptr(ids)) return fail(MCDC_E_INVALID, "ids is a device pointer of another device");
+  const uint64_t bound = b3_group_bound(n, nchunks);
+  const size_t tmpb = b3_tmp_bytes(nchunks);
+  if ((rc = ensure(ctx, ctx->b3_gcnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->b3_goff, (nchunks + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->b3_owner, bound * 4)) || (rc = ensure(ctx, ctx->b3_nodes, bound * 32)) ||
+      (rc = ensure(ctx, ctx->b3_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 16)))
+    return rc;
+  if (!ids_dev) {
+    if ((rc = ensure(ctx, ctx->b3_ids, nchunks * 32))) return rc;
+    ids_dev = (uint8_t *)ctx->b3_ids.p;
+  }
+  uint32_t *err = (uint32_t *)ctx->err.p + 3;
+  HIP_TRY(hipMemsetAsync(err, 0, 4, st));
+  HIP_TRY(hipEventRecord(ctx->ev_start, st));
+  launch_b3_prepare(dch, nchunks, n, (uint64_t *)ctx->b3_gcnt.p, (uint64_t *)ctx->b3_goff.p, err, ctx->b3_tmp.p, tmpb,
+                    st);
+  launch_b3_hash((const uint8_t *)d_data, dch, nchunks, (const uint64_t *)ctx->b3_goff.p, bound,
+                 (uint32_t *)ctx->b3_owner.p, (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev_end, st));
+  uint32_t herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (herr) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer", n);
+  if (ids_dev == ctx->b3_ids.p) {
+    HIP_TRY(hipMemcpyAsync(ids, ids_dev, nchunks * 32, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_end));
+  ctx->timing.ids_ms = ms;
+  ctx->timing.device_ms = ms;
+  ctx->timing.bytes = n;
+  ctx->timing.chunks = nchunks;
+  ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
 }
 

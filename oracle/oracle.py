@@ -88,6 +88,11 @@ def lib():
         L.oc_file_seed.restype = ctypes.c_uint64
         L.oc_digest_step.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         L.oc_digest_step.restype = ctypes.c_uint64
+        L.ob_hash.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.ob_hash.restype = None
+        L.ob_chunk_ids.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.c_int, ctypes.c_void_p]
+        L.ob_chunk_ids.restype = None
         _lib = L
     return _lib
 
@@ -242,3 +247,75 @@ def cut_gear_py(params: Params, src: bytes):
             return h, a + 1
         index += 1
     return h, remaining
+
+
+# --------------------------------------------------------------- BLAKE3 --
+# Chunk IDs: ID::from_content = blake3::Hasher (unkeyed, 32-byte output)
+# over each chunk's bytes (/root/reference/src/global/mod.rs:86-88,
+# src/utils/mod.rs:62-68, used at src/archiver/processor.rs:184).
+def blake3(data) -> bytes:
+    """BLAKE3 of `data` by the C restatement (oracle/blake3_oracle.c)."""
+    a, ptr = _buf(data)
+    out = ctypes.create_string_buffer(32)
+    lib().ob_hash(ptr, a.size, out)
+    return out.raw
+
+
+def chunk_ids(data, chunks: np.ndarray, threads: int = 1) -> np.ndarray:
+    """(n, 32) uint8: BLAKE3 of every chunk [offset, offset + length) of `data`."""
+    a, ptr = _buf(data)
+    off = np.ascontiguousarray(chunks["offset"], dtype=np.uint64)
+    ln = np.ascontiguousarray(chunks["length"], dtype=np.uint64)
+    out = np.zeros((max(len(off), 1), 32), dtype=np.uint8)
+    lib().ob_chunk_ids(ptr, off.ctypes.data, ln.ctypes.data, len(off), threads, out.ctypes.data)
+    return out[: len(off)]
+
+
+_B3_IV = (0x6A09E667, 0xBB67AE85, 0x3C6EF372, 0xA54FF53A, 0x510E527F, 0x9B05688C, 0x1F83D9AB, 0x5BE0CD19)
+_B3_PERM = (2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8)
+_M32 = 0xFFFFFFFF
+
+
+def _b3_compress(cv, m, counter, block_len, flags):
+    def rotr(x, n):
+        return ((x >> n) | (x << (32 - n))) & _M32
+    s = list(cv) + list(_B3_IV[:4]) + [counter & _M32, counter >> 32, block_len, flags]
+    m = list(m)
+    for r in range(7):
+        for (a, b, c, d), (x, y) in zip(((0, 4, 8, 12), (1, 5, 9, 13), (2, 6, 10, 14), (3, 7, 11, 15),
+                                         (0, 5, 10, 15), (1, 6, 11, 12), (2, 7, 8, 13), (3, 4, 9, 14)),
+                                        ((0, 1), (2, 3), (4, 5), (6, 7), (8, 9), (10, 11), (12, 13), (14, 15))):
+            s[a] = (s[a] + s[b] + m[x]) & _M32
+            s[d] = rotr(s[d] ^ s[a], 16)
+            s[c] = (s[c] + s[d]) & _M32
+            s[b] = rotr(s[b] ^ s[c], 12)
+            s[a] = (s[a] + s[b] + m[y]) & _M32
+            s[d] = rotr(s[d] ^ s[a], 8)
+            s[c] = (s[c] + s[d]) & _M32
+            s[b] = rotr(s[b] ^ s[c], 7)
+        m = [m[_B3_PERM[i]] for i in range(16)]
+    return [s[i] ^ s[i + 8] for i in range(8)]
+
+
+def blake3_py(data: bytes) -> bytes:
+    """Second, independent statement (pure Python, small inputs): the tree by
+    its recursive definition — the left subtree holds the largest power-of-two
+    number of 1024-byte chunks that leaves at least one chunk on the right."""
+    def chunk(p, counter, root):
+        cv = list(_B3_IV)
+        blocks = [p[i:i + 64] for i in range(0, len(p), 64)] or [b""]
+        for i, b in enumerate(blocks):
+            m = [int.from_bytes((b + bytes(64 - len(b)))[4 * k:4 * k + 4], "little") for k in range(16)]
+            fl = (1 if i == 0 else 0) | (2 if i == len(blocks) - 1 else 0) | (8 if root and i == len(blocks) - 1 else 0)
+            cv = _b3_compress(cv, m, counter, len(b), fl)
+        return cv
+
+    def node(p, c0, root):
+        n = max(1, -(-len(p) // 1024))
+        if n == 1:
+            return chunk(p, c0, root)
+        left = 1 << ((n - 1).bit_length() - 1)
+        lcv, rcv = node(p[:1024 * left], c0, False), node(p[1024 * left:], c0 + left, False)
+        return _b3_compress(_B3_IV, lcv + rcv, 0, 64, 4 | (8 if root else 0))
+
+    return b"".join(w.to_bytes(4, "little") for w in node(bytes(data), 0, True))
