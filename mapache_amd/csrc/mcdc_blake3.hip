@@ -96,8 +96,9 @@ __device__ __forceinline__ void parent(const uint32_t l[8], const uint32_t r[8],
 }
 
 // 16 little-endian message words of the block at byte address p (any
-// alignment) holding `len` valid bytes (1..64; 0 only for the empty input).
-// Reads never leave the 16-byte line of the block's last valid byte.
+// alignment) holding `len` valid bytes (0..64; bytes past len are zero, as
+// the specification pads a final block).  Reads never leave the 16-byte line
+// of the block's last valid byte.
 __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t len, uint32_t m[16]) {
   const uintptr_t a = (uintptr_t)p;
   const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
@@ -124,22 +125,6 @@ __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t len, uint3
       const int keep = (int)len - 4 * i;
       m[i] = keep >= 4 ? m[i] : keep <= 0 ? 0u : m[i] & ((1u << (8 * keep)) - 1u);
     }
-  }
-}
-
-// chaining value (or, with `root`, the root output) of one leaf of `len`
-// bytes (0..1024) at p, leaf counter `counter`
-__device__ __forceinline__ void leaf_cv(const uint8_t *p, uint32_t len, uint64_t counter, bool root, uint32_t cv[8]) {
-  iv(cv);
-  const uint32_t nb = len == 0 ? 1 : (len + 63) / 64;
-#pragma unroll 1
-  for (uint32_t b = 0; b < nb; ++b) {
-    const uint32_t bl = b + 1 < nb ? 64u : len - 64 * b;
-    uint32_t m[16];
-    load_block(p + 64 * b, bl, m);
-    uint32_t flags = (b == 0 ? kChunkStart : 0) | (b + 1 == nb ? kChunkEnd : 0);
-    if (root && b + 1 == nb) flags |= kRoot;
-    compress(cv, m, counter, bl, flags);
   }
 }
 
@@ -178,7 +163,9 @@ __global__ void k_b3_owner(const uint64_t *goff, uint64_t n, uint32_t *owner) {
 
 // One lane per group of <= 16 leaves.  The group's subtree (a complete binary
 // tree when it holds 16 leaves, the specification's tree of its leaves
-// otherwise) is built with a chaining-value stack in LDS.
+// otherwise) is built with a chaining-value stack in LDS.  The main loop runs
+// over the group's full 64-byte blocks only (one uniform code path for the
+// whole wave); the one partial block a group can end with is hashed after it.
 __global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const DevChunk *chunks,
                                                    const uint64_t *goff, const uint32_t *owner, uint64_t n,
                                                    uint32_t *nodes, uint8_t *ids) {
@@ -190,26 +177,53 @@ __global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const De
   const uint32_t nleaves = leaves_of(ch.length);
   const uint64_t gi = g - goff[i];                      // group index within the chunk
   const uint64_t l0 = gi * kGroupLeaves;                // first leaf of the group
-  const uint32_t cnt = (uint32_t)min<uint64_t>(kGroupLeaves, nleaves - l0);
   const bool whole = nleaves <= kGroupLeaves;           // this group is the chunk's whole tree
+  const bool root1 = nleaves == 1;                      // ... and its only leaf is the root
+  const uint64_t grem = ch.length - l0 * kLeaf;
+  const uint32_t gbytes = (uint32_t)(grem < (uint64_t)(kGroupLeaves * kLeaf) ? grem : kGroupLeaves * kLeaf);
+  const uint32_t nfull = gbytes / 64, tail = gbytes % 64;
+  const bool has_tail = tail != 0 || gbytes == 0;       // (the empty input is one empty block)
+  const uint32_t nblk = nfull + (has_tail ? 1u : 0u);
   const uint8_t *p = base + ch.offset + l0 * kLeaf;
+  const uint32_t r = (uint32_t)((uintptr_t)p & 3);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)p & ~(uintptr_t)3);
   uint32_t (*st)[8] = stk[threadIdx.x];
   uint32_t cv[8];
+  iv(cv);
   int sp = 0;
 #pragma unroll 1
-  for (uint32_t k = 0; k < cnt; ++k) {
-    const uint64_t lidx = l0 + k;
-    const uint64_t rem = ch.length - lidx * kLeaf;
-    const uint32_t len = (uint32_t)(rem < (uint64_t)kLeaf ? rem : (uint64_t)kLeaf);
-    leaf_cv(p + (uint64_t)k * kLeaf, len, lidx, whole && nleaves == 1, cv);
-    if (k + 1 == cnt) break;                            // the last leaf folds the stack below
-    for (uint32_t t = k + 1; (t & 1) == 0; t >>= 1) {    // merge completed subtrees
-      --sp;
-      parent(st[sp], cv, 0, cv);
-    }
+  for (uint32_t j = 0; j < nfull; ++j, w += 16) {
+    const uint32_t b = j & 15, k = j >> 4;
+    uint32_t m[16];
+    {
+      const uint4 q0 = *reinterpret_cast<const uint4 *>(w), q1 = *reinterpret_cast<const uint4 *>(w + 4),
+                  q2 = *reinterpret_cast<const uint4 *>(w + 8), q3 = *reinterpret_cast<const uint4 *>(w + 12);
+      const uint32_t x16 = r ? w[16] : 0u;  // holds the block's last bytes only when misaligned
+      const uint32_t raw[17] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, x16};
 #pragma unroll
-    for (int w = 0; w < 8; ++w) st[sp][w] = cv[w];
-    ++sp;
+      for (int t = 0; t < 16; ++t) m[t] = __builtin_amdgcn_alignbyte(raw[t + 1], raw[t], r);
+    }
+    const bool last = j + 1 == nblk;
+    const bool end = b == 15 || last;
+    compress(cv, m, l0 + k, 64,
+             (b == 0 ? kChunkStart : 0) | (end ? kChunkEnd : 0) | (root1 && last ? kRoot : 0));
+    if (end && !last) {  // leaf k done and more follow: push it, merging completed subtrees
+      for (uint32_t t = k + 1; (t & 1) == 0; t >>= 1) {
+        --sp;
+        parent(st[sp], cv, 0, cv);
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) st[sp][t] = cv[t];
+      ++sp;
+      iv(cv);
+    }
+  }
+  if (has_tail) {  // the group's final, partial block
+    const uint32_t b = nfull & 15, k = nfull >> 4;
+    uint32_t m[16];
+    load_block(p + 64ull * nfull, tail, m);
+    compress(cv, m, l0 + k, tail, (b == 0 ? kChunkStart : 0) | kChunkEnd | (root1 ? kRoot : 0));
   }
   while (sp > 0) {  // right edge; the top node is the chunk's root when `whole`
     --sp;
