@@ -26,7 +26,12 @@ for step in "$@"; do
     benchq) run benchq 600 python bench.py --steps 5 --warmup 2 --cpu-sample-gib 4 --e2e-gib 4 ;;
     prof)  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu --e2e-gib 0 \
+             --batch-files 0 --small-files 0 --no-ids \
              > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1); rc=$?; echo "== prof rc=$rc" | tee -a $OUT/session.log
+           if fatal $rc; then exit $rc; fi ;;
+    profall) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d $GRAFT_REPO_ROOT/$OUT/profall -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu \
+             --e2e-gib 0 > $GRAFT_REPO_ROOT/$OUT/profall.log 2>&1); rc=$?; echo "== profall rc=$rc" | tee -a $OUT/session.log
            if fatal $rc; then exit $rc; fi ;;
     pmc)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
              -d $GRAFT_REPO_ROOT/$OUT/pmc_fetch -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu --e2e-gib 0 \
