@@ -92,8 +92,12 @@ DevParams make_dev_params(const mcdc_params *p, uint64_t ms, uint64_t ml) {
 }
 
 // Segment length: ~16 expected chunks per speculative chain, >= 2 * max.
+// (MCDC_SEG_CHUNKS overrides the 16 for A/B runs; >= 2 * max keeps a single
+// chunk from skipping a whole segment.)
 uint64_t segment_bytes(const mcdc_params *p) {
-  uint64_t z = std::max<uint64_t>(2ull * p->max_size, 16ull * ((uint64_t)p->min_size + p->avg_size));
+  const char *v = std::getenv("MCDC_SEG_CHUNKS");
+  const uint64_t k = v && *v ? (uint64_t)std::max(1, std::atoi(v)) : 16ull;
+  uint64_t z = std::max<uint64_t>(2ull * p->max_size, k * ((uint64_t)p->min_size + p->avg_size));
   return (z + kRun - 1) / kRun * kRun;
 }
 
@@ -130,7 +134,7 @@ struct mcdc_ctx {
   // workspace
   DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
+      scan_tmp, seg_incl, irr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
   // pinned host staging
   void *h_stage = nullptr;
   size_t h_stage_cap = 0;
@@ -356,6 +360,10 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.err = (uint32_t *)ctx->err.p;
 
   if ((rc = ensure(ctx, ctx->seg_incl, (size_t)nsegs * 8))) return rc;
+  if ((rc = ensure(ctx, ctx->irr, (size_t)nsegs * 5 + 16))) return rc;
+  W.irr_n = (uint32_t *)ctx->irr.p;
+  W.irr_list = (uint32_t *)ctx->irr.p + 4;
+  W.irr_flag = (uint8_t *)ctx->irr.p + 16 + (size_t)nsegs * 4;
 
   // ---- staged pipeline plan ----
   // parts: full tiles [tb[i], tb[i+1]); the last part also scans the partial tile
@@ -585,7 +593,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
-                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->b3_chunks, &ctx->b3_gcnt,
+                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->b3_chunks, &ctx->b3_gcnt,
                     &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);

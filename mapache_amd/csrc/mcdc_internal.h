@@ -10,8 +10,8 @@
 //   k_link      one wave per segment: continue past the segment end until
 //               the chain merges with a later segment's speculative chain
 //   k_fallback  one wave per file whose continuation never merged: serial walk
-//   k_walk_*    mark the segments on the true chain (parallel common case,
-//               serial link-following for files whose chains skipped a segment)
+//   k_walk_*    mark the segments on the true chain (parallel default, then
+//               one jump per irregular link for files whose chains skipped)
 //   k_count / hipcub exclusive scan / k_emit: (offset, length, hash) per chunk
 #pragma once
 #include <hip/hip_runtime.h>
@@ -87,6 +87,9 @@ struct Work {
   DevChunk *out;
   uint64_t out_cap;
   uint32_t *err;         // [0] error bits, [1] files resolved by k_fallback, [2] dirty
+  uint8_t *irr_flag;     // general path: segment's link is not to the next segment
+  uint32_t *irr_list;    // sorted irregular segment indices, count in *irr_n
+  uint32_t *irr_n;
 };
 
 // launch wrappers (mcdc_kernels.hip); all enqueue on `stream`.

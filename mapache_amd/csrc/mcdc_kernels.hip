@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "mcdc_internal.h"
 
 
@@ -515,10 +517,10 @@ __device__ __forceinline__ uint32_t rel_clamp(uint64_t x, uint64_t rb) {
   return x <= rb ? 0u : (x - rb >= (uint64_t)kRun ? (uint32_t)kRun : (uint32_t)(x - rb));
 }
 
-// In run-relative 32-bit coordinates: entries 0-3 always, 4-7 only when the
-// run has more than 4 (rare on real data).
+// In run-relative 32-bit coordinates: entries 0-3 preloaded, 4-7 loaded here
+// only when the run has more than 4 (rare on real data).
 __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, const uint4 ea,
-                                                    const uint4 eb, uint64_t lo, uint64_t hi,
+                                                    const uint4 *eb_ptr, uint64_t lo, uint64_t hi,
                                                     uint64_t cce) {
   const uint64_t rb = r * (uint64_t)kRun;
   const uint32_t l = rel_clamp(lo, rb), h = rel_clamp(hi, rb), m = rel_clamp(cce, rb);
@@ -530,6 +532,7 @@ __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, co
   };
   take(0, ea.x); take(1, ea.y); take(2, ea.z); take(3, ea.w);
   if (cnt > 4) {
+    const uint4 eb = *eb_ptr;
     take(4, eb.x); take(5, eb.y); take(6, eb.z); take(7, eb.w);
   }
   return best == 0xffffffffu ? ~0ull : rb + best;
@@ -539,11 +542,12 @@ __device__ __forceinline__ uint64_t run_first_entry(uint64_t r, uint32_t cnt, co
 // from bytes when it overflowed, from the preloaded entries when cap == 8,
 // else from its entry list.
 __device__ __forceinline__ uint64_t run_first(const Work &W, const DevParams &P, const uint64_t *gt, uint64_t r,
-                                              uint32_t cnt, const uint4 ea, const uint4 eb, uint64_t lo,
-                                              uint64_t hi, uint64_t cce) {
+                                              uint32_t cnt, const uint4 ea, uint64_t lo, uint64_t hi,
+                                              uint64_t cce) {
   if (cnt == 0) return ~0ull;
   if (cnt > P.cap) return run_first_hit(W, P, gt, r, lo, hi, cce);
-  if (P.cap == 8) return run_first_entry(r, cnt, ea, eb, lo, hi, cce);
+  if (P.cap == 8)
+    return run_first_entry(r, cnt, ea, reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull) + 1, lo, hi, cce);
   uint64_t found = ~0ull;
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
@@ -604,7 +608,7 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
   const bool cand = lo < hi;
   const uint64_t r0 = lo / kRun, r1 = cand ? (hi - 1) / kRun : 0;
   uint32_t cn[RPL];
-  uint4 ea[RPL], eb[RPL];
+  uint4 ea[RPL];
   auto load_batch = [&](uint64_t rb) {
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
@@ -612,14 +616,10 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
       cn[k] = (cand && r <= r1) ? W.run_cnt[r] : 0;
     }
 #pragma unroll
-    for (int k = 0; k < RPL; ++k) {  // level 2: entries of non-empty runs (~15 % on random data)
+    for (int k = 0; k < RPL; ++k) {  // level 2: entries 0-3 of non-empty runs (~15 % on random data)
       ea[k] = make_uint4(0, 0, 0, 0);
-      eb[k] = make_uint4(0, 0, 0, 0);
-      if (P.cap == 8 && cn[k] > 0 && cn[k] <= 8) {
-        const uint4 *ep = reinterpret_cast<const uint4 *>(W.run_ent + (rb + RPL * G.gl + k) * 8ull);
-        ea[k] = ep[0];
-        if (cn[k] > 4) eb[k] = ep[1];
-      }
+      if (P.cap == 8 && cn[k] > 0 && cn[k] <= 8)
+        ea[k] = *reinterpret_cast<const uint4 *>(W.run_ent + (rb + RPL * G.gl + k) * 8ull);
     }
   };
   // ---- level-1 loads, all independent
@@ -663,7 +663,7 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       const uint64_t r = rb + RPL * G.gl + k;
-      if (found == ~0ull && r <= r1) found = run_first(W, P, gt, r, cn[k], ea[k], eb[k], lo, hi, cce);
+      if (found == ~0ull && r <= r1) found = run_first(W, P, gt, r, cn[k], ea[k], lo, hi, cce);
     }
     const uint64_t fb = G.ballot(found != ~0ull);
     if (fb) return G.bcast(found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
@@ -800,42 +800,56 @@ __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
 }
 
 // ============================================================ walk =======
-// Common case (every continuation merged into the next segment, or the file
-// was resolved serially): every segment is on the true chain; entry = the
-// merge index handed over by the previous segment.  One thread per segment.
+// Default for every segment: on the true chain, entered at the merge index
+// handed over by the previous segment (0 for a file's first segment and for
+// files the serial fallback rewrote).  One thread per segment.
 __global__ void k_walk_fast(Work W) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= W.nsegs) return;
   const Seg S = W.segs[s];
   const uint32_t fl = W.file_flags[S.file];
-  if (fl != 0 && !(fl & kFileFallbackDone)) return;  // k_walk_seq owns this file
   W.seg_true[s] = 1;
   W.entry_idx[s] = ((S.flags & kSegFirst) || (fl & kFileFallbackDone)) ? 0 : W.link_idx[s - 1];
 }
 
-// Files whose chain skipped a segment: follow the links serially (one wave).
-__global__ __launch_bounds__(64) void k_walk_seq(Work W) {
-  const uint32_t f = blockIdx.x;
+// Irregular segments: a continuation that did not merge into the next one.
+__global__ void k_irr_flags(Work W) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= W.nsegs) return;
+  W.irr_flag[s] = (!(W.segs[s].flags & kSegLast) && W.link_seg[s] != s + 1) ? 1 : 0;
+}
+
+// Files whose chain skipped segments: the path runs through consecutive
+// segments between irregular ones, so only the irregular segments on it are
+// visited (sorted list from DeviceSelect, binary search per jump): mark the
+// skipped segments off the chain and hand the merge index to each jump target.
+// One thread per file; serial steps = skips on the path, not segments.
+__global__ void k_walk_jumps(Work W) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= W.nfiles) return;
   const uint32_t fl = W.file_flags[f];
-  if (fl == 0 || (fl & kFileFallbackDone)) return;
-  const uint32_t lane = lane_id();
+  if (!(fl & kFileSkip) || (fl & kFileFallbackDone)) return;
   const File F = W.files[f];
-  for (uint32_t i = lane; i < F.nsegs; i += 64) W.seg_true[F.first_seg + i] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
-    uint32_t s = F.first_seg, e = 0;
-    const uint32_t last = F.first_seg + F.nsegs - 1;
-    for (;;) {
-      W.seg_true[s] = 1;
-      W.entry_idx[s] = e;
-      if (s == last) break;
-      const uint32_t j = W.link_seg[s];
-      if (j == kSegNone || j == kSegFail || j > last) break;
-      e = W.link_idx[s];
-      s = j;
+  if (F.nsegs == 0) return;
+  const uint32_t last = F.first_seg + F.nsegs - 1, n = *W.irr_n;
+  uint32_t p = F.first_seg;
+  for (;;) {
+    uint32_t lo = 0, hi = n;  // first irregular segment >= p
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (W.irr_list[mid] < p) lo = mid + 1;
+      else hi = mid;
     }
+    if (lo == n) break;
+    const uint32_t i = W.irr_list[lo];
+    if (i > last) break;
+    const uint32_t j = W.link_seg[i];
+    const bool end = j == kSegNone || j == kSegFail || j > last;
+    const uint32_t stop = end ? last + 1 : j;
+    for (uint32_t t = i + 1; t < stop; ++t) W.seg_true[t] = 0;
+    if (end) break;
+    W.entry_idx[j] = W.link_idx[i];
+    p = j;
   }
 }
 
@@ -1047,22 +1061,42 @@ __global__ void k_add_base(Work W, const uint64_t *incl, uint32_t s0, uint32_t s
 }
 
 size_t scan_tmp_bytes(uint32_t nsegs) {
-  size_t a = 0, b = 0;
+  size_t a = 0, b = 0, c = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nsegs + 1);
   (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nsegs + 1);
-  return a > b ? a : b;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, c, hipcub::CountingInputIterator<uint32_t>(0u), (uint8_t *)nullptr,
+                                      (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nsegs + 1);
+  return std::max(a, std::max(b, c));
 }
 
-static unsigned group_blocks(uint32_t n) { return (n + 256 / kGroup - 1) / (256 / kGroup); }
+static unsigned group_blocks(uint32_t n, int gs = kGroup) { return (n + 256 / gs - 1) / (256 / gs); }
+
+// chain-group size of k_spec / k_link (A/B knob MCDC_GROUP = 8, 16, 32; default kGroup)
+static int chain_group() {
+  static const int g = [] {
+    const char *v = std::getenv("MCDC_GROUP");
+    const int x = v ? std::atoi(v) : kGroup;
+    return (x == 8 || x == 16 || x == 32) ? x : kGroup;
+  }();
+  return g;
+}
 
 void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream) {
   if (s1 > s0)
-    hipLaunchKernelGGL(k_spec<kGroup>, dim3(group_blocks(s1 - s0)), dim3(256), 0, stream, w, p, s0, s1);
+    switch (chain_group()) {
+      case 8: hipLaunchKernelGGL(k_spec<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1); break;
+      case 32: hipLaunchKernelGGL(k_spec<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1); break;
+      default: hipLaunchKernelGGL(k_spec<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+    }
 }
 
 void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream) {
   if (s1 > s0)
-    hipLaunchKernelGGL(k_link<kGroup>, dim3(group_blocks(s1 - s0)), dim3(256), 0, stream, w, p, s0, s1);
+    switch (chain_group()) {
+      case 8: hipLaunchKernelGGL(k_link<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1); break;
+      case 32: hipLaunchKernelGGL(k_link<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1); break;
+      default: hipLaunchKernelGGL(k_link<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+    }
 }
 
 // counts, offsets and boundaries of segments [s0, s1) assuming the clean case
@@ -1090,9 +1124,13 @@ void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, s
   if (w.nsegs == 0) return;
   hipLaunchKernelGGL(k_fallback, dim3(w.nfiles), dim3(64), 0, stream, w, p);
   hipLaunchKernelGGL(k_walk_fast, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
-  hipLaunchKernelGGL(k_walk_seq, dim3(w.nfiles), dim3(64), 0, stream, w);
-  hipLaunchKernelGGL(k_count, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
+  hipLaunchKernelGGL(k_irr_flags, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
   size_t bytes = scan_tmp_bytes_;
+  (void)hipcub::DeviceSelect::Flagged(scan_tmp, bytes, hipcub::CountingInputIterator<uint32_t>(0u), w.irr_flag,
+                                      w.irr_list, w.irr_n, (int)w.nsegs, stream);
+  hipLaunchKernelGGL(k_walk_jumps, dim3((w.nfiles + 255) / 256), dim3(256), 0, stream, w);
+  hipLaunchKernelGGL(k_count, dim3((w.nsegs + 255) / 256), dim3(256), 0, stream, w);
+  bytes = scan_tmp_bytes_;
   // seg_count has nsegs + 1 entries (last = 0) so seg_off[nsegs] = total
   (void)hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, w.seg_count, w.seg_off, (int)w.nsegs + 1, stream);
   hipLaunchKernelGGL(k_emit<kGroup>, dim3(group_blocks(w.nsegs)), dim3(256), 0, stream, w, p, 0u, w.nsegs);
