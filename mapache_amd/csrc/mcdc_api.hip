@@ -134,7 +134,7 @@ struct mcdc_ctx {
   // workspace
   DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl, irr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
+      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
   // pinned host staging
   void *h_stage = nullptr;
   size_t h_stage_cap = 0;
@@ -361,6 +361,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
 
   if ((rc = ensure(ctx, ctx->seg_incl, (size_t)nsegs * 8))) return rc;
   if ((rc = ensure(ctx, ctx->irr, (size_t)nsegs * 5 + 16))) return rc;
+  if ((rc = ensure(ctx, ctx->tile_ctr, 64))) return rc;
+  W.tile_ctr = env_int("MCDC_DYN_TILES", 1) ? (uint64_t *)ctx->tile_ctr.p : nullptr;
   W.irr_n = (uint32_t *)ctx->irr.p;
   W.irr_list = (uint32_t *)ctx->irr.p + 4;
   W.irr_flag = (uint8_t *)ctx->irr.p + 16 + (size_t)nsegs * 4;
@@ -425,6 +427,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   hipStream_t st2 = ctx->stream2;
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
   for (int i = 0; i < K; ++i) {
+    if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
     if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
@@ -593,7 +596,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
-                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->b3_chunks, &ctx->b3_gcnt,
+                    &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->tile_ctr, &ctx->b3_chunks, &ctx->b3_gcnt,
                     &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);

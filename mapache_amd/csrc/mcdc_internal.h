@@ -64,6 +64,7 @@ struct Work {
   const uint64_t *gear16;// GEAR[256] << 16
   uint8_t *run_cnt;      // [nruns]
   uint32_t *run_ent;     // [nruns * cap]: off | S<<31 | L<<30
+  uint64_t *tile_ctr;    // scan tile counter (dynamic tile order) or nullptr (static)
 
   const Seg *segs;
   uint32_t nsegs, nfiles;

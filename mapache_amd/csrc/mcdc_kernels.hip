@@ -406,7 +406,20 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   char *wr = q.pad + 4 * qi * kQPad + 16 * qj;
   const char *rd = q.pad + lane * kQPad;
   const uint32_t o0 = 4 * qi * RUN + 16 * qj;  // lane's byte offset in the tile for load 0, group 0
-  for (uint64_t t = tile0 + wid; t < tile1; t += nwaves) {
+  // Tiles are handed out either statically (wave w: tiles w, w + nwaves, ...)
+  // or, with W.tile_ctr, in request order from one atomic counter: waves that
+  // run fast take more tiles, so the launch ends without a ragged last round.
+  // The next index is requested when a tile starts, so its latency is hidden.
+  const bool dyn = W.tile_ctr != nullptr;
+  auto grab = [&]() -> uint64_t {
+    uint64_t v = 0;
+    if (lane == 0) v = atomicAdd(reinterpret_cast<unsigned long long *>(W.tile_ctr), 1ull);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return tile0 + (((uint64_t)hi << 32) | lo);
+  };
+  uint64_t t = dyn ? grab() : tile0 + wid;
+  while (t < tile1) {
+    const uint64_t t_next = dyn ? grab() : t + nwaves;
     const uint64_t run0 = t * 64, run = run0 + lane;
     uint64_t h = 0;
     if (run > 0) {  // warm-up: the 48 bytes before the run complete every window
@@ -462,6 +475,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     const uint32_t cnt = q.lcnt[lane];
     q.lcnt[lane] = 0;
     W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
+    t = t_next;
   }
   // partial last tile: lane-strided runs, exact per-lane path
   if (!do_tail) return;
