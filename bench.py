@@ -67,6 +67,33 @@ def _pmc_traffic():
         return None, None
 
 
+def _bind_near_gpu(device: int):
+    """Run this process on the CPUs of the GPU's NUMA node (intersected with the
+    CPUs it may use), so pinned host buffers are first-touched next to the GPU's
+    PCIe root.  Returns the node or None; never fails the bench."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return None
+        bus = buf.value.decode().lower()
+        node = int(open(f"/sys/bus/pci/devices/{bus}/numa_node").read())
+        if node < 0:
+            return None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        mine = cpus & os.sched_getaffinity(0)
+        if not mine:
+            return None
+        os.sched_setaffinity(0, mine)
+        return node
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -275,6 +302,7 @@ def main() -> int:
     world, rank, local = _dist()
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    numa_node = _bind_near_gpu(local)
     dist = None
     if world > 1:
         import torch
@@ -288,6 +316,11 @@ def main() -> int:
     extras = rank == 0 and world == 1
     max_bytes = max(n, a.batch_files * (8 << 20) if extras else 0)
     ctx = _lib.Context(local, max_bytes)
+    # Allocation order matters on this device heap: memory that a freed
+    # multi-GiB buffer occupied is slower afterwards (tools/e2e_probe.py: a DMA
+    # into it runs at 33 instead of 57.6 GB/s).  So the headline runs first on
+    # a fresh heap, and the e2e host leg takes fresh memory of its own before
+    # the 64 GiB buffers are freed.
     dp = ctx.device_alloc(n)
     ctx.fill_random(dp, n, SEED ^ rank)  # rank 0 uses SEED itself
     cap = n // (p.min_size - 1) + 2
@@ -332,7 +365,8 @@ def main() -> int:
         "config": {"workload": f"one {a.gib:g} GiB uniform-random buffer per GPU, device-resident in and out "
                                f"(BASELINE configs[1])", "params": "FastCDC v2020 16/64/256 KiB Level1",
                    "bytes_per_gpu": n, "chunks_per_step": int(count),
-                   "parallelism": f"{n_gpus} independent streams, no collectives"},
+                   "parallelism": f"{n_gpus} independent streams, no collectives",
+                   "host_numa_node": numa_node},
         "roofline": {"bound": "hbm", "kernel": "k_scan_q", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": int(round(tpb * n)) if tpb else None, "traffic_unit": "bytes per launch",
@@ -354,11 +388,15 @@ def main() -> int:
                 result["chunk_ids"] = chunk_ids(ctx, p, dp, n, d_out, int(count), 3, 1.0, a.no_cpu)
             except Exception as e:  # reported, never silently dropped
                 result["chunk_ids"] = {"error": f"{type(e).__name__}: {e}"}
+        if a.e2e_gib > 0:
+            try:
+                result["e2e_host"] = e2e_host(ctx, p, a.e2e_gib)
+            except Exception as e:  # reported, never silently dropped
+                result["e2e_host"] = {"error": f"{type(e).__name__}: {e}"}
     ctx.device_free(d_out)
     ctx.device_free(dp)
     if extras:
-        for key, fn in (("e2e_host", lambda: e2e_host(ctx, p, a.e2e_gib) if a.e2e_gib > 0 else None),
-                        ("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3)
+        for key, fn in (("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3)
                          if a.batch_files > 0 else None),
                         ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None)):
             try:

@@ -19,7 +19,10 @@
 
 namespace mcdc {
 
-constexpr int kRun = 4096;            // bytes hashed per lane per scan run
+#ifndef MCDC_KRUN
+#define MCDC_KRUN 4096  // (compile-time A/B knob)
+#endif
+constexpr int kRun = MCDC_KRUN;       // bytes hashed per lane per scan run
 constexpr int kWin = 48;              // bits 0..47 of the Gear hash = last 48 bytes
 constexpr int kContMax = 64;          // continuation steps before serial fallback
 constexpr int kGroup = 16;            // lanes per chain in k_spec / k_link / k_emit
