@@ -28,7 +28,7 @@ print(json.dumps({"chunks": int(len(ch)), "scan": med[0], "resolve": med[1], "de
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 gib, libs = sys.argv[1], sys.argv[2:]
-for rep in range(2):
+for rep in range(int(os.environ.get("AB_REPS", "2"))):
     for lib in libs:
         env = dict(os.environ, MCDC_LIBRARY=os.path.abspath(lib))
         r = subprocess.run([sys.executable, "-c", CHILD, gib, root], env=env, capture_output=True, text=True,
