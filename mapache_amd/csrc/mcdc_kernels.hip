@@ -597,6 +597,26 @@ struct Group {
   }
 };
 
+// Candidate search of one run in chunk-relative int32 coordinates (positions
+// minus c; every window lies within max <= 16 MiB of c): the first entry in
+// [lo_r, hi_r) that is an S candidate before cce_r or an L candidate after it.
+// Entries 0-3 preloaded, 4-7 loaded only for a run holding more than four.
+__device__ __forceinline__ int32_t run_first_rel(uint32_t cnt, const uint4 ea, const uint4 *eb_ptr, int32_t rbase,
+                                                 int32_t lo_r, int32_t hi_r, int32_t cce_r) {
+  int32_t best = INT32_MAX;
+  auto take = [&](uint32_t i, uint32_t e) {
+    const int32_t p = rbase + (int32_t)(e & 0x00ffffffu);
+    const uint32_t kind = p < cce_r ? (e >> 31) : ((e >> 30) & 1u);
+    if (i < cnt && p >= lo_r && p < hi_r && kind) best = min(best, p);
+  };
+  take(0, ea.x); take(1, ea.y); take(2, ea.z); take(3, ea.w);
+  if (cnt > 4) {
+    const uint4 eb = *eb_ptr;
+    take(4, eb.x); take(5, eb.y); take(6, eb.z); take(7, eb.w);
+  }
+  return best;
+}
+
 // next(c): the chunk starting at arena position c (file ends at fend) ends
 // where fastcdc's cut_gear(&file[c..], min, avg, max, masks) says.  Called by
 // a whole group with group-uniform c, fend; returns the next chunk start.
@@ -604,6 +624,8 @@ struct Group {
 // runs [RPL*gl, RPL*gl + RPL).  Latency shape: two dependent global levels per
 // step — {restart-window bytes, the first 64 runs' candidate counts}, then
 // {entries of the non-empty runs}; GEAR comes from the block's LDS copy `gt`.
+// Window arithmetic is 32-bit relative to c; only overflowed runs and the
+// general entry lists (cap != 8) use absolute 64-bit positions.
 template <int GS>
 __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParams &P, const uint64_t *gt,
                                uint64_t c, uint64_t fend) {
@@ -611,16 +633,17 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
   constexpr int RPL = 64 / GS;
   const uint64_t rem = fend - c;
   if (rem <= P.min) return fend;                  // remaining <= min_size: whole tail
-  uint64_t center = P.avg, remaining = rem;
-  if (rem > P.max) remaining = P.max;
-  else if (rem < center) center = rem;
-  const uint64_t t0 = (uint64_t)(P.min / 2) * 2, ce = (center / 2) * 2, re = (remaining / 2) * 2;
+  // crate: center = avg, remaining = rem; rem > max -> remaining = max, else rem < avg -> center = rem
+  const uint32_t remaining = rem > P.max ? P.max : (uint32_t)rem;
+  const uint32_t center = (rem <= P.max && rem < P.avg) ? (uint32_t)rem : P.avg;
+  const uint32_t t0 = P.min / 2 * 2, ce = center / 2 * 2, re = remaining / 2 * 2;
   if (re <= t0) return c + remaining;             // loop never runs: forced
   const uint64_t t = c + t0;
-  const uint32_t wlen = (uint32_t)((re - t0) < (uint64_t)(kWin - 1) ? (re - t0) : (uint64_t)(kWin - 1));
-  const uint64_t lo = t + (kWin - 1), hi = c + re, cce = c + ce;
-  const bool cand = lo < hi;
-  const uint64_t r0 = lo / kRun, r1 = cand ? (hi - 1) / kRun : 0;
+  const uint32_t wlen = min(re - t0, (uint32_t)(kWin - 1));
+  const int32_t lo_r = (int32_t)(t0 + kWin - 1), hi_r = (int32_t)re, cce_r = (int32_t)ce;
+  const bool cand = lo_r < hi_r;
+  const uint64_t r0 = (c + (uint64_t)lo_r) / kRun, r1 = cand ? (c + (uint64_t)hi_r - 1) / kRun : 0;
+  const int32_t base0 = (int32_t)((int64_t)(r0 * (uint64_t)kRun) - (int64_t)c);  // run r0's start - c
   uint32_t cn[RPL];
   uint4 ea[RPL];
   auto load_batch = [&](uint64_t rb) {
@@ -671,16 +694,25 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
   if (b) return t + G.bcast(first, (uint32_t)(__ffsll((unsigned long long)b) - 1));
   if (!cand) return c + remaining;
   // ---- (2) windowed candidates for [t + 47, c + re), 64 runs per batch
+  const uint64_t lo = c + (uint64_t)lo_r, hi = c + (uint64_t)hi_r, cce = c + (uint64_t)cce_r;
   for (uint64_t rb = r0; rb <= r1; rb += 64) {
     if (rb != r0) load_batch(rb);
-    uint64_t found = ~0ull;
+    int32_t found = INT32_MAX;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       const uint64_t r = rb + RPL * G.gl + k;
-      if (found == ~0ull && r <= r1) found = run_first(W, P, gt, r, cn[k], ea[k], lo, hi, cce);
+      const int32_t rbase = base0 + (int32_t)((r - r0) * (uint64_t)kRun);
+      if (found != INT32_MAX || cn[k] == 0) continue;
+      if (cn[k] <= P.cap && P.cap == 8) {
+        found = run_first_rel(cn[k], ea[k], reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull) + 1, rbase,
+                              lo_r, hi_r, cce_r);
+      } else {  // overflowed run (rescan bytes) or a general entry list
+        const uint64_t f = run_first(W, P, gt, r, cn[k], ea[k], lo, hi, cce);
+        if (f != ~0ull) found = (int32_t)(f - c);
+      }
     }
-    const uint64_t fb = G.ballot(found != ~0ull);
-    if (fb) return G.bcast(found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
+    const uint64_t fb = G.ballot(found != INT32_MAX);
+    if (fb) return c + (uint64_t)G.bcast((uint64_t)(uint32_t)found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
   }
   return c + remaining;  // forced cut (e.g. all zeros)
 }
