@@ -302,13 +302,18 @@ def main() -> int:
     world, rank, local = _dist()
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    # Rehearsal only (a 1-GPU box standing in for a node): every rank on
+    # device 0, barriers and the max-over-ranks reduction over gloo.
+    rehearse = os.environ.get("MCDC_BENCH_ONE_DEVICE") == "1"
+    if rehearse:
+        local = 0
     numa_node = _bind_near_gpu(local)
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
 
     from mapache_amd import _lib
     p = _lib.params(*PARAMS)
@@ -348,7 +353,7 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
