@@ -168,7 +168,7 @@ def _timed(fn, steps: int, warmup: int):
     return (time.perf_counter() - t0) / steps, r
 
 
-def batch_files(ctx, p, nfiles: int, size: int, steps: int) -> dict:
+def batch_files(ctx, p, nfiles: int, size: int, steps: int, cpu_files: int = 0, cpu_threads: int = 16) -> dict:
     """BASELINE configs[2]: `nfiles` independent files of `size` bytes back to back
     in one device arena (each file's chain restarts at 0), one batched call."""
     from mapache_amd import _lib
@@ -188,15 +188,35 @@ def batch_files(ctx, p, nfiles: int, size: int, steps: int) -> dict:
         chunks = ctx.d2h_chunks(d_out, total)
         starts = np.concatenate([[0], np.cumsum(counts)])
         ok = int(counts.sum()) == total
-        for i in (0, nfiles // 2, nfiles - 1):
+        for i in (nfiles // 2, nfiles - 1):
             host = O.random_bytes(size, SEED ^ 0xB0, pos=i * size)
             ok &= _same(chunks[starts[i]:starts[i + 1]], O.chunk(O.Params(*PARAMS), host))
-        return {"files": nfiles, "file_bytes": size, "bytes": n, "steps": steps,
-                "ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
-                "files_per_s": round(nfiles / dt, 1), "chunks": int(total),
-                "scan_ms": round(t["scan_ms"], 3), "device_ms": round(t["device_ms"], 3),
-                "parity_probe_files": 3, "parity_probe_ok": bool(ok),
-                "data": "synthetic uniform-random (device PRNG), per-file counts returned"}
+        r = {"files": nfiles, "file_bytes": size, "bytes": n, "steps": steps,
+             "ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
+             "files_per_s": round(nfiles / dt, 1), "chunks": int(total),
+             "scan_ms": round(t["scan_ms"], 3), "device_ms": round(t["device_ms"], 3),
+             "data": "synthetic uniform-random (device PRNG), per-file counts returned"}
+        if cpu_files > 0:
+            # files in parallel on the host cores (the nproc-thread
+            # baseline), the first `cpu_files` files of the same arena; their
+            # boundary lists double as the parity probe
+            k = min(cpu_files, nfiles)
+            host = O.random_bytes(k * size, SEED ^ 0xB0)  # generation is not timed
+            files = [host[i * size:(i + 1) * size] for i in range(k)]
+            O.chunk_files(O.Params(*PARAMS), files[:cpu_threads], threads=cpu_threads)  # page-in, warm
+            t0 = time.perf_counter()
+            ref, rc = O.chunk_files(O.Params(*PARAMS), files, threads=cpu_threads)
+            cdt = time.perf_counter() - t0
+            ok &= bool((rc == counts[:k]).all()) and _same(chunks[:int(starts[k])], ref)
+            r["cpu_baseline"] = {"value": round(k * size / cdt / GIB, 3), "unit": "GiB/s", "cores": cpu_threads,
+                                 "kind": "port", "seconds": round(cdt, 3),
+                                 "sample": f"first {k} of the {nfiles} files ({k * size / GIB:g} GiB), "
+                                           f"oracle/fastcdc_oracle.c, one file per thread at a time, "
+                                           f"{cpu_threads} threads, input pre-generated in RAM",
+                                 "cpu": _cpu_model()}
+        r["parity_probe_files"] = 2 + (min(cpu_files, nfiles) if cpu_files > 0 else 0)
+        r["parity_probe_ok"] = bool(ok)
+        return r
     finally:
         ctx.device_free(d_out)
         ctx.device_free(arena)
@@ -296,6 +316,9 @@ def main() -> int:
     ap.add_argument("--batch-files", type=int, default=10000, help="configs[2] file count (0: skip)")
     ap.add_argument("--small-files", type=int, default=80000, help="configs[3] file count (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the files-in-parallel CPU baseline "
+                    "(16: this pool's CPU share per GPU)")
+    ap.add_argument("--cpu-batch-files", type=int, default=4096, help="files in the multi-thread CPU sample")
     ap.add_argument("--no-ids", action="store_true", help="skip the chunk-ID (BLAKE3) stage")
     a = ap.parse_args()
 
@@ -401,7 +424,9 @@ def main() -> int:
     ctx.device_free(d_out)
     ctx.device_free(dp)
     if extras:
-        for key, fn in (("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3)
+        cpu_files = 0 if a.no_cpu else a.cpu_batch_files
+        threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+        for key, fn in (("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3, cpu_files, threads)
                          if a.batch_files > 0 else None),
                         ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None)):
             try:
