@@ -132,7 +132,8 @@ struct mcdc_ctx {
   hipEvent_t ev_part[kMaxParts] = {};
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
-  DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt,
+  DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
+      cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
   // pinned host staging
@@ -314,6 +315,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if ((rc = ensure(ctx, ctx->seg_exit, nsegs * 8))) return rc;
   if ((rc = ensure(ctx, ctx->cont, (size_t)nsegs * kContMax * 8))) return rc;
   if ((rc = ensure(ctx, ctx->cont_cnt, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->cont_rep, (size_t)nsegs * kContMax * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->cont_ent, nsegs * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->long_list, nsegs * 4))) return rc;
   if ((rc = ensure(ctx, ctx->link_seg, nsegs * 4))) return rc;
   if ((rc = ensure(ctx, ctx->link_idx, nsegs * 4))) return rc;
   if ((rc = ensure(ctx, ctx->link_pos, nsegs * 8))) return rc;
@@ -347,6 +351,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.seg_exit = (uint64_t *)ctx->seg_exit.p;
   W.cont = (uint64_t *)ctx->cont.p;
   W.cont_cnt = (uint32_t *)ctx->cont_cnt.p;
+  W.cont_rep = (uint32_t *)ctx->cont_rep.p;
+  W.cont_ent = (uint32_t *)ctx->cont_ent.p;
+  W.long_list = (uint32_t *)ctx->long_list.p;
   W.link_seg = (uint32_t *)ctx->link_seg.p;
   W.link_idx = (uint32_t *)ctx->link_idx.p;
   W.link_pos = (uint64_t *)ctx->link_pos.p;
@@ -358,6 +365,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.out = out_dev ? (DevChunk *)out_dev : (DevChunk *)ctx->out.p;
   W.out_cap = out_dev ? std::min<uint64_t>(out_bound, cap) : out_bound;
   W.err = (uint32_t *)ctx->err.p;
+  W.long_n = W.err + 3;
 
   if ((rc = ensure(ctx, ctx->seg_incl, (size_t)nsegs * 8))) return rc;
   if ((rc = ensure(ctx, ctx->irr, (size_t)nsegs * 5 + 16))) return rc;
@@ -457,7 +465,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[i], 0));
     const uint32_t a_s = i ? spec_hi[i - 1] : 0, a_l = i ? link_hi[i - 1] : 0;
     launch_spec(W, P, a_s, spec_hi[i], st2);
-    launch_link(W, P, a_l, link_hi[i], st2);
+    // parts before the last: link_hi assumes <= kContMax continuation steps
+    launch_link(W, P, a_l, link_hi[i], i == K - 1 ? ~0ull : (uint64_t)kContMax, st2);
     launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
     HIP_TRY(hipGetLastError());
   }
@@ -593,7 +602,8 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
-                    &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt,
+                    &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
+                    &ctx->cont_ent, &ctx->long_list,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
                     &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->tile_ctr, &ctx->b3_chunks, &ctx->b3_gcnt,

@@ -9,6 +9,7 @@
 //               start (wave-level `next` = exact fastcdc cut_gear semantics)
 //   k_link      one wave per segment: continue past the segment end until
 //               the chain merges with a later segment's speculative chain
+//               (forced stretches taken whole: forced_run)
 //   k_fallback  one wave per file whose continuation never merged: serial walk
 //   k_walk_*    mark the segments on the true chain (parallel default, then
 //               one jump per irregular link for files whose chains skipped)
@@ -26,6 +27,8 @@ constexpr int kRun = MCDC_KRUN;       // bytes hashed per lane per scan run
 constexpr int kWin = 48;              // bits 0..47 of the Gear hash = last 48 bytes
 constexpr int kContMax = 64;          // continuation steps before serial fallback
 constexpr int kGroup = 16;            // lanes per chain in k_spec / k_link / k_emit
+constexpr uint64_t kRepMax = 1u << 30; // nodes per continuation entry (forced stretch)
+constexpr uint64_t kEmitInline = 256;  // longer continuations are emitted by k_emit_long
 constexpr uint8_t kRunOverflow = 255; // run_cnt marker: candidates exceed cap
 constexpr uint32_t kSegNone = 0xffffffffu;
 constexpr uint32_t kSegFail = 0xfffffffeu;
@@ -78,8 +81,10 @@ struct Work {
   const uint64_t *node_off;
   uint32_t *node_cnt;
   uint64_t *seg_exit;    // first chain position >= segment end
-  uint64_t *cont;        // [nsegs * kContMax] continuation nodes
-  uint32_t *cont_cnt;
+  uint64_t *cont;        // [nsegs * kContMax] continuation entries: first node
+  uint32_t *cont_rep;    // [nsegs * kContMax] nodes in the entry (cont + i*max)
+  uint32_t *cont_cnt;    // continuation nodes (expanded)
+  uint32_t *cont_ent;    // continuation entries
   uint32_t *link_seg;    // segment the continuation merged into (or None/Fail)
   uint32_t *link_idx;    // index of the merge node in that segment's list
   uint64_t *link_pos;    // merge position (= next true chunk start) or file end
@@ -90,7 +95,9 @@ struct Work {
   uint64_t *seg_off;     // exclusive prefix of seg_count
   DevChunk *out;
   uint64_t out_cap;
-  uint32_t *err;         // [0] error bits, [1] files resolved by k_fallback, [2] dirty
+  uint32_t *err;         // [0] error bits, [1] files resolved by k_fallback, [2] dirty, [3] long_n
+  uint32_t *long_list;   // segments whose continuation exceeds kEmitInline nodes
+  uint32_t *long_n;      // (= err + 3)
   uint8_t *irr_flag;     // general path: segment's link is not to the next segment
   uint32_t *irr_list;    // sorted irregular segment indices, count in *irr_n
   uint32_t *irr_n;
@@ -103,7 +110,9 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
                  uint64_t tile1, bool tail);
 uint64_t scan_waves(uint64_t ntiles, int num_cus);  // waves of a scan launch over ntiles
 void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream);
-void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream);
+// node_cap: expanded continuation nodes per segment (~0 when everything is scanned)
+void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t node_cap,
+                 hipStream_t stream);
 void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
                              void *scan_tmp, size_t scan_tmp_bytes, hipStream_t stream);
 void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,

@@ -717,6 +717,94 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
   return c + remaining;  // forced cut (e.g. all zeros)
 }
 
+// Nonzero bytes of x, as bit 7 of each byte.
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t x) { return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
+
+// Forced stretch.  On data without candidates (zero-filled extents, long runs
+// of one byte) every step is a forced cut at max, and chains that entered the
+// stretch at different phases never meet; walking it one group_next per chunk
+// is what made such inputs slow.  From a chain node c1, count the steps that
+// are plain forced cuts: step i (from c_i = c1 + i*max) is one when the file
+// continues past c_i + max, no candidate of either kind lies in its window
+// [c_i + t0 + 47, c_i + re) and its restart window [c_i + t0, c_i + t0 + 47)
+// has no hit.  Candidate-freedom is read at run granularity from run_cnt (a
+// non-empty run ends the stretch conservatively), at most kRounds * GS * 64
+// runs ahead.  Returns K <= kmax: next(c1 + i*max) == c1 + (i+1)*max, i < K.
+template <int GS>
+__device__ uint64_t forced_run(const Group<GS> &G, const Work &W, const DevParams &P, const uint64_t *gt,
+                               uint64_t c1, uint64_t fend, uint64_t kmax) {
+  constexpr int NL = 4;           // 16-run loads per lane per round: GS * 64 runs per round
+  constexpr uint32_t kRounds = 4;
+  const uint64_t mx = P.max;
+  const uint32_t t0 = P.min / 2 * 2, re = P.max / 2 * 2, ce = P.avg / 2 * 2;
+  if (kmax == 0 || fend <= c1 + mx || re <= t0 + kWin - 1) return 0;
+  uint64_t K = min(kmax, (fend - c1 - mx - 1) / mx + 1);  // steps whose remaining length exceeds max
+  // (1) first non-empty run at or after the first window, within the runs the
+  // K windows touch
+  const uint64_t rA = (c1 + t0 + kWin - 1) / kRun;
+  const uint64_t rEnd = min(W.nruns, (c1 + (K - 1) * mx + re + kRun - 1) / kRun);
+  uint64_t q = rEnd, rb = rA & ~15ull;
+  for (uint32_t round = 0; round < kRounds && rb < rEnd; ++round, rb += (uint64_t)GS * NL * 16) {
+    const uint64_t lb = rb + (uint64_t)G.gl * NL * 16;  // this lane: runs [lb, lb + 64)
+    uint4 v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k)  // (run_cnt is allocated to a multiple of 16 past nruns)
+      v[k] = lb + 16 * k < rEnd ? *reinterpret_cast<const uint4 *>(W.run_cnt + lb + 16 * k) : make_uint4(0, 0, 0, 0);
+    uint32_t first = 0xffffffffu;
+#pragma unroll
+    for (int d = 4 * NL - 1; d >= 0; --d) {  // descending: the lowest non-empty run wins
+      const uint4 u = v[d / 4];
+      const uint32_t x = (d % 4) == 0 ? u.x : (d % 4) == 1 ? u.y : (d % 4) == 2 ? u.z : u.w;
+      const uint64_t r = lb + 4 * d;
+      uint32_t m = nz_bytes(x);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (r + b < rA || r + b >= rEnd) m &= ~(0x80u << (8 * b));
+      if (m) first = 4 * d + (__builtin_ctz(m) >> 3);
+    }
+    const uint64_t fb = G.ballot(first != 0xffffffffu);
+    if (fb) {
+      const uint32_t src = (uint32_t)(__ffsll((unsigned long long)fb) - 1);
+      q = rb + (uint64_t)src * NL * 16 + G.bcast(first, src);
+      break;
+    }
+    if (round + 1 == kRounds) q = min(rEnd, rb + (uint64_t)GS * NL * 16);  // horizon: unscanned counts as non-empty
+  }
+  const uint64_t Q = q * (uint64_t)kRun;  // no candidate in [c1 + t0 + 47, Q)
+  if (Q < c1 + re) return 0;
+  K = min(K, (Q - c1 - re) / mx + 1);
+  // (2) restart windows, GS steps per batch: the first step with a hit ends the stretch
+  for (uint64_t i0 = 0; i0 < K; i0 += GS) {
+    const uint64_t i = i0 + G.gl;
+    bool hit = false;
+    if (i < K) {
+      const uint64_t t = c1 + i * mx + t0;
+      const uint64_t A = t & ~15ull;
+      const uint32_t lo = (uint32_t)(t - A);
+      uint64_t h = 0;
+#pragma unroll 1
+      for (uint32_t k = 0; k < 4; ++k) {  // (a rolled outer loop keeps k_link's register count)
+        const uint4 u = A + 16 * k < W.n_al ? *reinterpret_cast<const uint4 *>(W.base + A + 16 * k)
+                                            : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int bb = 0; bb < 16; ++bb) {
+          const uint32_t b = 16 * k + bb;
+          const uint32_t w = bb < 4 ? u.x : bb < 8 ? u.y : bb < 12 ? u.z : u.w;
+          const uint32_t x = (w >> (8 * (bb % 4))) & 0xffu;
+          const bool act = b >= lo && b < lo + (kWin - 1);
+          const uint64_t hn = (h << 1) + gt[x];
+          h = act ? hn : h;
+          const uint64_t m = (t0 + (b - lo) < ce) ? P.ms : P.ml;
+          hit |= act && (h & m) == 0;
+        }
+      }
+    }
+    const uint64_t hb = G.ballot(hit);
+    if (hb) return i0 + (uint64_t)(__ffsll((unsigned long long)hb) - 1);
+  }
+  return K;
+}
+
 // ============================================================ spec =======
 __device__ __forceinline__ void load_gear_lds(uint64_t *gt, const Work &W) {
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) gt[i] = W.gear[i];
@@ -767,8 +855,13 @@ __device__ int find_node(const Group<GS> &G, const Work &W, uint32_t j, uint64_t
 }
 
 // ============================================================ link =======
+// Continuation entries are (first node, repeat count): entry e stands for the
+// nodes cont[e] + i*max, i < cont_rep[e] (a forced stretch, forced_run), so a
+// continuation crosses a candidate-free extent of any length in a few entries.
+// cont_cnt = expanded node count, cont_ent = entries.  `node_cap` bounds the
+// expanded count (the staged pipeline's look-ahead assumes <= kContMax steps).
 template <int GS>
-__global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+__global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, uint32_t s1, uint64_t node_cap) {
   __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
@@ -779,27 +872,43 @@ __global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, 
   const File F = W.files[S.file];
   if (S.flags & kSegLast) {
     if (G.gl == 0) {
-      W.link_seg[s] = kSegNone; W.link_idx[s] = 0; W.link_pos[s] = F.end; W.cont_cnt[s] = 0;
+      W.link_seg[s] = kSegNone; W.link_idx[s] = 0; W.link_pos[s] = F.end; W.cont_cnt[s] = 0; W.cont_ent[s] = 0;
     }
     return;
   }
-  uint64_t c = W.seg_exit[s];
-  uint32_t steps = 0, ls = kSegFail, li = 0;
+  uint64_t c = W.seg_exit[s], total = 0;
+  uint32_t ents = 0, ls = kSegFail, li = 0;
   uint64_t lp = F.end;
   for (;;) {
     if (c >= F.end) { ls = kSegNone; lp = F.end; break; }
     const uint32_t j = F.first_seg + (uint32_t)((c - F.start) / W.zseg);
     const int idx = find_node<GS>(G, W, j, c);
     if (idx >= 0) { ls = j; li = (uint32_t)idx; lp = c; break; }
-    if (steps == (uint32_t)kContMax) break;  // give up: serial fallback
-    if (G.gl == 0) W.cont[(uint64_t)s * kContMax + steps] = c;
-    ++steps;
-    c = group_next<GS>(G, W, P, gt, c, F.end);
+    if (ents == (uint32_t)kContMax || total >= node_cap) break;  // give up: serial fallback
+    uint64_t nc = group_next<GS>(G, W, P, gt, c, F.end), reps = 1;
+    if (nc == c + P.max && nc < F.end) {  // forced cut: extend over the forced stretch behind it
+      const uint64_t k = forced_run<GS>(G, W, P, gt, nc, F.end, min(node_cap - total - 1, kRepMax - 1));
+      reps += k;
+      nc += k * P.max;
+    }
+    if (G.gl == 0) {
+      W.cont[(uint64_t)s * kContMax + ents] = c;
+      W.cont_rep[(uint64_t)s * kContMax + ents] = (uint32_t)reps;
+    }
+    ++ents;
+    total += reps;
+    c = nc;
   }
   if (G.gl == 0) {
-    W.link_seg[s] = ls; W.link_idx[s] = li; W.link_pos[s] = lp; W.cont_cnt[s] = steps;
+    W.link_seg[s] = ls; W.link_idx[s] = li; W.link_pos[s] = lp;
+    W.cont_cnt[s] = (uint32_t)total; W.cont_ent[s] = ents;
     if (ls == kSegFail) atomicOr(&W.file_flags[S.file], kFileFail);
     else if (ls != s + 1) atomicOr(&W.file_flags[S.file], kFileSkip);
+    // a long stretch is emitted by k_emit_long (general path only)
+    if (ls != kSegFail && total > kEmitInline) {
+      W.long_list[atomicAdd(W.long_n, 1u)] = s;
+      atomicOr(W.err + 2, 1u);
+    }
   }
 }
 
@@ -814,28 +923,43 @@ __global__ __launch_bounds__(64) void k_fallback(Work W, DevParams P) {
   const uint32_t lane = lane_id();
   const File F = W.files[f];
   if (F.nsegs == 0) return;
+  const Group<64> G;
   uint32_t j = F.first_seg;
   uint64_t k = 0, c = F.start;
-  for (;;) {
-    // c belongs to segment jj; close segments before it
-    const uint32_t jj = F.first_seg + (uint32_t)((c - F.start) / W.zseg);
+  bool ok = true;
+  // append chain node x (uniform): close the segments before x's, then store it
+  auto put = [&](uint64_t x) {
+    const uint32_t jj = F.first_seg + (uint32_t)((x - F.start) / W.zseg);
     while (j < jj) {
       if (lane == 0) {
-        W.node_cnt[j] = (uint32_t)k; W.link_pos[j] = c; W.cont_cnt[j] = 0; W.link_seg[j] = j + 1;
+        W.node_cnt[j] = (uint32_t)k; W.link_pos[j] = x; W.cont_cnt[j] = 0; W.cont_ent[j] = 0;
+        W.link_seg[j] = j + 1;
       }
       k = 0; ++j;
     }
     const uint64_t cap = W.node_off[j + 1] - W.node_off[j];
-    if (k >= cap) { if (lane == 0) atomicOr(W.err, kErrNodeCap); break; }
-    if (lane == 0) W.nodes[W.node_off[j] + k] = c;
+    if (k >= cap) { if (lane == 0) atomicOr(W.err, kErrNodeCap); ok = false; return; }
+    if (lane == 0) W.nodes[W.node_off[j] + k] = x;
     ++k;
-    c = group_next<64>(Group<64>(), W, P, gt, c, F.end);
-    if (c >= F.end) break;
+  };
+  for (;;) {
+    put(c);
+    if (!ok) break;
+    uint64_t nc = group_next<64>(G, W, P, gt, c, F.end);
+    if (nc >= F.end) break;
+    if (nc == c + P.max) {  // forced cut: take the forced stretch behind it in one go
+      const uint64_t kk = forced_run<64>(G, W, P, gt, nc, F.end, kRepMax);
+      for (uint64_t i = 0; i < kk && ok; ++i) put(nc + i * P.max);
+      if (!ok) break;
+      nc += kk * P.max;
+    }
+    c = nc;
   }
   const uint32_t last = F.first_seg + F.nsegs - 1;
   while (j <= last) {
     if (lane == 0) {
-      W.node_cnt[j] = (uint32_t)k; W.link_pos[j] = F.end; W.cont_cnt[j] = 0; W.link_seg[j] = kSegNone;
+      W.node_cnt[j] = (uint32_t)k; W.link_pos[j] = F.end; W.cont_cnt[j] = 0; W.cont_ent[j] = 0;
+      W.link_seg[j] = kSegNone;
     }
     k = 0; ++j;
   }
@@ -962,6 +1086,35 @@ __device__ __forceinline__ uint64_t chunk_hash(const Work &W, const uint64_t *gt
   return cq.dbl ? h << 1 : h;
 }
 
+// Node ii of a continuation list whose entries repeat (see k_link).
+__device__ __forceinline__ uint64_t cont_node(const uint64_t *ct, const uint32_t *cr, uint64_t ii, uint32_t mx) {
+  uint32_t e = 0;
+  uint64_t before = 0;
+  for (;;) {
+    const uint64_t r = cr[e];
+    if (ii < before + r) break;
+    before += r;
+    ++e;
+  }
+  return ct[e] + (ii - before) * mx;
+}
+
+// One output record: the chunk [pos, nxt) of file F at output index o.
+__device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, const uint64_t *gt, const File &F,
+                                         uint64_t o, uint64_t pos, uint64_t nxt) {
+  const ChunkQ cq = chunk_q(P, pos, nxt - pos, F.end);
+  const uint64_t hash = chunk_hash(W, gt, cq);
+  if (o < W.out_cap) {
+    DevChunk ch;
+    ch.offset = pos - F.start;
+    ch.length = nxt - pos;
+    ch.hash = hash;
+    W.out[o] = ch;
+  } else {
+    atomicOr(W.err, kErrOutCap);
+  }
+}
+
 // One group of GS lanes per segment, lane i owns chunk i (of each batch of
 // GS) and computes its hash itself.  Resolution kernels raise their wave priority:
 // they run beside the scan's later parts and are latency-bound.
@@ -981,25 +1134,49 @@ __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, 
   const uint64_t nn = W.node_cnt[s] - e;
   const uint64_t *nd = W.nodes + W.node_off[s] + e;
   const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
+  const uint32_t *cr = W.cont_rep + (uint64_t)s * kContMax;
+  const uint64_t ncont = n - nn;                    // continuation nodes, expanded
+  const bool plain = ncont == W.cont_ent[s];        // every entry a single node
+  const uint64_t n_here = ncont > kEmitInline ? nn : n;  // a long stretch: k_emit_long
   const uint64_t after = W.link_pos[s];
   const uint64_t base_out = W.seg_off[s];
-  for (uint64_t i0 = 0; i0 < n; i0 += GS) {
+  auto node = [&](uint64_t i) -> uint64_t {
+    if (i < nn) return nd[i];
+    return plain ? ct[i - nn] : cont_node(ct, cr, i - nn, P.max);
+  };
+  for (uint64_t i0 = 0; i0 < n_here; i0 += GS) {
     const uint64_t i = i0 + lane;
-    if (i >= n) break;
-    const uint64_t pos = i < nn ? nd[i] : ct[i - nn];
-    const uint64_t j = i + 1;
-    const uint64_t nxt = j < n ? (j < nn ? nd[j] : ct[j - nn]) : after;
-    const ChunkQ cq = chunk_q(P, pos, nxt - pos, F.end);
-    const uint64_t hash = chunk_hash(W, gt, cq);
-    const uint64_t o = base_out + i;
-    if (o < W.out_cap) {
-      DevChunk ch;
-      ch.offset = pos - F.start;
-      ch.length = nxt - pos;
-      ch.hash = hash;
-      W.out[o] = ch;
-    } else {
-      atomicOr(W.err, kErrOutCap);
+    if (i >= n_here) break;
+    const uint64_t pos = node(i);
+    const uint64_t nxt = i + 1 < n ? node(i + 1) : after;
+    emit_one(W, P, gt, F, base_out + i, pos, nxt);
+  }
+}
+
+// Continuation stretches longer than kEmitInline nodes (k_link appended their
+// segments to long_list): the whole grid strides over each one's nodes.  GEAR
+// is read through the vector cache here, not from an LDS copy: with the LDS
+// table this kernel intermittently produced whole waves of wrong chunk hashes
+// (boundaries right) after a large call on the same device, a fault not
+// reproduced with the global table or with extra code in the loop (DESIGN.md
+// §3, open item).  The kernel is off the hot path.
+__global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
+  const uint32_t nl = *W.long_n;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint32_t li = 0; li < nl; ++li) {
+    const uint32_t s = W.long_list[li];
+    const uint64_t n = W.seg_count[s];
+    if (n == 0) continue;  // off the true chain
+    const uint64_t nn = W.node_cnt[s] - W.entry_idx[s], ncont = n - nn;
+    if (ncont <= kEmitInline) continue;  // rewritten by k_fallback, or emitted by k_emit
+    const File F = W.files[W.segs[s].file];
+    const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
+    const uint32_t *cr = W.cont_rep + (uint64_t)s * kContMax;
+    const uint64_t after = W.link_pos[s], base_out = W.seg_off[s] + nn;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ncont; i += stride) {
+      const uint64_t pos = cont_node(ct, cr, i, P.max);
+      const uint64_t nxt = i + 1 < ncont ? cont_node(ct, cr, i + 1, P.max) : after;
+      emit_one(W, P, W.gear, F, base_out + i, pos, nxt);
     }
   }
 }
@@ -1136,12 +1313,13 @@ void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hi
     }
 }
 
-void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream) {
+void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t node_cap,
+                 hipStream_t stream) {
   if (s1 > s0)
     switch (chain_group()) {
-      case 8: hipLaunchKernelGGL(k_link<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1); break;
-      case 32: hipLaunchKernelGGL(k_link<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1); break;
-      default: hipLaunchKernelGGL(k_link<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+      case 8: hipLaunchKernelGGL(k_link<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1, node_cap); break;
+      case 32: hipLaunchKernelGGL(k_link<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1, node_cap); break;
+      default: hipLaunchKernelGGL(k_link<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1, node_cap);
     }
 }
 
@@ -1180,6 +1358,7 @@ void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, s
   // seg_count has nsegs + 1 entries (last = 0) so seg_off[nsegs] = total
   (void)hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, w.seg_count, w.seg_off, (int)w.nsegs + 1, stream);
   hipLaunchKernelGGL(k_emit<kGroup>, dim3(group_blocks(w.nsegs)), dim3(256), 0, stream, w, p, 0u, w.nsegs);
+  hipLaunchKernelGGL(k_emit_long, dim3(1024), dim3(256), 0, stream, w, p);
 }
 
 }  // namespace mcdc

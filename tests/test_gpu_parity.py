@@ -116,13 +116,60 @@ def test_adversarial_patterns(ctx, p):
         _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
 
 
-def test_non_merging_chains_take_the_serial_fallback(ctx):
+def test_forced_stretch_crossed_by_the_continuation(ctx):
     """Random prefix sets a forced-cut phase the segment-start speculation never
-    matches; long zero runs then keep every continuation from merging."""
+    matches; the continuation takes the 48 MiB zero run in a few repeated
+    entries (forced_run) and merges in the random data behind it."""
     p = PARAMS[0]
     d = np.concatenate([O.random_bytes(100_003, 9), np.zeros(48 << 20, np.uint8), O.random_bytes(3 << 20, 10)])
     _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    assert ctx.timing()["fallback_files"] == 0
+
+
+@pytest.mark.parametrize("p", PARAMS, ids=lambda p: "/".join(map(str, p)))
+def test_long_forced_stretch_emitted_by_the_grid(ctx, p):
+    """A continuation of more than kEmitInline (256) chunks: 80 MiB (16/64/256)
+    or 2.2 GiB (512K/1M/8M) of zeros out of phase, emitted by k_emit_long; and
+    the same stretch twice in one file with random data between and behind."""
+    z = (80 << 20) if p[2] <= (256 << 10) else (2200 << 20)
+    d = np.concatenate([O.random_bytes(100_003, 9), np.zeros(z, np.uint8), O.random_bytes(3 << 20, 10)])
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    assert ctx.timing()["fallback_files"] == 0
+    if p[2] <= (256 << 10):
+        d = np.concatenate([O.random_bytes(777_777, 3), np.zeros(z, np.uint8), O.random_bytes(5 << 20, 4),
+                            np.zeros(z + 12345, np.uint8), O.random_bytes(1 << 20, 5)])
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+
+
+def test_stretch_beyond_link_reach_takes_the_serial_fallback(ctx):
+    """1.2 GiB of zeros out of phase: more than 64 continuation entries of at
+    most 16 MiB each, so the file is walked by k_fallback (which takes forced
+    stretches whole as well)."""
+    p = PARAMS[0]
+    d = np.concatenate([O.random_bytes(100_003, 9), np.zeros(1200 << 20, np.uint8), O.random_bytes(3 << 20, 10)])
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
     assert ctx.timing()["fallback_files"] == 1
+
+
+@pytest.mark.parametrize("p", PARAMS, ids=lambda p: "/".join(map(str, p)))
+def test_mixed_zero_extents_and_runs(ctx, p):
+    """Disk-image-like layouts: random and zero extents alternating (1 and 9 MiB),
+    runs of one byte value (1 B .. 64 KiB), sparse random extents."""
+    rng = np.random.default_rng(21)
+    n = 96 << 20
+    for k in (1 << 20, 9 << 20):
+        d = O.random_bytes(n, 31)
+        for b in range(k, n, 2 * k):
+            d[b:b + k] = 0
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    lens = rng.integers(1, 65536, n // 32768 * 2)
+    vals = rng.integers(0, 256, len(lens)).astype(np.uint8)
+    d = np.repeat(vals, lens)[:n]
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    d = np.zeros(n, np.uint8)
+    for b in range(12345, n, 24 << 20):
+        d[b:b + (1 << 20)] = O.random_bytes(1 << 20, b)[: len(d[b:b + (1 << 20)])]
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
 
 
 def test_skipped_segment_walk(ctx):
