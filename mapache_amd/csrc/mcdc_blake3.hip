@@ -186,19 +186,37 @@ __global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const De
   const uint32_t nblk = nfull + (has_tail ? 1u : 0u);
   const uint8_t *p = base + ch.offset + l0 * kLeaf;
   const uint32_t r = (uint32_t)((uintptr_t)p & 3);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)p & ~(uintptr_t)3);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(p - r);  // (stays a global pointer)
   uint32_t (*st)[8] = stk[threadIdx.x];
   uint32_t cv[8];
   iv(cv);
   int sp = 0;
+  // Block j + 1 is requested before block j is compressed: a wave waits on
+  // memory only when its next block has not arrived during a whole
+  // compression, which keeps enough waves ready for the VALU's dual-rate issue
+  // (tools/ubench3.hip: the G mix runs at 2 cycles per instruction with 4 ready
+  // waves per SIMD, 4 with 2).
+  uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
+  uint32_t n16 = 0;
+  // (loads are unconditional — the last iteration re-reads its own block —
+  // so no wait is forced at a control-flow join)
+  auto fetch = [&](const uint32_t *ww) {
+    n0 = *reinterpret_cast<const uint4 *>(ww);
+    n1 = *reinterpret_cast<const uint4 *>(ww + 4);
+    n2 = *reinterpret_cast<const uint4 *>(ww + 8);
+    n3 = *reinterpret_cast<const uint4 *>(ww + 12);
+    const uint32_t x = ww[r ? 16 : 15];  // dword 16 holds the block's last bytes only when misaligned
+    n16 = r ? x : 0u;
+  };
+  if (nfull) fetch(w);
 #pragma unroll 1
   for (uint32_t j = 0; j < nfull; ++j, w += 16) {
     const uint32_t b = j & 15, k = j >> 4;
     uint32_t m[16];
     {
-      const uint4 q0 = *reinterpret_cast<const uint4 *>(w), q1 = *reinterpret_cast<const uint4 *>(w + 4),
-                  q2 = *reinterpret_cast<const uint4 *>(w + 8), q3 = *reinterpret_cast<const uint4 *>(w + 12);
-      const uint32_t x16 = r ? w[16] : 0u;  // holds the block's last bytes only when misaligned
+      const uint4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+      const uint32_t x16 = n16;
+      fetch(j + 1 < nfull ? w + 16 : w);
       const uint32_t raw[17] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                                 q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, x16};
 #pragma unroll
