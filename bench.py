@@ -276,20 +276,21 @@ def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_s
         got = ctx.d2h_bytes(d_ids, 32 * len(sel)).reshape(len(sel), 32)
         ok = bool(len(sel) > 0 and (got == O.chunk_ids(host, sel, threads=16)).all())
         # VALU roofline: 672 lane-ops per 64-byte block (7 rounds x 8 G x 12 ops)
-        # are the algorithmic work; peak = the issue rate of this mix measured in
-        # isolation (tools/ubench3.hip: the product's compression, registers only,
-        # >= 4 waves per SIMD: 2.32 cycles per wave64 instruction per SIMD, the
-        # SIMD dual-issuing across waves) x 256 CUs x 4 SIMDs x 64 lanes x 2.4 GHz.
+        # are the algorithmic work; peak = this mix's own issue rate on the whole
+        # chip, wall clock (tools/ubench3.hip: the product's compression in
+        # registers, 4 waves per SIMD on every CU: 1.68 ns per wave64
+        # instruction per SIMD -- 2.4 cycles at the ~1.45 GHz the chip holds
+        # under this load) x 256 CUs x 4 SIMDs x 64 lanes.
         alg_ops = n / 64 * 672
-        peak_tops = 256 * 4 * 64 / 2.32 * 2.4e9 / 1e12
+        peak_tops = 256 * 4 * 64 / 1.68e-9 / 1e12
         r = {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2), "device_ms": round(ids_ms, 3),
              "bound": "valu (32-bit add/xor/rotate of the BLAKE3 compression, ~11 ops per byte)",
              "roofline": {"bound": "valu", "achieved": round(alg_ops / (ids_ms * 1e-3) / 1e12, 2),
                           "peak": round(peak_tops, 2), "unit": "T int32 lane-ops/s",
                           "frac": round(alg_ops / (ids_ms * 1e-3) / 1e12 / peak_tops, 4),
                           "ops_per_block": 672,
-                          "note": "algorithmic compression ops only (leaves; parents add ~1/16); peak from "
-                                  "tools/ubench3.hip (2.32 cycles per instruction per SIMD)"},
+                          "note": "algorithmic compression ops only (leaves; parents add ~1/16); peak: "
+                                  "tools/ubench3.hip, the compression alone at full occupancy, wall clock"},
              "chunk_plus_ids_ms": round(dt2 * 1e3, 3), "chunk_plus_ids_gib_s": round(n / dt2 / GIB, 2),
              "parity_probe_chunks": int(len(sel)), "parity_probe_ok": ok}
         if not no_cpu:

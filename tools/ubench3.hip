@@ -76,10 +76,14 @@ __device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16], u
 }
 
 template <int MODE>
-__global__ __launch_bounds__(1024) void kb(uint64_t *out, uint32_t seed) {
+__global__ __launch_bounds__(1024) void kb(uint64_t *out, uint32_t seed, const uint4 *src = nullptr) {
   uint32_t s[16], m0 = seed * 7 + threadIdx.x, m1 = m0 ^ 0x55;
 #pragma unroll
   for (int i = 0; i < 16; ++i) s[i] = seed * (i + 3) + threadIdx.x * (i + 1);
+  uint4 nq[4] = {};
+  if constexpr (MODE == 11) {  // de-phase the waves: wave w sleeps ~w * 420 cycles first
+    for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) __builtin_amdgcn_s_sleep(7);
+  }
   const uint64_t c0 = memtime();
   for (int it = 0; it < ITERS; ++it) {
     if constexpr (MODE == 0) {  // xor x16 independent
@@ -101,13 +105,44 @@ __global__ __launch_bounds__(1024) void kb(uint64_t *out, uint32_t seed) {
     } else if constexpr (MODE == 5) {  // rotate as perm (16, 8) instead of alignbit
 #pragma unroll
       for (int i = 0; i < 16; ++i) asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(s[i]) : "v"(0x01000302u));
-    } else if constexpr (MODE == 7) {  // the real compression, message words in registers
+    } else if constexpr (MODE == 7 || MODE == 11) {  // the real compression, message words in registers
       uint32_t cv[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) cv[i] = s[i];
       uint32_t m[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) m[i] = s[i] ^ (uint32_t)it;
+      compress(cv, m, (uint32_t)it);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = cv[i];
+    } else if constexpr (MODE == 10) {  // as MODE 8, lanes 16 KiB apart (k_b3_leaves' pattern)
+      uint32_t cv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cv[i] = s[i];
+      const uint4 *q = src + ((((threadIdx.x & 63) * 1024 + (blockIdx.x * 16 + (threadIdx.x >> 6)) * 4 + it * 4) & 0x7ffff) & ~3);
+      const uint4 a0 = nq[0], a1 = nq[1], a2 = nq[2], a3 = nq[3];
+      nq[0] = q[0]; nq[1] = q[1]; nq[2] = q[2]; nq[3] = q[3];
+      const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                              a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+      compress(cv, m, (uint32_t)it);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = cv[i];
+    } else if constexpr (MODE == 8 || MODE == 9) {  // compression fed by global loads (L2-resident source),
+      // MODE 8: the next block requested before compressing (as k_b3_leaves), MODE 9: loaded and waited first
+      static_assert(true, "");
+      uint32_t cv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cv[i] = s[i];
+      const uint4 *q = src + ((threadIdx.x + blockIdx.x * 64 + it * 4096) & 0x1ffff) * 4;  // 8 MiB window
+      uint4 a0, a1, a2, a3;
+      if constexpr (MODE == 9) {
+        a0 = q[0]; a1 = q[1]; a2 = q[2]; a3 = q[3];
+      } else {
+        a0 = nq[0]; a1 = nq[1]; a2 = nq[2]; a3 = nq[3];
+        nq[0] = q[0]; nq[1] = q[1]; nq[2] = q[2]; nq[3] = q[3];
+      }
+      const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                              a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
       compress(cv, m, (uint32_t)it);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s[i] = cv[i];
@@ -129,10 +164,10 @@ __global__ __launch_bounds__(1024) void kb(uint64_t *out, uint32_t seed) {
 // waves/CU as `waves` waves per workgroup, one workgroup per CU; or (split > 1)
 // as `split` workgroups of waves/split waves each per CU
 template <int MODE>
-int run(const char *name, int ops, uint64_t *out, int cus, int waves, int split = 1) {
+int run(const char *name, int ops, uint64_t *out, int cus, int waves, int split = 1, const uint4 *src = nullptr) {
   const int wpg = waves / split;
   for (int rep = 0; rep < 2; ++rep) {
-    hipLaunchKernelGGL(kb<MODE>, dim3(cus * split), dim3(64 * wpg), 0, 0, out, 1u + rep);
+    hipLaunchKernelGGL(kb<MODE>, dim3(cus * split), dim3(64 * wpg), 0, 0, out, 1u + rep, src);
     CK(hipDeviceSynchronize());
   }
   std::vector<uint64_t> h((size_t)cus * split * 16 * 2);
@@ -148,12 +183,42 @@ int run(const char *name, int ops, uint64_t *out, int cus, int waves, int split 
   return 0;
 }
 
+template <int MODE>
+int run_wall(const char *name, int ops, uint64_t *out, int cus, int waves) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(kb<MODE>, dim3(cus), dim3(64 * waves), 0, 0, out, 1u + rep, nullptr);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    best = ms < best ? ms : best;
+  }
+  const double wi = (double)ITERS * ops * waves;  // wave-instructions per CU
+  printf("%-18s waves/CU=%2d  wall %.3f ms  %.3f ns per wave-instr per SIMD\n", name, waves, best,
+         best * 1e6 / (wi / 4));
+  return 0;
+}
+
 int main() {
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   uint64_t *out;
   CK(hipMalloc(&out, (size_t)cus * 16 * 16 * 2 * 8));  // room for 16 workgroups per CU
+  uint4 *src;
+  CK(hipMalloc(&src, (size_t)8 << 20));
+  CK(hipMemset(src, 0x5a, (size_t)8 << 20));
+  run_wall<11>("compress dephased", 696, out, cus, 16);
+  run_wall<7>("compress in phase", 696, out, cus, 16);
+  run<10>("compress+strided", 696, out, cus, 16, 1, src);
+  run<8>("compress+prefetch", 696, out, cus, 16, 1, src);
+  run<9>("compress+load", 696, out, cus, 16, 1, src);
+  run<8>("compress+prefetch", 696, out, cus, 8, 1, src);
   run<7>("compress (real)", 696, out, cus, 16, 4);
   run<7>("compress (real)", 696, out, cus, 16, 2);
   run<3>("4 x G", 48, out, cus, 16, 4);
