@@ -425,6 +425,24 @@ def main() -> int:
                 result["e2e_host"] = e2e_host(ctx, p, a.e2e_gib)
             except Exception as e:  # reported, never silently dropped
                 result["e2e_host"] = {"error": f"{type(e).__name__}: {e}"}
+    if extras:
+        # (after the chunk-ID stage, which reads the headline's list in d_out)
+        # mapache's own defaults (src/global/defaults.rs:35-40), same buffer
+        p512 = _lib.params(512 << 10, 1 << 20, 8 << 20, 1)
+        cap512 = n // ((512 << 10) - 1) + 2
+        dt5, c5 = _timed(lambda: ctx.chunk_device_to_device(p512, dp, n, d_out, cap512), max(3, a.steps // 2), 1)
+        t5 = ctx.timing()
+        from oracle import oracle as O
+        probe = 1 << 30  # parity probe: chunks that end before the first GiB's last max-window
+        g5 = ctx.d2h_chunks(d_out, c5)
+        g5 = g5[g5["offset"] + (8 << 20) <= probe - (8 << 20)]
+        r5 = O.chunk(O.Params(512 << 10, 1 << 20, 8 << 20, 1), O.random_bytes(probe, SEED))
+        result["params_512k_1m_8m"] = {"ms_per_step": round(dt5 * 1e3, 3), "gib_s": round(n / dt5 / GIB, 2),
+                                       "chunks": int(c5), "scan_ms": round(t5["scan_ms"], 3),
+                                       "device_ms": round(t5["device_ms"], 3),
+                                       "parity_probe_chunks": int(len(g5)),
+                                       "parity_probe_ok": bool(len(g5) > 0 and _same(g5, r5[:len(g5)])),
+                                       "note": "same 64 GiB buffer, device-resident in and out, mapache defaults"}
     ctx.device_free(d_out)
     ctx.device_free(dp)
     if extras:
