@@ -132,7 +132,7 @@ struct mcdc_ctx {
   hipEvent_t ev_part[kMaxParts] = {};
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
-  DevBuf arena, run_cnt, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
+  DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
@@ -304,6 +304,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // ---- workspace ----
   const void *tabs_before[3] = {ctx->segs.p, ctx->files.p, ctx->node_off.p};
   if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
+  if ((rc = ensure(ctx, ctx->run_sum, nruns * 4))) return rc;
   if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
   if ((rc = ensure(ctx, ctx->files, nfiles * sizeof(File)))) return rc;
@@ -339,6 +340,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.gear = ctx->d_gear;
   W.gear16 = ctx->d_gear16;
   W.run_cnt = (uint8_t *)ctx->run_cnt.p;
+  W.run_sum = (uint32_t *)ctx->run_sum.p;
   W.run_ent = (uint32_t *)ctx->run_ent.p;
   W.segs = (const Seg *)ctx->segs.p;
   W.nsegs = nsegs;
@@ -601,7 +603,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
-  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
+  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,

@@ -40,6 +40,16 @@ constexpr uint32_t kFileSkip = 1u, kFileFail = 2u, kFileFallbackDone = 4u;
 // error word bits
 constexpr uint32_t kErrNodeCap = 1u, kErrOutCap = 2u;
 
+// Run summary (written by the scan beside run_cnt): bits 0-13 = 1 + offset of
+// the run's first S candidate (0: none), bits 14-27 = 1 + offset of its first
+// L candidate, bits 28-31 = min(candidate count, 15).  Exact also for runs whose
+// entry list overflowed.  A chain step decides most runs from it alone.
+static_assert(kRun <= 16383, "run offsets must fit the 14-bit summary fields");
+__host__ __device__ inline uint32_t run_summary(uint32_t cnt, uint32_t first_s, uint32_t first_l) {
+  return (cnt > 15u ? 15u : cnt) << 28 | (first_l == 0xffffffffu ? 0u : first_l + 1u) << 14 |
+         (first_s == 0xffffffffu ? 0u : first_s + 1u);
+}
+
 struct Seg {
   uint64_t start, end;  // arena positions [start, end)
   uint32_t file, flags;
@@ -69,6 +79,7 @@ struct Work {
   const uint64_t *gear;  // GEAR[256]
   const uint64_t *gear16;// GEAR[256] << 16
   uint8_t *run_cnt;      // [nruns]
+  uint32_t *run_sum;     // [nruns] run summary: first S / first L candidate (see run_summary)
   uint32_t *run_ent;     // [nruns * cap]: off | S<<31 | L<<30
   uint64_t *tile_ctr;    // scan tile counter (dynamic tile order) or nullptr (static)
 

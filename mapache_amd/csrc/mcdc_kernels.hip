@@ -149,6 +149,21 @@ __device__ __forceinline__ void scan16(const uint64_t *tab, uint32_t lo, const u
   }
 }
 
+// Summary of a run whose entries were appended in position order (the
+// lane-strided paths): exact when the list holds them all; an overflowed list
+// may miss the first candidate of a kind, so it reads "unknown" (count set,
+// both offsets 0) and chain steps consult the bytes.
+__device__ __forceinline__ uint32_t summary_from_entries(const uint32_t *ent, uint32_t cnt, uint32_t cap) {
+  if (cnt > cap) return 15u << 28;
+  uint32_t fs = 0xffffffffu, fl = 0xffffffffu;
+  for (uint32_t i = cnt; i-- > 0;) {
+    const uint32_t e = ent[i];
+    if (e >> 31) fs = e & 0x00ffffffu;
+    if ((e >> 30) & 1u) fl = e & 0x00ffffffu;
+  }
+  return run_summary(cnt, fs, fl);
+}
+
 // One full run of RUN bytes.  PF = 64-byte groups kept in flight ahead of the
 // group being hashed (register ring of 4*PF uint4 per lane).
 template <int RUN, int PF>
@@ -193,6 +208,7 @@ __device__ __forceinline__ void scan_run_full(const uint64_t *tab, uint32_t lo, 
     }
   }
   W.run_cnt[run] = cnt > cap ? kRunOverflow : (uint8_t)cnt;
+  W.run_sum[run] = summary_from_entries(ent, cnt, cap);
 }
 
 // Last, partial run: byte loop with exact tests (one lane in the whole grid).
@@ -202,7 +218,7 @@ __device__ void scan_run_tail(const uint64_t *tab, uint32_t lo, const Work &W, c
   const uint64_t start = run * (uint64_t)RUN, end = W.n_al;
   const uint64_t w0 = start >= (uint64_t)kWin ? start - kWin : 0;
   uint64_t h = 0;
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, fs = 0xffffffffu, fl = 0xffffffffu;
   uint32_t *ent = W.run_ent + run * (uint64_t)P.cap;
   for (uint64_t q = w0; q < end; ++q) {
     h = (h << 1) + lds_gear(tab, ((uint32_t)W.base[q] << 8) | lo);
@@ -211,10 +227,13 @@ __device__ void scan_run_tail(const uint64_t *tab, uint32_t lo, const Work &W, c
       if (s_ | l_) {
         if (cnt < P.cap) ent[cnt] = (uint32_t)(q - start) | (s_ << 31) | (l_ << 30);
         ++cnt;
+        if (s_ && fs == 0xffffffffu) fs = (uint32_t)(q - start);
+        if (l_ && fl == 0xffffffffu) fl = (uint32_t)(q - start);
       }
     }
   }
   W.run_cnt[run] = cnt > P.cap ? kRunOverflow : (uint8_t)cnt;
+  W.run_sum[run] = run_summary(cnt, fs, fl);
 }
 
 template <int RUN, int WPE, int PF, int CH = 1, int BLOCK = 512>
@@ -257,10 +276,11 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan_t(Work W, DevParams P) {
 // walk takes the minimum).  Measured (tools/scanbench, 16 GiB): the deferred
 // queue alone +7-13 % over re-walking the block under an exec mask.
 //
-// LDS = 64 KiB table + 16 waves x (5 KiB pad + 256 B run counters) = 148 KiB.
+// LDS = 64 KiB table + 16 waves x (5 KiB pad + 768 B run counters and
+// first-candidate minima) = 156 KiB.
 constexpr int kQPad = 80;                        // run stride in the transpose pad
 constexpr int kQPadBytes = 64 * kQPad;           // 5 KiB
-constexpr int kQWaveBytes = kQPadBytes + 64 * 4; // + per-run candidate counters
+constexpr int kQWaveBytes = kQPadBytes + 64 * 12;  // + per-run candidate counters, first S, first L
 constexpr int kSTab = 65536;                     // GEAR<<16 x 32 copies
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4],
@@ -316,6 +336,8 @@ __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t 
       if (s_ | l_) {
         const uint32_t k = atomicAdd(&lcnt[rl], 1u);
         if (k < cap) ent[k] = (off + i) | (s_ << 31) | (l_ << 30);
+        if (s_) atomicMin(&lcnt[64 + rl], off + i);   // first S / first L of the run (summary)
+        if (l_) atomicMin(&lcnt[128 + rl], off + i);
       }
     }
   }
@@ -393,6 +415,8 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   q.base = W.base;
   q.run_ent = W.run_ent;
   q.lcnt[lane] = 0;
+  q.lcnt[64 + lane] = 0xffffffffu;
+  q.lcnt[128 + lane] = 0xffffffffu;
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
@@ -472,9 +496,12 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     }
 #undef MCDC_LDQ
     if (qn) q_drain<RUN>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
-    const uint32_t cnt = q.lcnt[lane];
+    const uint32_t cnt = q.lcnt[lane], fs = q.lcnt[64 + lane], fl = q.lcnt[128 + lane];
     q.lcnt[lane] = 0;
+    q.lcnt[64 + lane] = 0xffffffffu;
+    q.lcnt[128 + lane] = 0xffffffffu;
     W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
+    W.run_sum[run] = run_summary(cnt, fs, fl);
     t = t_next;
   }
   // partial last tile: lane-strided runs, exact per-lane path
@@ -644,19 +671,14 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
   const bool cand = lo_r < hi_r;
   const uint64_t r0 = (c + (uint64_t)lo_r) / kRun, r1 = cand ? (c + (uint64_t)hi_r - 1) / kRun : 0;
   const int32_t base0 = (int32_t)((int64_t)(r0 * (uint64_t)kRun) - (int64_t)c);  // run r0's start - c
-  uint32_t cn[RPL];
-  uint4 ea[RPL];
+  // level 1: each lane's runs' summaries (first S / first L candidate); the
+  // entry lists are read only for a run that a window boundary splits
+  uint32_t sm[RPL];
   auto load_batch = [&](uint64_t rb) {
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       const uint64_t r = rb + RPL * G.gl + k;
-      cn[k] = (cand && r <= r1) ? W.run_cnt[r] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {  // level 2: entries 0-3 of non-empty runs (~15 % on random data)
-      ea[k] = make_uint4(0, 0, 0, 0);
-      if (P.cap == 8 && cn[k] > 0 && cn[k] <= 8)
-        ea[k] = *reinterpret_cast<const uint4 *>(W.run_ent + (rb + RPL * G.gl + k) * 8ull);
+      sm[k] = (cand && r <= r1) ? W.run_sum[r] : 0u;
     }
   };
   // ---- level-1 loads, all independent
@@ -694,22 +716,44 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
   if (b) return t + G.bcast(first, (uint32_t)(__ffsll((unsigned long long)b) - 1));
   if (!cand) return c + remaining;
   // ---- (2) windowed candidates for [t + 47, c + re), 64 runs per batch
-  const uint64_t lo = c + (uint64_t)lo_r, hi = c + (uint64_t)hi_r, cce = c + (uint64_t)cce_r;
+  const int32_t s_end = min(cce_r, hi_r), l_beg = max(lo_r, cce_r);  // S tested before cce, L from it
   for (uint64_t rb = r0; rb <= r1; rb += 64) {
     if (rb != r0) load_batch(rb);
     int32_t found = INT32_MAX;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
+      const uint32_t u = sm[k];
+      if (found != INT32_MAX || u == 0) continue;
       const uint64_t r = rb + RPL * G.gl + k;
       const int32_t rbase = base0 + (int32_t)((r - r0) * (uint64_t)kRun);
-      if (found != INT32_MAX || cn[k] == 0) continue;
-      if (cn[k] <= P.cap && P.cap == 8) {
-        found = run_first_rel(cn[k], ea[k], reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull) + 1, rbase,
-                              lo_r, hi_r, cce_r);
-      } else {  // overflowed run (rescan bytes) or a general entry list
-        const uint64_t f = run_first(W, P, gt, r, cn[k], ea[k], lo, hi, cce);
-        if (f != ~0ull) found = (int32_t)(f - c);
+      const uint32_t nc = u >> 28, fs1 = u & 0x3fffu, fl1 = (u >> 14) & 0x3fffu;
+      // The run's first S candidate is the first in [lo, s_end) unless it lies
+      // before lo and others follow; likewise its first L for [l_beg, hi).
+      int32_t res = INT32_MAX;
+      bool split = (fs1 | fl1) == 0;  // "unknown" (an overflowed lane-strided run)
+      if (fs1) {
+        const int32_t p = rbase + (int32_t)fs1 - 1;
+        if (p >= lo_r && p < s_end) res = p;
+        else split = p < lo_r && nc >= 2 && lo_r < s_end;
       }
+      if (res == INT32_MAX && !split && fl1) {
+        const int32_t p = rbase + (int32_t)fl1 - 1;
+        if (p >= l_beg && p < hi_r) res = p;
+        else split = p < l_beg && nc >= 2 && l_beg < hi_r;
+      }
+      if (split) {  // rare: the entry list (or, overflowed, the bytes) decides
+        const uint32_t cnt = W.run_cnt[r];
+        if (cnt <= P.cap && P.cap == 8) {
+          const uint4 ea = *reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
+          res = run_first_rel(cnt, ea, reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull) + 1, rbase, lo_r,
+                              hi_r, cce_r);
+        } else {
+          const uint64_t f = run_first(W, P, gt, r, cnt, make_uint4(0, 0, 0, 0), c + (uint64_t)lo_r,
+                                       c + (uint64_t)hi_r, c + (uint64_t)cce_r);
+          if (f != ~0ull) res = (int32_t)(f - c);
+        }
+      }
+      found = res;
     }
     const uint64_t fb = G.ballot(found != INT32_MAX);
     if (fb) return c + (uint64_t)G.bcast((uint64_t)(uint32_t)found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
