@@ -259,6 +259,36 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if (!out_dev && is_device_ptr(out))
     return fail(MCDC_E_INVALID, "out is a device pointer of another device");
 
+  // ---- scan workspace, and the scan itself for a single-part call ----
+  // The scan reads none of the segment tables, so a single-part call enqueues
+  // it before the host plans segments: planning (O(files)) overlaps the scan.
+  const uint64_t nruns = (n_al + kRun - 1) / kRun;
+  const uint64_t ntiles_full = (n_al / kRun) / 64;
+  if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
+  if ((rc = ensure(ctx, ctx->run_sum, nruns * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->tile_ctr, 64))) return rc;
+  Work W{};
+  W.base = base;
+  W.n_al = n_al;
+  W.nruns = nruns;
+  W.gear = ctx->d_gear;
+  W.gear16 = ctx->d_gear16;
+  W.run_cnt = (uint8_t *)ctx->run_cnt.p;
+  W.run_sum = (uint32_t *)ctx->run_sum.p;
+  W.run_ent = (uint32_t *)ctx->run_ent.p;
+  W.tile_ctr = env_int("MCDC_DYN_TILES", 1) ? (uint64_t *)ctx->tile_ctr.p : nullptr;
+  hipStream_t st = ctx->stream;
+  const bool early = std::min(std::max(env_int("MCDC_PARTS", 1), 1), kMaxParts) == 1;
+  if (early) {
+    HIP_TRY(hipEventRecord(ctx->ev_start, st));
+    if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
+    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, ntiles_full, true);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev_part[0], st));
+    HIP_TRY(hipEventRecord(ctx->ev_scan, st));
+  }
+
   // ---- plan segments (host; reused when the layout repeats) ----
   uint64_t total_bytes = 0, out_bound = 0;
   for (size_t i = 0; i < nfiles; ++i) {
@@ -299,13 +329,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     }
   }
   const uint32_t nsegs = (uint32_t)ctx->h_segs.size();
-  const uint64_t nruns = (n_al + kRun - 1) / kRun;
 
   // ---- workspace ----
   const void *tabs_before[3] = {ctx->segs.p, ctx->files.p, ctx->node_off.p};
-  if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
-  if ((rc = ensure(ctx, ctx->run_sum, nruns * 4))) return rc;
-  if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
   if ((rc = ensure(ctx, ctx->files, nfiles * sizeof(File)))) return rc;
   if ((rc = ensure(ctx, ctx->nodes, ctx->h_node_off.back() * sizeof(uint64_t)))) return rc;
@@ -331,17 +357,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if ((rc = ensure(ctx, ctx->err, 16))) return rc;
   const size_t tmpb = scan_tmp_bytes(nsegs);
   if ((rc = ensure(ctx, ctx->scan_tmp, tmpb))) return rc;
-  hipStream_t st = ctx->stream;
 
-  Work W{};
-  W.base = base;
-  W.n_al = n_al;
-  W.nruns = nruns;
-  W.gear = ctx->d_gear;
-  W.gear16 = ctx->d_gear16;
-  W.run_cnt = (uint8_t *)ctx->run_cnt.p;
-  W.run_sum = (uint32_t *)ctx->run_sum.p;
-  W.run_ent = (uint32_t *)ctx->run_ent.p;
   W.segs = (const Seg *)ctx->segs.p;
   W.nsegs = nsegs;
   W.nfiles = (uint32_t)nfiles;
@@ -371,8 +387,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
 
   if ((rc = ensure(ctx, ctx->seg_incl, (size_t)nsegs * 8))) return rc;
   if ((rc = ensure(ctx, ctx->irr, (size_t)nsegs * 5 + 16))) return rc;
-  if ((rc = ensure(ctx, ctx->tile_ctr, 64))) return rc;
-  W.tile_ctr = env_int("MCDC_DYN_TILES", 1) ? (uint64_t *)ctx->tile_ctr.p : nullptr;
   W.irr_n = (uint32_t *)ctx->irr.p;
   W.irr_list = (uint32_t *)ctx->irr.p + 4;
   W.irr_flag = (uint8_t *)ctx->irr.p + 16 + (size_t)nsegs * 4;
@@ -380,7 +394,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // ---- staged pipeline plan ----
   // parts: full tiles [tb[i], tb[i+1]); the last part also scans the partial tile
   const uint64_t tile_bytes = 64ull * kRun;
-  const uint64_t ntiles_full = (n_al / kRun) / 64;
   // (MCDC_PART_TILES / MCDC_MIN_ROUNDS shrink the round unit and the size
   // threshold so that tests exercise the staged path on small inputs)
   const uint64_t waves = (uint64_t)std::max(
@@ -435,14 +448,16 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // The scan needs none of the segment tables, so it is enqueued first; the
   // table uploads and workspace resets run on stream2 beside it.
   hipStream_t st2 = ctx->stream2;
-  HIP_TRY(hipEventRecord(ctx->ev_start, st));
-  for (int i = 0; i < K; ++i) {
-    if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
-    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
+  if (!early) {
+    HIP_TRY(hipEventRecord(ctx->ev_start, st));
+    for (int i = 0; i < K; ++i) {
+      if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
+      if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_scan, st));
   }
-  HIP_TRY(hipEventRecord(ctx->ev_scan, st));
   if (!ctx->plan_valid) {  // tables -> pinned stage -> one async copy each
     const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
                  b_noff = ctx->h_node_off.size() * 8;

@@ -256,6 +256,70 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan_t(Work W, DevParams P) {
   }
 }
 
+// One run scanned by a whole wave (the runs of a partial last tile): lane l
+// takes bytes [64 l, 64 l + 64) of the run after a 48-byte warm-up, so the
+// run costs ~112 dependent hash steps instead of 4096 on one lane.  Exact
+// S / L tests at every position; entries in position order (wave prefix sum
+// over the lanes' counts, then a second walk that stores the first `cap`),
+// count and summary as the main path writes them.
+__device__ __forceinline__ uint64_t coop_walk(const uint64_t *tab, uint32_t lo, const Work &W, uint64_t a0,
+                                              uint64_t s, uint64_t e, uint64_t ms16, uint64_t ml16, bool store,
+                                              uint32_t *ent, uint32_t base_idx,
+                                              uint32_t cap, uint64_t rs, uint32_t *fs, uint32_t *fl) {
+  uint64_t h = 0;
+  uint32_t k = 0;
+  for (uint64_t b = a0; b < e; b += 16) {
+    const uint4 d = *reinterpret_cast<const uint4 *>(W.base + b);
+    const uint32_t wd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      h = (h << 1) + lds_gear(tab, ((wd[i >> 2] >> (8 * (i & 3))) & 0xffu) << 8 | lo);
+      const uint64_t q = b + i;
+      if (q >= s && q < e) {
+        const uint32_t s_ = (h & ms16) == 0, l_ = (h & ml16) == 0;
+        if (s_ | l_) {
+          const uint32_t off = (uint32_t)(q - rs);
+          if (store && base_idx + k < cap) ent[base_idx + k] = off | (s_ << 31) | (l_ << 30);
+          if (s_ && *fs == 0xffffffffu) *fs = off;
+          if (l_ && *fl == 0xffffffffu) *fl = off;
+          ++k;
+        }
+      }
+    }
+  }
+  return k;
+}
+
+__device__ void scan_run_coop(const uint64_t *tab, uint32_t lo, const Work &W, const DevParams &P, uint64_t run,
+                              uint32_t lane) {
+  const uint64_t rs = run * (uint64_t)kRun, re = min(rs + (uint64_t)kRun, W.n_al);
+  const uint64_t s = rs + 64ull * lane, e = min(s + 64, re);
+  const uint64_t a0 = s >= 48 ? s - 48 : 0;  // (16-aligned: rs and 64 * lane are)
+  uint32_t *ent = W.run_ent + run * (uint64_t)P.cap;
+  uint32_t fs = 0xffffffffu, fl = 0xffffffffu, dummy_s = 0, dummy_l = 0;
+  uint32_t c = 0;
+  if (s < re) c = (uint32_t)coop_walk(tab, lo, W, a0, s, e, P.ms16, P.ml16, false, ent, 0, P.cap, rs, &fs, &fl);
+  uint32_t x = c;  // inclusive wave prefix of the counts
+#pragma unroll
+  for (unsigned d = 1; d < 64; d <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= d) x += v;
+  }
+  const uint32_t pre = x - c, total = (uint32_t)__shfl((int)x, 63, 64);
+  if (c && pre < P.cap)  // second walk: store this lane's entries that fall among the first cap
+    coop_walk(tab, lo, W, a0, s, e, P.ms16, P.ml16, true, ent, pre, P.cap, rs, &dummy_s, &dummy_l);
+  uint32_t mfs = fs, mfl = fl;
+#pragma unroll
+  for (unsigned d = 1; d < 64; d <<= 1) {
+    mfs = min(mfs, (uint32_t)__shfl_xor((int)mfs, d, 64));
+    mfl = min(mfl, (uint32_t)__shfl_xor((int)mfl, d, 64));
+  }
+  if (lane == 0) {
+    W.run_cnt[run] = total > P.cap ? kRunOverflow : (uint8_t)total;
+    W.run_sum[run] = run_summary(total, mfs, mfl);
+  }
+}
+
 // ---- Product scan (k_scan_q).  One wave = one tile of 64 runs (one per
 // lane).  Loads are quad-coalesced: lane quad i fetches one whole 64-byte line
 // of run (4i+k) per load instruction k (16 lines per wave-instruction instead
@@ -419,7 +483,9 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   q.lcnt[128 + lane] = 0xffffffffu;
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  // wave index, CU-major: the first gridDim.x tiles of a static round land on
+  // different CUs (a launch with fewer tiles than waves then uses every CU)
+  const uint64_t wid = (uint64_t)wv * gridDim.x + blockIdx.x;
   const uint64_t nfull = W.n_al / RUN;
   const uint64_t ntiles_full = nfull / 64;
   if (tile1 > ntiles_full) tile1 = ntiles_full;
@@ -434,13 +500,22 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   // or, with W.tile_ctr, in request order from one atomic counter: waves that
   // run fast take more tiles, so the launch ends without a ragged last round.
   // The next index is requested when a tile starts, so its latency is hidden.
-  const bool dyn = W.tile_ctr != nullptr;
+  // (static when every wave gets at most one tile: nothing to balance)
+  const bool dyn = W.tile_ctr != nullptr && tile1 - tile0 > nwaves;
   auto grab = [&]() -> uint64_t {
     uint64_t v = 0;
     if (lane == 0) v = atomicAdd(reinterpret_cast<unsigned long long *>(W.tile_ctr), 1ull);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return tile0 + (((uint64_t)hi << 32) | lo);
   };
+  // The runs of the partial last tile (< 64) are taken first, one per wave
+  // (scan_run_coop), so they overlap the full tiles instead of trailing them
+  // (a 1.3 GB call: scan 0.80 -> ~0.4 ms).
+  if (do_tail) {  // one wave per run, the last waves first (in a static round they have the fewest tiles)
+    const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
+    for (uint64_t run = ntiles_full * 64 + (nwaves - 1 - wid); run < nruns; run += nwaves)
+      scan_run_coop(q.tab, q.lo, W, P, run, lane);
+  }
   uint64_t t = dyn ? grab() : tile0 + wid;
   while (t < tile1) {
     const uint64_t t_next = dyn ? grab() : t + nwaves;
@@ -504,14 +579,6 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     W.run_sum[run] = run_summary(cnt, fs, fl);
     t = t_next;
   }
-  // partial last tile: lane-strided runs, exact per-lane path
-  if (!do_tail) return;
-  const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
-  for (uint64_t t = ntiles_full + wid; t * 64 < nruns; t += nwaves) {
-    const uint64_t run = t * 64 + lane;
-    if (run < nfull) scan_run_full<RUN, 1>(q.tab, q.lo, W, P, run, run);
-    else if (run < nruns) scan_run_tail<RUN>(q.tab, q.lo, W, P, run);
-  }
 }
 
 // Product configuration: quad-coalesced scan, 16 waves (one 1024-thread
@@ -520,8 +587,8 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
                  uint64_t tile1, bool tail) {
   const uint64_t ntiles = tail ? (w.nruns + 63) / 64 - tile0 : tile1 - tile0;
-  uint64_t blocks = (ntiles + 15) / 16;
-  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);  // 148 KiB LDS -> 1 block/CU
+  uint64_t blocks = ntiles;  // one block per CU up to the CU count (156 KiB LDS -> 1 block/CU)
+  const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return;
   hipLaunchKernelGGL(k_scan_q<kRun>, dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1,
@@ -529,7 +596,7 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
 }
 
 uint64_t scan_waves(uint64_t ntiles, int num_cus) {
-  uint64_t blocks = (ntiles + 15) / 16;
+  uint64_t blocks = ntiles;
   const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);
   return 16 * (blocks > cap ? cap : blocks);
 }
