@@ -196,6 +196,8 @@ int main(int argc, char **argv) {
   uint32_t *ent, *sink;
   CK(hipMalloc(&cnt, nruns_max));
   CK(hipMalloc(&ent, nruns_max * 8 * 4));
+  uint32_t *sum;
+  CK(hipMalloc(&sum, nruns_max * 4));
   CK(hipMalloc(&sink, 64));
   DevParams P{};
   P.min = 16384; P.avg = 65536; P.max = 262144; P.cap = 8;
@@ -203,7 +205,7 @@ int main(int argc, char **argv) {
   P.ms16 = P.ms << 16; P.ml16 = P.ml << 16;
   P.pf_hi = (uint32_t)((P.ms & P.ml) >> 16);
   Work W{};
-  W.base = d; W.n_al = n; W.gear16 = dg16; W.run_cnt = cnt; W.run_ent = ent;
+  W.base = d; W.n_al = n; W.gear16 = dg16; W.run_cnt = cnt; W.run_ent = ent; W.run_sum = sum;
   W.nruns = (n + kRun - 1) / kRun;
   CK(hipStreamSynchronize(st));
   auto report = [&](const char *name, float med, float best) {
