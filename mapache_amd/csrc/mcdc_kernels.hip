@@ -689,6 +689,24 @@ struct Group {
     const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, GS);
     return ((uint64_t)hi << 32) | lo;
   }
+  // GS == 16 (a DPP row): v of lane gl - D, 0 for gl < D — DPP row_shr (a VALU
+  // move, no LDS crossbar round trip like ds_bpermute)
+  template <int D>
+  __device__ __forceinline__ uint64_t up0(uint64_t v) const {
+    static_assert(GS == 16 && D >= 1 && D <= 15, "row shift");
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x110 | D, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x110 | D, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+  }
+  // GS == 16: minimum over the row, in every lane (DPP row_ror butterfly)
+  __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) const {
+    static_assert(GS == 16, "row reduction");
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false));  // row_ror:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false));  // row_ror:2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false));  // row_ror:1
+    return v;
+  }
 };
 
 // Candidate search of one run in chunk-relative int32 coordinates (positions
@@ -765,13 +783,22 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
     loc[k] = acc;
   }
   uint64_t x = acc;  // hash at this lane's last position: shift-scan over the group
+  uint64_t excl;     // hash at the previous lane's last position
+  if constexpr (GS == 16) {
+    x += G.template up0<1>(x) << PPL;
+    x += G.template up0<2>(x) << (2 * PPL);
+    x += G.template up0<4>(x) << (4 * PPL);
+    x += G.template up0<8>(x) << (8 * PPL);
+    excl = G.template up0<1>(x);
+  } else {
 #pragma unroll
-  for (unsigned d = 1; d < (unsigned)GS; d <<= 1) {
-    const uint64_t v = G.up(x, d);
-    if (G.gl >= d) x += v << (PPL * d);
+    for (unsigned d = 1; d < (unsigned)GS; d <<= 1) {
+      const uint64_t v = G.up(x, d);
+      if (G.gl >= d) x += v << (PPL * d);
+    }
+    excl = G.up(x, 1);
+    if (G.gl == 0) excl = 0;
   }
-  uint64_t excl = G.up(x, 1);  // hash at the previous lane's last position
-  if (G.gl == 0) excl = 0;
   uint32_t first = 0xffffffffu;
 #pragma unroll
   for (int k = PPL - 1; k >= 0; --k) {
@@ -779,8 +806,13 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
     const uint64_t h = (excl << (k + 1)) + loc[k];
     if (idx < wlen && (h & ((t0 + idx < ce) ? P.ms : P.ml)) == 0) first = idx;
   }
-  const uint64_t b = G.ballot(first != 0xffffffffu);
-  if (b) return t + G.bcast(first, (uint32_t)(__ffsll((unsigned long long)b) - 1));
+  if constexpr (GS == 16) {  // lanes own increasing positions: the first hit is the row minimum
+    const uint32_t m = G.row_min_u32(first);
+    if (m != 0xffffffffu) return t + m;
+  } else {
+    const uint64_t b = G.ballot(first != 0xffffffffu);
+    if (b) return t + G.bcast(first, (uint32_t)(__ffsll((unsigned long long)b) - 1));
+  }
   if (!cand) return c + remaining;
   // ---- (2) windowed candidates for [t + 47, c + re), 64 runs per batch
   const int32_t s_end = min(cce_r, hi_r), l_beg = max(lo_r, cce_r);  // S tested before cce, L from it
@@ -822,8 +854,13 @@ __device__ uint64_t group_next(const Group<GS> &G, const Work &W, const DevParam
       }
       found = res;
     }
-    const uint64_t fb = G.ballot(found != INT32_MAX);
-    if (fb) return c + (uint64_t)G.bcast((uint64_t)(uint32_t)found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
+    if constexpr (GS == 16) {  // (found >= 0 or INT32_MAX: unsigned order = signed order)
+      const uint32_t m = G.row_min_u32((uint32_t)found);
+      if (m != (uint32_t)INT32_MAX) return c + (uint64_t)m;
+    } else {
+      const uint64_t fb = G.ballot(found != INT32_MAX);
+      if (fb) return c + (uint64_t)G.bcast((uint64_t)(uint32_t)found, (uint32_t)(__ffsll((unsigned long long)fb) - 1));
+    }
   }
   return c + remaining;  // forced cut (e.g. all zeros)
 }
