@@ -356,3 +356,18 @@ def test_staged_pipeline_batch(ctx, staged):
     ref, rc = O.chunk_files(O.Params(*PARAMS[0]), files)
     _same(out, ref)
     assert (counts == rc).all()
+
+
+def test_call_larger_than_context_fails_loudly():
+    """A context bounds the bytes of one call (max_bytes sizes its workspace):
+    a larger call reports MCDC_E_TOOBIG instead of allocating past it; a
+    call within the bound on the same context still works."""
+    small = _lib.Context(0, 1 << 20)
+    try:
+        d = O.random_bytes((1 << 20) + 1, 41)
+        with pytest.raises(_lib.McdcError) as e:
+            small.chunk_host(_lib.params(*PARAMS[2]), d)
+        assert e.value.code == -6
+        _same(small.chunk_host(_lib.params(*PARAMS[2]), d[:1 << 20]), O.chunk(O.Params(*PARAMS[2]), d[:1 << 20]))
+    finally:
+        small.close()
