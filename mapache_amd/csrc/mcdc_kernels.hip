@@ -378,7 +378,14 @@ __device__ __forceinline__ void chain4(const uint64_t *g, uint64_t &h, uint32_t 
   acc = min(min(acc, m2), m3);
 }
 
-// Drain the wave's queue: lane i re-walks entry i's 16 bytes exactly.
+// Prefilter block: dwords per wave-uniform test (and per queued block).
+#ifndef MCDC_QBLK_DW
+#define MCDC_QBLK_DW 4
+#endif
+constexpr int kQBlkDw = MCDC_QBLK_DW;
+static_assert(kQBlkDw == 4 || kQBlkDw == 8, "16- or 32-byte prefilter blocks");
+
+// Drain the wave's queue: lane i re-walks entry i's block exactly.
 template <int RUN>
 __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t lo, const uint8_t *base,
                                                   uint32_t *run_ent, uint64_t ms16, uint64_t ml16, uint32_t cap,
@@ -390,11 +397,15 @@ __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t 
     const uint32_t meta = *reinterpret_cast<const uint32_t *>(slot + 8);
     const uint32_t rl = meta >> 16, off = meta & 0xffffu;
     const uint64_t run = run0 + rl;
-    const uint4 d = *reinterpret_cast<const uint4 *>(base + run * (uint64_t)RUN + off);
     uint32_t *ent = run_ent + run * (uint64_t)cap;
-    const uint32_t wd[4] = {d.x, d.y, d.z, d.w};
+    uint32_t wd[kQBlkDw];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int j = 0; j < kQBlkDw / 4; ++j) {
+      const uint4 d = *reinterpret_cast<const uint4 *>(base + run * (uint64_t)RUN + off + 16 * j);
+      wd[4 * j] = d.x; wd[4 * j + 1] = d.y; wd[4 * j + 2] = d.z; wd[4 * j + 3] = d.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * kQBlkDw; ++i) {
       x = (x << 1) + lds_gear(tab, ((wd[i >> 2] >> (8 * (i & 3))) & 0xffu) << 8 | lo);
       const uint32_t s_ = (x & ms16) == 0, l_ = (x & ml16) == 0;
       if (s_ | l_) {
@@ -418,7 +429,8 @@ struct QScan {  // per-wave state of k_scan_q
 };
 
 // 64 bytes (16 dwords) of one run: lookups one dword ahead of the chain;
-// every 16 bytes a wave-uniform test queues the blocks whose prefilter fired.
+// every prefilter block (4 kQBlkDw bytes) a wave-uniform test queues the
+// blocks whose prefilter fired.
 template <int RUN>
 __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint64_t &h, uint32_t off,
                                         uint32_t &qn, uint64_t run0) {
@@ -436,7 +448,7 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
     else __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     chain4(g[d & 1], h, acc, q.pf);
-    if (d % 4 == 3) {
+    if (d % kQBlkDw == kQBlkDw - 1) {
       const uint64_t m = __ballot(acc == 0);
       if (__builtin_expect(m != 0, 0)) {
         const uint32_t n = (uint32_t)__popcll(m);
@@ -449,7 +461,7 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
               qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
           char *sp = q.pad + slot * kQPad + 64;
           *reinterpret_cast<uint64_t *>(sp) = hb;
-          *reinterpret_cast<uint32_t *>(sp + 8) = (q.lane << 16) | (off + 4 * (d - 3));
+          *reinterpret_cast<uint32_t *>(sp + 8) = (q.lane << 16) | (off + 4 * (d - (kQBlkDw - 1)));
         }
         qn += n;
       }
