@@ -278,12 +278,15 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.run_sum = (uint32_t *)ctx->run_sum.p;
   W.run_ent = (uint32_t *)ctx->run_ent.p;
   W.tile_ctr = env_int("MCDC_DYN_TILES", 1) ? (uint64_t *)ctx->tile_ctr.p : nullptr;
+  W.first_static = env_int("MCDC_FIRST_STATIC", 1) ? 1u : 0u;
   hipStream_t st = ctx->stream;
   const bool early = std::min(std::max(env_int("MCDC_PARTS", 1), 1), kMaxParts) == 1;
   if (early) {
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
     if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
-    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, ntiles_full, true);
+    int pc = env_int("MCDC_SCAN_PIECES", 0);
+    if (pc != 1 && pc != 2 && pc != 4) pc = scan_pieces(n_al / kRun, ctx->num_cus);
+    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, (n_al / kRun) / (64 / pc), true, pc);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_part[0], st));
     HIP_TRY(hipEventRecord(ctx->ev_scan, st));

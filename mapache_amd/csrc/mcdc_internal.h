@@ -82,6 +82,7 @@ struct Work {
   uint32_t *run_sum;     // [nruns] run summary: first S / first L candidate (see run_summary)
   uint32_t *run_ent;     // [nruns * cap]: off | S<<31 | L<<30
   uint64_t *tile_ctr;    // scan tile counter (dynamic tile order) or nullptr (static)
+  uint32_t first_static; // dynamic order: each wave's first tile is its static one, the counter hands out the rest
 
   const Seg *segs;
   uint32_t nsegs, nfiles;
@@ -118,7 +119,8 @@ struct Work {
 void launch_fill_random(void *dst, uint64_t pos, uint64_t n, uint64_t seed, hipStream_t stream);
 // scan of full tiles [tile0, tile1) (+ the partial last tile when `tail`)
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
-                 uint64_t tile1, bool tail);
+                 uint64_t tile1, bool tail, int pieces = 1);
+int scan_pieces(uint64_t nruns_full, int num_cus);  // lane pieces per run for a whole-call scan
 uint64_t scan_waves(uint64_t ntiles, int num_cus);  // waves of a scan launch over ntiles
 void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream);
 // node_cap: expanded continuation nodes per segment (~0 when everything is scanned)

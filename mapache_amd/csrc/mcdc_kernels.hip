@@ -386,16 +386,19 @@ constexpr int kQBlkDw = MCDC_QBLK_DW;
 static_assert(kQBlkDw == 4 || kQBlkDw == 8, "16- or 32-byte prefilter blocks");
 
 // Drain the wave's queue: lane i re-walks entry i's block exactly.
-template <int RUN>
+// PC pieces per run: lane l hashes bytes [l*SUB, (l+1)*SUB) of the tile, part
+// l % PC of run run0 + l / PC; offsets and counters are per run.
+template <int RUN, int PC>
 __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t lo, const uint8_t *base,
                                                   uint32_t *run_ent, uint64_t ms16, uint64_t ml16, uint32_t cap,
                                                   const char *pad, uint32_t *lcnt, uint32_t qn, uint64_t run0,
                                                   uint32_t lane) {
+  constexpr int SUB = RUN / PC;
   if (lane < qn) {
     const char *slot = pad + lane * kQPad + 64;
     uint64_t x = *reinterpret_cast<const uint64_t *>(slot);
     const uint32_t meta = *reinterpret_cast<const uint32_t *>(slot + 8);
-    const uint32_t rl = meta >> 16, off = meta & 0xffffu;
+    const uint32_t pl = meta >> 16, rl = pl / PC, off = (pl % PC) * SUB + (meta & 0xffffu);
     const uint64_t run = run0 + rl;
     uint32_t *ent = run_ent + run * (uint64_t)cap;
     uint32_t wd[kQBlkDw];
@@ -431,7 +434,7 @@ struct QScan {  // per-wave state of k_scan_q
 // 64 bytes (16 dwords) of one run: lookups one dword ahead of the chain;
 // every prefilter block (4 kQBlkDw bytes) a wave-uniform test queues the
 // blocks whose prefilter fired.
-template <int RUN>
+template <int RUN, int PC>
 __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint64_t &h, uint32_t off,
                                         uint32_t &qn, uint64_t run0) {
   uint64_t g[2][4];
@@ -453,7 +456,7 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
       if (__builtin_expect(m != 0, 0)) {
         const uint32_t n = (uint32_t)__popcll(m);
         if (qn + n > 64) {
-          q_drain<RUN>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, q.lane);
+          q_drain<RUN, PC>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, q.lane);
           qn = 0;
         }
         if (acc == 0) {
@@ -471,7 +474,7 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
   }
 }
 
-template <int RUN>
+template <int RUN, int PC>
 __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_t tile0, uint64_t tile1,
                                                    int do_tail) {
   __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8];
@@ -498,43 +501,48 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   // wave index, CU-major: the first gridDim.x tiles of a static round land on
   // different CUs (a launch with fewer tiles than waves then uses every CU)
   const uint64_t wid = (uint64_t)wv * gridDim.x + blockIdx.x;
+  constexpr int SUB = RUN / PC, RPT = 64 / PC;  // bytes per lane piece, runs per tile
   const uint64_t nfull = W.n_al / RUN;
-  const uint64_t ntiles_full = nfull / 64;
+  const uint64_t ntiles_full = nfull / RPT;
   if (tile1 > ntiles_full) tile1 = ntiles_full;
-  constexpr int G = RUN / 64;
+  constexpr int G = SUB / 64;
   static_assert(G % 2 == 0, "even group count");
   const uint32_t qi = lane >> 2, qj = lane & 3;
   // load k: lane (4i+j) fetches piece j of run 4i+k; it lands in the pad at run*80 + 16j
   char *wr = q.pad + 4 * qi * kQPad + 16 * qj;
   const char *rd = q.pad + lane * kQPad;
-  const uint32_t o0 = 4 * qi * RUN + 16 * qj;  // lane's byte offset in the tile for load 0, group 0
+  const uint32_t o0 = 4 * qi * SUB + 16 * qj;  // lane's byte offset in the tile for load 0, group 0
   // Tiles are handed out either statically (wave w: tiles w, w + nwaves, ...)
   // or, with W.tile_ctr, in request order from one atomic counter: waves that
   // run fast take more tiles, so the launch ends without a ragged last round.
   // The next index is requested when a tile starts, so its latency is hidden.
   // (static when every wave gets at most one tile: nothing to balance)
+  // With first_static the first tile of every wave is its static one and the
+  // counter hands out tiles from tile0 + nwaves on: the launch does not start
+  // with every wave queued on one atomic before its first load.
   const bool dyn = W.tile_ctr != nullptr && tile1 - tile0 > nwaves;
+  const uint64_t dyn0 = tile0 + (W.first_static ? nwaves : 0);
   auto grab = [&]() -> uint64_t {
     uint64_t v = 0;
     if (lane == 0) v = atomicAdd(reinterpret_cast<unsigned long long *>(W.tile_ctr), 1ull);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return tile0 + (((uint64_t)hi << 32) | lo);
+    return dyn0 + (((uint64_t)hi << 32) | lo);
   };
   // The runs of the partial last tile (< 64) are taken first, one per wave
   // (scan_run_coop), so they overlap the full tiles instead of trailing them
   // (a 1.3 GB call: scan 0.80 -> ~0.4 ms).
   if (do_tail) {  // one wave per run, the last waves first (in a static round they have the fewest tiles)
     const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
-    for (uint64_t run = ntiles_full * 64 + (nwaves - 1 - wid); run < nruns; run += nwaves)
+    for (uint64_t run = ntiles_full * RPT + (nwaves - 1 - wid); run < nruns; run += nwaves)
       scan_run_coop(q.tab, q.lo, W, P, run, lane);
   }
-  uint64_t t = dyn ? grab() : tile0 + wid;
+  uint64_t t = dyn && !W.first_static ? grab() : tile0 + wid;
   while (t < tile1) {
     const uint64_t t_next = dyn ? grab() : t + nwaves;
-    const uint64_t run0 = t * 64, run = run0 + lane;
+    const uint64_t run0 = t * RPT, piece = t * 64 + lane;
     uint64_t h = 0;
-    if (run > 0) {  // warm-up: the 48 bytes before the run complete every window
-      const uint4 *p = reinterpret_cast<const uint4 *>(W.base + run * (uint64_t)RUN);
+    if (piece > 0) {  // warm-up: the 48 bytes before the piece complete every window
+      const uint4 *p = reinterpret_cast<const uint4 *>(W.base + piece * (uint64_t)SUB);
       const uint4 w0 = p[-3], w1 = p[-2], w2 = p[-1];
       hash16(q.tab, q.lo, w0, h);
       hash16(q.tab, q.lo, w1, h);
@@ -542,7 +550,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     }
     uint32_t qn = 0;  // wave-uniform queue length
     const uint8_t *tb = W.base + run0 * (uint64_t)RUN;  // wave-uniform tile base (SGPR)
-#define MCDC_LDQ(k, gg) (*reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * RUN + 64 * (gg))))
+#define MCDC_LDQ(k, gg) (*reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * SUB + 64 * (gg))))
     uint4 a0 = MCDC_LDQ(0, 0), a1 = MCDC_LDQ(1, 0), a2 = MCDC_LDQ(2, 0), a3 = MCDC_LDQ(3, 0);
     uint4 b0 = MCDC_LDQ(0, 1), b1 = MCDC_LDQ(1, 1), b2 = MCDC_LDQ(2, 1), b3 = MCDC_LDQ(3, 1);
 #pragma unroll 1
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
         const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        scan64q<RUN>(q, w, h, 64u * g, qn, run0);
+        scan64q<RUN, PC>(q, w, h, 64u * g, qn, run0);
       }
       {
         *reinterpret_cast<uint4 *>(wr) = b0;
@@ -578,17 +586,20 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
         a2 = MCDC_LDQ(2, ga); b2 = MCDC_LDQ(2, gb); a3 = MCDC_LDQ(3, ga); b3 = MCDC_LDQ(3, gb);
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        scan64q<RUN>(q, w, h, 64u * (g + 1), qn, run0);
+        scan64q<RUN, PC>(q, w, h, 64u * (g + 1), qn, run0);
       }
     }
 #undef MCDC_LDQ
-    if (qn) q_drain<RUN>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
+    if (qn) q_drain<RUN, PC>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
     const uint32_t cnt = q.lcnt[lane], fs = q.lcnt[64 + lane], fl = q.lcnt[128 + lane];
     q.lcnt[lane] = 0;
     q.lcnt[64 + lane] = 0xffffffffu;
     q.lcnt[128 + lane] = 0xffffffffu;
-    W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
-    W.run_sum[run] = run_summary(cnt, fs, fl);
+    if (PC == 1 || lane < RPT) {
+      const uint64_t run = run0 + lane;
+      W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
+      W.run_sum[run] = run_summary(cnt, fs, fl);
+    }
     t = t_next;
   }
 }
@@ -596,15 +607,35 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
 // Product configuration: quad-coalesced scan, 16 waves (one 1024-thread
 // block) per CU; tools/scanbench.hip keeps the lane-strided k_scan_t variants
 // for comparison.
+// Tiles are in units of 64 / pieces runs (pieces = lane pieces per run).
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
-                 uint64_t tile1, bool tail) {
-  const uint64_t ntiles = tail ? (w.nruns + 63) / 64 - tile0 : tile1 - tile0;
+                 uint64_t tile1, bool tail, int pieces) {
+  const uint64_t rpt = 64 / (uint64_t)pieces;
+  const uint64_t ntiles = tail ? (w.nruns + rpt - 1) / rpt - tile0 : tile1 - tile0;
   uint64_t blocks = ntiles;  // one block per CU up to the CU count (156 KiB LDS -> 1 block/CU)
   const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return;
-  hipLaunchKernelGGL(k_scan_q<kRun>, dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1,
-                     tail ? 1 : 0);
+  const int t = tail ? 1 : 0;
+  if (pieces == 4)
+    hipLaunchKernelGGL((k_scan_q<kRun, 4>), dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1, t);
+  else if (pieces == 2)
+    hipLaunchKernelGGL((k_scan_q<kRun, 2>), dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1, t);
+  else
+    hipLaunchKernelGGL((k_scan_q<kRun, 1>), dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1, t);
+}
+
+// Lane pieces per run for a whole-call scan of nruns_full full runs.  A tile
+// (64 lane pieces) is 256 KiB at one piece per run, 128 KiB at two.  Measured
+// (tools/pieces_big.py, device time, first tiles static): two pieces are
+// faster at every size from 0.25 to 64 GiB (64 GiB 12.48 -> 12.37 ms; 80 000
+// small files 0.57 -> 0.52 ms; 2 GiB -9 %) except a call of more than half
+// and at most one round of one-piece tiles (1 GiB: 0.24 vs 0.28 ms); four
+// pieces (48-byte warm-up per KiB) never won.
+int scan_pieces(uint64_t nruns_full, int num_cus) {
+  const uint64_t waves = 16ull * (uint64_t)(num_cus > 0 ? num_cus : 256);
+  const uint64_t tiles1 = nruns_full / 64;  // tiles at one piece per run
+  return (tiles1 * 2 > waves && tiles1 <= waves) ? 1 : 2;
 }
 
 uint64_t scan_waves(uint64_t ntiles, int num_cus) {

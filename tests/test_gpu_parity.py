@@ -371,3 +371,27 @@ def test_call_larger_than_context_fails_loudly():
         _same(small.chunk_host(_lib.params(*PARAMS[2]), d[:1 << 20]), O.chunk(O.Params(*PARAMS[2]), d[:1 << 20]))
     finally:
         small.close()
+
+
+@pytest.mark.parametrize("pieces", [1, 2, 4])
+def test_scan_lane_pieces(ctx, monkeypatch, pieces):
+    """Every lane-piece variant of the scan (a 4 KiB run hashed by 1, 2 or 4
+    lanes; the library picks by call size) on the same inputs: edge sizes
+    around the tile and run grid, a partial last tile, overflowed runs whose
+    candidates come from several lanes, and a batch of ragged files."""
+    monkeypatch.setenv("MCDC_SCAN_PIECES", str(pieces))
+    for p in [PARAMS[0], PARAMS[2], PARAMS[6]]:
+        for n in [47, 1023, 1024, 1025, 4097, (256 << 10) + 1, (64 << 20) + 4096 * 17 + 3, (200 << 20) + 12345]:
+            d = O.random_bytes(n, SEED + 31 * n)
+            _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+        b = _find_dense_byte(p)
+        if b is not None:
+            d = np.full((5 << 20) + 77, b, np.uint8)
+            _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    rng = np.random.default_rng(11)
+    files = [O.random_bytes(int(s), 500 + i) for i, s in enumerate(rng.integers(0, 3 << 20, 120))]
+    p = PARAMS[0]
+    g, gc = ctx.chunk_batch(_lib.params(*p), files)
+    r, rc = O.chunk_files(O.Params(*p), files, threads=4)
+    assert (gc == rc).all()
+    _same(g, r)
