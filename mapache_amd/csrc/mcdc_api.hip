@@ -150,6 +150,9 @@ struct mcdc_ctx {
   std::vector<uint64_t> plan_key;
   bool plan_valid = false;
   uint64_t *h_res = nullptr;  // pinned call summary written by k_finish
+  uint64_t *h_fcnt = nullptr;  // pinned chunks-per-file, written by k_file_counts
+  uint64_t *d_fcnt = nullptr;  // its device alias
+  size_t h_fcnt_cap = 0;       // entries
   uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
@@ -210,6 +213,26 @@ int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
     return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", alloc);
   }
   ctx->h_tab_cap = alloc;
+  return MCDC_OK;
+}
+
+int ensure_fcnt(mcdc_ctx *ctx, size_t n) {
+  if (ctx->h_fcnt_cap >= n) return MCDC_OK;
+  if (ctx->h_fcnt) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipHostFree(ctx->h_fcnt));
+    ctx->h_fcnt = nullptr;
+    ctx->h_fcnt_cap = 0;
+  }
+  const size_t alloc = (n + n / 4 + 511) / 512 * 512;
+  if (hipHostMalloc((void **)&ctx->h_fcnt, alloc * 8, hipHostMallocDefault) != hipSuccess) {
+    ctx->h_fcnt = nullptr;
+    (void)hipGetLastError();
+    return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", alloc * 8);
+  }
+  HIP_TRY(hipHostGetDevicePointer((void **)&ctx->d_fcnt, ctx->h_fcnt, 0));
+  ctx->h_fcnt_cap = alloc;
   return MCDC_OK;
 }
 
@@ -477,6 +500,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tbuf + o_noff, b_noff, hipMemcpyHostToDevice, st2));
     ctx->plan_valid = true;
   }
+  const bool want_counts = counts && nfiles;
+  if (want_counts && (rc = ensure_fcnt(ctx, nfiles))) return rc;
   if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st2));
   HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st2));
   HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
@@ -491,6 +516,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(ctx->ev_end, st2));
+  if (want_counts) launch_file_counts(W, ctx->d_fcnt, st2);
   launch_finish(W, ctx->d_res, st2);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st2));
@@ -502,6 +528,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     launch_resolve_general(W, P, ctx->scan_tmp.p, tmpb, st2);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_end, st2));
+    if (want_counts) launch_file_counts(W, ctx->d_fcnt, st2);
     launch_finish(W, ctx->d_res, st2);
     HIP_TRY(hipGetLastError());
   }
@@ -521,22 +548,10 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st2));
     copies = true;
   }
-  std::vector<uint64_t> seg_off;
-  if (counts && nfiles) {
-    seg_off.resize(nsegs + 1);
-    if (nsegs) {
-      HIP_TRY(hipMemcpyAsync(seg_off.data(), ctx->seg_off.p, (nsegs + 1) * 8, hipMemcpyDeviceToHost, st2));
-      copies = true;
-    }
-  }
   if (copies) HIP_TRY(hipStreamSynchronize(st2));
   const double t_d2h1 = now_ms();
-  if (counts) {
-    for (size_t i = 0; i < nfiles; ++i) {
-      const File &F = ctx->h_files[i];
-      counts[i] = F.nsegs ? (size_t)(seg_off[F.first_seg + F.nsegs] - seg_off[F.first_seg]) : 0;
-    }
-  }
+  static_assert(sizeof(size_t) == sizeof(uint64_t), "counts are 64-bit");
+  if (want_counts) std::memcpy(counts, ctx->h_fcnt, nfiles * sizeof(uint64_t));
   float scan_ms = 0, dev_ms = 0;
   HIP_TRY(hipEventElapsedTime(&scan_ms, ctx->ev_start, ctx->ev_scan));
   HIP_TRY(hipEventElapsedTime(&dev_ms, ctx->ev_start, ctx->ev_end));
@@ -621,6 +636,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
+  if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,

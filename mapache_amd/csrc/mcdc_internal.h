@@ -132,5 +132,6 @@ void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, s
                             hipStream_t stream);
 size_t scan_tmp_bytes(uint32_t nsegs);
 void launch_finish(const Work &w, uint64_t *res, hipStream_t stream);
+void launch_file_counts(const Work &w, uint64_t *dst, hipStream_t stream);  // chunks per file -> dst
 
 }  // namespace mcdc
