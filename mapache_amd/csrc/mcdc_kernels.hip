@@ -434,25 +434,28 @@ struct QScan {  // per-wave state of k_scan_q
 // 64 bytes (16 dwords) of one run: lookups one dword ahead of the chain;
 // every prefilter block (4 kQBlkDw bytes) a wave-uniform test queues the
 // blocks whose prefilter fired.
-template <int RUN, int PC>
+// ND dwords (16: one 64-byte group; 12: the re-walked first 48 bytes of a
+// cold-started piece).  skip3: the first 48 positions of a cold-started piece
+// hold incomplete windows; their blocks are not tested here (see k_scan_q).
+template <int RUN, int PC, int ND = 16>
 __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint64_t &h, uint32_t off,
-                                        uint32_t &qn, uint64_t run0) {
+                                        uint32_t &qn, uint64_t run0, bool skip3 = false) {
   uint64_t g[2][4];
   lookup4(q.tab, q.lo, w[0], g[0]);
   uint32_t acc = 0xffffffffu;
   uint64_t hb = h;
 #pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    if (d + 1 < 16) lookup4(q.tab, q.lo, w[d + 1], g[(d + 1) & 1]);
+  for (int d = 0; d < ND; ++d) {
+    if (d + 1 < ND) lookup4(q.tab, q.lo, w[d + 1], g[(d + 1) & 1]);
     __builtin_amdgcn_sched_barrier(0);
     // one wait per dword for its 4 lookups (the next dword's 4 stay in flight)
     // instead of the compiler's one wait per lookup
-    if (d + 1 < 16) __builtin_amdgcn_s_waitcnt(kWaitLgkm4);
+    if (d + 1 < ND) __builtin_amdgcn_s_waitcnt(kWaitLgkm4);
     else __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     chain4(g[d & 1], h, acc, q.pf);
     if (d % kQBlkDw == kQBlkDw - 1) {
-      const uint64_t m = __ballot(acc == 0);
+      const uint64_t m = (d < 12 && skip3) ? 0ull : __ballot(acc == 0);
       if (__builtin_expect(m != 0, 0)) {
         const uint32_t n = (uint32_t)__popcll(m);
         if (qn + n > 64) {
@@ -474,7 +477,12 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
   }
 }
 
-template <int RUN, int PC>
+// CW (cold warm-up): a piece starts from h = 0 instead of re-reading the 48
+// bytes before it; its first 48 bytes stay in registers and are re-walked at
+// the end of the tile from the previous lane's final hash (the state after
+// the previous piece), so the previous piece's last line is fetched once.
+// Lane 0 still warms up from memory (the previous tile is another wave's).
+template <int RUN, int PC, bool CW>
 __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_t tile0, uint64_t tile1,
                                                    int do_tail) {
   __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8];
@@ -540,14 +548,16 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   while (t < tile1) {
     const uint64_t t_next = dyn ? grab() : t + nwaves;
     const uint64_t run0 = t * RPT, piece = t * 64 + lane;
-    uint64_t h = 0;
-    if (piece > 0) {  // warm-up: the 48 bytes before the piece complete every window
+    uint64_t h = 0, hw = 0;
+    if (piece > 0 && (!CW || lane == 0)) {  // warm-up: the 48 bytes before the piece complete every window
       const uint4 *p = reinterpret_cast<const uint4 *>(W.base + piece * (uint64_t)SUB);
       const uint4 w0 = p[-3], w1 = p[-2], w2 = p[-1];
-      hash16(q.tab, q.lo, w0, h);
-      hash16(q.tab, q.lo, w1, h);
-      hash16(q.tab, q.lo, w2, h);
+      hash16(q.tab, q.lo, w0, hw);
+      hash16(q.tab, q.lo, w1, hw);
+      hash16(q.tab, q.lo, w2, hw);
     }
+    if (!CW) h = hw;
+    uint4 f0, f1, f2;  // CW: the piece's first 48 bytes
     uint32_t qn = 0;  // wave-uniform queue length
     const uint8_t *tb = W.base + run0 * (uint64_t)RUN;  // wave-uniform tile base (SGPR)
 #define MCDC_LDQ(k, gg) (*reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * SUB + 64 * (gg))))
@@ -566,7 +576,8 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
         const uint4 c3 = *reinterpret_cast<const uint4 *>(rd + 48);
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        scan64q<RUN, PC>(q, w, h, 64u * g, qn, run0);
+        if (CW && g == 0) { f0 = c0; f1 = c1; f2 = c2; }
+        scan64q<RUN, PC>(q, w, h, 64u * g, qn, run0, CW && g == 0);
       }
       {
         *reinterpret_cast<uint4 *>(wr) = b0;
@@ -590,6 +601,12 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
       }
     }
 #undef MCDC_LDQ
+    if (CW) {  // re-walk the first 48 positions from the state after the previous piece
+      const uint32_t plo = __shfl_up((uint32_t)h, 1u), phi = __shfl_up((uint32_t)(h >> 32), 1u);
+      uint64_t hp = lane == 0 ? hw : (((uint64_t)phi << 32) | plo);
+      const uint32_t w[12] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, f2.x, f2.y, f2.z, f2.w};
+      scan64q<RUN, PC, 12>(q, w, hp, 0u, qn, run0);
+    }
     if (qn) q_drain<RUN, PC>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
     const uint32_t cnt = q.lcnt[lane], fs = q.lcnt[64 + lane], fl = q.lcnt[128 + lane];
     q.lcnt[lane] = 0;
@@ -617,12 +634,18 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return;
   const int t = tail ? 1 : 0;
-  if (pieces == 4)
-    hipLaunchKernelGGL((k_scan_q<kRun, 4>), dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1, t);
-  else if (pieces == 2)
-    hipLaunchKernelGGL((k_scan_q<kRun, 2>), dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1, t);
-  else
-    hipLaunchKernelGGL((k_scan_q<kRun, 1>), dim3((unsigned)blocks), dim3(1024), 0, stream, w, p, tile0, tile1, t);
+  const dim3 gr((unsigned)blocks), bl(1024);
+  const char *ce = std::getenv("MCDC_SCAN_COLD");
+  const bool cold = ce ? std::atoi(ce) != 0 : true;
+  if (cold && pieces != 1) {  // (one piece: the saved bytes would spill, 128 VGPRs)
+    if (pieces == 4) hipLaunchKernelGGL((k_scan_q<kRun, 4, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    else if (pieces == 2) hipLaunchKernelGGL((k_scan_q<kRun, 2, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    else hipLaunchKernelGGL((k_scan_q<kRun, 1, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+  } else {
+    if (pieces == 4) hipLaunchKernelGGL((k_scan_q<kRun, 4, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    else if (pieces == 2) hipLaunchKernelGGL((k_scan_q<kRun, 2, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    else hipLaunchKernelGGL((k_scan_q<kRun, 1, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+  }
 }
 
 // Lane pieces per run for a whole-call scan of nruns_full full runs.  A tile
