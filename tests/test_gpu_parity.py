@@ -373,13 +373,16 @@ def test_call_larger_than_context_fails_loudly():
         small.close()
 
 
-@pytest.mark.parametrize("pieces", [1, 2, 4])
-def test_scan_lane_pieces(ctx, monkeypatch, pieces):
+@pytest.mark.parametrize("pieces,cold", [(1, 0), (2, 0), (2, 1), (4, 0), (4, 1)])
+def test_scan_lane_pieces(ctx, monkeypatch, pieces, cold):
     """Every lane-piece variant of the scan (a 4 KiB run hashed by 1, 2 or 4
-    lanes; the library picks by call size) on the same inputs: edge sizes
-    around the tile and run grid, a partial last tile, overflowed runs whose
-    candidates come from several lanes, and a batch of ragged files."""
+    lanes; the library picks by call size), warm (each piece re-reads the 48
+    bytes before it) and cold (first 48 positions re-walked at tile end from
+    the previous lane's hash), on the same inputs: edge sizes around the tile
+    and run grid, a partial last tile, overflowed runs whose candidates come
+    from several lanes, and a batch of ragged files."""
     monkeypatch.setenv("MCDC_SCAN_PIECES", str(pieces))
+    monkeypatch.setenv("MCDC_SCAN_COLD", str(cold))
     for p in [PARAMS[0], PARAMS[2], PARAMS[6]]:
         for n in [47, 1023, 1024, 1025, 4097, (256 << 10) + 1, (64 << 20) + 4096 * 17 + 3, (200 << 20) + 12345]:
             d = O.random_bytes(n, SEED + 31 * n)
