@@ -1434,16 +1434,31 @@ void launch_file_counts(const Work &w, uint64_t *dst, hipStream_t stream) {
 // and the per-segment counts / offsets / boundaries follow locally.  A segment
 // whose continuation did anything else sets err[2] ("dirty"); the host then
 // re-resolves the whole call with the general path (fallback, serial walk).
+// Clean-path link rule: segment s continues into s + 1, or its continuation
+// ran to the end of the file (kSegNone) and s + 1 is the file's last segment,
+// which is then off the true chain (count 0).  The second case is local
+// (nothing after s + 1 depends on it); a continuation to the file end that
+// skips more segments is left to the general path.
+__device__ __forceinline__ bool incr_link_ok(const Work &W, uint32_t s, uint32_t fl) {
+  if (fl & kSegLast) return true;
+  const uint32_t l = W.link_seg[s];
+  return l == s + 1 || (l == kSegNone && (W.segs[s + 1].flags & kSegLast));
+}
+__device__ __forceinline__ bool incr_off_chain(const Work &W, uint32_t s, uint32_t fl) {
+  return (fl & kSegLast) && !(fl & kSegFirst) && W.link_seg[s - 1] == kSegNone;
+}
+
 __global__ void k_incr_count(Work W, uint32_t s0, uint32_t s1) {
   const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= s1) return;
   const uint32_t fl = W.segs[s].flags;
   const uint32_t entry = (fl & kSegFirst) ? 0u : W.link_idx[s - 1];
   const uint32_t nc = W.node_cnt[s];
-  const bool bad = (!(fl & kSegLast) && W.link_seg[s] != s + 1) || entry > nc;
-  W.seg_true[s] = 1;
+  const bool off = incr_off_chain(W, s, fl);
+  const bool bad = !incr_link_ok(W, s, fl) || (!off && entry > nc);
+  W.seg_true[s] = off ? 0 : 1;
   W.entry_idx[s] = entry;
-  W.seg_count[s] = bad ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
+  W.seg_count[s] = (bad || off) ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
   if (bad) atomicOr(W.err + 2, 1u);
 }
 
@@ -1454,9 +1469,10 @@ __device__ __forceinline__ uint64_t incr_count_one(const Work &W, uint32_t s, ui
   const uint32_t fl = W.segs[s].flags;
   const uint32_t entry = (fl & kSegFirst) ? 0u : W.link_idx[s - 1];
   const uint32_t nc = W.node_cnt[s];
-  const bool bad = (!(fl & kSegLast) && W.link_seg[s] != s + 1) || entry > nc;
-  const uint64_t c = bad ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
-  W.seg_true[s] = 1;
+  const bool off = incr_off_chain(W, s, fl);
+  const bool bad = !incr_link_ok(W, s, fl) || (!off && entry > nc);
+  const uint64_t c = (bad || off) ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
+  W.seg_true[s] = off ? 0 : 1;
   W.entry_idx[s] = entry;
   W.seg_count[s] = c;
   dirty |= bad ? 1u : 0u;

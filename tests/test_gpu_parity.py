@@ -398,3 +398,29 @@ def test_scan_lane_pieces(ctx, monkeypatch, pieces, cold):
     r, rc = O.chunk_files(O.Params(*p), files, threads=4)
     assert (gc == rc).all()
     _same(g, r)
+
+
+def _segment_bytes(p):
+    """The library's segment size (mcdc_api.hip segment_bytes, default 16 chunks)."""
+    z = max(2 * p[2], 16 * (p[0] + p[1]))
+    return (z + 4095) // 4096 * 4096
+
+
+@pytest.mark.parametrize("p", [PARAMS[0], PARAMS[2], PARAMS[3], PARAMS[6]], ids=lambda p: "/".join(map(str, p)))
+def test_short_last_segment(ctx, p):
+    """Files of k segments plus a short remainder: the previous segment's
+    continuation often runs to the end of the file without meeting the last
+    segment's speculative chain; the clean path then takes the last segment
+    off the chain (count 0) instead of re-resolving the whole call."""
+    z = _segment_bytes(p)
+    rems = sorted({1, 47, 100, 5000, p[0] - 1, p[0], p[0] + 1, p[1], p[2] - 1, p[2] + 1, 3 * p[2]})
+    files = []
+    for k in (1, 2):
+        for r in rems:
+            d = O.random_bytes(k * z + r, SEED + 97 * r + k)
+            _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+            files.append(d)
+    g, gc = ctx.chunk_batch(_lib.params(*p), files)
+    r_, rc = O.chunk_files(O.Params(*p), files, threads=4)
+    assert (gc == rc).all()
+    _same(g, r_)
