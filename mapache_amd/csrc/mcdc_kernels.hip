@@ -1027,7 +1027,7 @@ __device__ __forceinline__ void load_gear_lds(uint64_t *gt, const Work &W) {
 
 // One group per segment.
 template <int GS>
-__global__ __launch_bounds__(256) void k_spec(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+__device__ __forceinline__ void spec_body(Work &W, const DevParams &P, uint32_t s0, uint32_t s1) {
   __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
@@ -1051,6 +1051,20 @@ __global__ __launch_bounds__(256) void k_spec(Work W, DevParams P, uint32_t s0, 
     W.node_cnt[s] = (uint32_t)k;
     W.seg_exit[s] = exitp;
   }
+}
+
+template <int GS>
+__global__ __launch_bounds__(256) void k_spec(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  spec_body<GS>(W, P, s0, s1);
+}
+
+// Same, compiled for 6 waves per SIMD (<= 80 VGPRs instead of 82: 5 -> 6
+// resident waves per SIMD for a latency-bound chain walk).  The default at
+// 16-lane groups; same-box ABAB at 64 GiB: resolution 0.425 -> 0.407 ms.
+template <int GS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_spec6(Work W, DevParams P,
+                                                                                         uint32_t s0, uint32_t s1) {
+  spec_body<GS>(W, P, s0, s1);
 }
 
 // index of c in nodes(j) (sorted), or -1; group-cooperative
@@ -1555,7 +1569,13 @@ void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hi
     switch (chain_group()) {
       case 8: hipLaunchKernelGGL(k_spec<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1); break;
       case 32: hipLaunchKernelGGL(k_spec<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1); break;
-      default: hipLaunchKernelGGL(k_spec<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+      default: {
+        const char *o = std::getenv("MCDC_SPEC_OCC");  // 5: the 82-VGPR build (A/B)
+        if (!(o && std::atoi(o) == 5))
+          hipLaunchKernelGGL(k_spec6<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+        else
+          hipLaunchKernelGGL(k_spec<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+      }
     }
 }
 
