@@ -281,6 +281,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   void *out_dev = direct_out(ctx, out);
   if (!out_dev && is_device_ptr(out))
     return fail(MCDC_E_INVALID, "out is a device pointer of another device");
+  // pinned host `out`: k_emit writes it over PCIe (default) or, with
+  // MCDC_PINNED_DIRECT=0, emits into HBM and one DMA copies the list
+  if (out_dev && !is_device_ptr(out) && env_int("MCDC_PINNED_DIRECT", 1) == 0) out_dev = nullptr;
 
   // ---- scan workspace, and the scan itself for a single-part call ----
   // The scan reads none of the segment tables, so a single-part call enqueues
