@@ -236,10 +236,13 @@ def test_timing_reported(ctx):
     assert 0 < t["scan_ms"] <= t["device_ms"] and t["h2d_ms"] > 0
 
 
-def test_pinned_output_written_directly(ctx):
-    """A pinned caller array is written by k_emit over PCIe (no staging copy):
-    same result as the pageable path; a too-small pinned array reports
-    MCDC_E_CAPACITY with the required count."""
+@pytest.mark.parametrize("direct", [1, 0])
+def test_pinned_output_written_directly(ctx, monkeypatch, direct):
+    """A pinned caller array is written by k_emit over PCIe (no staging copy;
+    MCDC_PINNED_DIRECT=0: emitted into HBM and copied by one DMA): same result
+    as the pageable path; a too-small pinned array reports MCDC_E_CAPACITY
+    with the required count."""
+    monkeypatch.setenv("MCDC_PINNED_DIRECT", str(direct))
     n = (96 << 20) + 777
     dp = ctx.device_alloc(n)
     try:
