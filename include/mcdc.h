@@ -135,7 +135,9 @@ int mcdc_chunk_batch(struct mcdc_ctx *ctx, const mcdc_params *params,
 
 /* Same, but the buffers already sit back to back in one device arena:
  * buffer i is d_arena[offsets[i], offsets[i] + lens[i]).  offsets/lens are
- * host arrays; the ranges must not overlap. */
+ * host arrays, in any order; overlapping non-empty ranges -> MCDC_E_INVALID,
+ * an arena span max(offsets[i] + lens[i]) above the context's max_bytes ->
+ * MCDC_E_TOOBIG. */
 int mcdc_chunk_batch_device(struct mcdc_ctx *ctx, const mcdc_params *params,
                             const void *d_arena, const uint64_t *offsets, const uint64_t *lens,
                             size_t nbufs, mcdc_chunk *out, size_t cap, size_t *counts,
@@ -150,9 +152,39 @@ int mcdc_chunk_batch_device(struct mcdc_ctx *ctx, const mcdc_params *params,
  * produced by mcdc_chunk_device (offset/length relative to d_data; the hash
  * field is ignored), either a device pointer on the context's device (the
  * boundary list stays in HBM) or host memory; ids: 32 * nchunks bytes,
- * device pointer or host memory.  A chunk outside [0, n) -> MCDC_E_INVALID. */
+ * device pointer or host memory.  Chunks may overlap or repeat (each is hashed
+ * on its own).  A chunk outside [0, n) -> MCDC_E_INVALID. */
 int mcdc_chunk_ids_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
                           size_t nchunks, uint8_t *ids);
+
+/* ---------------------------------------------------------------- batching
+ * Cross-worker batching front-end.  mapache chunks files on read_concurrency
+ * rayon workers at once (/root/reference/src/archiver/mod.rs:162-215, default
+ * 4: src/global/defaults.rs:22), each with its own StreamCDC per file
+ * (src/archiver/processor.rs:173).  A batcher lets every worker submit its
+ * file and returns that file's chunks, while one mcdc_chunk_batch call serves
+ * all files submitted together (group commit: the first submitter waits up to
+ * gather_us for others, or until max_batch_files / max_batch_bytes is
+ * reached; files arriving while a batch runs form the next one).  Per file the
+ * result is exactly mcdc_chunk_host's (chains restart at the file's first
+ * byte); statuses are per caller (MCDC_E_CAPACITY reports the file's count).
+ * A file larger than max_batch_bytes -> MCDC_E_TOOBIG (chunk it with
+ * mcdc_chunk_host or in StreamCDC windows).  mcdc_batcher_chunk is
+ * thread-safe; the batcher owns one context on `device`. */
+typedef struct mcdc_batcher mcdc_batcher;
+
+typedef struct {
+  uint64_t batches;         /* batch calls run                      */
+  uint64_t files;           /* files chunked                        */
+  uint64_t bytes;           /* bytes chunked                        */
+  uint64_t max_batch_files; /* most files served by one batch call  */
+} mcdc_batcher_counters;
+
+int mcdc_batcher_create(int device, const mcdc_params *params, size_t max_batch_bytes, size_t max_batch_files,
+                        uint32_t gather_us, mcdc_batcher **out);
+void mcdc_batcher_destroy(mcdc_batcher *b);
+int mcdc_batcher_chunk(mcdc_batcher *b, const void *data, size_t n, mcdc_chunk *out, size_t cap, size_t *n_out);
+int mcdc_batcher_stats(const mcdc_batcher *b, mcdc_batcher_counters *out);
 
 /* Timing of the last call on ctx. */
 int mcdc_ctx_timing(const struct mcdc_ctx *ctx, mcdc_timing *out);

@@ -7,7 +7,9 @@ entry point raises.
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
+import threading
 
 import numpy as np
 
@@ -30,7 +32,8 @@ EXPORTS = (
     "mcdc_chunk_host", "mcdc_chunk_batch", "mcdc_chunk_batch_device", "mcdc_ctx_timing",
     "mcdc_last_error", "mcdc_device_alloc", "mcdc_device_free", "mcdc_host_alloc",
     "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_memcpy_d2h", "mcdc_fill_random_device", "mcdc_digest",
-    "mcdc_abi_version", "mcdc_chunk_ids_device",
+    "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
+    "mcdc_batcher_chunk", "mcdc_batcher_stats",
 )
 
 
@@ -50,6 +53,11 @@ class McdcTiming(ctypes.Structure):
                 ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
                 ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64),
                 ("ids_ms", ctypes.c_double)]
+
+
+class McdcBatcherStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("files", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("max_batch_files", ctypes.c_uint64)]
 
 
 CHUNK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("hash", "<u8")])
@@ -95,6 +103,11 @@ def load():
     L.mcdc_digest.restype = u64
     L.mcdc_abi_version.argtypes = []
     L.mcdc_chunk_ids_device.argtypes = [vp, vp, sz, vp, sz, vp]
+    L.mcdc_batcher_create.argtypes = [i32, P(McdcParams), sz, sz, ctypes.c_uint32, P(vp)]
+    L.mcdc_batcher_destroy.argtypes = [vp]
+    L.mcdc_batcher_destroy.restype = None
+    L.mcdc_batcher_chunk.argtypes = [vp, vp, sz, vp, sz, P(sz)]
+    L.mcdc_batcher_stats.argtypes = [vp, P(McdcBatcherStats)]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -110,11 +123,30 @@ def params(min_size: int, avg_size: int, max_size: int, level: int = 1) -> McdcP
     return McdcParams(min_size, avg_size, max_size, level)
 
 
+def _locked(fn):
+    """Serialise a Context method: mcdc.h forbids two threads in one context at
+    once, and ctypes releases the GIL during every C call."""
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        with self._lock:
+            if not self._h:
+                raise McdcError(MCDC_E_INVALID, "context is closed")
+            return fn(self, *args, **kwargs)
+    return wrapper
+
+
 class Context:
-    """One mcdc_ctx: a HIP device, a stream and its workspace."""
+    """One mcdc_ctx: a HIP device, a stream and its workspace.
+
+    Thread-safe: every call holds the context's lock (the C context must not be
+    entered by two threads at once), and close() waits for a call in flight.
+    For concurrency, give each worker thread its own Context (as the Archiver
+    adapter in INTEGRATION.md does) — calls on one context serialise."""
 
     def __init__(self, device: int = 0, max_bytes: int = 1 << 30):
         L = load()
+        self._lock = threading.RLock()
+        self._h = None
         h = ctypes.c_void_p()
         check(L.mcdc_ctx_create(device, max_bytes, ctypes.byref(h)))
         self._h = h
@@ -124,13 +156,18 @@ class Context:
         self._out_ptr = None
 
     def close(self):
-        if self._h:
-            if self._out_ptr:
-                load().mcdc_host_free(self._h, ctypes.c_void_p(self._out_ptr))
-                self._out, self._out_ptr = None, None
-            load().mcdc_ctx_destroy(self._h)
-            self._h = None
+        lock = getattr(self, "_lock", None)
+        if lock is None:
+            return
+        with lock:
+            if self._h:
+                if self._out_ptr:
+                    load().mcdc_host_free(self._h, ctypes.c_void_p(self._out_ptr))
+                    self._out, self._out_ptr = None, None
+                load().mcdc_ctx_destroy(self._h)
+                self._h = None
 
+    @_locked
     def pinned_out(self, cap: int) -> np.ndarray:
         """A reusable pinned-host chunk array of at least `cap` entries (grown on demand).
         Results written into it are only valid until the next call that reuses it."""
@@ -160,6 +197,7 @@ class Context:
     def _bound(n: int, p: McdcParams) -> int:
         return n // max(p.min_size - 1, 1) + 2
 
+    @_locked
     def _run(self, fn, p: McdcParams, *args, cap: int, out: np.ndarray | None = None):
         if out is None:
             out = np.empty(max(cap, 1), dtype=CHUNK_DTYPE)
@@ -184,6 +222,7 @@ class Context:
         return self._run(load().mcdc_chunk_host, p, ctypes.c_void_p(a.ctypes.data), a.size,
                          cap=self._bound(a.size, p))
 
+    @_locked
     def chunk_batch(self, p: McdcParams, bufs):
         arrs = [np.ascontiguousarray(np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray)
                                      else b.view(np.uint8).reshape(-1)) for b in bufs]
@@ -198,6 +237,7 @@ class Context:
                                       counts.ctypes.data, ctypes.byref(n_out)))
         return out[: n_out.value].copy(), counts[:n].astype(np.int64)
 
+    @_locked
     def chunk_batch_device(self, p: McdcParams, d_arena: int, offsets, lens):
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
         ls = np.ascontiguousarray(lens, dtype=np.uint64)
@@ -211,6 +251,7 @@ class Context:
                                              counts.ctypes.data, ctypes.byref(n_out)))
         return out[: n_out.value].copy(), counts[:n].astype(np.int64)
 
+    @_locked
     def chunk_device_to_device(self, p: McdcParams, d_ptr: int, n: int, d_out: int, cap: int) -> int:
         """Chunk a device-resident buffer into a device-resident boundary list
         (`cap` mcdc_chunk records at device pointer `d_out`); returns the count."""
@@ -219,6 +260,7 @@ class Context:
                                        ctypes.c_void_p(d_out), cap, ctypes.byref(n_out)))
         return n_out.value
 
+    @_locked
     def chunk_batch_device_to_device(self, p: McdcParams, d_arena: int, offsets, lens, d_out: int, cap: int):
         """Many device-resident files -> device-resident boundary list; returns
         (total chunks, per-file counts)."""
@@ -232,6 +274,7 @@ class Context:
                                              counts.ctypes.data, ctypes.byref(n_out)))
         return n_out.value, counts[:n].astype(np.int64)
 
+    @_locked
     def chunk_ids(self, d_data: int, n: int, chunks, ids=None) -> np.ndarray:
         """BLAKE3 chunk IDs (ID::from_content) of a boundary list over the device
         buffer d_data[0, n).  `chunks`: a CHUNK_DTYPE array (host) or an int
@@ -252,12 +295,14 @@ class Context:
                                            out.ctypes.data))
         return out[:count]
 
+    @_locked
     def d2h_bytes(self, d_src: int, nbytes: int) -> np.ndarray:
         out = np.empty(max(nbytes, 1), dtype=np.uint8)
         if nbytes:
             check(load().mcdc_memcpy_d2h(self._h, out.ctypes.data, ctypes.c_void_p(d_src), nbytes))
         return out[:nbytes]
 
+    @_locked
     def d2h_chunks(self, d_out: int, count: int) -> np.ndarray:
         out = np.empty(max(count, 1), dtype=CHUNK_DTYPE)
         if count:
@@ -265,35 +310,83 @@ class Context:
                                          count * CHUNK_DTYPE.itemsize))
         return out[:count]
 
+    @_locked
     def timing(self) -> dict:
         t = McdcTiming()
         check(load().mcdc_ctx_timing(self._h, ctypes.byref(t)))
         return {k: getattr(t, k) for k, _ in McdcTiming._fields_}
 
     # ---------------------------------------------------------- plumbing --
+    @_locked
     def device_alloc(self, n: int) -> int:
         p = ctypes.c_void_p()
         check(load().mcdc_device_alloc(self._h, n, ctypes.byref(p)))
         return p.value
 
+    @_locked
     def device_free(self, ptr: int) -> None:
         check(load().mcdc_device_free(self._h, ctypes.c_void_p(ptr)))
 
+    @_locked
     def host_alloc(self, n: int) -> int:
         p = ctypes.c_void_p()
         check(load().mcdc_host_alloc(self._h, n, ctypes.byref(p)))
         return p.value
 
+    @_locked
     def host_free(self, ptr: int) -> None:
         check(load().mcdc_host_free(self._h, ctypes.c_void_p(ptr)))
 
+    @_locked
     def h2d(self, d_dst: int, data) -> None:
         a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
                                  else data.view(np.uint8).reshape(-1))
         check(load().mcdc_memcpy_h2d(self._h, ctypes.c_void_p(d_dst), ctypes.c_void_p(a.ctypes.data), a.size))
 
+    @_locked
     def fill_random(self, d_dst: int, n: int, seed: int, pos: int = 0) -> None:
         check(load().mcdc_fill_random_device(self._h, ctypes.c_void_p(d_dst), pos, n, seed))
+
+
+class Batcher:
+    """mcdc_batcher: worker threads call chunk() concurrently; files submitted
+    together are chunked by one batched call (include/mcdc.h, "batching")."""
+
+    def __init__(self, p: McdcParams, device: int = 0, max_batch_bytes: int = 1 << 30,
+                 max_batch_files: int = 4096, gather_us: int = 200):
+        L = load()
+        self.params = p
+        self._h = None
+        h = ctypes.c_void_p()
+        check(L.mcdc_batcher_create(device, ctypes.byref(p), max_batch_bytes, max_batch_files, gather_us,
+                                    ctypes.byref(h)))
+        self._h = h
+
+    def chunk(self, data) -> np.ndarray:
+        a = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                 else data.view(np.uint8).reshape(-1))
+        cap = a.size // max(self.params.min_size - 1, 1) + 2
+        out = np.empty(cap, dtype=CHUNK_DTYPE)
+        n_out = ctypes.c_size_t()
+        check(load().mcdc_batcher_chunk(self._h, ctypes.c_void_p(a.ctypes.data), a.size, out.ctypes.data, cap,
+                                        ctypes.byref(n_out)))
+        return out[: n_out.value].copy()
+
+    def stats(self) -> dict:
+        st = McdcBatcherStats()
+        check(load().mcdc_batcher_stats(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in McdcBatcherStats._fields_}
+
+    def close(self):
+        if self._h:
+            load().mcdc_batcher_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def digest(chunks: np.ndarray) -> int:

@@ -13,11 +13,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "../../include/mcdc.h"
+#include "../host/batcher.hpp"
 #include "gear_table.h"
 #include "mcdc_blake3.h"
 #include "mcdc_internal.h"
@@ -91,12 +93,11 @@ DevParams make_dev_params(const mcdc_params *p, uint64_t ms, uint64_t ml) {
   return d;
 }
 
-// Segment length: ~16 expected chunks per speculative chain, >= 2 * max.
-// (MCDC_SEG_CHUNKS overrides the 16 for A/B runs; >= 2 * max keeps a single
-// chunk from skipping a whole segment.)
-uint64_t segment_bytes(const mcdc_params *p) {
-  const char *v = std::getenv("MCDC_SEG_CHUNKS");
-  const uint64_t k = v && *v ? (uint64_t)std::max(1, std::atoi(v)) : 16ull;
+// Segment length: ~16 expected chunks per speculative chain (Knobs::seg_chunks,
+// an A/B-build knob), >= 2 * max so that a single chunk never skips a whole
+// segment.
+uint64_t segment_bytes(const mcdc_params *p, const Knobs &kn) {
+  const uint64_t k = (uint64_t)kn.seg_chunks;
   uint64_t z = std::max<uint64_t>(2ull * p->max_size, k * ((uint64_t)p->min_size + p->avg_size));
   return (z + kRun - 1) / kRun * kRun;
 }
@@ -108,16 +109,6 @@ struct DevBuf {
 
 constexpr int kMaxParts = 4;
 
-// Scan parts (DESIGN.md §3 "Staged pipeline"): the scan is split into
-// consecutive tile ranges; the resolution of every segment whose inputs lie in
-// the parts already scanned runs on a second stream while the next part is
-// scanned.  Parts after the first are whole rounds (one tile per scan wave)
-// so no launch ends with a ragged last round.  MCDC_PARTS (1..4) overrides the
-// part count, MCDC_TAIL_ROUNDS the size of the last part.
-int env_int(const char *name, int dflt) {
-  const char *v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
-}
 
 }  // namespace
 
@@ -130,6 +121,9 @@ struct mcdc_ctx {
   hipEvent_t ev_start = nullptr, ev_scan = nullptr, ev_end = nullptr, ev_h2d0 = nullptr,
              ev_h2d1 = nullptr;
   hipEvent_t ev_part[kMaxParts] = {};
+  hipEvent_t ev_tab = nullptr;    // after the last async upload out of h_tab
+  bool tab_inflight = false;
+  Knobs knobs;                    // read once at creation (read_knobs)
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
   DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
@@ -277,13 +271,14 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   int rc = check_params(params, &ms, &ml);
   if (rc) return rc;
   const DevParams P = make_dev_params(params, ms, ml);
-  const uint64_t Z = segment_bytes(params);
+  const Knobs &kn = ctx->knobs;
+  const uint64_t Z = segment_bytes(params, kn);
   void *out_dev = direct_out(ctx, out);
   if (!out_dev && is_device_ptr(out))
     return fail(MCDC_E_INVALID, "out is a device pointer of another device");
   // pinned host `out`: k_emit writes it over PCIe (default) or, with
   // MCDC_PINNED_DIRECT=0, emits into HBM and one DMA copies the list
-  if (out_dev && !is_device_ptr(out) && env_int("MCDC_PINNED_DIRECT", 1) == 0) out_dev = nullptr;
+  if (out_dev && !is_device_ptr(out) && !kn.pinned_direct) out_dev = nullptr;
 
   // ---- scan workspace, and the scan itself for a single-part call ----
   // The scan reads none of the segment tables, so a single-part call enqueues
@@ -303,16 +298,15 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.run_cnt = (uint8_t *)ctx->run_cnt.p;
   W.run_sum = (uint32_t *)ctx->run_sum.p;
   W.run_ent = (uint32_t *)ctx->run_ent.p;
-  W.tile_ctr = env_int("MCDC_DYN_TILES", 1) ? (uint64_t *)ctx->tile_ctr.p : nullptr;
-  W.first_static = env_int("MCDC_FIRST_STATIC", 1) ? 1u : 0u;
+  W.tile_ctr = kn.dyn_tiles ? (uint64_t *)ctx->tile_ctr.p : nullptr;
+  W.first_static = kn.first_static ? 1u : 0u;
   hipStream_t st = ctx->stream;
-  const bool early = std::min(std::max(env_int("MCDC_PARTS", 1), 1), kMaxParts) == 1;
+  const bool early = kn.parts == 1;
   if (early) {
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
     if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
-    int pc = env_int("MCDC_SCAN_PIECES", 0);
-    if (pc != 1 && pc != 2 && pc != 4) pc = scan_pieces(n_al / kRun, ctx->num_cus);
-    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, (n_al / kRun) / (64 / pc), true, pc);
+    const int pc = kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus);
+    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, (n_al / kRun) / (64 / pc), true, pc, kn.scan_cold);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_part[0], st));
     HIP_TRY(hipEventRecord(ctx->ev_scan, st));
@@ -423,13 +417,13 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // ---- staged pipeline plan ----
   // parts: full tiles [tb[i], tb[i+1]); the last part also scans the partial tile
   const uint64_t tile_bytes = 64ull * kRun;
-  // (MCDC_PART_TILES / MCDC_MIN_ROUNDS shrink the round unit and the size
-  // threshold so that tests exercise the staged path on small inputs)
-  const uint64_t waves = (uint64_t)std::max(
-      env_int("MCDC_PART_TILES", (int)std::max<uint64_t>(1, scan_waves(ntiles_full, ctx->num_cus))), 1);
-  int K = std::min(std::max(env_int("MCDC_PARTS", 1), 1), kMaxParts);
-  const uint64_t tail_rounds = (uint64_t)std::max(env_int("MCDC_TAIL_ROUNDS", 2), 1);
-  const uint64_t min_rounds = (uint64_t)std::max(env_int("MCDC_MIN_ROUNDS", 8), 0);
+  // (part_tiles / min_rounds shrink the round unit and the size threshold so
+  // that tests exercise the staged path on small inputs)
+  const uint64_t waves =
+      kn.part_tiles ? (uint64_t)kn.part_tiles : std::max<uint64_t>(1, scan_waves(ntiles_full, ctx->num_cus));
+  int K = std::min(kn.parts, kMaxParts);
+  const uint64_t tail_rounds = (uint64_t)kn.tail_rounds;
+  const uint64_t min_rounds = (uint64_t)kn.min_rounds;
   uint64_t tb[kMaxParts + 1];
   {
     uint64_t rounds_needed = 0, r = tail_rounds;
@@ -481,7 +475,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
     for (int i = 0; i < K; ++i) {
       if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
-      if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1);
+      if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1, 1, false);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
     }
@@ -491,8 +485,13 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
                  b_noff = ctx->h_node_off.size() * 8;
     const size_t o_files = (b_segs + 255) / 256 * 256, o_noff = o_files + (b_files + 255) / 256 * 256;
-    // (the previous call synchronised before returning, so the pinned stage
-    // is idle; staging on the host overlaps the scan just enqueued)
+    // (staging on the host overlaps the scan just enqueued; the previous
+    // uploads out of the pinned stage are waited for first: a call that
+    // failed after enqueuing them returned without synchronising)
+    if (ctx->tab_inflight) {
+      HIP_TRY(hipEventSynchronize(ctx->ev_tab));
+      ctx->tab_inflight = false;
+    }
     if ((rc = ensure_tab(ctx, o_noff + b_noff))) return rc;
     char *tbuf = (char *)ctx->h_tab;
     if (b_segs) std::memcpy(tbuf, ctx->h_segs.data(), b_segs);
@@ -501,6 +500,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tbuf, b_segs, hipMemcpyHostToDevice, st2));
     if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tbuf + o_files, b_files, hipMemcpyHostToDevice, st2));
     HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tbuf + o_noff, b_noff, hipMemcpyHostToDevice, st2));
+    HIP_TRY(hipEventRecord(ctx->ev_tab, st2));
+    ctx->tab_inflight = true;
     ctx->plan_valid = true;
   }
   const bool want_counts = counts && nfiles;
@@ -512,9 +513,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   for (int i = 0; i < K; ++i) {
     HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[i], 0));
     const uint32_t a_s = i ? spec_hi[i - 1] : 0, a_l = i ? link_hi[i - 1] : 0;
-    launch_spec(W, P, a_s, spec_hi[i], st2);
+    launch_spec(W, P, kn, a_s, spec_hi[i], st2);
     // parts before the last: link_hi assumes <= kContMax continuation steps
-    launch_link(W, P, a_l, link_hi[i], i == K - 1 ? ~0ull : (uint64_t)kContMax, st2);
+    launch_link(W, P, kn, a_l, link_hi[i], i == K - 1 ? ~0ull : (uint64_t)kContMax, st2);
     launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
     HIP_TRY(hipGetLastError());
   }
@@ -618,6 +619,9 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
   for (hipEvent_t &e : ctx->ev_part)  // ordering only: no timestamps
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
       return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&ctx->ev_tab, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
+  ctx->knobs = read_knobs();
   uint64_t g16[256];
   for (int i = 0; i < 256; ++i) g16[i] = kGear[i] << 16;
   if (hipMalloc(&ctx->d_gear, 2048) != hipSuccess || hipMalloc(&ctx->d_gear16, 2048) != hipSuccess)
@@ -657,6 +661,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ev_part)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_tab) (void)hipEventDestroy(ctx->ev_tab);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
@@ -697,14 +702,31 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
   const uint8_t *base = (const uint8_t *)(addr & ~(uintptr_t)15);
   const uint64_t delta = addr & 15;
   std::vector<uint64_t> fs(nbufs), fe(nbufs);
-  uint64_t hi = 0, total = 0;
+  uint64_t hi = 0;
+  bool sorted = true;
   for (size_t i = 0; i < nbufs; ++i) {
+    if (offsets[i] > UINT64_MAX - 32 - lens[i])
+      return fail(MCDC_E_INVALID, "buffer %zu: offset + length overflows", i);
     fs[i] = delta + offsets[i];
     fe[i] = fs[i] + lens[i];
+    if (lens[i] == 0) continue;
+    sorted = sorted && fs[i] >= hi;  // non-empty ranges in increasing order, disjoint
     hi = std::max(hi, fe[i]);
-    total += lens[i];
   }
-  if (total > ctx->max_bytes) return fail(MCDC_E_TOOBIG, "batch bytes %llu > max_bytes", (unsigned long long)total);
+  if (!sorted) {  // any order is allowed, overlaps are not (one chunk chain per byte range)
+    std::vector<size_t> idx;
+    idx.reserve(nbufs);
+    for (size_t i = 0; i < nbufs; ++i)
+      if (lens[i]) idx.push_back(i);
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return fs[a] < fs[b]; });
+    for (size_t k = 1; k < idx.size(); ++k)
+      if (fs[idx[k]] < fe[idx[k - 1]])
+        return fail(MCDC_E_INVALID, "buffers %zu and %zu overlap", idx[k - 1], idx[k]);
+  }
+  // the workspace is sized from the arena span (gaps included), so the span is
+  // what the context bound limits
+  if (hi - delta > ctx->max_bytes)
+    return fail(MCDC_E_TOOBIG, "arena span %llu > max_bytes=%zu", (unsigned long long)(hi - delta), ctx->max_bytes);
   const uint64_t n_al = (hi + 15) / 16 * 16;
   rc = run_pipeline(ctx, params, base, n_al, fs.data(), fe.data(), nbufs, out, cap, counts, n_out);
   ctx->timing.h2d_ms = 0;
@@ -873,7 +895,9 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   }
   uint8_t *ids_dev = (uint8_t *)direct_out(ctx, ids);
   if (!ids_dev && is_device_ptr(ids)) return fail(MCDC_E_INVALID, "ids is a device pointer of another device");
-  const uint64_t bound = b3_group_bound(n, nchunks);
+  // groups of disjoint chunks never exceed this bound; overlapping or repeated
+  // chunks can, and are then hashed again with the exact count read back
+  uint64_t bound = b3_group_bound(n, nchunks);
   const size_t tmpb = b3_tmp_bytes(nchunks);
   if ((rc = ensure(ctx, ctx->b3_gcnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->b3_goff, (nchunks + 1) * 8)) ||
       (rc = ensure(ctx, ctx->b3_owner, bound * 4)) || (rc = ensure(ctx, ctx->b3_nodes, bound * 32)) ||
@@ -884,18 +908,31 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
     ids_dev = (uint8_t *)ctx->b3_ids.p;
   }
   uint32_t *err = (uint32_t *)ctx->err.p + 3;
+  const uint64_t *goff = (const uint64_t *)ctx->b3_goff.p;
   HIP_TRY(hipMemsetAsync(err, 0, 4, st));
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
   launch_b3_prepare(dch, nchunks, n, (uint64_t *)ctx->b3_gcnt.p, (uint64_t *)ctx->b3_goff.p, err, ctx->b3_tmp.p, tmpb,
                     st);
-  launch_b3_hash((const uint8_t *)d_data, dch, nchunks, (const uint64_t *)ctx->b3_goff.p, bound,
-                 (uint32_t *)ctx->b3_owner.p, (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
+  launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, (uint32_t *)ctx->b3_owner.p,
+                 (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
   uint32_t herr = 0;
+  uint64_t groups = 0;
   HIP_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&groups, goff + nchunks, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (herr) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer", n);
+  if (groups > bound) {  // overlapping / repeated chunks: the kernels skipped; hash with the exact bound
+    bound = groups;
+    if ((rc = ensure(ctx, ctx->b3_owner, bound * 4)) || (rc = ensure(ctx, ctx->b3_nodes, bound * 32))) return rc;
+    HIP_TRY(hipEventRecord(ctx->ev_start, st));
+    launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, (uint32_t *)ctx->b3_owner.p,
+                   (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev_end, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   if (ids_dev == ctx->b3_ids.p) {
     HIP_TRY(hipMemcpyAsync(ids, ids_dev, nchunks * 32, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -907,6 +944,78 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   ctx->timing.bytes = n;
   ctx->timing.chunks = nchunks;
   ctx->timing.total_ms = now_ms() - t0;
+  return MCDC_OK;
+}
+
+// ------------------------------------------------------------ batcher --
+// C ABI of the cross-worker batching front-end (mapache_amd/host/batcher.hpp)
+// over this library's mcdc_chunk_batch on a context of its own.
+}  // extern "C"
+
+struct mcdc_batcher {
+  mcdc_ctx *ctx = nullptr;
+  mcdc_params params{};
+  std::unique_ptr<mcdc::host::Batcher> core;
+};
+
+extern "C" {
+
+int mcdc_batcher_create(int device, const mcdc_params *params, size_t max_batch_bytes, size_t max_batch_files,
+                        uint32_t gather_us, mcdc_batcher **out) {
+  if (!out) return fail(MCDC_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = check_params(params, nullptr, nullptr);
+  if (rc) return rc;
+  if (max_batch_bytes == 0 || max_batch_files == 0) return fail(MCDC_E_INVALID, "empty batch limits");
+  mcdc_batcher *b = new (std::nothrow) mcdc_batcher();
+  if (!b) return fail(MCDC_E_NOMEM, "host allocation failed");
+  if ((rc = mcdc_ctx_create(device, max_batch_bytes, &b->ctx))) {
+    delete b;
+    return rc;
+  }
+  b->params = *params;
+  mcdc_ctx *ctx = b->ctx;
+  const mcdc_params P = *params;
+  auto fn = [ctx, P](const uint8_t *const *bufs, const size_t *lens, size_t k, mcdc_chunk *o, size_t cap,
+                     size_t *counts, size_t *n_out, std::string *msg) {
+    const int r = mcdc_chunk_batch(ctx, &P, bufs, lens, k, o, cap, counts, n_out);
+    if (r && msg) *msg = mcdc_last_error();
+    return r;
+  };
+  const uint32_t mn = params->min_size;
+  b->core.reset(new (std::nothrow) mcdc::host::Batcher(fn, [mn](size_t len) { return len / (mn - 1) + 2; },
+                                                       max_batch_bytes, max_batch_files, gather_us));
+  if (!b->core) {
+    mcdc_ctx_destroy(b->ctx);
+    delete b;
+    return fail(MCDC_E_NOMEM, "host allocation failed");
+  }
+  *out = b;
+  return MCDC_OK;
+}
+
+void mcdc_batcher_destroy(mcdc_batcher *b) {
+  if (!b) return;
+  b->core.reset();
+  mcdc_ctx_destroy(b->ctx);
+  delete b;
+}
+
+int mcdc_batcher_chunk(mcdc_batcher *b, const void *data, size_t n, mcdc_chunk *out, size_t cap, size_t *n_out) {
+  if (!b) return fail(MCDC_E_INVALID, "batcher is NULL");
+  std::string msg;
+  const int rc = b->core->chunk((const uint8_t *)data, n, out, cap, n_out, &msg);
+  if (rc) return fail(rc, "%s", msg.c_str());
+  return MCDC_OK;
+}
+
+int mcdc_batcher_stats(const mcdc_batcher *b, mcdc_batcher_counters *out) {
+  if (!b || !out) return fail(MCDC_E_INVALID, "NULL argument");
+  const mcdc::host::BatcherStats s = b->core->stats();
+  out->batches = s.batches;
+  out->files = s.files;
+  out->bytes = s.bytes;
+  out->max_batch_files = s.max_batch_files;
   return MCDC_OK;
 }
 

@@ -17,7 +17,9 @@ uint64_t b3_group_bound(uint64_t total_bytes, uint64_t nchunks);
 void launch_b3_prepare(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *gcnt, uint64_t *goff,
                        uint32_t *err, void *tmp, size_t tmp_bytes, hipStream_t stream);
 // ids[32 * i] = BLAKE3(base[chunks[i].offset, + chunks[i].length)); group_bound
-// >= goff[n] sizes the grid (b3_group_bound)
+// sizes the grid (b3_group_bound, exact for disjoint chunks).  When goff[n]
+// exceeds it (overlapping or repeated chunks) the kernels write nothing and
+// the caller re-runs with group_bound = goff[n].
 void launch_b3_hash(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *goff,
                     uint64_t group_bound, uint32_t *owner, uint32_t *nodes, uint8_t *ids, hipStream_t stream);
 

@@ -155,9 +155,13 @@ __global__ void k_b3_groups(const DevChunk *chunks, uint64_t n, uint64_t nbytes,
   }
 }
 
-__global__ void k_b3_owner(const uint64_t *goff, uint64_t n, uint32_t *owner) {
+// Every hashing kernel first checks the group total against the host's bound
+// (b3_group_bound assumes disjoint chunks; overlapping or repeated chunks
+// exceed it): over the bound nothing is written, and the host re-runs the
+// hashing with the exact total it reads back (mcdc_chunk_ids_device).
+__global__ void k_b3_owner(const uint64_t *goff, uint64_t n, uint64_t bound, uint32_t *owner) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || goff[n] > bound) return;
   for (uint64_t g = goff[i]; g < goff[i + 1]; ++g) owner[g] = (uint32_t)i;
 }
 
@@ -168,10 +172,11 @@ __global__ void k_b3_owner(const uint64_t *goff, uint64_t n, uint32_t *owner) {
 // whole wave); the one partial block a group can end with is hashed after it.
 __global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const DevChunk *chunks,
                                                    const uint64_t *goff, const uint32_t *owner, uint64_t n,
-                                                   uint32_t *nodes, uint8_t *ids) {
+                                                   uint64_t bound, uint32_t *nodes, uint8_t *ids) {
   __shared__ uint32_t stk[256][4][8];
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= goff[n]) return;  // the grid is sized by a host bound
+  const uint64_t total = goff[n];
+  if (g >= total || total > bound) return;  // the grid is sized by the host bound
   const uint32_t i = owner[g];
   const DevChunk ch = chunks[i];
   const uint32_t nleaves = leaves_of(ch.length);
@@ -258,10 +263,10 @@ __global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const De
 
 // One lane per chunk of more than one group: level-by-level pairing of its
 // group nodes in place (nodes [goff[i], goff[i+1]) belong to this lane only).
-__global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t n, uint32_t *nodes,
+__global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t n, uint64_t bound, uint32_t *nodes,
                           uint8_t *ids) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || goff[n] > bound) return;
   uint64_t m = goff[i + 1] - goff[i];
   if (m < 2) return;  // finished by k_b3_leaves
   uint32_t *nd = nodes + 8 * goff[i];
@@ -305,11 +310,11 @@ void launch_b3_prepare(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 void launch_b3_hash(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *goff,
                     uint64_t group_bound, uint32_t *owner, uint32_t *nodes, uint8_t *ids, hipStream_t stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_b3_owner, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, goff, n, owner);
+  hipLaunchKernelGGL(k_b3_owner, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, goff, n, group_bound, owner);
   hipLaunchKernelGGL(k_b3_leaves, dim3((unsigned)((group_bound + 255) / 256)), dim3(256), 0, stream, base, chunks,
-                     goff, (const uint32_t *)owner, n, nodes, ids);
-  hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n, nodes,
-                     ids);
+                     goff, (const uint32_t *)owner, n, group_bound, nodes, ids);
+  hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n, group_bound,
+                     nodes, ids);
 }
 
 }  // namespace mcdc

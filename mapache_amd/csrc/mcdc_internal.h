@@ -1,19 +1,22 @@
 // mcdc_internal.h — device data layout shared by the HIP kernels
 // (mcdc_kernels.hip) and the C-ABI host code (mcdc_api.hip).
 //
-// Pipeline (DESIGN.md §Kernels):
-//   k_scan      streaming, HBM-bound: per-position windowed Gear hash, exact
+// Pipeline (DESIGN.md §3):
+//   k_scan_q    streaming, HBM-bound: per-position windowed Gear hash, exact
 //               S/L flags for every position whose 48-byte window passes the
-//               prefilter -> per-run candidate lists (run = kRun bytes/lane)
-//   k_spec      one wave per segment: speculative cut chain from the segment
-//               start (wave-level `next` = exact fastcdc cut_gear semantics)
-//   k_link      one wave per segment: continue past the segment end until
-//               the chain merges with a later segment's speculative chain
-//               (forced stretches taken whole: forced_run)
-//   k_fallback  one wave per file whose continuation never merged: serial walk
-//   k_walk_*    mark the segments on the true chain (parallel default, then
-//               one jump per irregular link for files whose chains skipped)
-//   k_count / hipcub exclusive scan / k_emit: (offset, length, hash) per chunk
+//               prefilter -> per-run candidate lists and summaries (run = kRun
+//               bytes)
+//   k_spec6     one 16-lane group (a DPP row) per segment: speculative cut
+//               chain from the segment start (group_next = exact fastcdc
+//               cut_gear semantics)
+//   k_link      one 16-lane group per segment: continue past the segment end
+//               until the chain merges with a later segment's speculative
+//               chain (forced stretches taken whole: forced_run)
+//   clean path  k_incr_scan (or k_incr_count + scan + k_add_base) + k_emit
+//   general     k_fallback (one wave per file whose continuation never
+//               merged: serial walk), k_walk_fast / k_irr_flags / k_walk_jumps
+//               (segments on the true chain, one jump per irregular link),
+//               k_count + hipcub scan, k_emit, k_emit_long
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -115,16 +118,39 @@ struct Work {
   uint32_t *irr_n;
 };
 
+// Tuning switches of a context, read from the environment once, when the
+// context is created (mcdc_ctx_create), never per call.  The first group
+// selects tested alternative paths (the staged pipeline, lane pieces, warm /
+// cold pieces, pinned-output mode); the second only exists in A/B builds
+// (-DMCDC_AB_KNOBS, `python -m mapache_amd.build --ab`), the product build
+// ignores those variables.
+struct Knobs {
+  int parts = 1;          // MCDC_PARTS: scan parts of the staged pipeline (1..4)
+  int tail_rounds = 2;    // MCDC_TAIL_ROUNDS: rounds of the last part
+  int part_tiles = 0;     // MCDC_PART_TILES: tiles per round (0: the scan's wave count)
+  int min_rounds = 8;     // MCDC_MIN_ROUNDS: smallest call that is staged, in rounds
+  int scan_pieces = 0;    // MCDC_SCAN_PIECES: lane pieces per run (0: by size, scan_pieces())
+  int scan_cold = 1;      // MCDC_SCAN_COLD: cold-started lane pieces
+  int pinned_direct = 1;  // MCDC_PINNED_DIRECT: k_emit writes pinned host output directly
+  // A/B builds only
+  int group = 16;         // MCDC_GROUP: lanes per chain group (8, 16, 32)
+  int spec_occ = 6;       // MCDC_SPEC_OCC: k_spec waves-per-SIMD build (5 or 6)
+  int dyn_tiles = 1;      // MCDC_DYN_TILES: scan tiles from an atomic counter
+  int first_static = 1;   // MCDC_FIRST_STATIC: each wave's first tile static
+  int seg_chunks = 16;    // MCDC_SEG_CHUNKS: expected chunks per segment
+};
+Knobs read_knobs();
+
 // launch wrappers (mcdc_kernels.hip); all enqueue on `stream`.
 void launch_fill_random(void *dst, uint64_t pos, uint64_t n, uint64_t seed, hipStream_t stream);
 // scan of full tiles [tile0, tile1) (+ the partial last tile when `tail`)
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
-                 uint64_t tile1, bool tail, int pieces = 1);
+                 uint64_t tile1, bool tail, int pieces, bool cold);
 int scan_pieces(uint64_t nruns_full, int num_cus);  // lane pieces per run for a whole-call scan
 uint64_t scan_waves(uint64_t ntiles, int num_cus);  // waves of a scan launch over ntiles
-void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream);
+void launch_spec(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0, uint32_t s1, hipStream_t stream);
 // node_cap: expanded continuation nodes per segment (~0 when everything is scanned)
-void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t node_cap,
+void launch_link(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0, uint32_t s1, uint64_t node_cap,
                  hipStream_t stream);
 void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
                              void *scan_tmp, size_t scan_tmp_bytes, hipStream_t stream);

@@ -626,7 +626,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
 // for comparison.
 // Tiles are in units of 64 / pieces runs (pieces = lane pieces per run).
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
-                 uint64_t tile1, bool tail, int pieces) {
+                 uint64_t tile1, bool tail, int pieces, bool cold) {
   const uint64_t rpt = 64 / (uint64_t)pieces;
   const uint64_t ntiles = tail ? (w.nruns + rpt - 1) / rpt - tile0 : tile1 - tile0;
   uint64_t blocks = ntiles;  // one block per CU up to the CU count (156 KiB LDS -> 1 block/CU)
@@ -635,12 +635,9 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
   if (blocks == 0) return;
   const int t = tail ? 1 : 0;
   const dim3 gr((unsigned)blocks), bl(1024);
-  const char *ce = std::getenv("MCDC_SCAN_COLD");
-  const bool cold = ce ? std::atoi(ce) != 0 : true;
   if (cold && pieces != 1) {  // (one piece: the saved bytes would spill, 128 VGPRs)
     if (pieces == 4) hipLaunchKernelGGL((k_scan_q<kRun, 4, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
-    else if (pieces == 2) hipLaunchKernelGGL((k_scan_q<kRun, 2, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
-    else hipLaunchKernelGGL((k_scan_q<kRun, 1, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    else hipLaunchKernelGGL((k_scan_q<kRun, 2, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
   } else {
     if (pieces == 4) hipLaunchKernelGGL((k_scan_q<kRun, 4, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
     else if (pieces == 2) hipLaunchKernelGGL((k_scan_q<kRun, 2, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
@@ -1025,6 +1022,7 @@ __device__ __forceinline__ void load_gear_lds(uint64_t *gt, const Work &W) {
   __syncthreads();
 }
 
+
 // One group per segment.
 template <int GS>
 __device__ __forceinline__ void spec_body(Work &W, const DevParams &P, uint32_t s0, uint32_t s1) {
@@ -1346,11 +1344,15 @@ __device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, cons
 // One group of GS lanes per segment, lane i owns chunk i (of each batch of
 // GS) and computes its hash itself.  Resolution kernels raise their wave priority:
 // they run beside the scan's later parts and are latency-bound.
+//
+// GEAR comes from the global table (a 2 KiB L1/L2-resident read), not from an
+// LDS copy: with an LDS copy, k_emit_long lost the LDS reads of whole waves
+// ("LDS-table item"), and the hash is the one output no later
+// stage re-checks.
 template <int GS>
 __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1) {
   __builtin_amdgcn_s_setprio(3);
-  __shared__ uint64_t gt[256];
-  load_gear_lds(gt, W);
+  const uint64_t *gt = W.gear;
   const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
   if (s >= s1) return;
   const uint64_t n = W.seg_count[s];
@@ -1383,12 +1385,29 @@ __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, 
 
 // Continuation stretches longer than kEmitInline nodes (k_link appended their
 // segments to long_list): the whole grid strides over each one's nodes.  GEAR
-// is read through the vector cache here, not from an LDS copy: with the LDS
-// table this kernel intermittently produced whole waves of wrong chunk hashes
-// (boundaries right) after a large call on the same device, a fault not
-// reproduced with the global table or with extra code in the loop (DESIGN.md
-// §3, open item).  The kernel is off the hot path.
+// is read from the global table (see k_emit).  The LDS-table builds of the
+// investigation ("LDS-table item"; tools/dbg/build_dbg.sh):
+//   MCDC_DBG_LDS=1  GEAR from an LDS copy at offset 0 (88 VGPRs: loses the LDS
+//                   reads of whole waves, 1.5-5 % of calls; 19-44 % under a
+//                   rocprofv3 --pmc pass)
+//   MCDC_DBG_LDS=5  same, the copy 512 bytes into the allocation (fails alike)
+//   MCDC_DBG_LDS=6  =1 with one more VGPR touched (90 -> 96 allocated): no loss
 __global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
+#ifdef MCDC_DBG_LDS
+#if MCDC_DBG_LDS == 5
+  __shared__ uint64_t gtl_raw[256 + 64];
+  uint64_t *gtl = gtl_raw + 64;
+#else
+  __shared__ uint64_t gtl[256];
+#endif
+  load_gear_lds(gtl, W);
+#if MCDC_DBG_LDS == 6
+  asm volatile("v_mov_b32 v89, 0" ::: "v89");
+#endif
+  const uint64_t *gt = gtl;
+#else
+  const uint64_t *gt = W.gear;
+#endif
   const uint32_t nl = *W.long_n;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint32_t li = 0; li < nl; ++li) {
@@ -1404,7 +1423,7 @@ __global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ncont; i += stride) {
       const uint64_t pos = cont_node(ct, cr, i, P.max);
       const uint64_t nxt = i + 1 < ncont ? cont_node(ct, cr, i + 1, P.max) : after;
-      emit_one(W, P, W.gear, F, base_out + i, pos, nxt);
+      emit_one(W, P, gt, F, base_out + i, pos, nxt);
     }
   }
 }
@@ -1554,39 +1573,68 @@ size_t scan_tmp_bytes(uint32_t nsegs) {
 
 static unsigned group_blocks(uint32_t n, int gs = kGroup) { return (n + 256 / gs - 1) / (256 / gs); }
 
-// chain-group size of k_spec / k_link (A/B knob MCDC_GROUP = 8, 16, 32; default kGroup)
-static int chain_group() {
-  static const int g = [] {
-    const char *v = std::getenv("MCDC_GROUP");
-    const int x = v ? std::atoi(v) : kGroup;
-    return (x == 8 || x == 16 || x == 32) ? x : kGroup;
-  }();
-  return g;
+Knobs read_knobs() {
+  auto env = [](const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+  };
+  Knobs k;
+  k.parts = std::min(std::max(env("MCDC_PARTS", k.parts), 1), 4);
+  k.tail_rounds = std::max(env("MCDC_TAIL_ROUNDS", k.tail_rounds), 1);
+  k.part_tiles = std::max(env("MCDC_PART_TILES", k.part_tiles), 0);
+  k.min_rounds = std::max(env("MCDC_MIN_ROUNDS", k.min_rounds), 0);
+  k.scan_pieces = env("MCDC_SCAN_PIECES", k.scan_pieces);
+  if (k.scan_pieces != 1 && k.scan_pieces != 2 && k.scan_pieces != 4) k.scan_pieces = 0;
+  k.scan_cold = env("MCDC_SCAN_COLD", k.scan_cold) != 0;
+  k.pinned_direct = env("MCDC_PINNED_DIRECT", k.pinned_direct) != 0;
+#ifdef MCDC_AB_KNOBS
+  k.group = env("MCDC_GROUP", k.group);
+  if (k.group != 8 && k.group != 16 && k.group != 32) k.group = kGroup;
+  k.spec_occ = env("MCDC_SPEC_OCC", k.spec_occ) == 5 ? 5 : 6;
+  k.dyn_tiles = env("MCDC_DYN_TILES", k.dyn_tiles) != 0;
+  k.first_static = env("MCDC_FIRST_STATIC", k.first_static) != 0;
+  k.seg_chunks = std::max(env("MCDC_SEG_CHUNKS", k.seg_chunks), 1);
+#endif
+  return k;
 }
 
-void launch_spec(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, hipStream_t stream) {
-  if (s1 > s0)
-    switch (chain_group()) {
-      case 8: hipLaunchKernelGGL(k_spec<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1); break;
-      case 32: hipLaunchKernelGGL(k_spec<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1); break;
-      default: {
-        const char *o = std::getenv("MCDC_SPEC_OCC");  // 5: the 82-VGPR build (A/B)
-        if (!(o && std::atoi(o) == 5))
-          hipLaunchKernelGGL(k_spec6<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
-        else
-          hipLaunchKernelGGL(k_spec<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
-      }
-    }
+void launch_spec(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0, uint32_t s1, hipStream_t stream) {
+  if (s1 <= s0) return;
+#ifdef MCDC_AB_KNOBS
+  if (k.group == 8) {
+    hipLaunchKernelGGL(k_spec<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1);
+    return;
+  }
+  if (k.group == 32) {
+    hipLaunchKernelGGL(k_spec<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1);
+    return;
+  }
+  if (k.spec_occ == 5) {  // the 82-VGPR build
+    hipLaunchKernelGGL(k_spec<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
+    return;
+  }
+#else
+  (void)k;
+#endif
+  hipLaunchKernelGGL(k_spec6<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1);
 }
 
-void launch_link(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t node_cap,
+void launch_link(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0, uint32_t s1, uint64_t node_cap,
                  hipStream_t stream) {
-  if (s1 > s0)
-    switch (chain_group()) {
-      case 8: hipLaunchKernelGGL(k_link<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1, node_cap); break;
-      case 32: hipLaunchKernelGGL(k_link<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1, node_cap); break;
-      default: hipLaunchKernelGGL(k_link<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1, node_cap);
-    }
+  if (s1 <= s0) return;
+#ifdef MCDC_AB_KNOBS
+  if (k.group == 8) {
+    hipLaunchKernelGGL(k_link<8>, dim3(group_blocks(s1 - s0, 8)), dim3(256), 0, stream, w, p, s0, s1, node_cap);
+    return;
+  }
+  if (k.group == 32) {
+    hipLaunchKernelGGL(k_link<32>, dim3(group_blocks(s1 - s0, 32)), dim3(256), 0, stream, w, p, s0, s1, node_cap);
+    return;
+  }
+#else
+  (void)k;
+#endif
+  hipLaunchKernelGGL(k_link<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1, node_cap);
 }
 
 // counts, offsets and boundaries of segments [s0, s1) assuming the clean case

@@ -96,20 +96,25 @@ def _check_sizes(min_size: int, avg_size: int, max_size: int, level) -> None:
 
 
 # ------------------------------------------------------------- contexts --
-_ctx_lock = threading.Lock()
-_ctx_default: Optional[_lib.Context] = None
+# One default context per thread: mapache chunks files on several rayon
+# workers at once (/root/reference/src/archiver/mod.rs:162-215), a context
+# serves one thread at a time (mcdc.h), and replacing a too-small context must
+# never close one that another thread is using.
+_tls = threading.local()
 DEFAULT_MAX_BYTES = 1 << 30
 
 
 def default_context(max_bytes: int = DEFAULT_MAX_BYTES, device: int = 0) -> _lib.Context:
-    """Process-wide context on `device` (created on first use)."""
-    global _ctx_default
-    with _ctx_lock:
-        if _ctx_default is None or _ctx_default.max_bytes < max_bytes:
-            if _ctx_default is not None:
-                _ctx_default.close()
-            _ctx_default = _lib.Context(device, max(max_bytes, DEFAULT_MAX_BYTES))
-        return _ctx_default
+    """This thread's context on `device` (created on first use, grown on demand)."""
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    c = ctxs.get(device)
+    if c is None or c.max_bytes < max_bytes:
+        if c is not None:
+            c.close()  # only this thread ever used it
+        c = ctxs[device] = _lib.Context(device, max(max_bytes, DEFAULT_MAX_BYTES))
+    return c
 
 
 class Chunker:

@@ -122,3 +122,23 @@ def test_out_of_range_chunk_rejected(ctx):
         assert ids.shape == (0, 32)
     finally:
         ctx.device_free(dp)
+
+
+def test_overlapping_and_repeated_chunks(ctx):
+    """A list whose chunks overlap or repeat (not a chunker output, but the
+    header allows it): its 16-KiB leaf groups exceed the disjoint-chunk bound
+    the grid is sized by; the kernels write nothing over the bound and the
+    call re-hashes with the exact group count — every ID still exact."""
+    n = 6 << 20
+    data = O.random_bytes(n, SEED + 9)
+    pairs = [(0, n)] * 5 + [(17, n - 17), (1 << 20, 3 << 20), (1 << 20, 3 << 20), (5, 70_000), (5, 70_000)]
+    pairs += [(o, 300_000) for o in range(0, n - 300_000, 99_991)]
+    c = _chunks(pairs)
+    dp = _device_bytes(ctx, data)
+    try:
+        got = ctx.chunk_ids(dp, n, c)
+        again = ctx.chunk_ids(dp, n, c)  # the grown workspace is reused
+    finally:
+        ctx.device_free(dp)
+    ref = O.chunk_ids(data, c, threads=8)
+    assert (got == ref).all() and (again == ref).all()

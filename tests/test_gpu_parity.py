@@ -236,13 +236,30 @@ def test_timing_reported(ctx):
     assert 0 < t["scan_ms"] <= t["device_ms"] and t["h2d_ms"] > 0
 
 
+@pytest.fixture
+def knob_ctx(monkeypatch):
+    """A fresh context created after the test sets its MCDC_* switches (a
+    context reads them once, at mcdc_ctx_create)."""
+    made = []
+
+    def make(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(v))
+        c = _lib.Context(0, 4 << 30)
+        made.append(c)
+        return c
+    yield make
+    for c in made:
+        c.close()
+
+
 @pytest.mark.parametrize("direct", [1, 0])
-def test_pinned_output_written_directly(ctx, monkeypatch, direct):
+def test_pinned_output_written_directly(knob_ctx, direct):
     """A pinned caller array is written by k_emit over PCIe (no staging copy;
     MCDC_PINNED_DIRECT=0: emitted into HBM and copied by one DMA): same result
     as the pageable path; a too-small pinned array reports MCDC_E_CAPACITY
     with the required count."""
-    monkeypatch.setenv("MCDC_PINNED_DIRECT", str(direct))
+    ctx = knob_ctx(MCDC_PINNED_DIRECT=direct)
     n = (96 << 20) + 777
     dp = ctx.device_alloc(n)
     try:
@@ -319,27 +336,31 @@ def test_plan_reuse_across_layouts(ctx):
         ctx.device_free(dp)
 
 
-@pytest.fixture
-def staged(monkeypatch):
-    """Force the staged pipeline (scan in 4 parts, resolution of the scanned
-    prefix overlapping the next part) on small inputs: a round = 16 tiles
-    (4 MiB), parts of 1, 3 and 9 rounds at the end."""
-    monkeypatch.setenv("MCDC_PARTS", "4")
-    monkeypatch.setenv("MCDC_TAIL_ROUNDS", "1")
-    monkeypatch.setenv("MCDC_PART_TILES", "16")
-    monkeypatch.setenv("MCDC_MIN_ROUNDS", "0")
-    yield
+@pytest.fixture(scope="module")
+def staged():
+    """A context forced into the staged pipeline (scan in 4 parts, resolution
+    of the scanned prefix overlapping the next part) on small inputs: a round =
+    16 tiles (4 MiB), parts of 1, 3 and 9 rounds at the end."""
+    mp = pytest.MonkeyPatch()
+    for k, v in (("MCDC_PARTS", 4), ("MCDC_TAIL_ROUNDS", 1), ("MCDC_PART_TILES", 16), ("MCDC_MIN_ROUNDS", 0)):
+        mp.setenv(k, str(v))
+    c = _lib.Context(0, 4 << 30)
+    mp.undo()  # the context keeps the switches; later contexts do not see them
+    yield c
+    c.close()
 
 
 @pytest.mark.parametrize("p", PARAMS, ids=lambda p: "/".join(map(str, p)))
-def test_staged_pipeline_random(ctx, staged, p):
+def test_staged_pipeline_random(staged, p):
+    ctx = staged
     n = (200 << 20) + 12345
     d = O.random_bytes(n, SEED + 7)
     _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
     assert ctx.timing()["scan_launches"] == 4
 
 
-def test_staged_pipeline_dirty_paths(ctx, staged):
+def test_staged_pipeline_dirty_paths(staged):
+    ctx = staged
     """Skipped segments and never-merging chains inside a staged call: the
     incremental pass flags them and the general resolution redoes the call."""
     p = PARAMS[0]
@@ -351,7 +372,8 @@ def test_staged_pipeline_dirty_paths(ctx, staged):
         _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
 
 
-def test_staged_pipeline_batch(ctx, staged):
+def test_staged_pipeline_batch(staged):
+    ctx = staged
     rng = np.random.default_rng(8)
     sizes = [int(x) for x in rng.integers(0, 3 << 20, 150)] + [0, 1, 16384, 40 << 20]
     files = [O.random_bytes(s, 500 + i) for i, s in enumerate(sizes)]
@@ -377,15 +399,14 @@ def test_call_larger_than_context_fails_loudly():
 
 
 @pytest.mark.parametrize("pieces,cold", [(1, 0), (2, 0), (2, 1), (4, 0), (4, 1)])
-def test_scan_lane_pieces(ctx, monkeypatch, pieces, cold):
+def test_scan_lane_pieces(knob_ctx, pieces, cold):
     """Every lane-piece variant of the scan (a 4 KiB run hashed by 1, 2 or 4
     lanes; the library picks by call size), warm (each piece re-reads the 48
     bytes before it) and cold (first 48 positions re-walked at tile end from
     the previous lane's hash), on the same inputs: edge sizes around the tile
     and run grid, a partial last tile, overflowed runs whose candidates come
     from several lanes, and a batch of ragged files."""
-    monkeypatch.setenv("MCDC_SCAN_PIECES", str(pieces))
-    monkeypatch.setenv("MCDC_SCAN_COLD", str(cold))
+    ctx = knob_ctx(MCDC_SCAN_PIECES=pieces, MCDC_SCAN_COLD=cold)
     for p in [PARAMS[0], PARAMS[2], PARAMS[6]]:
         for n in [47, 1023, 1024, 1025, 4097, (256 << 10) + 1, (64 << 20) + 4096 * 17 + 3, (200 << 20) + 12345]:
             d = O.random_bytes(n, SEED + 31 * n)
@@ -427,3 +448,68 @@ def test_short_last_segment(ctx, p):
     r_, rc = O.chunk_files(O.Params(*p), files, threads=4)
     assert (gc == rc).all()
     _same(g, r_)
+
+
+def test_long_stretch_hashes_repeated(ctx):
+    """The reproducer of the LDS-table item: 80 MiB of zeros
+    after a random prefix at 64/256/1024, whose ~80 000 forced chunks are
+    emitted by k_emit_long, chunked 60 times in one process.  With GEAR read
+    from an LDS copy this sequence lost whole waves of ChunkData.hash values
+    in 1.5-5 % of calls (19-44 % under a rocprofv3 --pmc pass); the product
+    reads the global table and must be exact in every call."""
+    p = (64, 256, 1024, 1)
+    d = np.concatenate([O.random_bytes(100_003, 9), np.zeros(80 << 20, np.uint8), O.random_bytes(3 << 20, 10)])
+    ref = O.chunk(O.Params(*p), d)
+    n = d.size
+    dp = ctx.device_alloc(n + 64)
+    cap = n // (p[0] - 1) + 2
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        ctx.h2d(dp, d)
+        bad_calls = []
+        for k in range(60):
+            c = ctx.chunk_device_to_device(_lib.params(*p), dp, n, d_out, cap)
+            g = ctx.d2h_chunks(d_out, c)
+            if not (len(g) == len(ref) and (g == ref).all()):
+                bad_calls.append(k)
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(dp)
+    assert not bad_calls, f"calls with wrong output: {bad_calls}"
+
+
+def test_batch_device_ranges_validated(ctx):
+    """mcdc_chunk_batch_device: files in any order are fine; overlapping
+    ranges, offset + length overflow and an arena span beyond the context's
+    max_bytes are rejected (MCDC_E_INVALID / MCDC_E_TOOBIG) before any launch."""
+    n = 8 << 20
+    dp = ctx.device_alloc(n)
+    p = _lib.params(*PARAMS[0])
+    try:
+        ctx.fill_random(dp, n, SEED + 12)
+        host = O.random_bytes(n, SEED + 12)
+        offs, lens = [5 << 20, 0, 1 << 20, 7 << 20], [1 << 20, 1 << 20, 0, 1 << 20]
+        g, gc = ctx.chunk_batch_device(p, dp, offs, lens)
+        r, rc = O.chunk_files(O.Params(*PARAMS[0]), [host[o:o + ln] for o, ln in zip(offs, lens)])
+        assert (gc == rc).all()
+        _same(g, r)
+        for offs, lens in (([0, 1 << 20], [(1 << 20) + 1, 5]), ([100, 50], [100, 100])):
+            with pytest.raises(_lib.McdcError) as ei:
+                ctx.chunk_batch_device(p, dp, offs, lens)
+            assert ei.value.code == _lib.MCDC_E_INVALID
+        with pytest.raises(_lib.McdcError) as ei:
+            ctx.chunk_batch_device(p, dp, [2**64 - 10], [100])
+        assert ei.value.code == _lib.MCDC_E_INVALID
+    finally:
+        ctx.device_free(dp)
+    small = _lib.Context(0, 1 << 20)
+    try:  # two 256 KiB files 4 MiB apart: 512 KiB of data, a 4.25 MiB span
+        dq = small.device_alloc(5 << 20)
+        try:
+            with pytest.raises(_lib.McdcError) as ei:
+                small.chunk_batch_device(p, dq, [0, 4 << 20], [256 << 10, 256 << 10])
+            assert ei.value.code == _lib.MCDC_E_TOOBIG
+        finally:
+            small.device_free(dq)
+    finally:
+        small.close()

@@ -221,7 +221,7 @@ int main(int argc, char **argv) {
   };
   float best, med;
   const int it = 7;
-  auto prod = [&] { launch_scan(W, P, cus, st, 0, ~0ull, true, scan_pieces(W.n_al / kRun, cus)); };
+  auto prod = [&] { launch_scan(W, P, cus, st, 0, ~0ull, true, scan_pieces(W.n_al / kRun, cus), true); };
   if (mode == "quadread") {
     med = time_it(st, 3, [&] {
       hipLaunchKernelGGL(k_read_quad<kRun>, dim3(cus), dim3(1024), 0, st, (const uint8_t *)d, n, sink);
@@ -273,7 +273,7 @@ int main(int argc, char **argv) {
     for (uint64_t sz = 32ull << 20; sz <= n; sz *= 2) {
       Work Ws = W; Ws.n_al = sz; Ws.nruns = (sz + kRun - 1) / kRun;
       const int reps = (int)std::max<uint64_t>(1, (4ull << 30) / sz);
-      med = time_it(st, 5, [&] { for (int r = 0; r < reps; ++r) launch_scan(Ws, P, cus, st, 0, ~0ull, true, scan_pieces(Ws.n_al / kRun, cus)); }, &best);
+      med = time_it(st, 5, [&] { for (int r = 0; r < reps; ++r) launch_scan(Ws, P, cus, st, 0, ~0ull, true, scan_pieces(Ws.n_al / kRun, cus), true); }, &best);
       printf("sweep %8.1f MiB x%3d: %7.3f TB/s (best %7.3f)\n", sz / 1048576.0, reps,
              sz * (double)reps / (med * 1e9), sz * (double)reps / (best * 1e9));
       fflush(stdout);
