@@ -572,6 +572,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
 
 int check_ctx(mcdc_ctx *ctx) {
   if (!ctx) return fail(MCDC_E_INVALID, "ctx is NULL");
+  (void)hipGetLastError();  // a failure of an earlier call on this thread must not be reported by this one
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return fail(MCDC_E_DEVICE, "hipSetDevice: %s", hipGetErrorString(e));
   return MCDC_OK;

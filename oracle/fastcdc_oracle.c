@@ -327,6 +327,49 @@ size_t oc_chunk_digest(const oc_params *p, const uint8_t *data, size_t n, uint64
   return k;
 }
 
+/* The counter-based stream [0, n) of `seed` chunked as one file, without
+ * holding it: slabs are regenerated with oc_fill_random and the unfinished
+ * window carried into the next slab.  A cut is taken only with >= max bytes
+ * ahead (or at the end of the stream), so each cut_gear sees what it would see
+ * over the whole slice (StreamCDC's refill rule).  Returns the
+ * chunk count; *digest as oc_chunk_digest, *sum = sum of lengths. */
+size_t oc_random_stream_digest(const oc_params *p, uint64_t seed, uint64_t n, size_t slab, uint64_t *digest,
+                               uint64_t *sum) {
+  pthread_once(&gear_once, gear_init);
+  if (slab < 4096) slab = 4096;
+  const size_t cap = slab + p->max_size;
+  uint8_t *buf = (uint8_t *)malloc(cap);
+  if (!buf) return 0;
+  size_t s = 0, e = 0, k = 0;  /* valid bytes buf[s, e) */
+  uint64_t gen = 0, off = 0, d = 0;
+  for (;;) {
+    if (e - s < p->max_size && gen < n) { /* refill */
+      memmove(buf, buf + s, e - s);
+      e -= s;
+      s = 0;
+      size_t take = cap - e;
+      if (take > n - gen) take = (size_t)(n - gen);
+      oc_fill_random(buf + e, gen, take, seed);
+      gen += take;
+      e += take;
+      continue;
+    }
+    if (e == s) break;
+    uint64_t h;
+    size_t c;
+    oc_cut_gear(p, buf + s, e - s, &h, &c);
+    if (c == 0) break;
+    d = oc_digest_step(d, off, c);
+    ++k;
+    off += c;
+    s += c;
+  }
+  free(buf);
+  *digest = d;
+  if (sum) *sum = off;
+  return k;
+}
+
 void oc_fill_random(uint8_t *dst, uint64_t pos, size_t n, uint64_t seed) {
   size_t i = 0;
   if ((pos & 7) == 0) { /* word-aligned fast path (little-endian host) */

@@ -105,6 +105,12 @@ size_t oc_chunk_files(const oc_params *p, const uint8_t *const *bufs,
 size_t oc_chunk_digest(const oc_params *p, const uint8_t *data, size_t n,
                        uint64_t *digest);
 
+/* The counter-based stream [0, n) of `seed` (oc_fill_random) chunked as one
+ * file, regenerated slab by slab (memory O(slab + max)): count, digest, and
+ * the sum of lengths.  For full-size (64 GiB) parity checks. */
+size_t oc_random_stream_digest(const oc_params *p, uint64_t seed, uint64_t n, size_t slab, uint64_t *digest,
+                               uint64_t *sum);
+
 /* Counter-based byte generator shared with the device fill kernel and the
  * bench: byte i = (splitmix64_at(seed, i/8) >> 8*(i%8)) & 0xff. */
 void oc_fill_random(uint8_t *dst, uint64_t pos, size_t n, uint64_t seed);

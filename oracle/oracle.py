@@ -82,6 +82,9 @@ def lib():
         L.oc_chunk_files.restype = ctypes.c_size_t
         L.oc_chunk_digest.argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_size_t, u64p]
         L.oc_chunk_digest.restype = ctypes.c_size_t
+        L.oc_random_stream_digest.argtypes = [ctypes.POINTER(OcParams), ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_size_t, u64p, u64p]
+        L.oc_random_stream_digest.restype = ctypes.c_size_t
         L.oc_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint64]
         L.oc_fill_random.restype = None
         L.oc_file_seed.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
@@ -187,6 +190,14 @@ def chunk_digest(params: Params, data):
     d = ctypes.c_uint64()
     k = lib().oc_chunk_digest(ctypes.byref(params.c()), ptr, a.size, ctypes.byref(d))
     return k, d.value
+
+
+def random_stream_digest(params: Params, seed: int, n: int, slab: int = 256 << 20):
+    """(count, digest, sum of lengths) of the counter-based stream [0, n) chunked
+    as one file, regenerated slab by slab (no n-byte buffer): full-size parity."""
+    d, sm = ctypes.c_uint64(), ctypes.c_uint64()
+    k = lib().oc_random_stream_digest(ctypes.byref(params.c()), seed, n, slab, ctypes.byref(d), ctypes.byref(sm))
+    return k, d.value, sm.value
 
 
 def digest_of(chunks: np.ndarray) -> int:

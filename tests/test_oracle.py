@@ -134,3 +134,15 @@ def test_prng_matches_definition():
     ref = bytes(((mix((7 + (((p >> 3) + 1) * 0x9e3779b97f4a7c15)) & ((1 << 64) - 1)) >> (8 * (p & 7))) & 0xff)
                 for p in range(3, 67))
     assert bytes(d) == ref
+
+
+@pytest.mark.parametrize("p", [(16384, 65536, 262144, 1), (64, 256, 1024, 1), (524288, 1048576, 8388608, 1)])
+def test_streamed_random_digest_equals_in_memory(p):
+    """oc_random_stream_digest (slabs regenerated, window carried across them)
+    gives the in-memory whole-slice result, for slabs smaller and larger than
+    max and stream lengths not a multiple of the slab."""
+    n = (40 << 20) + 12345
+    d = O.random_bytes(n, 77)
+    k, dig = O.chunk_digest(O.Params(*p), d)
+    for slab in (4096, 1 << 20, 5_000_000, 64 << 20):
+        assert O.random_stream_digest(O.Params(*p), 77, n, slab) == (k, dig, n)

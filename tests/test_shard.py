@@ -104,3 +104,104 @@ def test_gpu_rank_chunker_through_shard(ctx):
     for f, g in zip(files, got):
         r = O.chunk(O.Params(*P), f)
         assert len(g) == len(r) and (g == r).all()
+
+
+# ------------------------------------------------------ one stream, split --
+def _split_threads(data, p, world, fix_window=None):
+    """split_stream on `world` threads (a barrier-synchronised allgather), the
+    oracle as every rank's chunker; returns the concatenated list and stats."""
+    import threading
+    n = len(data)
+    slices = shard.stream_slices(n, world)
+    bar = threading.Barrier(world)
+    box = [None] * world
+    res, errs = [None] * world, []
+
+    def ag_for(r):
+        def ag(v):
+            box[r] = v
+            bar.wait()
+            out = list(box)
+            bar.wait()
+            return out
+        return ag
+
+    def run(r):
+        try:
+            s, e = slices[r]
+            res[r] = shard.split_stream(lambda a, b: O.chunk(O.Params(*p), data[a:b]), ag_for(r), s, e, n, p[2], r,
+                                        world, fix_window)
+        except BaseException as ex:
+            errs.append(repr(ex))
+            bar.abort()
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    return np.concatenate([x[0] for x in res]), [x[1] for x in res]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("p", [(16384, 65536, 262144, 1), (64, 256, 1024, 1), (524288, 1048576, 8388608, 1)],
+                         ids=lambda p: "/".join(map(str, p)))
+def test_split_stream_random(p, world):
+    d = O.random_bytes((24 << 20) + 12345, 61)
+    got, st = _split_threads(d, p, world)
+    ref = O.chunk(O.Params(*p), d)
+    assert len(got) == len(ref) and (got == ref).all()
+    assert all(s["rounds"] <= 2 for s in st)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_split_stream_seams_in_forced_stretches(world):
+    """Zero stretches out of phase with every slice start, some spanning several
+    seams: continuations run past slice ends, exits change, the exchange repeats."""
+    p = (4096, 16384, 65536, 1)
+    parts = [O.random_bytes(100_003, 71)]
+    for k in range(6):
+        parts += [np.zeros((3 << 20) + 777 * k, np.uint8), O.random_bytes(200_000 + 33 * k, 72 + k)]
+    parts += [np.zeros(9 << 20, np.uint8), O.random_bytes(1 << 20, 90)]
+    d = np.concatenate(parts)
+    got, st = _split_threads(d, p, world, fix_window=4 * p[2])
+    ref = O.chunk(O.Params(*p), d)
+    assert len(got) == len(ref) and (got == ref).all()
+    assert max(s["rounds"] for s in st) >= 2
+
+
+def _split_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = (16384, 65536, 262144, 1)
+        n = (20 << 20) + 99
+        s, e = shard.stream_slices(n, world)[rank]
+        hi = min(e + p[2], n)
+        mine = O.random_bytes(hi - s, 63, pos=s)  # this rank's bytes only: slice + right halo
+        got, st = shard.split_stream(lambda a, b: O.chunk(O.Params(*p), mine[a - s:b - s]),
+                                     shard.torch_allgather(), s, e, n, p[2], rank, world)
+        parts = [None] * world
+        dist.all_gather_object(parts, got)
+        if rank == 0:
+            ref = O.chunk(O.Params(*p), O.random_bytes(n, 63))
+            allc = np.concatenate(parts)
+            q.put((rank, bool(len(allc) == len(ref) and (allc == ref).all()), st["rounds"]))
+        else:
+            q.put((rank, True, st["rounds"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_stream_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert [r[1] for r in res] == [True, True], res
