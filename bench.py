@@ -1,31 +1,36 @@
 #!/usr/bin/env python3
 """bench.py — device-resident GiB/s chunked, FastCDC 16/64/256 KiB L1, MI355X.
 
-Workload (BASELINE.json configs[1]): per GPU one 64 GiB uniform-random byte
-buffer resident in HBM (counter-based PRNG generated on the device, seed per
-rank), FastCDC v2020 at min/avg/max = 16/64/256 KiB, Normalization::Level1.
-A step = one full chunking pass over that buffer through the C ABI
-(mcdc_chunk_device: scan + chain resolution + boundary emission), with the
-boundary list written to a device-resident output array (device-resident in,
-device-resident out: the next pipeline stage consumes it in HBM).  The same
-call with the list written to pinned host memory is reported beside it
-("host_out").  N GPUs = N independent streams (weak scaling, no collectives on
-the data path; torch.distributed is used only for the barrier and the
-max-over-ranks timing).
+Workload (BASELINE.json configs[1]): per GPU 64 GiB of one uniform-random
+byte stream resident in HBM (counter-based PRNG generated on the device),
+FastCDC v2020 at min/avg/max = 16/64/256 KiB, Normalization::Level1.  A step =
+one full chunking pass over the stream through the C ABI (mcdc_chunk_device:
+scan + chain resolution + boundary emission), boundary list written to a
+device-resident array (the next pipeline stage consumes it in HBM).
+
+N GPUs (one process per GPU, torchrun): ONE stream of N x 64 GiB split across
+the GPUs (weak scaling: 64 GiB per GPU) — mapache_amd.shard.split_stream: each
+rank chunks its slice plus a max-byte right halo, the ranks exchange their exit
+positions (one int64 each, RCCL all_gather) and each continues the previous
+rank's exit until it meets its own chain.  At N = 1 that is exactly configs[1].
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline      - the scan kernel (dominant) vs HBM peak: algorithmic bytes per
-                  launch (1 byte read per input byte) / average launch time from
-                  HIP events recorded on the library's stream.
-  cpu_baseline  - oracle/ C restatement of the crate, 1 thread, bounded sample
-                  of the same stream (rank 0, N=1 only).
-  host_out      - same step, boundary list to pinned host memory (PCIe-inclusive)
-  e2e_host      - pinned host input -> H2D -> kernels -> boundaries to host
-  batch_files   - BASELINE configs[2]: 10 000 independent 8 MiB files, one call
-  small_files   - BASELINE configs[3] stand-in: synthetic kernel-tree-like mix
-  chunk_ids     - SURVEY.md §8(f) next stage: BLAKE3 chunk IDs of the same 64 GiB
-                  boundary list in HBM (ID::from_content, processor.rs:184), and
-                  the chunk + ID pipeline
+  roofline        - the scan kernel (dominant) vs HBM peak: algorithmic bytes per
+                    launch (1 byte read per input byte) / average launch time from
+                    HIP events recorded on the library's stream.
+  cpu_baseline    - oracle/ C restatement of the crate, 1 thread, median of 5
+                    runs on a bounded sample of the same stream (rank 0, N=1).
+  corpus_sharded  - BASELINE configs[4]: a corpus of N x 8192 files of 8 MiB
+                    sharded by file across the GPUs (shard.assign_files), one
+                    batched device call per rank per step; every N.
+  host_out        - same step, boundary list to pinned host memory (PCIe-inclusive)
+  e2e_host        - pinned host input -> H2D -> kernels -> boundaries to host
+  e2e_pageable    - pageable host input (the Archiver's Vec<u8>), staged
+  batch_files     - BASELINE configs[2]: 10 000 independent 8 MiB files, one call
+  small_files     - BASELINE configs[3] stand-in: synthetic kernel-tree-like mix
+  chunk_ids       - SURVEY.md §8(f) next stage: BLAKE3 chunk IDs of the same 64 GiB
+                    boundary list in HBM (ID::from_content, processor.rs:184), and
+                    the chunk + ID pipeline
 """
 from __future__ import annotations
 
@@ -109,24 +114,37 @@ def _same(a: np.ndarray, b: np.ndarray) -> bool:
                 and (a["hash"] == b["hash"]).all())
 
 
-def cpu_baseline(sample_gib: float, gpu_chunks: np.ndarray) -> dict:
-    """Oracle (C restatement of fastcdc v2020), single thread, on the first
-    `sample_gib` GiB of rank 0's stream.  Also cross-checks the GPU boundaries
-    that lie wholly inside the sample (a size-independent parity probe)."""
+def _cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(sample_gib: float, gpu_chunks: np.ndarray, runs: int = 5) -> dict:
+    """Oracle (C restatement of fastcdc v2020), single thread, median of `runs`
+    timed runs on the first `sample_gib` GiB of rank 0's stream (pre-generated,
+    pre-faulted).  Also cross-checks the GPU boundaries that lie wholly inside
+    the sample (a size-independent parity probe)."""
     from oracle import oracle as O
     n = int(sample_gib * GIB)
     d = O.random_bytes(n, SEED)  # generation is not timed
-    t0 = time.perf_counter()
-    c = O.chunk(O.Params(*PARAMS), d)
-    dt = time.perf_counter() - t0
+    times, c = [], None
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        c = O.chunk(O.Params(*PARAMS), d)
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
     # GPU chunks that end before the sample's last max-window are final in both
     lim = n - PARAMS[2]
     g = gpu_chunks[gpu_chunks["offset"] + PARAMS[2] <= lim]
     ok = len(g) > 0 and _same(g, c[: len(g)])
     return {"value": round(n / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {sample_gib:g} GiB of the rank-0 stream (seed 0x{SEED:x}), 16/64/256 KiB L1, "
-                      f"oracle/fastcdc_oracle.c cut_gear loop, 1 thread, input pre-generated in RAM",
-            "cpu": _cpu_model(), "seconds": round(dt, 3), "parity_probe_chunks": int(len(g)),
+                      f"oracle/fastcdc_oracle.c cut_gear loop, 1 thread, input pre-generated in RAM, "
+                      f"median of {runs} runs",
+            "runs_s": [round(t, 3) for t in times], "cpu": _cpu_model(), "nproc": os.cpu_count(),
+            "cpus_usable": _cpus(), "seconds": round(dt, 3), "parity_probe_chunks": int(len(g)),
             "parity_probe_ok": bool(ok)}
 
 
@@ -157,6 +175,23 @@ def e2e_host(ctx, p, gib: float) -> dict:
     finally:
         ctx.host_free(hp)
         ctx.device_free(dp)
+
+
+def e2e_pageable(ctx, p, gib: float) -> dict:
+    """End-to-end from PAGEABLE host memory, the Archiver adapter's real input:
+    tests/cpp/test_host_api bench_stream (C++, its own process and contexts):
+    one mcdc_chunk_host over the whole buffer (pinned staging slabs filled by
+    the copy pool while the previous slab's DMA runs), and the windowed
+    StreamCDC mirror (256 MiB windows, each chunk's bytes copied out as the
+    crate's ChunkData.data)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "test_host_api")
+    r = subprocess.run([exe, "bench_stream", str(gib)], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-500:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    d["source"] = "pageable std::vector (C++ host mirror), 16/64/256 KiB"
+    return d
 
 
 def _timed(fn, steps: int, warmup: int):
@@ -309,16 +344,78 @@ def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_s
         ctx.device_free(d_ids)
 
 
+def corpus_sharded(ctx, p, files_per_gpu: int, file_bytes: int, steps: int, warmup: int, world: int, rank: int,
+                   barrier, allreduce_max, gather) -> dict:
+    """BASELINE configs[4]: a corpus of world x files_per_gpu files of file_bytes
+    (file i = the counter-based stream of seed SEED ^ (i + 1)), assigned to
+    ranks by shard.assign_files (no data exchange); each rank chunks its files
+    with one mcdc_chunk_batch_device call per step over its own arena."""
+    from mapache_amd import _lib, shard
+    nfiles = world * files_per_gpu
+    sizes = [file_bytes] * nfiles
+    mine = shard.assign_files(sizes, world)[rank]
+    offs = np.arange(len(mine), dtype=np.uint64) * np.uint64(file_bytes)
+    lens = np.full(len(mine), file_bytes, dtype=np.uint64)
+    nbytes = len(mine) * file_bytes
+    arena = ctx.device_alloc(nbytes)
+    cap = len(mine) * (file_bytes // (p.min_size - 1) + 2)
+    d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        for k, i in enumerate(mine):
+            ctx.fill_random(arena + k * file_bytes, file_bytes, SEED ^ (i + 1))
+        run = lambda: ctx.chunk_batch_device_to_device(p, arena, offs, lens, d_out, cap)  # noqa: E731
+        for _ in range(warmup):
+            run()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            total, counts = run()
+        barrier()
+        mine_s = time.perf_counter() - t0
+        elapsed = allreduce_max(mine_s)
+        # gathered result: per-file counts and an order-sensitive digest of the
+        # whole corpus's boundary lists (file order); parity probe: the rank's
+        # first and last files against the oracle
+        chunks = ctx.d2h_chunks(d_out, total)
+        starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        per_file = [(i, int(counts[k]), _lib.digest(chunks[starts[k]:starts[k + 1]])) for k, i in enumerate(mine)]
+        from oracle import oracle as O
+        ok = True
+        for k in sorted({0, len(mine) - 1}):
+            ref = O.chunk(O.Params(*PARAMS), O.random_bytes(file_bytes, SEED ^ (mine[k] + 1)))
+            ok &= _same(chunks[starts[k]:starts[k + 1]], ref)
+        parts = gather((per_file, bool(ok), mine_s))
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(arena)
+    if parts is None:
+        return {}
+    allf = sorted(x for part in parts for x in part[0])
+    dig = 0
+    for _, c, d in allf:
+        dig = (dig * 0x100000001b3 ^ d ^ c) & ((1 << 64) - 1)
+    total_bytes = nfiles * file_bytes
+    return {"files": nfiles, "file_bytes": file_bytes, "bytes": total_bytes, "steps": steps,
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "gib_s": round(total_bytes * steps / elapsed / GIB, 2),
+            "per_rank_gib_s": [round(nbytes * steps / part[2] / GIB, 2) for part in parts],
+            "chunks": int(sum(c for _, c, _ in allf)), "corpus_digest": f"{dig:016x}",
+            "parity_probe_files": 2 * len(parts), "parity_probe_ok": bool(all(part[1] for part in parts)),
+            "assignment": "shard.assign_files (LPT by bytes; equal sizes -> round robin), no data exchange",
+            "data": "synthetic uniform-random files (device PRNG, per-file seeds)"}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gib", type=float, default=64.0, help="bytes per GPU (GiB)")
-    ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
+    ap.add_argument("--cpu-sample-gib", type=float, default=4.0)
+    ap.add_argument("--cpu-runs", type=int, default=5)
     ap.add_argument("--e2e-gib", type=float, default=8.0)
     ap.add_argument("--batch-files", type=int, default=10000, help="configs[2] file count (0: skip)")
     ap.add_argument("--small-files", type=int, default=80000, help="configs[3] file count (0: skip)")
+    ap.add_argument("--corpus-files-per-gpu", type=int, default=8192, help="configs[4]: 8 MiB files per GPU (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the files-in-parallel CPU baseline "
                     "(16: this pool's CPU share per GPU)")
@@ -330,7 +427,7 @@ def main() -> int:
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
     # Rehearsal only (a 1-GPU box standing in for a node): every rank on
-    # device 0, barriers and the max-over-ranks reduction over gloo.
+    # device 0, the exchange and barriers over gloo.
     rehearse = os.environ.get("MCDC_BENCH_ONE_DEVICE") == "1"
     if rehearse:
         local = 0
@@ -339,75 +436,126 @@ def main() -> int:
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
+        if not rehearse:
+            torch.cuda.set_device(local)
         dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
 
-    from mapache_amd import _lib
+    from mapache_amd import _lib, shard
     p = _lib.params(*PARAMS)
     n = int(a.gib * GIB)
     extras = rank == 0 and world == 1
-    max_bytes = max(n, a.batch_files * (8 << 20) if extras else 0)
+    corpus_bytes = a.corpus_files_per_gpu * (8 << 20)
+    max_bytes = max(n + PARAMS[2], corpus_bytes, a.batch_files * (8 << 20) if extras else 0)
     ctx = _lib.Context(local, max_bytes)
+    dev = None if (dist is None or rehearse) else f"cuda:{local}"
+
+    def barrier():
+        if dist is not None:
+            import torch
+            if dev is not None:
+                torch.cuda.synchronize()
+            dist.barrier()
+
+    def allreduce_max(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=dev or "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(obj):
+        if dist is None:
+            return [obj]
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(obj, parts, dst=0)
+        return parts
+
+    # The stream: N x n bytes, rank r holds slice r plus a max-byte right halo.
     # Allocation order matters on this device heap: memory that a freed
     # multi-GiB buffer occupied is slower afterwards (tools/e2e_probe.py: a DMA
     # into it runs at 33 instead of 57.6 GB/s).  So the headline runs first on
     # a fresh heap, and the e2e host leg takes fresh memory of its own before
     # the 64 GiB buffers are freed.
-    dp = ctx.device_alloc(n)
-    ctx.fill_random(dp, n, SEED ^ rank)  # rank 0 uses SEED itself
-    cap = n // (p.min_size - 1) + 2
+    total = world * n
+    s, e = shard.stream_slices(total, world)[rank] if world > 1 else (0, n)
+    hi = min(e + PARAMS[2], total)
+    dp = ctx.device_alloc(hi - s)
+    ctx.fill_random(dp, hi - s, SEED, pos=s)  # the one stream (rank 0 at N = 1: configs[1])
+    cap = (hi - s) // (p.min_size - 1) + 2
     d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    allgather = shard.torch_allgather(device=dev) if dist is not None else None
+    split_stats = {}
 
-    def barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+    def step():
+        k = ctx.chunk_device_to_device(p, dp, hi - s, d_out, cap)
+        if world == 1:
+            return k
+        spec = shard.DeviceChunks(ctx, d_out, k, base=s, window=64)
+        res, st = shard.split_stream(lambda x, y: ctx.chunk_device(p, dp + (x - s), y - x), allgather, s, e, total,
+                                     PARAMS[2], rank, world, spec=spec, materialize=False)
+        split_stats.update(st)
+        split_stats["fixup_calls_total"] = split_stats.get("fixup_calls_total", 0) + st["fixup_calls"]
+        return len(res)
 
     for _ in range(a.warmup):
-        ctx.chunk_device_to_device(p, dp, n, d_out, cap)
+        step()
+    split_stats.clear()
     scan_ms, dev_ms, total_ms = [], [], []
     barrier()
     t0 = time.perf_counter()
     count = 0
     for _ in range(a.steps):
-        count = ctx.chunk_device_to_device(p, dp, n, d_out, cap)
-        t = ctx.timing()
-        scan_ms.append(t["scan_ms"])
-        dev_ms.append(t["device_ms"])
-        total_ms.append(t["total_ms"])
+        count = step()
+        t = ctx.timing() if world == 1 else None
+        if t:
+            scan_ms.append(t["scan_ms"])
+            dev_ms.append(t["device_ms"])
+            total_ms.append(t["total_ms"])
     barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = allreduce_max(time.perf_counter() - t0)
+    if world > 1:  # the main call's device timings (outside the timed loop)
+        ctx.chunk_device_to_device(p, dp, hi - s, d_out, cap)
+        t = ctx.timing()
+        scan_ms, dev_ms, total_ms = [t["scan_ms"]], [t["device_ms"]], [t["total_ms"]]
 
     n_gpus = world if world > 1 else 1
     total_bytes = n_gpus * n * a.steps
     value = total_bytes / elapsed / GIB
     scan_avg = float(np.mean(scan_ms))
-    achieved = n / (scan_avg * 1e-3) / 1e9
+    achieved = (hi - s) / (scan_avg * 1e-3) / 1e9
     tpb, tsrc = _pmc_traffic()
+    counts = gather(int(count))
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": n_gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"one {a.gib:g} GiB uniform-random buffer per GPU, device-resident in and out "
-                               f"(BASELINE configs[1])", "params": "FastCDC v2020 16/64/256 KiB Level1",
-                   "bytes_per_gpu": n, "chunks_per_step": int(count),
-                   "parallelism": f"{n_gpus} independent streams, no collectives",
+        "config": {"workload": (f"one {a.gib:g} GiB uniform-random stream, device-resident in and out "
+                                f"(BASELINE configs[1])" if world == 1 else
+                                f"one {n_gpus * a.gib:g} GiB uniform-random stream split across {n_gpus} GPUs "
+                                f"({a.gib:g} GiB per GPU + 256 KiB halo), device-resident in and out"),
+                   "params": "FastCDC v2020 16/64/256 KiB Level1",
+                   "bytes_per_gpu": n, "chunks_per_step": int(sum(counts)) if counts else int(count),
+                   "parallelism": ("1 GPU" if world == 1 else
+                                   f"{n_gpus} slices of one stream; exits exchanged (RCCL all_gather, int64 per "
+                                   f"rank), seam continuations on the receiving GPU"),
                    "host_numa_node": numa_node},
         "roofline": {"bound": "hbm", "kernel": "k_scan_q", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": int(round(tpb * n)) if tpb else None, "traffic_unit": "bytes per launch",
-                     "traffic_source": tsrc, "bytes_per_launch": n, "avg_launch_ms": round(scan_avg, 3)},
+                     "traffic": int(round(tpb * (hi - s))) if tpb else None, "traffic_unit": "bytes per launch",
+                     "traffic_source": tsrc, "bytes_per_launch": hi - s, "avg_launch_ms": round(scan_avg, 3)},
         "device_only": {"scan_ms": round(scan_avg, 3), "device_ms": round(float(np.mean(dev_ms)), 3),
-                        "gib_s": round(n / (float(np.mean(dev_ms)) * 1e-3) / GIB, 2),
+                        "gib_s": round((hi - s) / (float(np.mean(dev_ms)) * 1e-3) / GIB, 2),
                         "call_ms": round(float(np.mean(total_ms)), 3)},
     }
-    chunks = ctx.d2h_chunks(d_out, count)
+    if world > 1:
+        st = gather(dict(split_stats))
+        if st:
+            result["split_stream"] = {"rounds_max": max(x.get("rounds", 0) for x in st),
+                                      "fixup_calls_per_step": round(sum(x.get("fixup_calls_total", 0) for x in st)
+                                                                    / a.steps, 2),
+                                      "merged_in_slice": all(x.get("merged", True) for x in st)}
+    chunks = ctx.d2h_chunks(d_out, ctx.chunk_device_to_device(p, dp, hi - s, d_out, cap)) if extras else None
     if extras:
         # same step, boundary list to pinned host memory (crosses PCIe inside the call)
         out = ctx.pinned_out(cap)
@@ -417,15 +565,15 @@ def main() -> int:
                               "output": "pinned host array (hipHostMalloc), written by k_emit over PCIe"}
         if not a.no_ids:
             try:
-                result["chunk_ids"] = chunk_ids(ctx, p, dp, n, d_out, int(count), 3, 1.0, a.no_cpu)
-            except Exception as e:  # reported, never silently dropped
-                result["chunk_ids"] = {"error": f"{type(e).__name__}: {e}"}
+                result["chunk_ids"] = chunk_ids(ctx, p, dp, n, d_out, len(chunks), 3, 1.0, a.no_cpu)
+            except Exception as ex:  # reported, never silently dropped
+                result["chunk_ids"] = {"error": f"{type(ex).__name__}: {ex}"}
         if a.e2e_gib > 0:
-            try:
-                result["e2e_host"] = e2e_host(ctx, p, a.e2e_gib)
-            except Exception as e:  # reported, never silently dropped
-                result["e2e_host"] = {"error": f"{type(e).__name__}: {e}"}
-    if extras:
+            for key, fn in (("e2e_host", e2e_host), ("e2e_pageable", e2e_pageable)):
+                try:
+                    result[key] = fn(ctx, p, a.e2e_gib)
+                except Exception as ex:  # reported, never silently dropped
+                    result[key] = {"error": f"{type(ex).__name__}: {ex}"}
         # (after the chunk-ID stage, which reads the headline's list in d_out)
         # mapache's own defaults (src/global/defaults.rs:35-40), same buffer
         p512 = _lib.params(512 << 10, 1 << 20, 8 << 20, 1)
@@ -445,18 +593,26 @@ def main() -> int:
                                        "note": "same 64 GiB buffer, device-resident in and out, mapache defaults"}
     ctx.device_free(d_out)
     ctx.device_free(dp)
+    if a.corpus_files_per_gpu > 0:
+        try:
+            r = corpus_sharded(ctx, p, a.corpus_files_per_gpu, 8 << 20, max(3, a.steps // 2), 1, world, rank,
+                               barrier, allreduce_max, gather)
+            if r:
+                result["corpus_sharded"] = r
+        except Exception as ex:  # reported, never silently dropped
+            result["corpus_sharded"] = {"error": f"{type(ex).__name__}: {ex}"}
     if extras:
         cpu_files = 0 if a.no_cpu else a.cpu_batch_files
-        threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+        threads = max(1, min(a.cpu_threads, _cpus()))
         for key, fn in (("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3, cpu_files, threads)
                          if a.batch_files > 0 else None),
                         ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None)):
             try:
                 result[key] = fn()
-            except Exception as e:  # reported, never silently dropped
-                result[key] = {"error": f"{type(e).__name__}: {e}"}
+            except Exception as ex:  # reported, never silently dropped
+                result[key] = {"error": f"{type(ex).__name__}: {ex}"}
         if not a.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(a.cpu_sample_gib, chunks)
+            result["cpu_baseline"] = cpu_baseline(a.cpu_sample_gib, chunks, a.cpu_runs)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

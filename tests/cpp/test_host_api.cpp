@@ -11,7 +11,10 @@
 // Usage: test_host_api cpu | gpu      (exit 0 = pass; prints one line per test)
 #include "fastcdc_v2020.hpp"
 
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <functional>
 #include <string>
@@ -134,8 +137,71 @@ static void gpu_tests() {
   }
 }
 
+// End-to-end from pageable memory, the Archiver adapter's real input (a file's
+// bytes in a Vec<u8> read through BufReader, /root/reference/src/archiver/
+// processor.rs:165-167): (a) one mcdc_chunk_host call over the whole pageable
+// buffer; (b) the windowed StreamCDC mirror over an in-memory reader (256 MiB
+// windows, every chunk's bytes copied into its ChunkData as the crate does).
+// Prints one JSON line; both outputs are compared with each other.
+static int bench_stream(double gib) {
+  using clk = std::chrono::steady_clock;
+  const size_t n = static_cast<size_t>(gib * double(1ull << 30));
+  std::vector<uint8_t> data(n);
+  oc_fill_random(data.data(), 0, n, 0x6d61706163686521ull ^ 0x77);
+  const uint32_t mn = 16384, av = 65536, mx = 262144;
+  Context ctx(0, (size_t(512) << 20) > n ? (size_t(512) << 20) : n);
+  const mcdc_params p = detail::make_params(mn, av, mx, Normalization::Level1);
+  double best_host = 1e30;
+  std::vector<mcdc_chunk> ref;
+  mcdc_timing t{};
+  for (int r = 0; r < 3; ++r) {
+    const auto t0 = clk::now();
+    ref = ctx.chunk_host(p, data.data(), n);
+    const double s = std::chrono::duration<double>(clk::now() - t0).count();
+    if (s < best_host) {
+      best_host = s;
+      t = ctx.timing();
+    }
+  }
+  struct MemReader {
+    const uint8_t *p;
+    size_t n, at = 0;
+    long read(uint8_t *dst, size_t want) {
+      const size_t k = std::min(want, n - at);
+      std::memcpy(dst, p + at, k);
+      at += k;
+      return static_cast<long>(k);
+    }
+  };
+  Context wctx(0, size_t(256) << 20);
+  double best_stream = 1e30;
+  bool same = true;
+  for (int r = 0; r < 3; ++r) {
+    StreamCDC<MemReader> sc(MemReader{data.data(), n}, mn, av, mx, Normalization::Level1, size_t(256) << 20, &wctx);
+    size_t i = 0;
+    bool ok = true;
+    const auto t0 = clk::now();
+    while (auto c = sc.next()) {
+      const ChunkData &d = std::get<ChunkData>(*c);
+      ok = ok && i < ref.size() && d.offset == ref[i].offset && d.length == ref[i].length && d.hash == ref[i].hash;
+      ++i;
+    }
+    const double s = std::chrono::duration<double>(clk::now() - t0).count();
+    same = same && ok && i == ref.size();
+    best_stream = std::min(best_stream, s);
+  }
+  const double g = double(n) / double(1ull << 30);
+  std::printf("{\"bytes\": %zu, \"chunks\": %zu, \"chunk_host_pageable_gib_s\": %.2f, \"chunk_host_ms\": %.3f, "
+              "\"h2d_ms\": %.3f, \"device_ms\": %.3f, \"stream_cdc_gib_s\": %.2f, \"stream_cdc_ms\": %.3f, "
+              "\"identical\": %s}\n",
+              n, ref.size(), g / best_host, best_host * 1e3, t.h2d_ms, t.device_ms, g / best_stream,
+              best_stream * 1e3, same ? "true" : "false");
+  return same ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
   const std::string mode = argc > 1 ? argv[1] : "cpu";
+  if (mode == "bench_stream") return bench_stream(argc > 2 ? std::atof(argv[2]) : 8.0);
   cpu_tests();
   if (mode == "gpu") gpu_tests();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);

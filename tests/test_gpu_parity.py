@@ -513,3 +513,21 @@ def test_batch_device_ranges_validated(ctx):
             small.device_free(dq)
     finally:
         small.close()
+
+
+def test_pageable_staging_sizes(ctx):
+    """Host entry points from pageable memory: the staging copy is split over
+    the copy pool's threads and two pinned slabs; every byte must arrive for
+    sizes whose per-thread shares do not divide evenly (8 044 034 lost its
+    last 2 bytes to a rounding error once), around the 4 MiB hand-off
+    threshold, across the 256 MiB slab edge, and for batches of many files."""
+    p = PARAMS[2]
+    for n in [(4 << 20) - 1, 4 << 20, (4 << 20) + 1, 8_044_034, 8 * 1_005_504 + 7, (256 << 20) + 3, (512 << 20) - 5]:
+        d = O.random_bytes(n, SEED + n)
+        _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    rng = np.random.default_rng(19)
+    files = [O.random_bytes(int(s), 700 + i) for i, s in enumerate(rng.integers(0, 9 << 20, 70))]
+    g, gc = ctx.chunk_batch(_lib.params(*p), files)
+    r, rc = O.chunk_files(O.Params(*p), files, threads=8)
+    assert (gc == rc).all()
+    _same(g, r)
