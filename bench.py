@@ -61,15 +61,17 @@ def _dist():
 
 
 def _pmc_traffic():
-    """Calibrated PMC read traffic of the scan (profiles/r01/pmc_traffic.json, written from a
-    separate rocprofv3 --pmc FETCH_SIZE pass by tools/pmc_calib.sh): HBM bytes per input byte."""
-    path = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return float(d["traffic_per_input_byte"]), os.path.relpath(path, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+    """Calibrated PMC read traffic of the scan (profiles/rNN/pmc_traffic.json, written from
+    separate rocprofv3 --pmc FETCH_SIZE passes by tools/profile_round.sh): HBM bytes per input byte."""
+    for rnd in ("r02", "r01"):  # the latest round's measurement
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            return float(d["traffic_per_input_byte"]), os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def _bind_near_gpu(device: int):
