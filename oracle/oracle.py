@@ -96,6 +96,18 @@ def lib():
         L.ob_chunk_ids.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                    ctypes.c_int, ctypes.c_void_p]
         L.ob_chunk_ids.restype = None
+        vp = ctypes.c_void_p
+        L.oa_sbox.argtypes = [vp]
+        L.oa_aes_encrypt_block.argtypes = [vp, ctypes.c_int, vp, vp]
+        L.oa_aes_encrypt_block.restype = ctypes.c_int
+        L.oa_dot.argtypes = [vp, vp, vp]
+        L.oa_polyval.argtypes = [vp, vp, ctypes.c_size_t, vp]
+        L.oa_siv_derive.argtypes = [vp, vp, vp, vp]
+        for name in ("oa_siv_encrypt", "oa_siv_decrypt"):
+            getattr(L, name).argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp]
+            getattr(L, name).restype = ctypes.c_int
+        L.oa_seal_blobs.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, vp, vp, ctypes.c_int]
+        L.oa_seal_blobs.restype = None
         _lib = L
     return _lib
 
@@ -330,3 +342,101 @@ def blake3_py(data: bytes) -> bytes:
         return _b3_compress(_B3_IV, lcv + rcv, 0, 64, 4 | (8 if root else 0))
 
     return b"".join(w.to_bytes(4, "little") for w in node(bytes(data), 0, True))
+
+
+# ---------------------------------------------------------- AES-GCM-SIV --
+# SecureStorage's encryption: AES-256-GCM-SIV (crate aes-gcm-siv 0.11.1), no
+# AAD, random 12-byte nonce, blob = nonce || ciphertext || tag
+# (/root/reference/src/repository/storage.rs:97-118).  C restatement in
+# oracle/aead_oracle.c (RFC 8452 over FIPS-197).
+NONCE_BYTES, TAG_BYTES = 12, 16
+SEAL_OVERHEAD = NONCE_BYTES + TAG_BYTES
+
+
+def _bytes(x) -> bytes:
+    return bytes(x) if not isinstance(x, np.ndarray) else x.tobytes()
+
+
+def aes_sbox() -> bytes:
+    out = ctypes.create_string_buffer(256)
+    lib().oa_sbox(out)
+    return out.raw
+
+
+def aes_encrypt_block(key, block) -> bytes:
+    key, block = _bytes(key), _bytes(block)
+    assert len(block) == 16
+    out = ctypes.create_string_buffer(16)
+    if lib().oa_aes_encrypt_block(key, len(key), block, out) != 0:
+        raise ValueError("AES key must be 16 or 32 bytes")
+    return out.raw
+
+
+def polyval_dot(a, b) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().oa_dot(_bytes(a), _bytes(b), out)
+    return out.raw
+
+
+def polyval(h, x) -> bytes:
+    x = _bytes(x)
+    assert len(x) % 16 == 0
+    out = ctypes.create_string_buffer(16)
+    lib().oa_polyval(_bytes(h), x, len(x) // 16, out)
+    return out.raw
+
+
+def siv_derive(key, nonce):
+    """(message-authentication key, message-encryption key) of RFC 8452 §4."""
+    a, e = ctypes.create_string_buffer(16), ctypes.create_string_buffer(32)
+    lib().oa_siv_derive(_bytes(key), _bytes(nonce), a, e)
+    return a.raw, e.raw
+
+
+def siv_encrypt(key, nonce, plaintext, aad=b"") -> bytes:
+    """ciphertext || tag (RFC 8452 §4); key 16 or 32 bytes."""
+    key, nonce, pt, aad = _bytes(key), _bytes(nonce), _bytes(plaintext), _bytes(aad)
+    assert len(nonce) == NONCE_BYTES
+    out = ctypes.create_string_buffer(len(pt) + TAG_BYTES)
+    if lib().oa_siv_encrypt(key, len(key), nonce, aad, len(aad), pt, len(pt), out) != 0:
+        raise ValueError("bad key length")
+    return out.raw
+
+
+def siv_decrypt(key, nonce, ct_tag, aad=b""):
+    """plaintext, or None when the tag does not verify (RFC 8452 §5)."""
+    key, nonce, ct, aad = _bytes(key), _bytes(nonce), _bytes(ct_tag), _bytes(aad)
+    if len(ct) < TAG_BYTES:
+        return None
+    out = ctypes.create_string_buffer(max(len(ct) - TAG_BYTES, 1))
+    if lib().oa_siv_decrypt(key, len(key), nonce, aad, len(aad), ct, len(ct), out) != 0:
+        return None
+    return out.raw[: len(ct) - TAG_BYTES]
+
+
+def encrypt_with_key(key, nonce, data) -> bytes:
+    """storage.rs:97-118 with the nonce made explicit: nonce || ct || tag."""
+    return _bytes(nonce) + siv_encrypt(key, nonce, data)
+
+
+def decrypt_with_key(key, blob):
+    """storage.rs:120-139: split the nonce off, open; None on failure."""
+    blob = _bytes(blob)
+    if len(blob) < SEAL_OVERHEAD:
+        return None
+    return siv_decrypt(key, blob[:NONCE_BYTES], blob[NONCE_BYTES:])
+
+
+def seal_blobs(key, data, offsets, lengths, nonces, threads: int = 1):
+    """Every blob [offsets[i], +lengths[i]) of `data` sealed as nonce || ct ||
+    tag, packed back to back -> (out bytes as uint8 array, out offsets)."""
+    a, ptr = _buf(data)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint64)
+    nz = np.ascontiguousarray(nonces, dtype=np.uint8).reshape(-1, NONCE_BYTES)
+    assert len(off) == len(ln) == len(nz)
+    out_off = np.concatenate([[0], np.cumsum(ln + SEAL_OVERHEAD)]).astype(np.uint64)
+    out = np.zeros(max(int(out_off[-1]), 1), dtype=np.uint8)
+    lib().oa_seal_blobs(_bytes(key), ptr, off.ctypes.data, ln.ctypes.data, len(off), nz.ctypes.data,
+                        out.ctypes.data, out_off.ctypes.data, threads)
+    return out[: int(out_off[-1])], out_off[:-1]
