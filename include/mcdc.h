@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MCDC_ABI_VERSION 2
+#define MCDC_ABI_VERSION 3
 
 /* status codes */
 #define MCDC_OK 0
@@ -46,6 +46,7 @@ extern "C" {
 #define MCDC_E_NOMEM (-5)    /* device or pinned host allocation failed              */
 #define MCDC_E_TOOBIG (-6)   /* input larger than the context was created for       */
 #define MCDC_E_INTERNAL (-7) /* internal consistency check failed                  */
+#define MCDC_E_AUTH (-8)     /* mcdc_open_device: a blob failed authentication     */
 
 /* fastcdc::v2020::Normalization (crate enum; Level1 is what mapache uses,
  * processor.rs:178). */
@@ -89,6 +90,7 @@ typedef struct {
   uint64_t scan_launches; /* number of scan kernel launches             */
   uint64_t fallback_files; /* files resolved by the serial fallback     */
   double ids_ms;       /* chunk-ID (BLAKE3) kernels of mcdc_chunk_ids_device */
+  double aead_ms;      /* sealing kernels of mcdc_seal_device / mcdc_open_device */
 } mcdc_timing;
 
 /* ------------------------------------------------------------------ API -- */
@@ -156,6 +158,48 @@ int mcdc_chunk_batch_device(struct mcdc_ctx *ctx, const mcdc_params *params,
  * on its own).  A chunk outside [0, n) -> MCDC_E_INVALID. */
 int mcdc_chunk_ids_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
                           size_t nchunks, uint8_t *ids);
+
+/* ------------------------------------------------------ SecureStorage sealing
+ * mapache encodes every blob it stores as zstd, then AES-256-GCM-SIV
+ * (/root/reference/src/repository/storage.rs:61-65 encode; :97-118
+ * encrypt_with_key, crate aes-gcm-siv 0.11.1): a 32-byte key, a fresh random
+ * 12-byte nonce per blob, no associated data, and the stored bytes
+ *     nonce (12) || ciphertext (= plaintext length) || tag (16).
+ * These entry points run that encryption for many blobs at once on the GPU
+ * (RFC 8452; bit-identical to the crate).  The nonce is an argument: the
+ * caller draws it from its CSPRNG (OsRng in storage.rs:103) exactly as before.
+ *
+ * d_in: device buffer of n_in bytes (any alignment); blob i is
+ * d_in[blobs[i].offset, + blobs[i].length) — for sealing, the compressed
+ * blobs; extents may overlap; one outside [0, n_in) -> MCDC_E_INVALID.
+ * Output: the results packed back to back from d_out in blob order;
+ * out_offsets (optional, nblobs + 1 entries, host or device memory) receives
+ * each result's offset and, last, the total; a total above out_cap ->
+ * MCDC_E_CAPACITY (nothing written; *out_offsets still filled when given).
+ * blobs, nonces: host or device memory. */
+#define MCDC_NONCE_BYTES 12
+#define MCDC_TAG_BYTES 16
+#define MCDC_SEAL_OVERHEAD 28
+
+typedef struct {
+  uint64_t offset;
+  uint64_t length;
+} mcdc_blob;
+
+/* encrypt_with_key for every blob: result i = nonces[12 i, + 12) ||
+ * ciphertext || tag, length blobs[i].length + 28. */
+int mcdc_seal_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in,
+                     const mcdc_blob *blobs, size_t nblobs, const uint8_t *nonces, void *d_out,
+                     size_t out_cap, uint64_t *out_offsets);
+
+/* decrypt_with_key (storage.rs:128-144) for every sealed extent: result i is
+ * the plaintext (length - 28 bytes).  status (optional, host or device, nblobs
+ * entries): 0 authentic, -1 not (tag mismatch, or an extent shorter than 28
+ * bytes, where the crate errors too); a failed blob's result bytes are zero.
+ * Returns MCDC_E_AUTH when any blob failed, MCDC_OK otherwise. */
+int mcdc_open_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in,
+                     const mcdc_blob *sealed, size_t nblobs, void *d_out, size_t out_cap,
+                     uint64_t *out_offsets, int32_t *status);
 
 /* ---------------------------------------------------------------- batching
  * Cross-worker batching front-end.  mapache chunks files on read_concurrency

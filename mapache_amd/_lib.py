@@ -25,6 +25,8 @@ MCDC_E_DEVICE = -4
 MCDC_E_NOMEM = -5
 MCDC_E_TOOBIG = -6
 MCDC_E_INTERNAL = -7
+MCDC_E_AUTH = -8
+NONCE_BYTES, TAG_BYTES, SEAL_OVERHEAD = 12, 16, 28
 
 # every symbol include/mcdc.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -33,7 +35,7 @@ EXPORTS = (
     "mcdc_last_error", "mcdc_device_alloc", "mcdc_device_free", "mcdc_host_alloc",
     "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_memcpy_d2h", "mcdc_fill_random_device", "mcdc_digest",
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
-    "mcdc_batcher_chunk", "mcdc_batcher_stats",
+    "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device",
 )
 
 
@@ -52,7 +54,7 @@ class McdcTiming(ctypes.Structure):
                 ("d2h_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
                 ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64),
-                ("ids_ms", ctypes.c_double)]
+                ("ids_ms", ctypes.c_double), ("aead_ms", ctypes.c_double)]
 
 
 class McdcBatcherStats(ctypes.Structure):
@@ -108,6 +110,8 @@ def load():
     L.mcdc_batcher_destroy.restype = None
     L.mcdc_batcher_chunk.argtypes = [vp, vp, sz, vp, sz, P(sz)]
     L.mcdc_batcher_stats.argtypes = [vp, P(McdcBatcherStats)]
+    L.mcdc_seal_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
+    L.mcdc_open_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -294,6 +298,49 @@ class Context:
         check(load().mcdc_chunk_ids_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(cptr), count,
                                            out.ctypes.data))
         return out[:count]
+
+    # ----------------------------------------------------------- sealing --
+    @staticmethod
+    def _extents(offsets, lengths) -> np.ndarray:
+        ext = np.empty((len(offsets), 2), dtype=np.uint64)
+        ext[:, 0] = np.asarray(offsets, dtype=np.uint64)
+        ext[:, 1] = np.asarray(lengths, dtype=np.uint64)
+        return ext
+
+    @staticmethod
+    def _key(key) -> bytes:
+        key = bytes(key)
+        if len(key) != 32:
+            raise ValueError("AES-256-GCM-SIV key must be 32 bytes")
+        return key
+
+    @_locked
+    def seal(self, key, d_in: int, n_in: int, offsets, lengths, nonces, d_out: int, out_cap: int) -> np.ndarray:
+        """SecureStorage::encrypt_with_key for every blob d_in[offsets[i], +lengths[i])
+        (mcdc_seal_device): results nonce || ct || tag packed from d_out.  Returns the
+        nblobs + 1 output offsets (last = total bytes)."""
+        ext = self._extents(offsets, lengths)
+        nz = np.ascontiguousarray(nonces, dtype=np.uint8).reshape(-1)
+        if nz.size != NONCE_BYTES * len(ext):
+            raise ValueError("need 12 nonce bytes per blob")
+        oo = np.zeros(len(ext) + 1, dtype=np.uint64)
+        check(load().mcdc_seal_device(self._h, self._key(key), ctypes.c_void_p(d_in), n_in, ext.ctypes.data,
+                                      len(ext), nz.ctypes.data, ctypes.c_void_p(d_out), out_cap, oo.ctypes.data))
+        return oo
+
+    @_locked
+    def open(self, key, d_in: int, n_in: int, offsets, lengths, d_out: int, out_cap: int, raise_on_auth=True):
+        """SecureStorage::decrypt_with_key for every sealed extent (mcdc_open_device):
+        plaintexts packed from d_out.  Returns (out offsets, status per blob: 0 ok, -1 not);
+        raises McdcError(MCDC_E_AUTH) when a blob fails and raise_on_auth."""
+        ext = self._extents(offsets, lengths)
+        oo = np.zeros(len(ext) + 1, dtype=np.uint64)
+        stat = np.zeros(max(len(ext), 1), dtype=np.int32)
+        rc = load().mcdc_open_device(self._h, self._key(key), ctypes.c_void_p(d_in), n_in, ext.ctypes.data, len(ext),
+                                     ctypes.c_void_p(d_out), out_cap, oo.ctypes.data, stat.ctypes.data)
+        if rc != MCDC_E_AUTH or raise_on_auth:
+            check(rc)
+        return oo, stat[: len(ext)]
 
     @_locked
     def d2h_bytes(self, d_src: int, nbytes: int) -> np.ndarray:

@@ -24,6 +24,7 @@
 #include "../../include/mcdc.h"
 #include "../host/batcher.hpp"
 #include "gear_table.h"
+#include "mcdc_aead.h"
 #include "mcdc_blake3.h"
 #include "mcdc_internal.h"
 
@@ -217,7 +218,8 @@ struct mcdc_ctx {
   DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp;
+      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp,
+      ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -671,6 +673,121 @@ int check_ctx(mcdc_ctx *ctx) {
   return MCDC_OK;
 }
 
+// ------------------------------------------------------------- sealing --
+// Copy an argument array (host or device memory) into a context buffer.
+int stage_arg(mcdc_ctx *ctx, DevBuf &b, const void *src, size_t bytes) {
+  int rc = ensure(ctx, b, bytes);
+  if (rc) return rc;
+  if (!bytes) return MCDC_OK;
+  HIP_TRY(hipMemcpyAsync(b.p, src, bytes, is_device_ptr(src) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                         ctx->stream));
+  return MCDC_OK;
+}
+
+// Copy n entries of a device result array to the caller's array (host or device).
+int give_back(mcdc_ctx *ctx, void *dst, const void *d_src, size_t bytes) {
+  if (!dst || !bytes) return MCDC_OK;
+  HIP_TRY(hipMemcpyAsync(dst, d_src, bytes, is_device_ptr(dst) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                         ctx->stream));
+  return MCDC_OK;
+}
+
+// mcdc_seal_device (open = 0) / mcdc_open_device (open = 1).
+int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size_t n_in, const mcdc_blob *blobs,
+             size_t nblobs, const uint8_t *nonces, void *d_out, size_t out_cap, uint64_t *out_offsets,
+             int32_t *status) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!key || (!d_in && n_in) || (nblobs && !blobs) || (!open && nblobs && !nonces))
+    return fail(MCDC_E_INVALID, "NULL argument");
+  if (d_in && !is_device_ptr(d_in)) return fail(MCDC_E_INVALID, "d_in is not a device pointer");
+  if (d_out && !is_device_ptr(d_out)) return fail(MCDC_E_INVALID, "d_out is not a device pointer");
+  if (nblobs >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many blobs (%zu)", nblobs);
+  const double t0 = now_ms();
+  hipStream_t st = ctx->stream;
+  ctx->timing = mcdc_timing{};
+  if (nblobs == 0) {
+    const uint64_t zero = 0;
+    if (out_offsets) {
+      HIP_TRY(hipMemcpyAsync(out_offsets, &zero, 8, is_device_ptr(out_offsets) ? hipMemcpyHostToDevice
+                                                                               : hipMemcpyHostToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    ctx->timing.total_ms = now_ms() - t0;
+    return MCDC_OK;
+  }
+  const size_t n = nblobs;
+  const size_t tmpb = aead_scan_tmp_bytes(n);
+  if ((rc = stage_arg(ctx, ctx->ae_ext, blobs, n * sizeof(mcdc_blob))) ||
+      (!open && (rc = stage_arg(ctx, ctx->ae_nonce, nonces, n * kAeadNonce))) ||
+      (rc = ensure(ctx, ctx->ae_olen, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_tcnt, (n + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->ae_ooff, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_toff, (n + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->ae_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 16)))
+    return rc;
+  uint32_t *err = (uint32_t *)ctx->err.p + 2;
+  uint64_t *ooff = (uint64_t *)ctx->ae_ooff.p, *toff = (uint64_t *)ctx->ae_toff.p;
+  HIP_TRY(hipMemsetAsync(err, 0, 4, st));
+  HIP_TRY(hipEventRecord(ctx->ev_start, st));
+  launch_aead_sizes(open, (const uint64_t *)ctx->ae_ext.p, n, n_in, (uint64_t *)ctx->ae_olen.p,
+                    (uint64_t *)ctx->ae_tcnt.p, ooff, toff, err, ctx->ae_tmp.p, tmpb, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev_scan, st));
+  uint32_t herr = 0;
+  uint64_t total = 0, ntiles = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&total, ooff + n, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&ntiles, toff + n, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (herr) return fail(MCDC_E_INVALID, "a blob extent lies outside the %zu-byte input", n_in);
+  if ((rc = give_back(ctx, out_offsets, ooff, (n + 1) * 8))) return rc;
+  if (total > out_cap || (total && !d_out)) {
+    HIP_TRY(hipStreamSynchronize(st));
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", out_cap, (unsigned long long)total);
+  }
+  if (ntiles >= (1ull << 32)) return fail(MCDC_E_TOOBIG, "input too large (%llu tiles)", (unsigned long long)ntiles);
+  if ((rc = ensure(ctx, ctx->ae_rec, n * sizeof(AeadRec))) || (rc = ensure(ctx, ctx->ae_keys, n * sizeof(AeadKeys))) ||
+      (rc = ensure(ctx, ctx->ae_owner, ntiles * 4)) || (rc = ensure(ctx, ctx->ae_tsum, ntiles * 16)) ||
+      (rc = ensure(ctx, ctx->ae_status, n * 4)))
+    return rc;
+  AeadMaster mk;
+  aead_expand_key256(key, mk.rk);
+  HIP_TRY(hipEventRecord(ctx->ev_h2d0, st));
+  if (!open)
+    launch_aead_seal(mk, (const uint8_t *)d_in, (const uint64_t *)ctx->ae_ext.p, (const uint32_t *)ctx->ae_nonce.p, n,
+                     (uint8_t *)d_out, ooff, toff, ntiles, (AeadRec *)ctx->ae_rec.p, (AeadKeys *)ctx->ae_keys.p,
+                     (uint32_t *)ctx->ae_owner.p, (uint4 *)ctx->ae_tsum.p, st);
+  else
+    launch_aead_open(mk, (const uint8_t *)d_in, (const uint64_t *)ctx->ae_ext.p, n, (uint8_t *)d_out, ooff, toff,
+                     ntiles, (AeadRec *)ctx->ae_rec.p, (AeadKeys *)ctx->ae_keys.p, (uint32_t *)ctx->ae_owner.p,
+                     (uint4 *)ctx->ae_tsum.p, (int32_t *)ctx->ae_status.p, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev_end, st));
+  std::memset(mk.rk, 0, sizeof mk.rk);
+  std::vector<int32_t> hstat;
+  if (open) {
+    hstat.resize(n);
+    HIP_TRY(hipMemcpyAsync(hstat.data(), ctx->ae_status.p, n * 4, hipMemcpyDeviceToHost, st));
+    if ((rc = give_back(ctx, status, ctx->ae_status.p, n * 4))) return rc;
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  float ms0 = 0, ms1 = 0;
+  HIP_TRY(hipEventElapsedTime(&ms0, ctx->ev_start, ctx->ev_scan));
+  HIP_TRY(hipEventElapsedTime(&ms1, ctx->ev_h2d0, ctx->ev_end));
+  ctx->timing.aead_ms = ms1;
+  ctx->timing.device_ms = ms0 + ms1;
+  ctx->timing.bytes = open ? total : 0;
+  ctx->timing.chunks = n;
+  ctx->timing.total_ms = now_ms() - t0;
+  if (!open) {
+    ctx->timing.bytes = total - (uint64_t)n * kAeadOverhead;
+    return MCDC_OK;
+  }
+  size_t bad = 0;
+  for (int32_t v : hstat) bad += v != 0;
+  if (bad) return fail(MCDC_E_AUTH, "%zu of %zu blobs failed authentication", bad, n);
+  return MCDC_OK;
+}
+
 }  // namespace
 
 // ================================================================= C ABI ==
@@ -745,7 +862,9 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
                     &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->tile_ctr, &ctx->b3_chunks, &ctx->b3_gcnt,
-                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp};
+                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp,
+                    &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
+                    &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1057,6 +1176,16 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   ctx->timing.chunks = nchunks;
   ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
+}
+
+int mcdc_seal_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in, const mcdc_blob *blobs,
+                     size_t nblobs, const uint8_t *nonces, void *d_out, size_t out_cap, uint64_t *out_offsets) {
+  return aead_run(ctx, 0, key, d_in, n_in, blobs, nblobs, nonces, d_out, out_cap, out_offsets, nullptr);
+}
+
+int mcdc_open_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in, const mcdc_blob *sealed,
+                     size_t nblobs, void *d_out, size_t out_cap, uint64_t *out_offsets, int32_t *status) {
+  return aead_run(ctx, 1, key, d_in, n_in, sealed, nblobs, nullptr, d_out, out_cap, out_offsets, status);
 }
 
 // ------------------------------------------------------------ batcher --
