@@ -31,6 +31,10 @@ Prints ONE JSON line (rank 0).  Extra objects:
   chunk_ids       - SURVEY.md §8(f) next stage: BLAKE3 chunk IDs of the same 64 GiB
                     boundary list in HBM (ID::from_content, processor.rs:184), and
                     the chunk + ID pipeline
+  seal            - SURVEY.md §8(f) rank 3: SecureStorage encryption (AES-256-GCM-SIV,
+                    storage.rs:97-118) of every chunk of the same stream as a blob
+                    (mcdc_seal_device), its inverse (mcdc_open_device), parity probe
+                    vs the oracle, CPU references
 """
 from __future__ import annotations
 
@@ -346,6 +350,102 @@ def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_s
         ctx.device_free(d_ids)
 
 
+def _openssl_gcm_gib_s(sample_bytes: int, runs: int = 3):
+    """AES-256-GCM of one buffer with the system OpenSSL (AES-NI + carry-less
+    multiply), 1 thread: a CPU proxy for the crate's AES-256-GCM-SIV, which costs
+    the same two primitives (one AES-256 CTR pass, one GF(2^128) hash pass).
+    None when libcrypto is absent."""
+    import ctypes
+    import ctypes.util
+    name = ctypes.util.find_library("crypto")
+    if not name:
+        return None
+    L = ctypes.CDLL(name)
+    vp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)
+    L.EVP_CIPHER_CTX_new.restype = vp
+    L.EVP_CIPHER_CTX_free.argtypes = [vp]
+    L.EVP_aes_256_gcm.restype = vp
+    L.EVP_EncryptInit_ex.argtypes = [vp, vp, vp, vp, vp]
+    L.EVP_EncryptUpdate.argtypes = [vp, vp, ip, vp, ctypes.c_int]
+    L.EVP_EncryptFinal_ex.argtypes = [vp, vp, ip]
+    src = np.frombuffer(np.random.default_rng(1).bytes(sample_bytes), np.uint8)
+    dst = np.empty(sample_bytes + 64, np.uint8)
+    key, iv = bytes(range(32)), bytes(12)
+    best = []
+    for _ in range(runs):
+        c = L.EVP_CIPHER_CTX_new()
+        n = ctypes.c_int()
+        L.EVP_EncryptInit_ex(c, L.EVP_aes_256_gcm(), None, key, iv)
+        t0 = time.perf_counter()
+        for o in range(0, sample_bytes, 1 << 30):  # int-sized updates
+            m = min(1 << 30, sample_bytes - o)
+            L.EVP_EncryptUpdate(c, dst.ctypes.data + o, ctypes.byref(n), src.ctypes.data + o, m)
+        L.EVP_EncryptFinal_ex(c, dst.ctypes.data + sample_bytes, ctypes.byref(n))
+        best.append(time.perf_counter() - t0)
+        L.EVP_CIPHER_CTX_free(c)
+    return sample_bytes / float(np.median(best)) / GIB
+
+
+def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> dict:
+    """Every chunk of the headline stream sealed as one blob (random data: zstd
+    would store it raw, so the blobs stand in for the compressed chunks), device
+    in, device out; then opened again.  Parity probe: 96 sealed blobs against
+    the oracle; the round trip: every tag verifies and sampled windows of the
+    opened stream equal the input."""
+    from oracle import oracle as O
+    k = len(chunks)
+    offs, lens = chunks["offset"], chunks["length"]
+    key = bytes(range(0x40, 0x60))
+    nonces = np.zeros((k, 3), np.uint32)  # nonce i = le32(i) || "mapache!"
+    nonces[:, 0] = np.arange(k, dtype=np.uint32)
+    nonces[:, 1:] = np.frombuffer(b"mapache!", np.uint32)
+    nonces = nonces.view(np.uint8).reshape(k, 12)
+    cap = n + 28 * k
+    d_seal = ctx.device_alloc(cap)
+    d_open = ctx.device_alloc(n)
+    try:
+        dt, oo = _timed(lambda: ctx.seal(key, dp, n, offs, lens, nonces, d_seal, cap), steps, 1)
+        ts = ctx.timing()
+        dto, (po, st) = _timed(lambda: ctx.open(key, d_seal, int(oo[-1]), oo[:-1], np.diff(oo), d_open, n), steps, 1)
+        to = ctx.timing()
+        rng = np.random.default_rng(3)
+        pick = np.unique(np.concatenate([np.arange(32), rng.integers(0, k, 64)]))
+        got = [ctx.d2h_bytes(d_seal + int(oo[i]), int(lens[i]) + 28).tobytes() for i in pick]
+        ref = [O.encrypt_with_key(key, nonces[i], O.random_bytes(int(lens[i]), SEED, pos=int(offs[i]))) for i in pick]
+        windows = [int(x) for x in rng.integers(0, n - (1 << 20), 16)]
+        rt_ok = bool((st == 0).all()) and all(
+            (ctx.d2h_bytes(d_open + w, 1 << 20) == O.random_bytes(1 << 20, SEED, pos=w)).all() for w in windows)
+        r = {"blobs": k, "bytes": n, "steps": steps,
+             "seal_ms_per_step": round(dt * 1e3, 3), "seal_gib_s": round(n / dt / GIB, 2),
+             "seal_device_ms": round(ts["device_ms"], 3), "seal_kernels_ms": round(ts["aead_ms"], 3),
+             "open_ms_per_step": round(dto * 1e3, 3), "open_gib_s": round(n / dto / GIB, 2),
+             "open_device_ms": round(to["device_ms"], 3),
+             "parity_probe_blobs": int(len(pick)), "parity_probe_ok": got == ref,
+             "round_trip_ok": rt_ok,
+             "output": "nonce || ciphertext || tag per blob, packed in blob order (the pack body)",
+             "data": "synthetic: the chunks of the 64 GiB headline stream as blobs, nonce i = le32(i) || 'mapache!'"}
+        if not no_cpu:
+            sample = chunks[:max(1, int(np.searchsorted(np.cumsum(lens), 32 << 20)))]
+            host = O.random_bytes(int(sample["offset"][-1] + sample["length"][-1]), SEED)
+            t0 = time.perf_counter()
+            O.seal_blobs(key, host, sample["offset"], sample["length"], nonces[:len(sample)], threads=1)
+            cdt = time.perf_counter() - t0
+            r["cpu_baseline"] = {"value": round(int(sample["length"].sum()) / cdt / GIB, 4), "unit": "GiB/s",
+                                 "cores": 1, "kind": "port",
+                                 "sample": f"the first {len(sample)} blobs (~32 MiB), oracle/aead_oracle.c "
+                                           f"(byte-oriented AES, bitwise POLYVAL: a restatement, not a fast CPU "
+                                           f"implementation), 1 thread"}
+            g = _openssl_gcm_gib_s(1 << 30)
+            if g is not None:
+                r["cpu_proxy_openssl_aes256gcm"] = {"value": round(g, 3), "unit": "GiB/s", "cores": 1,
+                                                    "sample": "1 GiB, one AES-256-GCM message, system OpenSSL "
+                                                              "(AES-NI/PCLMUL): the crate's per-core cost class"}
+        return r
+    finally:
+        ctx.device_free(d_open)
+        ctx.device_free(d_seal)
+
+
 def corpus_sharded(ctx, p, files_per_gpu: int, file_bytes: int, steps: int, warmup: int, world: int, rank: int,
                    barrier, allreduce_max, gather) -> dict:
     """BASELINE configs[4]: a corpus of world x files_per_gpu files of file_bytes
@@ -423,6 +523,7 @@ def main() -> int:
                     "(16: this pool's CPU share per GPU)")
     ap.add_argument("--cpu-batch-files", type=int, default=4096, help="files in the multi-thread CPU sample")
     ap.add_argument("--no-ids", action="store_true", help="skip the chunk-ID (BLAKE3) stage")
+    ap.add_argument("--no-seal", action="store_true", help="skip the SecureStorage sealing stage")
     a = ap.parse_args()
 
     world, rank, local = _dist()
@@ -593,6 +694,11 @@ def main() -> int:
                                        "parity_probe_chunks": int(len(g5)),
                                        "parity_probe_ok": bool(len(g5) > 0 and _same(g5, r5[:len(g5)])),
                                        "note": "same 64 GiB buffer, device-resident in and out, mapache defaults"}
+        if not a.no_seal:  # (last: its 128 GiB of buffers are freed before nothing else is allocated)
+            try:
+                result["seal"] = seal(ctx, dp, n, chunks, max(3, a.steps // 2), a.no_cpu)
+            except Exception as ex:  # reported, never silently dropped
+                result["seal"] = {"error": f"{type(ex).__name__}: {ex}"}
     ctx.device_free(d_out)
     ctx.device_free(dp)
     if a.corpus_files_per_gpu > 0:

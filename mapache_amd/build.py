@@ -10,8 +10,10 @@ from __future__ import annotations
 
 import argparse
 import os
+import re
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -36,13 +38,46 @@ def _run(cmd, cwd):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
+# Kernels allowed to fill their VGPR allocation exactly: the
+# headline scan at 128/128 keeps 4 waves per SIMD; one more register would
+# allocate 136 and drop it to 3.  Its outputs are checked at full size on every
+# GPU run (64 GiB digests, repeated-call determinism).
+EXACT_FILL_OK = ("_ZN4mcdc8k_scan_qILi4096ELi2ELb1E",)
+
+
+def vgpr_report(asm_dir: str):
+    """(kernel, next_free_vgpr) of every mcdc kernel in the device assembly hipcc
+    left in asm_dir (-save-temps)."""
+    out = []
+    for f in sorted(os.listdir(asm_dir)):
+        if not (f.endswith(".s") and "amdgcn" in f):
+            continue
+        txt = open(os.path.join(asm_dir, f)).read()
+        for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", txt, re.S):
+            if m.group(1).startswith("_ZN4mcdc"):
+                out.append((m.group(1), int(re.search(r"\.amdhsa_next_free_vgpr\s+(\d+)", m.group(2)).group(1))))
+    return out
+
+
+def exact_fills(report):
+    """Kernels whose registers fill their 8-VGPR-granular allocation exactly
+    (MCDC_VGPR_PAD in csrc/mcdc_internal.h), outside EXACT_FILL_OK."""
+    return [(k, v) for k, v in report if v % 8 == 0 and not k.startswith(EXACT_FILL_OK)]
+
+
 def build_lib(force: bool = False, ab: bool = False) -> str:
     out = os.path.join(HERE, "libmcdc_ab.so" if ab else "libmcdc.so")
     deps = [os.path.join(HERE, d) for d in LIB_DEPS]
     if force or _stale(out, deps):
         tmp = out + ".tmp"
-        _run([HIPCC, *CXXFLAGS, *(["-DMCDC_AB_KNOBS"] if ab else []), "-fPIC", "-shared", "-I../include", "-o", tmp,
-              *LIB_SRCS], HERE)
+        with tempfile.TemporaryDirectory() as td:  # -save-temps: the device assembly for the VGPR check
+            _run([HIPCC, *CXXFLAGS, *(["-DMCDC_AB_KNOBS"] if ab else []), "-save-temps", "-fPIC", "-shared",
+                  f"-I{os.path.join(ROOT, 'include')}", "-o", tmp, *[os.path.join(HERE, x) for x in LIB_SRCS]], td)
+            bad = exact_fills(vgpr_report(td))
+        if bad and not ab:
+            os.remove(tmp)
+            raise RuntimeError("kernels fill their VGPR allocation exactly (pad them with MCDC_VGPR_PAD, "
+                               "DESIGN.md §3a): " + ", ".join(f"{k} ({v})" for k, v in bad))
         os.replace(tmp, out)
     return out
 

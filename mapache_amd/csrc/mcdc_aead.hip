@@ -35,6 +35,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "mcdc_aead.h"
+#include "mcdc_internal.h"
 
 namespace mcdc {
 
@@ -532,6 +533,7 @@ __global__ __launch_bounds__(256) void k_aead_ctr(int open, const AeadRec *__res
 // open: a blob that failed authentication gets zeros instead of its plaintext.
 __global__ __launch_bounds__(256) void k_aead_zero(const AeadRec *__restrict__ rec, const uint32_t *__restrict__ owner,
                                                    const int32_t *__restrict__ status, uint64_t ntiles) {
+  MCDC_VGPR_PAD(8);  // 8 used: not an exact fill (MCDC_VGPR_PAD)
   const uint32_t wv = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t tile = blockIdx.x * 4 + wv;
   if (tile >= ntiles) return;

@@ -265,6 +265,7 @@ __global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const De
 // group nodes in place (nodes [goff[i], goff[i+1]) belong to this lane only).
 __global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t n, uint64_t bound, uint32_t *nodes,
                           uint8_t *ids) {
+  MCDC_VGPR_PAD(48);  // 48 used: not an exact fill (MCDC_VGPR_PAD)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || goff[n] > bound) return;
   uint64_t m = goff[i + 1] - goff[i];

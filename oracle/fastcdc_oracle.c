@@ -335,13 +335,24 @@ size_t oc_chunk_digest(const oc_params *p, const uint8_t *data, size_t n, uint64
  * chunk count; *digest as oc_chunk_digest, *sum = sum of lengths. */
 size_t oc_random_stream_digest(const oc_params *p, uint64_t seed, uint64_t n, size_t slab, uint64_t *digest,
                                uint64_t *sum) {
+  return oc_random_stream_digest_h(p, seed, n, slab, digest, sum, NULL);
+}
+
+uint64_t oc_hash_digest(const uint64_t *hashes, size_t n) {
+  uint64_t d = 0;
+  for (size_t i = 0; i < n; ++i) d = oc_digest_step(d, i, hashes[i]);
+  return d;
+}
+
+size_t oc_random_stream_digest_h(const oc_params *p, uint64_t seed, uint64_t n, size_t slab, uint64_t *digest,
+                                 uint64_t *sum, uint64_t *hdigest) {
   pthread_once(&gear_once, gear_init);
   if (slab < 4096) slab = 4096;
   const size_t cap = slab + p->max_size;
   uint8_t *buf = (uint8_t *)malloc(cap);
   if (!buf) return 0;
   size_t s = 0, e = 0, k = 0;  /* valid bytes buf[s, e) */
-  uint64_t gen = 0, off = 0, d = 0;
+  uint64_t gen = 0, off = 0, d = 0, hd = 0;
   for (;;) {
     if (e - s < p->max_size && gen < n) { /* refill */
       memmove(buf, buf + s, e - s);
@@ -360,6 +371,7 @@ size_t oc_random_stream_digest(const oc_params *p, uint64_t seed, uint64_t n, si
     oc_cut_gear(p, buf + s, e - s, &h, &c);
     if (c == 0) break;
     d = oc_digest_step(d, off, c);
+    hd = oc_digest_step(hd, k, h);
     ++k;
     off += c;
     s += c;
@@ -367,6 +379,7 @@ size_t oc_random_stream_digest(const oc_params *p, uint64_t seed, uint64_t n, si
   free(buf);
   *digest = d;
   if (sum) *sum = off;
+  if (hdigest) *hdigest = hd;
   return k;
 }
 

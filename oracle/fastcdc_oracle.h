@@ -110,6 +110,12 @@ size_t oc_chunk_digest(const oc_params *p, const uint8_t *data, size_t n,
  * the sum of lengths.  For full-size (64 GiB) parity checks. */
 size_t oc_random_stream_digest(const oc_params *p, uint64_t seed, uint64_t n, size_t slab, uint64_t *digest,
                                uint64_t *sum);
+/* Same, plus *hdigest = oc_hash_digest of the chunks' ChunkData.hash values. */
+size_t oc_random_stream_digest_h(const oc_params *p, uint64_t seed, uint64_t n, size_t slab, uint64_t *digest,
+                                 uint64_t *sum, uint64_t *hdigest);
+/* Order-sensitive digest of a list of chunk hashes: fold of
+ * oc_digest_step(d, index, hash). */
+uint64_t oc_hash_digest(const uint64_t *hashes, size_t n);
 
 /* Counter-based byte generator shared with the device fill kernel and the
  * bench: byte i = (splitmix64_at(seed, i/8) >> 8*(i%8)) & 0xff. */

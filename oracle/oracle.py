@@ -85,6 +85,11 @@ def lib():
         L.oc_random_stream_digest.argtypes = [ctypes.POINTER(OcParams), ctypes.c_uint64, ctypes.c_uint64,
                                               ctypes.c_size_t, u64p, u64p]
         L.oc_random_stream_digest.restype = ctypes.c_size_t
+        L.oc_random_stream_digest_h.argtypes = [ctypes.POINTER(OcParams), ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_size_t, u64p, u64p, u64p]
+        L.oc_random_stream_digest_h.restype = ctypes.c_size_t
+        L.oc_hash_digest.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.oc_hash_digest.restype = ctypes.c_uint64
         L.oc_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint64]
         L.oc_fill_random.restype = None
         L.oc_file_seed.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
@@ -204,12 +209,20 @@ def chunk_digest(params: Params, data):
     return k, d.value
 
 
-def random_stream_digest(params: Params, seed: int, n: int, slab: int = 256 << 20):
+def random_stream_digest(params: Params, seed: int, n: int, slab: int = 256 << 20, hashes: bool = False):
     """(count, digest, sum of lengths) of the counter-based stream [0, n) chunked
-    as one file, regenerated slab by slab (no n-byte buffer): full-size parity."""
-    d, sm = ctypes.c_uint64(), ctypes.c_uint64()
-    k = lib().oc_random_stream_digest(ctypes.byref(params.c()), seed, n, slab, ctypes.byref(d), ctypes.byref(sm))
-    return k, d.value, sm.value
+    as one file, regenerated slab by slab (no n-byte buffer): full-size parity.
+    hashes=True appends the hash digest (hash_digest of every ChunkData.hash)."""
+    d, sm, hd = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    k = lib().oc_random_stream_digest_h(ctypes.byref(params.c()), seed, n, slab, ctypes.byref(d), ctypes.byref(sm),
+                                        ctypes.byref(hd))
+    return (k, d.value, sm.value, hd.value) if hashes else (k, d.value, sm.value)
+
+
+def hash_digest(chunks: np.ndarray) -> int:
+    """Order-sensitive digest of a boundary list's hash column (oc_hash_digest)."""
+    h = np.ascontiguousarray(chunks["hash"], dtype=np.uint64)
+    return int(lib().oc_hash_digest(h.ctypes.data, h.size))
 
 
 def digest_of(chunks: np.ndarray) -> int:

@@ -2,11 +2,14 @@
 
 * configs[1]: the 64 GiB uniform-random stream of the headline, device
   resident, chunked as one file at 16/64/256 KiB: the whole boundary list's
-  (count, digest, sum of lengths) against the oracle's, which regenerates the
-  same counter-based stream slab by slab (oracle/fastcdc_oracle.c
-  oc_random_stream_digest) so the host never holds 64 GiB; plus the
-  size-independent invariants (lengths sum to n, offsets contiguous, every
-  non-tail chunk within [min, max]) and ChunkData.hash spot checks.
+  (count, digest, sum of lengths) and the digest of every ChunkData.hash
+  against the oracle's, which regenerates the same counter-based stream slab
+  by slab (oracle/fastcdc_oracle.c oc_random_stream_digest_h) so the host
+  never holds 64 GiB; plus the size-independent invariants (lengths sum to n,
+  offsets contiguous, every non-tail chunk within [min, max]), hash spot
+  checks, and four more calls (device and pinned-host output) identical to
+  the first, record for record (the k_emit VGPR item, DESIGN.md §3a, changed
+  ~3 % of the hashes of some calls).
 * configs[3] stand-in: the bench's 80 000-file log-normal mix (median 8 KiB,
   1.34 GB; bench.py small_files), one batched device call, every file's
   boundary list and count against oracle.chunk_files.
@@ -35,6 +38,10 @@ def test_configs1_full_64gib_digest(ctx):
             big.fill_random(dp, n, SEED)
             k = big.chunk_device_to_device(p, dp, n, d_out, cap)
             g = big.d2h_chunks(d_out, k)
+            again = []
+            for _ in range(2):
+                again.append(big.d2h_chunks(d_out, big.chunk_device_to_device(p, dp, n, d_out, cap)))
+                again.append(big.chunk_device(p, dp, n, out=big.pinned_out(cap)).copy())
             samples = []
             for i in np.linspace(0, k - 2, 24).astype(int):
                 o = int(g["offset"][i])
@@ -47,10 +54,13 @@ def test_configs1_full_64gib_digest(ctx):
     assert int(g["length"].sum()) == n
     assert (g["offset"][1:] == np.cumsum(g["length"])[:-1]).all() and g["offset"][0] == 0
     assert g["length"][:-1].min() >= P16[0] and g["length"].max() <= P16[2]
-    rk, rdig, rsum = O.random_stream_digest(O.Params(*P16), SEED, n)
+    rk, rdig, rsum, rhd = O.random_stream_digest(O.Params(*P16), SEED, n, hashes=True)
     assert rsum == n
     assert rk == k, (rk, k)
     assert _lib.digest(g) == rdig
+    assert O.hash_digest(g) == rhd
+    for j, a in enumerate(again):
+        assert len(a) == k and (a == g).all(), (j, int(np.count_nonzero(a["hash"] != g["hash"])))
     for i, window in samples:  # hash and length from cut_gear restarted at the chunk
         assert O.cut_gear(O.Params(*P16), window) == (int(g["hash"][i]), int(g["length"][i]))
 

@@ -144,5 +144,7 @@ def test_streamed_random_digest_equals_in_memory(p):
     n = (40 << 20) + 12345
     d = O.random_bytes(n, 77)
     k, dig = O.chunk_digest(O.Params(*p), d)
+    hd = O.hash_digest(O.chunk(O.Params(*p), d))
     for slab in (4096, 1 << 20, 5_000_000, 64 << 20):
         assert O.random_stream_digest(O.Params(*p), 77, n, slab) == (k, dig, n)
+        assert O.random_stream_digest(O.Params(*p), 77, n, slab, hashes=True) == (k, dig, n, hd)
