@@ -73,6 +73,15 @@ constexpr Tables kHostTab = make_tables();
 static_assert(kHostTab.sbox[0] == 0x63 && kHostTab.sbox[0x53] == 0xED && kHostTab.sbox[0xFF] == 0x16, "S-box");
 __constant__ Tables kDevTab = make_tables();
 
+#ifndef MCDC_CTR_WAVES
+#define MCDC_CTR_WAVES 8
+#endif
+#ifndef MCDC_CTR_ILP
+#define MCDC_CTR_ILP 1
+#endif
+// k_aead_ctr: waves (tiles) per block, all sharing one 64-KiB table; two
+// blocks per CU.  With 16 waves and <= 64 VGPRs a SIMD holds 8 waves.
+constexpr int kCtrWaves = MCDC_CTR_WAVES;
 constexpr int kRep = 32;  // T-table replicas: ds_read_b32 banks are (addr/4) mod 32 per 32-lane half
 constexpr int kTabWords = 256 * kRep;
 
@@ -115,6 +124,75 @@ __device__ __forceinline__ uint4 aes256(const uint32_t *tl, const uint32_t *rk, 
   };
   return make_uint4(fin(a0, a1, a2, a3, rk[56]), fin(a1, a2, a3, a0, rk[57]), fin(a2, a3, a0, a1, rk[58]),
                     fin(a3, a0, a1, a2, rk[59]));
+}
+
+// The CTR kernel's AES: Te0 with 64 replicas, entry x of lane l's replica at
+// byte x * 256 + 4 l (64 KiB), so one v_perm_b32 builds a lookup's LDS address
+// from the state word (byte k -> bits 8-15) and 4 l (bits 0-7); ds_read_b32
+// banks are (addr / 4) mod 32, so the 32 lanes of a half hit 32 banks.
+// v_bitop3_b32 merges three terms per instruction.  ~500 VALU + 224 LDS reads
+// per block (the 32-replica version above: ~850 VALU).
+constexpr int kRepP = 64;
+constexpr int kTabPWords = 256 * kRepP;
+
+__device__ __forceinline__ void fill_table_p(uint32_t *tt) {
+  for (int k = threadIdx.x; k < kTabPWords; k += blockDim.x) tt[k] = kDevTab.te0[k / kRepP];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t tp(const uint8_t *tb, uint32_t w, uint32_t lane4) {
+  const uint32_t a = __builtin_amdgcn_perm(w, lane4, 0x0c0c0000u | ((4u + K) << 8));  // (byte K of w) << 8 | 4 l
+  return *reinterpret_cast<const uint32_t *>(tb + a);
+}
+
+// N independent blocks per call: N x 16 lookups per round in flight per lane,
+// which is what hides the LDS latency (one block per lane left the LDS ~50 %
+// and the VALU ~30 % busy, PMC: tools/aead_pmc.sh).
+template <int N>
+__device__ __forceinline__ void aes256p(const uint8_t *tb, uint32_t lane4, const uint32_t *rk, uint4 (&st)[N]) {
+  uint32_t a[N][4];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    a[j][0] = st[j].x ^ rk[0];
+    a[j][1] = st[j].y ^ rk[1];
+    a[j][2] = st[j].z ^ rk[2];
+    a[j][3] = st[j].w ^ rk[3];
+  }
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    uint32_t b[N][4];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        b[j][c] = xor3(xor3(tp<0>(tb, a[j][c], lane4), rl8(tp<1>(tb, a[j][(c + 1) & 3], lane4)),
+                            rl16(tp<2>(tb, a[j][(c + 2) & 3], lane4))),
+                       rl24(tp<3>(tb, a[j][(c + 3) & 3], lane4)), rk[4 * r + c]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a[j][c] = b[j][c];
+  }
+  // last round: S[x] = byte 1 of Te0[x]; two perms gather the four S bytes, then (u | v) ^ k
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    uint32_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t u = __builtin_amdgcn_perm(tp<1>(tb, a[j][(c + 1) & 3], lane4), tp<0>(tb, a[j][c], lane4),
+                                               0x0c0c0501u);
+      const uint32_t v = __builtin_amdgcn_perm(tp<3>(tb, a[j][(c + 3) & 3], lane4),
+                                               tp<2>(tb, a[j][(c + 2) & 3], lane4), 0x05010c0cu);
+      o[c] = __builtin_amdgcn_bitop3_b32(u, v, rk[56 + c], 0x56);  // (u | v) ^ k
+    }
+    st[j] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
 }
 
 // FIPS-197 §5.2 for Nk = 8, words little-endian (RotWord = rotate right 8)
@@ -484,16 +562,17 @@ __device__ __forceinline__ void store_quad(const AeadRec &R, uint64_t T, uint64_
   }
 }
 
-// One wave per tile of output quads: CTR keystream, plaintext xor, nonce/tag.
-__global__ __launch_bounds__(256) void k_aead_ctr(int open, const AeadRec *__restrict__ rec,
+// One wave per tile of output quads (8 waves per block share the 64-KiB table): CTR keystream, plaintext xor, nonce/tag.
+__global__ __launch_bounds__(64 * kCtrWaves) void k_aead_ctr(int open, const AeadRec *__restrict__ rec,
                                                   const AeadKeys *__restrict__ keys,
                                                   const uint32_t *__restrict__ owner, uint64_t ntiles) {
-  __shared__ uint32_t tt[kTabWords];
-  fill_table(tt);
+  __shared__ uint32_t tt[kTabPWords];
+  fill_table_p(tt);
   const uint32_t wv = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const uint32_t tile = blockIdx.x * 4 + wv;
+  const uint32_t tile = blockIdx.x * kCtrWaves + wv;
   if (tile >= ntiles) return;
-  const uint32_t *tl = tt + (threadIdx.x % kRep);
+  const uint8_t *tb = reinterpret_cast<const uint8_t *>(tt);
+  const uint32_t lane4 = 4 * lane;
   const uint32_t i = rfl(owner[tile]);
   const AeadRec &R = rec[i];
   const uint32_t t = tile - (uint32_t)R.tile0;
@@ -511,23 +590,41 @@ __global__ __launch_bounds__(256) void k_aead_ctr(int open, const AeadRec *__res
   const int64_t c0b = (int64_t)(16 * Qb) - (int64_t)R.dst;  // >= -27
   const int64_t B0 = (c0b + 48) / 16 - 3 + 1;
   const uint32_t d = (uint32_t)(0 - R.dst) & 15, e = (uint32_t)(R.src - R.dst) & 15;
-  uint4 carry = aes256(tl, rk, make_uint4(ctr.x + (uint32_t)(B0 - 1), ctr.y, ctr.z, ctr.w));
-#pragma unroll 1
-  for (uint32_t r = 0; r < rows; ++r) {
+  uint4 carry[1] = {make_uint4(ctr.x + (uint32_t)(B0 - 1), ctr.y, ctr.z, ctr.w)};
+  aes256p<1>(tb, lane4, rk, carry);
+  // one row: the keystream of its lanes' blocks and of the lane before (DPP
+  // wave_shr; lane 0 takes the previous row's lane 63), the plaintext, the store
+  auto row = [&](uint32_t r, const uint4 &ks) {
     const uint64_t Q = Qb + 64ull * r + lane;
-    const uint32_t B = (uint32_t)(B0 + 64 * (int64_t)r + lane);
-    const uint4 ks = aes256(tl, rk, make_uint4(ctr.x + B, ctr.y, ctr.z, ctr.w));
-    const uint4 kp = make_uint4((uint32_t)__builtin_amdgcn_update_dpp((int)carry.x, (int)ks.x, 0x138, 0xf, 0xf, false),
-                                (uint32_t)__builtin_amdgcn_update_dpp((int)carry.y, (int)ks.y, 0x138, 0xf, 0xf, false),
-                                (uint32_t)__builtin_amdgcn_update_dpp((int)carry.z, (int)ks.z, 0x138, 0xf, 0xf, false),
-                                (uint32_t)__builtin_amdgcn_update_dpp((int)carry.w, (int)ks.w, 0x138, 0xf, 0xf, false));
-    carry = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)ks.x, 63), (uint32_t)__builtin_amdgcn_readlane((int)ks.y, 63),
-                       (uint32_t)__builtin_amdgcn_readlane((int)ks.z, 63), (uint32_t)__builtin_amdgcn_readlane((int)ks.w, 63));
+    const uint4 kp = make_uint4((uint32_t)__builtin_amdgcn_update_dpp((int)carry[0].x, (int)ks.x, 0x138, 0xf, 0xf, false),
+                                (uint32_t)__builtin_amdgcn_update_dpp((int)carry[0].y, (int)ks.y, 0x138, 0xf, 0xf, false),
+                                (uint32_t)__builtin_amdgcn_update_dpp((int)carry[0].z, (int)ks.z, 0x138, 0xf, 0xf, false),
+                                (uint32_t)__builtin_amdgcn_update_dpp((int)carry[0].w, (int)ks.w, 0x138, 0xf, 0xf, false));
+    carry[0] = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)ks.x, 63), (uint32_t)__builtin_amdgcn_readlane((int)ks.y, 63),
+                          (uint32_t)__builtin_amdgcn_readlane((int)ks.z, 63), (uint32_t)__builtin_amdgcn_readlane((int)ks.w, 63));
     const uint4 k16 = shift16(kp, ks, d);
     const uint64_t qa = 16 * Q;
     const uint4 p = load16(R.src + (qa - R.dst), R.src, R.src + R.len, e);
     if (Q <= q_last) store_quad(R, T, qa, u4xor(p, k16));
+  };
+#if MCDC_CTR_ILP == 2
+#pragma unroll 1
+  for (uint32_t r = 0; r < rows; r += 2) {  // two rows' blocks per AES call
+    const uint32_t B = (uint32_t)(B0 + 64 * (int64_t)r + lane);
+    uint4 ks[2] = {make_uint4(ctr.x + B, ctr.y, ctr.z, ctr.w), make_uint4(ctr.x + B + 64, ctr.y, ctr.z, ctr.w)};
+    aes256p<2>(tb, lane4, rk, ks);
+    row(r, ks[0]);
+    if (r + 1 < rows) row(r + 1, ks[1]);
   }
+#else
+#pragma unroll 1
+  for (uint32_t r = 0; r < rows; ++r) {
+    const uint32_t B = (uint32_t)(B0 + 64 * (int64_t)r + lane);
+    uint4 ks[1] = {make_uint4(ctr.x + B, ctr.y, ctr.z, ctr.w)};
+    aes256p<1>(tb, lane4, rk, ks);
+    row(r, ks[0]);
+  }
+#endif
 }
 
 // open: a blob that failed authentication gets zeros instead of its plaintext.
@@ -601,7 +698,9 @@ void launch_aead_seal(const AeadMaster &mk, const uint8_t *in, const uint64_t *e
                      owner);
   if (ntiles) hipLaunchKernelGGL(k_aead_polyval, gt, dim3(256), 0, stream, rec, keys, owner, ntiles, tsum);
   hipLaunchKernelGGL(k_aead_tag, gb, dim3(256), 0, stream, 0, rec, keys, tsum, n, (int32_t *)nullptr);
-  if (ntiles) hipLaunchKernelGGL(k_aead_ctr, gt, dim3(256), 0, stream, 0, rec, keys, owner, ntiles);
+  if (ntiles)
+    hipLaunchKernelGGL(k_aead_ctr, dim3((unsigned)((ntiles + kCtrWaves - 1) / kCtrWaves)), dim3(64 * kCtrWaves), 0,
+                       stream, 0, rec, keys, owner, ntiles);
 }
 
 void launch_aead_open(const AeadMaster &mk, const uint8_t *in, const uint64_t *ext, uint64_t n, uint8_t *out,
@@ -610,7 +709,9 @@ void launch_aead_open(const AeadMaster &mk, const uint8_t *in, const uint64_t *e
   const dim3 gb((unsigned)((n + 255) / 256)), gt((unsigned)((ntiles + 3) / 4));
   hipLaunchKernelGGL(k_aead_prep, gb, dim3(256), 0, stream, 1, mk, in, ext, (const uint32_t *)nullptr, n, out, ooff,
                      toff, rec, keys, owner);
-  if (ntiles) hipLaunchKernelGGL(k_aead_ctr, gt, dim3(256), 0, stream, 1, rec, keys, owner, ntiles);
+  if (ntiles)
+    hipLaunchKernelGGL(k_aead_ctr, dim3((unsigned)((ntiles + kCtrWaves - 1) / kCtrWaves)), dim3(64 * kCtrWaves), 0,
+                       stream, 1, rec, keys, owner, ntiles);
   if (ntiles) hipLaunchKernelGGL(k_aead_polyval, gt, dim3(256), 0, stream, rec, keys, owner, ntiles, tsum);
   hipLaunchKernelGGL(k_aead_tag, gb, dim3(256), 0, stream, 1, rec, keys, tsum, n, status);
   if (ntiles) hipLaunchKernelGGL(k_aead_zero, gt, dim3(256), 0, stream, rec, owner, status, ntiles);

@@ -1351,25 +1351,27 @@ __device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, cons
 // GS) and computes its hash itself.  Resolution kernels raise their wave priority:
 // they run beside the scan's later parts and are latency-bound.
 //
-// GEAR comes from the global table (a 2 KiB L1/L2-resident read), not from an
-// LDS copy: with an LDS copy, k_emit_long lost the LDS reads of whole waves
-// ("LDS-table item"), and the hash is the one output no later
-// stage re-checks.
-//
-// k_emit uses 184 VGPRs (the 80 table reads of chunk_hash in flight): padded
-// to 185 (192 allocated), see MCDC_VGPR_PAD.  At 184/184 about 3 % of the
-// hashes of a 64 GiB call came out wrong in whole-wave runs, a different set
-// per call (tools/dbg/hash_check.py); with 192 or 200 allocated, 0 in 5 calls.
+// GEAR comes from an LDS copy.  Both emitters pad their VGPR allocation
+// (MCDC_VGPR_PAD): filling it exactly lost the memory returns
+// of whole waves -- k_emit_long at 88/88 with this LDS table (round 2), k_emit
+// at 184/184 with the global one and with this one -- and a wrong
+// ChunkData.hash is the one output no later stage re-checks.
+// tools/dbg/build_vpad.sh builds k_emit unpadded (MCDC_EMIT_VPAD=0).
 #ifndef MCDC_EMIT_VPAD
 #define MCDC_EMIT_VPAD 184
 #endif
+#ifndef MCDC_EMIT_LONG_VPAD
+#define MCDC_EMIT_LONG_VPAD 0  // (177 used, 184 allocated: not an exact fill)
+#endif
 template <int GS>
 __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1) {
-#if MCDC_EMIT_VPAD  // (tools/dbg/build_vpad.sh varies it; 0: no pad, the failing build)
+#if MCDC_EMIT_VPAD
   MCDC_VGPR_PAD(MCDC_EMIT_VPAD);
 #endif
   __builtin_amdgcn_s_setprio(3);
-  const uint64_t *gt = W.gear;
+  __shared__ uint64_t gtl[256];
+  load_gear_lds(gtl, W);
+  const uint64_t *gt = gtl;
   const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
   if (s >= s1) return;
   const uint64_t n = W.seg_count[s];
@@ -1402,29 +1404,14 @@ __global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, 
 
 // Continuation stretches longer than kEmitInline nodes (k_link appended their
 // segments to long_list): the whole grid strides over each one's nodes.  GEAR
-// is read from the global table (see k_emit).  The LDS-table builds of the
-// investigation ("LDS-table item"; tools/dbg/build_dbg.sh):
-//   MCDC_DBG_LDS=1  GEAR from an LDS copy at offset 0 (88 VGPRs: loses the LDS
-//                   reads of whole waves, 1.5-5 % of calls; 19-44 % under a
-//                   rocprofv3 --pmc pass)
-//   MCDC_DBG_LDS=5  same, the copy 512 bytes into the allocation (fails alike)
-//   MCDC_DBG_LDS=6  =1 with one more VGPR touched (90 -> 96 allocated): no loss
+// from LDS, VGPR allocation padded (see k_emit).
 __global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
-#ifdef MCDC_DBG_LDS
-#if MCDC_DBG_LDS == 5
-  __shared__ uint64_t gtl_raw[256 + 64];
-  uint64_t *gtl = gtl_raw + 64;
-#else
+#if MCDC_EMIT_LONG_VPAD
+  MCDC_VGPR_PAD(MCDC_EMIT_LONG_VPAD);
+#endif
   __shared__ uint64_t gtl[256];
-#endif
   load_gear_lds(gtl, W);
-#if MCDC_DBG_LDS == 6
-  asm volatile("v_mov_b32 v89, 0" ::: "v89");
-#endif
   const uint64_t *gt = gtl;
-#else
-  const uint64_t *gt = W.gear;
-#endif
   const uint32_t nl = *W.long_n;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint32_t li = 0; li < nl; ++li) {
