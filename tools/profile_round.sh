@@ -2,7 +2,9 @@
 # Round profile set (run on the GPU box): rocprofv3 kernel-trace + stats of
 # the bench command, then separate --pmc passes (one counter group each, as
 # MI355X_MICROARCH.md prescribes) on tools/prof_workload.py, and the
-# FETCH_SIZE calibration of tools/pmc_calib.sh.   Usage: profile_round.sh <tag>
+# FETCH_SIZE calibration of tools/pmc_calib.sh; then the sealing kernels'
+# kernel trace (tools/aead_bench.py) and PMC passes (tools/aead_pmc.sh).
+# Usage: profile_round.sh <tag>
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -20,4 +22,7 @@ done
 for mode in quadread prod; do
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib/$mode -o run -- $R/tools/scanbench 8 $mode > $OUT/calib_$mode.log 2>&1 || { echo "calib $mode rc=$?"; exit 1; }
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/aead_stats -o aead --output-format csv -- \
+  python3 tools/aead_bench.py 64 3 > $OUT/aead_under_rocprof.log 2>&1 || { echo "aead stats rc=$?"; exit 1; }
+bash tools/aead_pmc.sh $OUT/aead_pmc || { echo "aead pmc rc=$?"; exit 1; }
 echo profile done
