@@ -50,11 +50,13 @@ struct AeadMaster {
 };
 
 // seal: nonces = 12 * n bytes (device, 4-aligned); open: nonces from the extents.
+// ctr: 2 words of device scratch (the persistent launches' tile counters).
 void launch_aead_seal(const AeadMaster &mk, const uint8_t *in, const uint64_t *ext, const uint32_t *nonces,
                       uint64_t n, uint8_t *out, const uint64_t *ooff, const uint64_t *toff, uint64_t ntiles,
-                      AeadRec *rec, AeadKeys *keys, uint32_t *owner, uint4 *tsum, hipStream_t stream);
+                      AeadRec *rec, AeadKeys *keys, uint32_t *owner, uint4 *tsum, uint32_t *ctr, int num_cus,
+                      hipStream_t stream);
 void launch_aead_open(const AeadMaster &mk, const uint8_t *in, const uint64_t *ext, uint64_t n, uint8_t *out,
                       const uint64_t *ooff, const uint64_t *toff, uint64_t ntiles, AeadRec *rec, AeadKeys *keys,
-                      uint32_t *owner, uint4 *tsum, int32_t *status, hipStream_t stream);
+                      uint32_t *owner, uint4 *tsum, int32_t *status, uint32_t *ctr, int num_cus, hipStream_t stream);
 
 }  // namespace mcdc

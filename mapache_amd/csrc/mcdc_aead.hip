@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "mcdc_aead.h"
 #include "mcdc_internal.h"
 
@@ -74,13 +76,17 @@ static_assert(kHostTab.sbox[0] == 0x63 && kHostTab.sbox[0x53] == 0xED && kHostTa
 __constant__ Tables kDevTab = make_tables();
 
 #ifndef MCDC_CTR_WAVES
-#define MCDC_CTR_WAVES 8
+#define MCDC_CTR_WAVES 12
+#endif
+#ifndef MCDC_AEAD_PERSIST  // bit 0: k_aead_polyval, bit 1: k_aead_ctr draw tiles from a counter (A/B: tools/dbg/build_persist_ab.sh)
+#define MCDC_AEAD_PERSIST 3
 #endif
 #ifndef MCDC_CTR_ILP
 #define MCDC_CTR_ILP 1
 #endif
-// k_aead_ctr: waves (tiles) per block, all sharing one 64-KiB table; two
-// blocks per CU.  With 16 waves and <= 64 VGPRs a SIMD holds 8 waves.
+// k_aead_ctr: waves per block, all sharing one 64-KiB table; two blocks per
+// CU.  12: 73 VGPRs -> 6 waves per SIMD (A/B over 8-16, tools/dbg/build_ctr_ab.sh:
+// 12 fastest; 16 fills 64 of 64 VGPRs, see MCDC_VGPR_PAD, and is SGPR-bound at 7).
 constexpr int kCtrWaves = MCDC_CTR_WAVES;
 constexpr int kRep = 32;  // T-table replicas: ds_read_b32 banks are (addr/4) mod 32 per 32-lane half
 constexpr int kTabWords = 256 * kRep;
@@ -423,27 +429,36 @@ __global__ __launch_bounds__(256) void k_aead_prep(int open, AeadMaster mk, cons
   *reinterpret_cast<uint4 *>(K.h4096) = w;
 }
 
-// One wave per tile: the tile's POLYVAL sum, exponents relative to its end.
-__global__ __launch_bounds__(256) void k_aead_polyval(const AeadRec *__restrict__ rec,
-                                                      const AeadKeys *__restrict__ keys,
-                                                      const uint32_t *__restrict__ owner, uint64_t ntiles,
-                                                      uint4 *__restrict__ tsum) {
-  __shared__ uint4 mt[4][256];
-  const uint32_t wv = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const uint32_t tile = blockIdx.x * 4 + wv;
-  bool act = tile < ntiles;
-  uint32_t i = 0, t = 0;
-  if (act) {
-    i = rfl(owner[tile]);
-    t = tile - (uint32_t)rec[i].tile0;
-    act = t < rec[i].ptiles;
-  }
-  uint4 *M = mt[wv];
-  if (act) {  // M[b] = b(x) G, G = H^64: lane builds entries lane + 64 q
+// Order LDS writes of a wave before its own later reads (wave-private tables).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The wave's next tile from the launch's counter (persistent waves: a wave
+// that drew a short tile draws again instead of idling in its block).  Lane
+// 0 draws, and lane 0's value is read explicitly (readlane, not
+// readfirstlane).  Call it only in wave-uniform control flow, outside the loop
+// condition: with the draw at the head of `for (;;)` the compiler lowered the
+// loop exit as divergent and some waves re-drew tile 0 forever (a hang of
+// every call with fewer tiles than waves, round 3).
+__device__ __forceinline__ uint32_t next_tile(uint32_t *ctr) {
+  uint32_t t = 0;
+  if ((threadIdx.x & 63) == 0) t = atomicAdd(ctr, 1u);
+  return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+}
+
+// One POLYVAL tile: its sum, exponents relative to its end.
+__device__ __forceinline__ void polyval_tile(const AeadRec *__restrict__ rec, const AeadKeys *__restrict__ keys,
+                                             uint4 *M, uint32_t lane, uint32_t i, uint32_t t, uint32_t tile,
+                                             uint4 *__restrict__ tsum) {
+  {  // M[b] = b(x) G, G = H^64: lane builds entries lane + 64 q
     uint4 base[8];
     base[0] = *reinterpret_cast<const uint4 *>(keys[i].w[0]);
 #pragma unroll
     for (int j = 1; j < 8; ++j) base[j] = mulx(base[j - 1]);
+    wave_sync();  // the previous tile's reads of M are done
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t e = lane + 64 * q;
@@ -455,9 +470,8 @@ __global__ __launch_bounds__(256) void k_aead_polyval(const AeadRec *__restrict_
       }
       M[e] = v;
     }
+    wave_sync();
   }
-  __syncthreads();
-  if (!act) return;
   const AeadRec &R = rec[i];
   const uint64_t s = R.len, nblk = (s + 15) / 16, V = (nblk + 63) / 64 * 64, rows_all = V / 64;
   const uint64_t rows0 = rows_all - (uint64_t)kAeadRows * (R.ptiles - 1);
@@ -484,6 +498,24 @@ __global__ __launch_bounds__(256) void k_aead_polyval(const AeadRec *__restrict_
     U.w ^= (uint32_t)__shfl_xor((int)U.w, o);
   }
   if (lane == 0) tsum[tile] = U;
+}
+
+// Persistent waves over the tiles; a tile past a blob's POLYVAL tiles is skipped.
+__global__ __launch_bounds__(256) void k_aead_polyval(const AeadRec *__restrict__ rec,
+                                                      const AeadKeys *__restrict__ keys,
+                                                      const uint32_t *__restrict__ owner, uint64_t ntiles,
+                                                      uint4 *__restrict__ tsum, uint32_t *ctr) {
+  __shared__ uint4 mt[4][256];
+  const uint32_t wv = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint32_t tile = (MCDC_AEAD_PERSIST & 1) ? next_tile(ctr) : blockIdx.x * 4 + wv;
+  for (;;) {
+    if (tile >= ntiles) break;
+    const uint32_t i = rfl(owner[tile]);
+    const uint32_t t = tile - (uint32_t)rec[i].tile0;
+    if (t < rec[i].ptiles) polyval_tile(rec, keys, mt[wv], lane, i, t, tile, tsum);
+    if (!(MCDC_AEAD_PERSIST & 1)) break;
+    tile = next_tile(ctr);
+  }
 }
 
 // One lane per blob: POLYVAL of the whole blob, the tag.
@@ -562,17 +594,10 @@ __device__ __forceinline__ void store_quad(const AeadRec &R, uint64_t T, uint64_
   }
 }
 
-// One wave per tile of output quads (8 waves per block share the 64-KiB table): CTR keystream, plaintext xor, nonce/tag.
-__global__ __launch_bounds__(64 * kCtrWaves) void k_aead_ctr(int open, const AeadRec *__restrict__ rec,
-                                                  const AeadKeys *__restrict__ keys,
-                                                  const uint32_t *__restrict__ owner, uint64_t ntiles) {
-  __shared__ uint32_t tt[kTabPWords];
-  fill_table_p(tt);
-  const uint32_t wv = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const uint32_t tile = blockIdx.x * kCtrWaves + wv;
-  if (tile >= ntiles) return;
-  const uint8_t *tb = reinterpret_cast<const uint8_t *>(tt);
-  const uint32_t lane4 = 4 * lane;
+// One tile of output quads: CTR keystream, plaintext xor, nonce/tag.
+__device__ __forceinline__ void ctr_tile(int open, const AeadRec *__restrict__ rec, const AeadKeys *__restrict__ keys,
+                                         const uint32_t *__restrict__ owner, const uint8_t *tb, uint32_t lane,
+                                         uint32_t lane4, uint32_t tile) {
   const uint32_t i = rfl(owner[tile]);
   const AeadRec &R = rec[i];
   const uint32_t t = tile - (uint32_t)R.tile0;
@@ -625,6 +650,24 @@ __global__ __launch_bounds__(64 * kCtrWaves) void k_aead_ctr(int open, const Aea
     row(r, ks[0]);
   }
 #endif
+}
+
+// Persistent waves (kCtrWaves per block share the 64-KiB table) over the tiles.
+__global__ __launch_bounds__(64 * kCtrWaves) void k_aead_ctr(int open, const AeadRec *__restrict__ rec,
+                                                             const AeadKeys *__restrict__ keys,
+                                                             const uint32_t *__restrict__ owner, uint64_t ntiles,
+                                                             uint32_t *ctr) {
+  __shared__ uint32_t tt[kTabPWords];
+  fill_table_p(tt);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint8_t *tb = reinterpret_cast<const uint8_t *>(tt);
+  uint32_t tile = (MCDC_AEAD_PERSIST & 2) ? next_tile(ctr) : blockIdx.x * kCtrWaves + rfl(threadIdx.x >> 6);
+  for (;;) {
+    if (tile >= ntiles) break;
+    ctr_tile(open, rec, keys, owner, tb, lane, 4 * lane, tile);
+    if (!(MCDC_AEAD_PERSIST & 2)) break;
+    tile = next_tile(ctr);
+  }
 }
 
 // open: a blob that failed authentication gets zeros instead of its plaintext.
@@ -690,31 +733,50 @@ void launch_aead_sizes(int open, const uint64_t *ext, uint64_t n, uint64_t n_in,
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, tcnt, toff, (int)n + 1, stream);
 }
 
+// Persistent grids: as many blocks as fit at once (k_aead_polyval: 16 KiB LDS,
+// 4 waves -> 8 per CU; k_aead_ctr: 64 KiB LDS -> 2 per CU), never more than
+// there are tiles; ctr[0], ctr[1]: the two launches' tile counters.
+static void launch_tiles(int open, const AeadRec *rec, const AeadKeys *keys, const uint32_t *owner, uint64_t ntiles,
+                         uint4 *tsum, uint32_t *ctr, int num_cus, bool polyval, hipStream_t stream) {
+  if (!ntiles) return;
+  if (polyval) {
+    const uint64_t nb = (MCDC_AEAD_PERSIST & 1) ? std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)num_cus * 8)
+                                                : (ntiles + 3) / 4;
+    hipLaunchKernelGGL(k_aead_polyval, dim3((unsigned)nb), dim3(256), 0, stream, rec, keys, owner, ntiles, tsum, ctr);
+  } else {
+    const uint64_t nb = (MCDC_AEAD_PERSIST & 2)
+                            ? std::min<uint64_t>((ntiles + kCtrWaves - 1) / kCtrWaves, (uint64_t)num_cus * 2)
+                            : (ntiles + kCtrWaves - 1) / kCtrWaves;
+    hipLaunchKernelGGL(k_aead_ctr, dim3((unsigned)nb), dim3(64 * kCtrWaves), 0, stream, open, rec, keys, owner, ntiles,
+                       ctr + 1);
+  }
+}
+
 void launch_aead_seal(const AeadMaster &mk, const uint8_t *in, const uint64_t *ext, const uint32_t *nonces,
                       uint64_t n, uint8_t *out, const uint64_t *ooff, const uint64_t *toff, uint64_t ntiles,
-                      AeadRec *rec, AeadKeys *keys, uint32_t *owner, uint4 *tsum, hipStream_t stream) {
-  const dim3 gb((unsigned)((n + 255) / 256)), gt((unsigned)((ntiles + 3) / 4));
+                      AeadRec *rec, AeadKeys *keys, uint32_t *owner, uint4 *tsum, uint32_t *ctr, int num_cus,
+                      hipStream_t stream) {
+  const dim3 gb((unsigned)((n + 255) / 256));
+  (void)hipMemsetAsync(ctr, 0, 8, stream);
   hipLaunchKernelGGL(k_aead_prep, gb, dim3(256), 0, stream, 0, mk, in, ext, nonces, n, out, ooff, toff, rec, keys,
                      owner);
-  if (ntiles) hipLaunchKernelGGL(k_aead_polyval, gt, dim3(256), 0, stream, rec, keys, owner, ntiles, tsum);
+  launch_tiles(0, rec, keys, owner, ntiles, tsum, ctr, num_cus, true, stream);
   hipLaunchKernelGGL(k_aead_tag, gb, dim3(256), 0, stream, 0, rec, keys, tsum, n, (int32_t *)nullptr);
-  if (ntiles)
-    hipLaunchKernelGGL(k_aead_ctr, dim3((unsigned)((ntiles + kCtrWaves - 1) / kCtrWaves)), dim3(64 * kCtrWaves), 0,
-                       stream, 0, rec, keys, owner, ntiles);
+  launch_tiles(0, rec, keys, owner, ntiles, tsum, ctr, num_cus, false, stream);
 }
 
 void launch_aead_open(const AeadMaster &mk, const uint8_t *in, const uint64_t *ext, uint64_t n, uint8_t *out,
                       const uint64_t *ooff, const uint64_t *toff, uint64_t ntiles, AeadRec *rec, AeadKeys *keys,
-                      uint32_t *owner, uint4 *tsum, int32_t *status, hipStream_t stream) {
-  const dim3 gb((unsigned)((n + 255) / 256)), gt((unsigned)((ntiles + 3) / 4));
+                      uint32_t *owner, uint4 *tsum, int32_t *status, uint32_t *ctr, int num_cus, hipStream_t stream) {
+  const dim3 gb((unsigned)((n + 255) / 256));
+  (void)hipMemsetAsync(ctr, 0, 8, stream);
   hipLaunchKernelGGL(k_aead_prep, gb, dim3(256), 0, stream, 1, mk, in, ext, (const uint32_t *)nullptr, n, out, ooff,
                      toff, rec, keys, owner);
-  if (ntiles)
-    hipLaunchKernelGGL(k_aead_ctr, dim3((unsigned)((ntiles + kCtrWaves - 1) / kCtrWaves)), dim3(64 * kCtrWaves), 0,
-                       stream, 1, rec, keys, owner, ntiles);
-  if (ntiles) hipLaunchKernelGGL(k_aead_polyval, gt, dim3(256), 0, stream, rec, keys, owner, ntiles, tsum);
+  launch_tiles(1, rec, keys, owner, ntiles, tsum, ctr, num_cus, false, stream);
+  launch_tiles(1, rec, keys, owner, ntiles, tsum, ctr, num_cus, true, stream);
   hipLaunchKernelGGL(k_aead_tag, gb, dim3(256), 0, stream, 1, rec, keys, tsum, n, status);
-  if (ntiles) hipLaunchKernelGGL(k_aead_zero, gt, dim3(256), 0, stream, rec, owner, status, ntiles);
+  if (ntiles) hipLaunchKernelGGL(k_aead_zero, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, stream, rec, owner,
+                                 status, ntiles);
 }
 
 }  // namespace mcdc

@@ -722,9 +722,9 @@ int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size
       (!open && (rc = stage_arg(ctx, ctx->ae_nonce, nonces, n * kAeadNonce))) ||
       (rc = ensure(ctx, ctx->ae_olen, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_tcnt, (n + 1) * 8)) ||
       (rc = ensure(ctx, ctx->ae_ooff, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_toff, (n + 1) * 8)) ||
-      (rc = ensure(ctx, ctx->ae_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 16)))
+      (rc = ensure(ctx, ctx->ae_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 32)))
     return rc;
-  uint32_t *err = (uint32_t *)ctx->err.p + 2;
+  uint32_t *err = (uint32_t *)ctx->err.p + 2;  // (words 4-5: the tile counters)
   uint64_t *ooff = (uint64_t *)ctx->ae_ooff.p, *toff = (uint64_t *)ctx->ae_toff.p;
   HIP_TRY(hipMemsetAsync(err, 0, 4, st));
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
@@ -755,11 +755,13 @@ int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size
   if (!open)
     launch_aead_seal(mk, (const uint8_t *)d_in, (const uint64_t *)ctx->ae_ext.p, (const uint32_t *)ctx->ae_nonce.p, n,
                      (uint8_t *)d_out, ooff, toff, ntiles, (AeadRec *)ctx->ae_rec.p, (AeadKeys *)ctx->ae_keys.p,
-                     (uint32_t *)ctx->ae_owner.p, (uint4 *)ctx->ae_tsum.p, st);
+                     (uint32_t *)ctx->ae_owner.p, (uint4 *)ctx->ae_tsum.p, (uint32_t *)ctx->err.p + 4,
+                     ctx->num_cus, st);
   else
     launch_aead_open(mk, (const uint8_t *)d_in, (const uint64_t *)ctx->ae_ext.p, n, (uint8_t *)d_out, ooff, toff,
                      ntiles, (AeadRec *)ctx->ae_rec.p, (AeadKeys *)ctx->ae_keys.p, (uint32_t *)ctx->ae_owner.p,
-                     (uint4 *)ctx->ae_tsum.p, (int32_t *)ctx->ae_status.p, st);
+                     (uint4 *)ctx->ae_tsum.p, (int32_t *)ctx->ae_status.p, (uint32_t *)ctx->err.p + 4,
+                     ctx->num_cus, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
   std::memset(mk.rk, 0, sizeof mk.rk);
