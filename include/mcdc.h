@@ -192,6 +192,16 @@ int mcdc_seal_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_
                      const mcdc_blob *blobs, size_t nblobs, const uint8_t *nonces, void *d_out,
                      size_t out_cap, uint64_t *out_offsets);
 
+/* Same, with the blob extents given as a boundary list (mcdc_chunk records,
+ * the hash field ignored; host memory or a device pointer on the context's
+ * device, e.g. the device-resident `out` of mcdc_chunk_device), so that chunk
+ * -> IDs -> seal stays in HBM.  mapache compresses each chunk before sealing
+ * it; this entry serves blobs that are the chunks themselves (data that the
+ * caller stores uncompressed, or a measurement of the sealing stage). */
+int mcdc_seal_chunks_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in,
+                            const mcdc_chunk *chunks, size_t nchunks, const uint8_t *nonces, void *d_out,
+                            size_t out_cap, uint64_t *out_offsets);
+
 /* decrypt_with_key (storage.rs:128-144) for every sealed extent: result i is
  * the plaintext (length - 28 bytes).  status (optional, host or device, nblobs
  * entries): 0 authentic, -1 not (tag mismatch, or an extent shorter than 28

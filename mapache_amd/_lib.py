@@ -35,7 +35,7 @@ EXPORTS = (
     "mcdc_last_error", "mcdc_device_alloc", "mcdc_device_free", "mcdc_host_alloc",
     "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_memcpy_d2h", "mcdc_fill_random_device", "mcdc_digest",
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
-    "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device",
+    "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
 )
 
 
@@ -112,6 +112,7 @@ def load():
     L.mcdc_batcher_stats.argtypes = [vp, P(McdcBatcherStats)]
     L.mcdc_seal_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
     L.mcdc_open_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp]
+    L.mcdc_seal_chunks_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -326,6 +327,26 @@ class Context:
         oo = np.zeros(len(ext) + 1, dtype=np.uint64)
         check(load().mcdc_seal_device(self._h, self._key(key), ctypes.c_void_p(d_in), n_in, ext.ctypes.data,
                                       len(ext), nz.ctypes.data, ctypes.c_void_p(d_out), out_cap, oo.ctypes.data))
+        return oo
+
+    @_locked
+    def seal_chunks(self, key, d_in: int, n_in: int, chunks, nonces, d_out: int, out_cap: int, offsets_out=None):
+        """mcdc_seal_chunks_device: the blobs are the records of a boundary list --
+        a CHUNK_DTYPE array (host) or (device pointer, count).  Returns the nblobs + 1
+        output offsets, or writes them to the device pointer `offsets_out`."""
+        if isinstance(chunks, tuple):
+            cptr, count = chunks
+        else:
+            arr = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+            cptr, count = arr.ctypes.data, arr.size
+            keep = arr  # noqa: F841  (alive across the call)
+        nz = np.ascontiguousarray(nonces, dtype=np.uint8).reshape(-1) if not isinstance(nonces, int) else None
+        nptr = nonces if nz is None else nz.ctypes.data
+        oo = None if offsets_out is not None else np.zeros(count + 1, dtype=np.uint64)
+        check(load().mcdc_seal_chunks_device(self._h, self._key(key), ctypes.c_void_p(d_in), n_in,
+                                             ctypes.c_void_p(cptr), count, ctypes.c_void_p(nptr),
+                                             ctypes.c_void_p(d_out), out_cap,
+                                             ctypes.c_void_p(offsets_out if oo is None else oo.ctypes.data)))
         return oo
 
     @_locked

@@ -38,6 +38,9 @@ void aead_expand_key256(const uint8_t key[32], uint32_t rk[60]);
 
 size_t aead_scan_tmp_bytes(uint64_t n);
 
+// ext[2 i], ext[2 i + 1] = offset, length of boundary record i (24-byte records, device)
+void launch_aead_from_chunks(const void *chunks, uint64_t n, uint64_t *ext, hipStream_t stream);
+
 // Sizes: olen[i] (output bytes of blob i), tcnt[i] (tiles), exclusive scans
 // into ooff / toff (n + 1 entries; [n] = totals).  An extent outside
 // [0, n_in) sets err bit 0.  open: an extent shorter than 28 bytes gets no

@@ -359,6 +359,22 @@ __global__ void k_aead_sizes(int open, const uint64_t *ext, uint64_t n, uint64_t
   }
 }
 
+// Blob extents from a boundary list (offset, length, hash records).
+__global__ void k_aead_from_chunks(const uint64_t *chunks, uint64_t n, uint64_t *ext) {
+  MCDC_VGPR_PAD(8);  // 8 used: not an exact fill (MCDC_VGPR_PAD)
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    ext[2 * i] = chunks[3 * i];
+    ext[2 * i + 1] = chunks[3 * i + 1];
+  }
+}
+
+void launch_aead_from_chunks(const void *chunks, uint64_t n, uint64_t *ext, hipStream_t stream) {
+  if (n)
+    hipLaunchKernelGGL(k_aead_from_chunks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                       (const uint64_t *)chunks, n, ext);
+}
+
 // One lane per blob.
 __global__ __launch_bounds__(256) void k_aead_prep(int open, AeadMaster mk, const uint8_t *in, const uint64_t *ext,
                                                    const uint32_t *nonces, uint64_t n, uint8_t *out,

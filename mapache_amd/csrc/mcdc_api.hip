@@ -692,13 +692,14 @@ int give_back(mcdc_ctx *ctx, void *dst, const void *d_src, size_t bytes) {
   return MCDC_OK;
 }
 
-// mcdc_seal_device (open = 0) / mcdc_open_device (open = 1).
+// mcdc_seal_device (open = 0) / mcdc_open_device (open = 1); chunks != nullptr:
+// the extents come from a boundary list instead (mcdc_seal_chunks_device).
 int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size_t n_in, const mcdc_blob *blobs,
              size_t nblobs, const uint8_t *nonces, void *d_out, size_t out_cap, uint64_t *out_offsets,
-             int32_t *status) {
+             int32_t *status, const mcdc_chunk *chunks = nullptr) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  if (!key || (!d_in && n_in) || (nblobs && !blobs) || (!open && nblobs && !nonces))
+  if (!key || (!d_in && n_in) || (nblobs && !blobs && !chunks) || (!open && nblobs && !nonces))
     return fail(MCDC_E_INVALID, "NULL argument");
   if (d_in && !is_device_ptr(d_in)) return fail(MCDC_E_INVALID, "d_in is not a device pointer");
   if (d_out && !is_device_ptr(d_out)) return fail(MCDC_E_INVALID, "d_out is not a device pointer");
@@ -718,8 +719,15 @@ int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size
   }
   const size_t n = nblobs;
   const size_t tmpb = aead_scan_tmp_bytes(n);
-  if ((rc = stage_arg(ctx, ctx->ae_ext, blobs, n * sizeof(mcdc_blob))) ||
-      (!open && (rc = stage_arg(ctx, ctx->ae_nonce, nonces, n * kAeadNonce))) ||
+  if (chunks) {  // a boundary list: to the device if needed, then (offset, length) pairs
+    if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, n * sizeof(mcdc_chunk))) ||
+        (rc = ensure(ctx, ctx->ae_ext, n * sizeof(mcdc_blob))))
+      return rc;
+    launch_aead_from_chunks(ctx->b3_chunks.p, n, (uint64_t *)ctx->ae_ext.p, ctx->stream);
+  } else if ((rc = stage_arg(ctx, ctx->ae_ext, blobs, n * sizeof(mcdc_blob)))) {
+    return rc;
+  }
+  if ((!open && (rc = stage_arg(ctx, ctx->ae_nonce, nonces, n * kAeadNonce))) ||
       (rc = ensure(ctx, ctx->ae_olen, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_tcnt, (n + 1) * 8)) ||
       (rc = ensure(ctx, ctx->ae_ooff, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_toff, (n + 1) * 8)) ||
       (rc = ensure(ctx, ctx->ae_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 32)))
@@ -1183,6 +1191,13 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
 int mcdc_seal_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in, const mcdc_blob *blobs,
                      size_t nblobs, const uint8_t *nonces, void *d_out, size_t out_cap, uint64_t *out_offsets) {
   return aead_run(ctx, 0, key, d_in, n_in, blobs, nblobs, nonces, d_out, out_cap, out_offsets, nullptr);
+}
+
+int mcdc_seal_chunks_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in,
+                            const mcdc_chunk *chunks, size_t nchunks, const uint8_t *nonces, void *d_out,
+                            size_t out_cap, uint64_t *out_offsets) {
+  if (nchunks && !chunks) return fail(MCDC_E_INVALID, "chunks is NULL");
+  return aead_run(ctx, 0, key, d_in, n_in, nullptr, nchunks, nonces, d_out, out_cap, out_offsets, nullptr, chunks);
 }
 
 int mcdc_open_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in, const mcdc_blob *sealed,

@@ -226,3 +226,42 @@ def test_seal_chunks_of_a_stream(ctx):
         ctx.device_free(dp)
     ref, roo = O.seal_blobs(key, O.random_bytes(n, 31337), ch["offset"], ch["length"], nonces, threads=8)
     assert got.tobytes() == ref.tobytes()
+
+
+def test_seal_chunks_device_list(ctx):
+    """mcdc_seal_chunks_device with the chunker's device-resident boundary list
+    (and with a host list, and with device nonces / device offsets) gives
+    exactly mcdc_seal_device's output."""
+    n = 64 << 20
+    p = _lib.params(16384, 65536, 262144, 1)
+    dp = ctx.device_alloc(n + 64)
+    cap_c = n // (16384 - 1) + 2
+    d_ch = ctx.device_alloc(cap_c * _lib.CHUNK_DTYPE.itemsize)
+    try:
+        ctx.fill_random(dp, n, 4242)
+        k = ctx.chunk_device_to_device(p, dp, n, d_ch, cap_c)
+        ch = ctx.d2h_chunks(d_ch, k)
+        key = bytes(range(7, 39))
+        nonces = np.random.default_rng(1).integers(0, 256, (k, 12), dtype=np.uint8)
+        d_nonce = _dev(ctx, nonces.reshape(-1))
+        d_offs = ctx.device_alloc(8 * (k + 1))
+        cap = n + 28 * k
+        outs = [ctx.device_alloc(cap) for _ in range(3)]
+        try:
+            oo = ctx.seal(key, dp, n, ch["offset"], ch["length"], nonces, outs[0], cap)
+            oo2 = ctx.seal_chunks(key, dp, n, ch, nonces, outs[1], cap)
+            assert ctx.seal_chunks(key, dp, n, (d_ch, k), d_nonce, outs[2], cap, offsets_out=d_offs) is None
+            got = [ctx.d2h_bytes(o, int(oo[-1])) for o in outs]
+            oo3 = np.frombuffer(ctx.d2h_bytes(d_offs, 8 * (k + 1)).tobytes(), np.uint64)
+        finally:
+            for o in outs + [d_offs, d_nonce]:
+                ctx.device_free(o)
+    finally:
+        ctx.device_free(d_ch)
+        ctx.device_free(dp)
+    assert (oo == oo2).all() and (oo == oo3).all()
+    assert got[0].tobytes() == got[1].tobytes() == got[2].tobytes()
+    host = O.random_bytes(n, 4242)
+    for i in (0, 1, k // 2, k - 1):
+        assert got[0][oo[i]:oo[i + 1]].tobytes() == O.encrypt_with_key(
+            key, nonces[i], host[ch["offset"][i]:ch["offset"][i] + ch["length"][i]])
