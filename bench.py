@@ -330,8 +330,13 @@ def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_s
                           "peak": round(peak_tops, 2), "unit": "T int32 lane-ops/s",
                           "frac": round(alg_ops / (ids_ms * 1e-3) / 1e12 / peak_tops, 4),
                           "ops_per_block": 672,
+                          # nominal: 256 CUs x 128 int32 lanes per clock x 2.4 GHz
+                          "peak_nominal": 78.64,
+                          "frac_nominal": round(alg_ops / (ids_ms * 1e-3) / 1e12 / 78.64, 4),
                           "note": "algorithmic compression ops only (leaves; parents add ~1/16); peak: "
-                                  "tools/ubench3.hip, the compression alone at full occupancy, wall clock"},
+                                  "tools/ubench3.hip, the compression alone at full occupancy, wall clock "
+                                  "(the clock the chip holds under this load); peak_nominal at the 2.4 GHz "
+                                  "peak engine clock"},
              "chunk_plus_ids_ms": round(dt2 * 1e3, 3), "chunk_plus_ids_gib_s": round(n / dt2 / GIB, 2),
              "parity_probe_chunks": int(len(sel)), "parity_probe_ok": ok}
         if not no_cpu:

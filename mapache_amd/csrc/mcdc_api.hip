@@ -218,7 +218,7 @@ struct mcdc_ctx {
   DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp,
+      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
@@ -872,7 +872,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
                     &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->tile_ctr, &ctx->b3_chunks, &ctx->b3_gcnt,
-                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp,
+                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp, &ctx->b3_hist,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status};
   for (DevBuf *b : bufs)
@@ -1142,8 +1142,10 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   const size_t tmpb = b3_tmp_bytes(nchunks);
   if ((rc = ensure(ctx, ctx->b3_gcnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->b3_goff, (nchunks + 1) * 8)) ||
       (rc = ensure(ctx, ctx->b3_owner, bound * 4)) || (rc = ensure(ctx, ctx->b3_nodes, bound * 32)) ||
-      (rc = ensure(ctx, ctx->b3_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 16)))
+      (rc = ensure(ctx, ctx->b3_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 16)) ||
+      (rc = ensure(ctx, ctx->b3_hist, kB3HistWords * 4)))
     return rc;
+  uint32_t *hist = (uint32_t *)ctx->b3_hist.p;
   if (!ids_dev) {
     if ((rc = ensure(ctx, ctx->b3_ids, nchunks * 32))) return rc;
     ids_dev = (uint8_t *)ctx->b3_ids.p;
@@ -1152,9 +1154,9 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   const uint64_t *goff = (const uint64_t *)ctx->b3_goff.p;
   HIP_TRY(hipMemsetAsync(err, 0, 4, st));
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
-  launch_b3_prepare(dch, nchunks, n, (uint64_t *)ctx->b3_gcnt.p, (uint64_t *)ctx->b3_goff.p, err, ctx->b3_tmp.p, tmpb,
-                    st);
-  launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, (uint32_t *)ctx->b3_owner.p,
+  launch_b3_prepare(dch, nchunks, n, (uint64_t *)ctx->b3_gcnt.p, (uint64_t *)ctx->b3_goff.p, hist, err, ctx->b3_tmp.p,
+                    tmpb, st);
+  launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, hist, (uint32_t *)ctx->b3_owner.p,
                  (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
@@ -1163,12 +1165,13 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   HIP_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(&groups, goff + nchunks, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  groups = b3_groups_total(groups);
   if (herr) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer", n);
   if (groups > bound) {  // overlapping / repeated chunks: the kernels skipped; hash with the exact bound
     bound = groups;
     if ((rc = ensure(ctx, ctx->b3_owner, bound * 4)) || (rc = ensure(ctx, ctx->b3_nodes, bound * 32))) return rc;
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
-    launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, (uint32_t *)ctx->b3_owner.p,
+    launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, hist, (uint32_t *)ctx->b3_owner.p,
                    (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_end, st));

@@ -11,12 +11,15 @@
 // number of leaves; the last compression carries the ROOT flag.
 //
 // GPU shape:
-//   k_b3_groups   groups of 16 leaves (16 KiB) per chunk -> counts
-//   (hipcub)      exclusive scan -> group offsets
-//   k_b3_owner    group -> chunk map
-//   k_b3_leaves   one lane per group: 16 x 16 block compressions, the group's
-//                 subtree reduced on the fly (a 4-deep chaining-value stack in
-//                 LDS); a chunk of <= 16 leaves finishes its ID here (ROOT)
+//   k_b3_groups   groups of 16 leaves (16 KiB) per chunk -> counts (full
+//                 groups | tail group), tail-length histogram
+//   (hipcub)      exclusive scan -> node slots and processing order
+//   k_b3_owner    item -> chunk map: full groups first, then the tail groups
+//                 longest first (counting sort)
+//   k_b3_leaves   one lane per group: 16 x 16 block compressions from
+//                 quad-coalesced loads transposed through LDS, the group's
+//                 subtree reduced on the fly (completed subtrees in registers);
+//                 a chunk of <= 16 leaves finishes its ID here (ROOT)
 //   k_b3_tree     one lane per larger chunk: level-by-level pairing of its
 //                 group nodes (the last node of an odd level moves up
 //                 unchanged — the same tree as the specification's stack rule)
@@ -142,120 +145,296 @@ __device__ __forceinline__ uint32_t leaves_of(uint64_t len) {
 
 using namespace b3;
 
+// Work items are 16-KiB groups of leaves.  Per chunk: len / 16 KiB full groups
+// (256 full blocks each) and at most one tail group (the rest, or the empty
+// input's one empty block).  Group counts are packed: low 32 bits full
+// groups, high 32 bits tail groups, so one scan gives both the node slots
+// (their sum) and the processing order: every full group first, in chunk
+// order, then the tail groups sorted by block count, longest first (a
+// counting sort over 256 bins) — the lanes of a wave then run loops of equal
+// length (in chunk order a wave ran as long as its longest lane: ~10 % of
+// its lane-cycles idle on the 64 GiB stream).
+constexpr uint32_t kGroupBytes = kGroupLeaves * kLeaf;
+constexpr int kTailBins = 256;
+
+__device__ __forceinline__ uint64_t gtotal(uint64_t x) { return (x & 0xffffffffull) + (x >> 32); }
+
+__device__ __forceinline__ uint32_t tail_bin(uint64_t len) {  // 0 = 256 blocks ... 255 = one block
+  const uint32_t rem = (uint32_t)(len % kGroupBytes);
+  return kTailBins - (len == 0 ? 1u : (rem + 63) / 64);
+}
+
 // A chunk outside [0, nbytes) of the buffer gets no groups and sets *err.
-__global__ void k_b3_groups(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *gcnt, uint32_t *err) {
+__global__ __launch_bounds__(256) void k_b3_groups(const DevChunk *chunks, uint64_t n, uint64_t nbytes,
+                                                   uint64_t *gcnt, uint32_t *hist, uint32_t *err) {
+  __shared__ uint32_t lh[kTailBins];
+  lh[threadIdx.x] = 0;
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const DevChunk c = chunks[i];
     const bool ok = c.offset <= nbytes && c.length <= nbytes - c.offset;
-    gcnt[i] = ok ? (leaves_of(c.length) + kGroupLeaves - 1) / kGroupLeaves : 0;
+    const uint64_t full = ok ? c.length / kGroupBytes : 0;
+    const bool tail = ok && (c.length % kGroupBytes != 0 || c.length == 0);
+    gcnt[i] = full | ((uint64_t)tail << 32);
+    if (tail) atomicAdd(&lh[tail_bin(c.length)], 1u);
     if (!ok) atomicOr(err, 1u);
   } else if (i == n) {
     gcnt[i] = 0;
   }
+  __syncthreads();
+  if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
 }
 
 // Every hashing kernel first checks the group total against the host's bound
 // (b3_group_bound assumes disjoint chunks; overlapping or repeated chunks
 // exceed it): over the bound nothing is written, and the host re-runs the
 // hashing with the exact total it reads back (mcdc_chunk_ids_device).
-__global__ void k_b3_owner(const uint64_t *goff, uint64_t n, uint64_t bound, uint32_t *owner) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || goff[n] > bound) return;
-  for (uint64_t g = goff[i]; g < goff[i + 1]; ++g) owner[g] = (uint32_t)i;
-}
-
-// One lane per group of <= 16 leaves.  The group's subtree (a complete binary
-// tree when it holds 16 leaves, the specification's tree of its leaves
-// otherwise) is built with a chaining-value stack in LDS.  The main loop runs
-// over the group's full 64-byte blocks only (one uniform code path for the
-// whole wave); the one partial block a group can end with is hashed after it.
-__global__ __launch_bounds__(256) void k_b3_leaves(const uint8_t *base, const DevChunk *chunks,
-                                                   const uint64_t *goff, const uint32_t *owner, uint64_t n,
-                                                   uint64_t bound, uint32_t *nodes, uint8_t *ids) {
-  __shared__ uint32_t stk[256][4][8];
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t total = goff[n];
-  if (g >= total || total > bound) return;  // the grid is sized by the host bound
-  const uint32_t i = owner[g];
-  const DevChunk ch = chunks[i];
-  const uint32_t nleaves = leaves_of(ch.length);
-  const uint64_t gi = g - goff[i];                      // group index within the chunk
-  const uint64_t l0 = gi * kGroupLeaves;                // first leaf of the group
-  const bool whole = nleaves <= kGroupLeaves;           // this group is the chunk's whole tree
-  const bool root1 = nleaves == 1;                      // ... and its only leaf is the root
-  const uint64_t grem = ch.length - l0 * kLeaf;
-  const uint32_t gbytes = (uint32_t)(grem < (uint64_t)(kGroupLeaves * kLeaf) ? grem : kGroupLeaves * kLeaf);
-  const uint32_t nfull = gbytes / 64, tail = gbytes % 64;
-  const bool has_tail = tail != 0 || gbytes == 0;       // (the empty input is one empty block)
-  const uint32_t nblk = nfull + (has_tail ? 1u : 0u);
-  const uint8_t *p = base + ch.offset + l0 * kLeaf;
-  const uint32_t r = (uint32_t)((uintptr_t)p & 3);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(p - r);  // (stays a global pointer)
-  uint32_t (*st)[8] = stk[threadIdx.x];
-  uint32_t cv[8];
-  iv(cv);
-  int sp = 0;
-  // Block j + 1 is requested before block j is compressed: a wave waits on
-  // memory only when its next block has not arrived during a whole
-  // compression, which keeps enough waves ready for the VALU's dual-rate issue
-  // (tools/ubench3.hip: the G mix runs at 2 cycles per instruction with 4 ready
-  // waves per SIMD, 4 with 2).
-  uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
-  uint32_t n16 = 0;
-  // (loads are unconditional — the last iteration re-reads its own block —
-  // so no wait is forced at a control-flow join)
-  auto fetch = [&](const uint32_t *ww) {
-    n0 = *reinterpret_cast<const uint4 *>(ww);
-    n1 = *reinterpret_cast<const uint4 *>(ww + 4);
-    n2 = *reinterpret_cast<const uint4 *>(ww + 8);
-    n3 = *reinterpret_cast<const uint4 *>(ww + 12);
-    const uint32_t x = ww[r ? 16 : 15];  // dword 16 holds the block's last bytes only when misaligned
-    n16 = r ? x : 0u;
-  };
-  if (nfull) fetch(w);
-#pragma unroll 1
-  for (uint32_t j = 0; j < nfull; ++j, w += 16) {
-    const uint32_t b = j & 15, k = j >> 4;
-    uint32_t m[16];
-    {
-      const uint4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
-      const uint32_t x16 = n16;
-      fetch(j + 1 < nfull ? w + 16 : w);
-      const uint32_t raw[17] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, x16};
-#pragma unroll
-      for (int t = 0; t < 16; ++t) m[t] = __builtin_amdgcn_alignbyte(raw[t + 1], raw[t], r);
-    }
-    const bool last = j + 1 == nblk;
-    const bool end = b == 15 || last;
-    compress(cv, m, l0 + k, 64,
-             (b == 0 ? kChunkStart : 0) | (end ? kChunkEnd : 0) | (root1 && last ? kRoot : 0));
-    if (end && !last) {  // leaf k done and more follow: push it, merging completed subtrees
-      for (uint32_t t = k + 1; (t & 1) == 0; t >>= 1) {
-        --sp;
-        parent(st[sp], cv, 0, cv);
-      }
-#pragma unroll
-      for (int t = 0; t < 8; ++t) st[sp][t] = cv[t];
-      ++sp;
-      iv(cv);
+// owner[item] = chunk: full groups at [0, F) in chunk order, tail groups at
+// F + (start of their bin) + (arrival order within the bin).
+__global__ __launch_bounds__(256) void k_b3_owner(const DevChunk *chunks, const uint64_t *goff, uint64_t n,
+                                                  uint64_t bound, const uint32_t *hist, uint32_t *cur,
+                                                  uint32_t *owner) {
+  __shared__ uint32_t bs[kTailBins], lc[kTailBins];
+  const uint32_t t = threadIdx.x;
+  bs[t] = hist[t];
+  lc[t] = 0;
+  __syncthreads();
+  for (uint32_t d = 1; d < kTailBins; d <<= 1) {  // inclusive scan of the bins
+    const uint32_t v = t >= d ? bs[t - d] : 0u;
+    __syncthreads();
+    bs[t] += v;
+    __syncthreads();
+  }
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
+  const uint64_t last = goff[n];
+  const bool ok = i < n && gtotal(last) <= bound;
+  uint64_t a = 0, b = 0;
+  uint32_t bin = 0, rank = 0;
+  bool tl = false;
+  if (ok) {
+    a = goff[i];
+    b = goff[i + 1];
+    tl = (b >> 32) != (a >> 32);
+    if (tl) {
+      bin = tail_bin(chunks[i].length);
+      rank = atomicAdd(&lc[bin], 1u);  // rank within the block's share of the bin
     }
   }
+  __syncthreads();
+  // one global reservation per bin and block (a global atomic per tail
+  // serialised on 256 addresses: 0.44 ms per 64 GiB call)
+  if (lc[t]) lc[t] = atomicAdd(&cur[t], lc[t]);
+  __syncthreads();
+  if (!ok) return;
+  for (uint64_t g = a & 0xffffffffull; g < (b & 0xffffffffull); ++g) owner[g] = (uint32_t)i;
+  if (tl) owner[(last & 0xffffffffull) + (bs[bin] - hist[bin]) + lc[bin] + rank] = (uint32_t)i;
+}
+
+// One lane per group (<= 16 leaves).  The group's subtree (a complete binary
+// tree when it holds 16 leaves, the specification's tree of its leaves
+// otherwise) is built on the fly: a finished leaf merges with the completed
+// subtrees below it (one per set bit of its index) and is kept at its level
+// (levels 0-1 in registers, 2-3 in LDS: 32 VGPRs would cost the fourth wave
+// per SIMD).  The main loop runs over 64-byte blocks with a wave-uniform trip
+// count (the wave's longest lane; shorter lanes idle under the exec mask,
+// rare once the items are ordered); the one partial block a group can end
+// with is hashed after it.
+//
+// Loads (MCDC_B3_QUAD, default): quad-coalesced, as in the scan — for block
+// j, load q of lane 4k + i fetches the 16 bytes at offset 16 i of block j of
+// lane 16 q + k at the block's own byte address (gfx950 reads a misaligned
+// dwordx4 as the 16 bytes at that address: tools/dbg/unaligned_probe.hip), so
+// a wave-instruction touches 16 runs of 64 contiguous bytes instead of 64
+// scattered 16-byte pieces; the wave transposes through a private LDS pad
+// (row stride 80 B: conflict-free reads) and each lane reads its own block.
+// MCDC_B3_QUAD=0: each lane loads its own block (four 16-byte loads).  Block
+// j + 1 is requested before block j is compressed.
+#ifndef MCDC_B3_QUAD
+#define MCDC_B3_QUAD 1
+#endif
+#if MCDC_B3_QUAD
+constexpr int kB3Pad = 5;  // uint4 per pad row (80 B)
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *gq;  // global (not flat) loads
+
+__device__ __forceinline__ uint4 gload(uint64_t a) {
+  const u32x4 v = *reinterpret_cast<gq>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_b3_leaves(
+    const uint8_t *base, const DevChunk *chunks, const uint64_t *goff, const uint32_t *owner, uint64_t n,
+    uint64_t bound, uint32_t *nodes, uint8_t *ids) {
+#if MCDC_B3_QUAD
+  __shared__ uint4 pad_all[4][64 * kB3Pad];
+#endif
+  __shared__ uint32_t up_all[4][2 * 8 * 64];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t last_off = goff[n];
+  const uint64_t total = gtotal(last_off);
+  const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + 64 * wv;  // the wave's first item
+  if (g0 >= total || total > bound) return;  // wave-uniform; the grid is sized by the host bound
+  const uint64_t p = g0 + lane;
+  const bool act = p < total;
+  uint32_t i = 0, nfull = 0, tail = 0, nleaves = 1;
+  uint64_t l0 = 0, slot_idx = 0;
+  bool has_tail = false;
+  const uint8_t *gp = reinterpret_cast<const uint8_t *>(chunks);  // (a readable address for idle lanes)
+  if (act) {
+    i = owner[p];
+    const DevChunk ch = chunks[i];
+    const uint64_t a = goff[i];
+    const uint64_t gi = p < (last_off & 0xffffffffull) ? p - (a & 0xffffffffull) : ch.length / kGroupBytes;
+    nleaves = leaves_of(ch.length);
+    l0 = gi * kGroupLeaves;
+    const uint64_t grem = ch.length - gi * kGroupBytes;
+    const uint32_t gbytes = (uint32_t)(grem < kGroupBytes ? grem : kGroupBytes);
+    nfull = gbytes / 64;
+    tail = gbytes % 64;
+    has_tail = tail != 0 || gbytes == 0;  // (the empty input is one empty block)
+    gp = base + ch.offset + gi * kGroupBytes;
+    slot_idx = gtotal(a) + gi;
+  }
+  const uint32_t nblk = nfull + (has_tail ? 1u : 0u);
+  const bool whole = nleaves <= kGroupLeaves;  // this group is the chunk's whole tree
+  const bool root1 = nleaves == 1;             // ... and its only leaf is the root
+  // the wave's longest and shortest lanes (wave-uniform)
+  uint32_t nmax = nfull, nmin = nfull;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, d));
+    nmin = min(nmin, (uint32_t)__shfl_xor((int)nmin, d));
+  }
+  nmax = __builtin_amdgcn_readfirstlane(nmax);
+  nmin = __builtin_amdgcn_readfirstlane(nmin);
+  const uint64_t gpa = reinterpret_cast<uint64_t>(gp);
+#if MCDC_B3_QUAD
+  // the four blocks this lane fetches: lane 16 q + k's block, piece i
+  const uint32_t qk = lane >> 2, qi = lane & 3;
+  uint64_t aq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int src = 16 * q + (int)qk;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)gpa, src), hi = (uint32_t)__shfl((int)(uint32_t)(gpa >> 32), src);
+    aq[q] = (((uint64_t)hi << 32) | lo) + 16 * qi;
+  }
+  uint4 *pad = pad_all[wv];
+  uint4 *wr = pad + kB3Pad * qk + qi;
+  const uint4 *rd = pad + kB3Pad * lane;
+  uint4 a0, a1, a2, a3;
+  // block b of every source lane; past a lane's last full block (only in
+  // waves of unequal lanes) the address is clamped to it, or to a readable
+  // dummy when it has none (the data is not used)
+  auto fetch = [&](uint32_t b) {
+    if (b < nmin) {
+      a0 = gload(aq[0] + 64ull * b);
+      a1 = gload(aq[1] + 64ull * b);
+      a2 = gload(aq[2] + 64ull * b);
+      a3 = gload(aq[3] + 64ull * b);
+    } else {
+      auto clamped = [&](int q) {
+        const uint32_t nf = (uint32_t)__shfl((int)nfull, 16 * q + (int)qk);
+        return nf ? aq[q] + 64ull * min(b, nf - 1) : reinterpret_cast<uint64_t>(chunks);
+      };
+      a0 = gload(clamped(0));
+      a1 = gload(clamped(1));
+      a2 = gload(clamped(2));
+      a3 = gload(clamped(3));
+    }
+  };
+#else
+  uint4 a0, a1, a2, a3;
+  auto fetch = [&](uint32_t b) {
+    const uint64_t x = nfull ? gpa + 64ull * min(b, nfull - 1) : reinterpret_cast<uint64_t>(chunks);
+    a0 = gload(x); a1 = gload(x + 16); a2 = gload(x + 32); a3 = gload(x + 48);
+  };
+#endif
+  // completed subtrees: levels 0-1 in registers, 2-3 in LDS ([level][word][lane])
+  uint32_t s0[8], s1[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) s0[w] = s1[w] = 0;
+  uint32_t *up = up_all[wv];
+  auto sget = [&](uint32_t l, uint32_t out[8]) {
+    if (l < 2) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) out[w] = l == 0 ? s0[w] : s1[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) out[w] = up[((l - 2) * 8 + w) * 64 + lane];
+    }
+  };
+  auto sput = [&](uint32_t l, const uint32_t in[8]) {
+    if (l < 2) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        s0[w] = l == 0 ? in[w] : s0[w];
+        s1[w] = l == 1 ? in[w] : s1[w];
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) up[((l - 2) * 8 + w) * 64 + lane] = in[w];
+    }
+  };
+  uint32_t cv[8];
+  iv(cv);
+  if (nmax) fetch(0);
+#pragma unroll 1
+  for (uint32_t j = 0; j < nmax; ++j) {
+#if MCDC_B3_QUAD
+    wr[0] = a0;
+    wr[16 * kB3Pad] = a1;
+    wr[32 * kB3Pad] = a2;
+    wr[48 * kB3Pad] = a3;
+    const uint4 c0 = rd[0], c1 = rd[1], c2 = rd[2], c3 = rd[3];
+#else
+    const uint4 c0 = a0, c1 = a1, c2 = a2, c3 = a3;
+#endif
+    if (j + 1 < nmax) fetch(j + 1);
+    if (j < nfull) {
+      const uint32_t m[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                              c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+      const uint32_t b = j & 15, k = j >> 4;
+      const bool last = j + 1 == nblk;
+      const bool end = b == 15 || last;
+      compress(cv, m, l0 + k, 64,
+               (b == 0 ? kChunkStart : 0) | (end ? kChunkEnd : 0) | (root1 && last ? kRoot : 0));
+      if (end && !last) {  // leaf k done and more follow: merge the completed subtrees, keep it
+        uint32_t l = 0;
+        while ((k >> l) & 1) {
+          uint32_t left[8];
+          sget(l, left);
+          parent(left, cv, 0, cv);
+          ++l;
+        }
+        sput(l, cv);
+        iv(cv);
+      }
+    }
+  }
+  if (!act) return;
   if (has_tail) {  // the group's final, partial block
     const uint32_t b = nfull & 15, k = nfull >> 4;
     uint32_t m[16];
-    load_block(p + 64ull * nfull, tail, m);
+    load_block(gp + 64ull * nfull, tail, m);
     compress(cv, m, l0 + k, tail, (b == 0 ? kChunkStart : 0) | kChunkEnd | (root1 ? kRoot : 0));
   }
-  while (sp > 0) {  // right edge; the top node is the chunk's root when `whole`
-    --sp;
-    parent(st[sp], cv, (whole && sp == 0) ? kRoot : 0, cv);
+  // right edge: fold the kept subtrees, smallest first; the last fold is the
+  // chunk's root when the group is the whole tree
+  const uint32_t K = (nblk - 1) >> 4;  // leaves kept = index of the last leaf
+#pragma unroll
+  for (uint32_t l = 0; l < 4; ++l) {
+    if ((K >> l) & 1) {
+      uint32_t left[8];
+      sget(l, left);
+      parent(left, cv, (whole && (K >> (l + 1)) == 0) ? kRoot : 0, cv);
+    }
   }
   if (whole) {
     store_id(ids + 32ull * i, cv);
   } else {
-    uint4 *d = reinterpret_cast<uint4 *>(nodes + 8 * g);
+    uint4 *d = reinterpret_cast<uint4 *>(nodes + 8 * slot_idx);
     d[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
     d[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
   }
@@ -267,10 +446,10 @@ __global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t
                           uint8_t *ids) {
   MCDC_VGPR_PAD(48);  // 48 used: not an exact fill (MCDC_VGPR_PAD)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || goff[n] > bound) return;
-  uint64_t m = goff[i + 1] - goff[i];
+  if (i >= n || gtotal(goff[n]) > bound) return;
+  uint64_t m = gtotal(goff[i + 1]) - gtotal(goff[i]);
   if (m < 2) return;  // finished by k_b3_leaves
-  uint32_t *nd = nodes + 8 * goff[i];
+  uint32_t *nd = nodes + 8 * gtotal(goff[i]);
   uint32_t l[8], r[8], o[8];
   while (m > 1) {
     const uint64_t pairs = m / 2;
@@ -301,21 +480,27 @@ uint64_t b3_group_bound(uint64_t total_bytes, uint64_t nchunks) {
 }
 
 void launch_b3_prepare(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *gcnt, uint64_t *goff,
-                       uint32_t *err, void *tmp, size_t tmp_bytes, hipStream_t stream) {
+                       uint32_t *hist, uint32_t *err, void *tmp, size_t tmp_bytes, hipStream_t stream) {
+  (void)hipMemsetAsync(hist, 0, 2 * kTailBins * sizeof(uint32_t), stream);
   hipLaunchKernelGGL(k_b3_groups, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, chunks, n, nbytes,
-                     gcnt, err);
+                     gcnt, hist, err);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, gcnt, goff, (int)n + 1, stream);
 }
 
 void launch_b3_hash(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *goff,
-                    uint64_t group_bound, uint32_t *owner, uint32_t *nodes, uint8_t *ids, hipStream_t stream) {
+                    uint64_t group_bound, uint32_t *hist, uint32_t *owner, uint32_t *nodes, uint8_t *ids,
+                    hipStream_t stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_b3_owner, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, goff, n, group_bound, owner);
+  (void)hipMemsetAsync(hist + kTailBins, 0, kTailBins * sizeof(uint32_t), stream);  // bin cursors
+  hipLaunchKernelGGL(k_b3_owner, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n,
+                     group_bound, (const uint32_t *)hist, hist + kTailBins, owner);
   hipLaunchKernelGGL(k_b3_leaves, dim3((unsigned)((group_bound + 255) / 256)), dim3(256), 0, stream, base, chunks,
                      goff, (const uint32_t *)owner, n, group_bound, nodes, ids);
   hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n, group_bound,
                      nodes, ids);
 }
+
+uint64_t b3_groups_total(uint64_t packed) { return (packed & 0xffffffffull) + (packed >> 32); }
 
 }  // namespace mcdc

@@ -142,3 +142,27 @@ def test_overlapping_and_repeated_chunks(ctx):
         ctx.device_free(dp)
     ref = O.chunk_ids(data, c, threads=8)
     assert (got == ref).all() and (again == ref).all()
+
+
+def test_many_tail_lengths_in_list_order(ctx):
+    """Thousands of chunks whose last 16-KiB groups have every block count,
+    listed out of offset order: the tail groups are counting-sorted across
+    many workgroups (per-block bin reservations), full groups come first,
+    and waves whose lanes have unequal loops still hash every lane exactly."""
+    rng = np.random.default_rng(SEED + 11)
+    lens = np.concatenate([rng.integers(0, 70_000, 5000), np.arange(0, 16385, 64), 16384 * rng.integers(1, 5, 200),
+                           np.array([0, 1, 63, 64, 65, 16383, 16385])]).astype(np.int64)
+    gaps = rng.integers(0, 16, lens.size)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1] + gaps[:-1]])) + gaps[0]
+    n = int(offs[-1] + lens[-1])
+    perm = rng.permutation(lens.size)
+    c = _chunks(list(zip(offs[perm].tolist(), lens[perm].tolist())))
+    data = O.random_bytes(n, SEED + 11)
+    dp = _device_bytes(ctx, data)
+    try:
+        got = ctx.chunk_ids(dp, n, c)
+    finally:
+        ctx.device_free(dp)
+    ref = O.chunk_ids(data, c, threads=8)
+    bad = np.nonzero(~(got == ref).all(axis=1))[0]
+    assert bad.size == 0, [(int(c["offset"][i]), int(c["length"][i])) for i in bad[:10]]

@@ -1,6 +1,8 @@
 """Chunk-ID (BLAKE3) kernel microbenchmark: chunk a device-resident random
 buffer once (P16), then time mcdc_chunk_ids_device over its boundary list.
-usage: python tools/b3bench.py [GiB] [reps]"""
+usage: python tools/b3bench.py [GiB] [reps]   (MCDC_LIBRARY selects a build;
+the digest of all IDs lets builds be compared)"""
+import hashlib
 import os
 import sys
 import time
@@ -26,5 +28,6 @@ with _lib.Context(0, n) as ctx:
         ts.append(time.perf_counter() - t0)
         dev = ctx.timing()["ids_ms"]
     best = min(ts)
-    print(f"chunks {k}  wall best {best*1e3:.3f} ms  device {dev:.3f} ms  {n/best/1e12:.3f} TB/s  "
+    dig = hashlib.sha256(ctx.d2h_bytes(d_ids, 32 * k).tobytes()).hexdigest()[:16]
+    print(f"{os.path.basename(_lib.LIB_PATH)}  ids {dig}  chunks {k}  wall best {best*1e3:.3f} ms  device {dev:.3f} ms  {n/best/1e12:.3f} TB/s  "
           f"{n/(dev*1e-3)/1e12:.3f} TB/s device", flush=True)
