@@ -67,7 +67,7 @@ def _dist():
 def _pmc_traffic():
     """Calibrated PMC read traffic of the scan (profiles/rNN/pmc_traffic.json, written from
     separate rocprofv3 --pmc FETCH_SIZE passes by tools/profile_round.sh): HBM bytes per input byte."""
-    for rnd in ("r03", "r02", "r01"):  # the latest round's measurement
+    for rnd in ("r02", "r02/part2", "r02/part1", "r01"):  # the latest measurement
         path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         try:
             with open(path) as f:
