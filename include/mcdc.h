@@ -211,6 +211,31 @@ int mcdc_open_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_
                      const mcdc_blob *sealed, size_t nblobs, void *d_out, size_t out_cap,
                      uint64_t *out_offsets, int32_t *status);
 
+/* ------------------------------------------------------------- dedup index
+ * Repository::save_blob stores a blob only when its ID is neither in the
+ * index nor already pending (/root/reference/src/repository/repository_v1.rs:
+ * 169-180: index.contains(&id) || !index.add_pending_blob(id)), so of equal
+ * IDs the first in processing order is encoded and packed and the others
+ * only referenced.  An mcdc_index is a device-resident set of the IDs stored
+ * or pending so far (sorted in HBM on the context's device); mcdc_index_add
+ * answers that check for a whole batch of chunk IDs at once and adds the new
+ * ones.  The index belongs to the device of the context that created it and is
+ * used through any context of that device (one call at a time). */
+struct mcdc_index;
+int mcdc_index_create(struct mcdc_ctx *ctx, struct mcdc_index **out);
+void mcdc_index_destroy(struct mcdc_index *ix);
+/* IDs held */
+size_t mcdc_index_size(const struct mcdc_index *ix);
+/* ids: n IDs (32 bytes each, processing order), host or device memory.
+ * is_new (optional, n bytes, host or device): 1 for every ID to store (not in
+ * the index, not equal to an earlier ID of the batch), else 0.
+ * chunks / new_chunks (optional, both or neither; n records each, host or
+ * device): the records of the new IDs, compacted in order — e.g. the boundary
+ * list whose chunks go on to be sealed.  *n_new (optional): their number.
+ * The new IDs are added to the index. */
+int mcdc_index_add(struct mcdc_ctx *ctx, struct mcdc_index *ix, const uint8_t *ids, size_t n,
+                   uint8_t *is_new, const mcdc_chunk *chunks, mcdc_chunk *new_chunks, size_t *n_new);
+
 /* ---------------------------------------------------------------- batching
  * Cross-worker batching front-end.  mapache chunks files on read_concurrency
  * rayon workers at once (/root/reference/src/archiver/mod.rs:162-215, default

@@ -36,6 +36,7 @@ EXPORTS = (
     "mcdc_host_free", "mcdc_memcpy_h2d", "mcdc_memcpy_d2h", "mcdc_fill_random_device", "mcdc_digest",
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
+    "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
 )
 
 
@@ -113,6 +114,12 @@ def load():
     L.mcdc_seal_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
     L.mcdc_open_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp]
     L.mcdc_seal_chunks_device.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
+    L.mcdc_index_create.argtypes = [vp, P(vp)]
+    L.mcdc_index_destroy.argtypes = [vp]
+    L.mcdc_index_destroy.restype = None
+    L.mcdc_index_size.argtypes = [vp]
+    L.mcdc_index_size.restype = sz
+    L.mcdc_index_add.argtypes = [vp, vp, vp, sz, vp, vp, vp, P(sz)]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -300,6 +307,14 @@ class Context:
                                            out.ctypes.data))
         return out[:count]
 
+    # ------------------------------------------------------- dedup index --
+    @_locked
+    def index_create(self) -> "Index":
+        """A device-resident dedup index on this context's device (mcdc_index_create)."""
+        h = ctypes.c_void_p()
+        check(load().mcdc_index_create(self._h, ctypes.byref(h)))
+        return Index(self, h.value)
+
     # ----------------------------------------------------------- sealing --
     @staticmethod
     def _extents(offsets, lengths) -> np.ndarray:
@@ -460,3 +475,61 @@ class Batcher:
 def digest(chunks: np.ndarray) -> int:
     a = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
     return int(load().mcdc_digest(ctypes.c_void_p(a.ctypes.data), a.size))
+
+
+class Index:
+    """mcdc_index: the IDs stored or pending so far (Repository::save_blob's
+    index.contains / add_pending_blob check, repository_v1.rs:169-180)."""
+
+    def __init__(self, ctx: "Context", h: int):
+        self._ctx, self._h = ctx, h
+
+    def close(self):
+        if self._h:
+            load().mcdc_index_destroy(ctypes.c_void_p(self._h))
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self) -> int:
+        return int(load().mcdc_index_size(ctypes.c_void_p(self._h)))
+
+    def add(self, ids, chunks=None, d_ids: int = None, n: int = None):
+        """Mark which IDs of a batch are new (mcdc_index_add) and add them.
+        ids: (n, 32) uint8 host array, or d_ids (device pointer) with n.
+        Returns is_new (n bools); with `chunks` (CHUNK_DTYPE, n records) also
+        the new chunks in order."""
+        if d_ids is None:
+            a = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 32)
+            iptr, n = a.ctypes.data, a.shape[0]
+        else:
+            a, iptr = None, d_ids
+        flags = np.zeros(max(n, 1), dtype=np.uint8)
+        nn = ctypes.c_size_t()
+        if chunks is not None:
+            c = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+            if c.size != n:
+                raise ValueError("one chunk record per ID")
+            out = np.zeros(max(n, 1), dtype=CHUNK_DTYPE)
+            cptr, optr = c.ctypes.data, out.ctypes.data
+        else:
+            c = out = None
+            cptr = optr = None
+        with self._ctx._lock:
+            check(load().mcdc_index_add(self._ctx._h, ctypes.c_void_p(self._h), ctypes.c_void_p(iptr), n,
+                                        flags.ctypes.data, ctypes.c_void_p(cptr), ctypes.c_void_p(optr),
+                                        ctypes.byref(nn)))
+        is_new = flags[:n].astype(bool)
+        if chunks is None:
+            return is_new
+        return is_new, out[:nn.value]

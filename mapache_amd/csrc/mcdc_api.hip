@@ -26,6 +26,7 @@
 #include "gear_table.h"
 #include "mcdc_aead.h"
 #include "mcdc_blake3.h"
+#include "mcdc_index.h"
 #include "mcdc_internal.h"
 
 using namespace mcdc;
@@ -1206,6 +1207,105 @@ int mcdc_seal_chunks_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_
 int mcdc_open_device(mcdc_ctx *ctx, const uint8_t key[32], const void *d_in, size_t n_in, const mcdc_blob *sealed,
                      size_t nblobs, void *d_out, size_t out_cap, uint64_t *out_offsets, int32_t *status) {
   return aead_run(ctx, 1, key, d_in, n_in, sealed, nblobs, nullptr, d_out, out_cap, out_offsets, status);
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ dedup index --
+// The blob-exists check of Repository::save_blob for a batch
+// (/root/reference/src/repository/repository_v1.rs:169-180), csrc/mcdc_index.hip.
+struct mcdc_index {
+  int device = 0;
+  DevBuf pfx[2], ids[2];  // sorted by prefix; [cur] is live, the other is the merge target
+  int cur = 0;
+  uint64_t size = 0;
+  // per-call scratch
+  DevBuf keys, skeys, pos, spos, sflag, is_new, count, tmp, ids_in, chunks_in, chunks_out;
+};
+
+extern "C" {
+
+int mcdc_index_create(mcdc_ctx *ctx, mcdc_index **out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out) return fail(MCDC_E_INVALID, "NULL argument");
+  *out = new (std::nothrow) mcdc_index;
+  if (!*out) return fail(MCDC_E_NOMEM, "out of host memory");
+  (*out)->device = ctx->device;
+  return MCDC_OK;
+}
+
+void mcdc_index_destroy(mcdc_index *ix) {
+  if (!ix) return;
+  (void)hipSetDevice(ix->device);
+  DevBuf *bufs[] = {&ix->pfx[0], &ix->pfx[1], &ix->ids[0], &ix->ids[1], &ix->keys, &ix->skeys, &ix->pos,
+                    &ix->spos, &ix->sflag, &ix->is_new, &ix->count, &ix->tmp, &ix->ids_in, &ix->chunks_in,
+                    &ix->chunks_out};
+  for (DevBuf *b : bufs)
+    if (b->p) (void)hipFree(b->p);
+  delete ix;
+}
+
+size_t mcdc_index_size(const mcdc_index *ix) { return ix ? (size_t)ix->size : 0; }
+
+int mcdc_index_add(mcdc_ctx *ctx, mcdc_index *ix, const uint8_t *ids, size_t n, uint8_t *is_new,
+                   const mcdc_chunk *chunks, mcdc_chunk *new_chunks, size_t *n_new) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!ix || (n && !ids) || (!chunks != !new_chunks)) return fail(MCDC_E_INVALID, "NULL argument");
+  if (ix->device != ctx->device) return fail(MCDC_E_INVALID, "the index lives on device %d", ix->device);
+  if (n >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many IDs (%zu)", n);
+  const double t0 = now_ms();
+  hipStream_t st = ctx->stream;
+  ctx->timing = mcdc_timing{};
+  if (n_new) *n_new = 0;
+  if (n == 0) {
+    ctx->timing.total_ms = now_ms() - t0;
+    return MCDC_OK;
+  }
+  const size_t tmpb = idx_tmp_bytes(n);
+  if ((rc = stage_arg(ctx, ix->ids_in, ids, n * 32)) || (rc = ensure(ctx, ix->keys, n * 8)) ||
+      (rc = ensure(ctx, ix->skeys, n * 8)) || (rc = ensure(ctx, ix->pos, n * 4)) || (rc = ensure(ctx, ix->spos, n * 4)) ||
+      (rc = ensure(ctx, ix->sflag, n)) || (rc = ensure(ctx, ix->is_new, n)) || (rc = ensure(ctx, ix->count, 16)) ||
+      (rc = ensure(ctx, ix->tmp, tmpb)))
+    return rc;
+  const uint8_t *d_ids = (const uint8_t *)ix->ids_in.p;
+  IdxScratch sc{(uint64_t *)ix->keys.p, (uint64_t *)ix->skeys.p, (uint32_t *)ix->pos.p, (uint32_t *)ix->spos.p,
+                (uint8_t *)ix->sflag.p, (uint64_t *)ix->count.p, ix->tmp.p, tmpb};
+  IdxIndexView view{(const uint64_t *)ix->pfx[ix->cur].p, (const uint8_t *)ix->ids[ix->cur].p, ix->size};
+  HIP_TRY(hipEventRecord(ctx->ev_start, st));
+  launch_idx_mark(d_ids, n, view, sc, (uint8_t *)ix->is_new.p, st);
+  HIP_TRY(hipGetLastError());
+  uint64_t m = 0;
+  HIP_TRY(hipMemcpyAsync(&m, sc.count, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int nxt = ix->cur ^ 1;
+  if ((rc = ensure(ctx, ix->pfx[nxt], (ix->size + m) * 8)) || (rc = ensure(ctx, ix->ids[nxt], (ix->size + m) * 32)))
+    return rc;
+  launch_idx_merge(d_ids, m, view, sc, (uint64_t *)ix->pfx[nxt].p, (uint8_t *)ix->ids[nxt].p, st);
+  HIP_TRY(hipGetLastError());
+  if (chunks) {
+    if ((rc = stage_arg(ctx, ix->chunks_in, chunks, n * sizeof(mcdc_chunk))) ||
+        (rc = ensure(ctx, ix->chunks_out, n * sizeof(mcdc_chunk))))
+      return rc;
+    launch_idx_compact_chunks((const DevChunk *)ix->chunks_in.p, (const uint8_t *)ix->is_new.p, n,
+                              (DevChunk *)ix->chunks_out.p, sc.count + 1, sc.tmp, tmpb, st);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(ctx->ev_end, st));
+  if ((rc = give_back(ctx, is_new, ix->is_new.p, n)) ||
+      (chunks && (rc = give_back(ctx, new_chunks, ix->chunks_out.p, m * sizeof(mcdc_chunk)))))
+    return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  ix->cur = nxt;
+  ix->size += m;
+  if (n_new) *n_new = (size_t)m;
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_end));
+  ctx->timing.device_ms = ms;
+  ctx->timing.chunks = n;
+  ctx->timing.total_ms = now_ms() - t0;
+  return MCDC_OK;
 }
 
 // ------------------------------------------------------------ batcher --

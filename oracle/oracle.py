@@ -453,3 +453,28 @@ def seal_blobs(key, data, offsets, lengths, nonces, threads: int = 1):
     lib().oa_seal_blobs(_bytes(key), ptr, off.ctypes.data, ln.ctypes.data, len(off), nz.ctypes.data,
                         out.ctypes.data, out_off.ctypes.data, threads)
     return out[: int(out_off[-1])], out_off[:-1]
+
+
+# ------------------------------------------------------------ dedup index --
+class DedupIndex:
+    """Restates the blob-exists check of Repository::save_blob
+    (/root/reference/src/repository/repository_v1.rs:169-180):
+        blob_exists = index.contains(&id) || !index.add_pending_blob(id)
+    in processing order: an ID is stored (new) the first time it is seen,
+    within a batch and across batches; later equal IDs are only referenced."""
+
+    def __init__(self):
+        self.seen = set()
+
+    def __len__(self):
+        return len(self.seen)
+
+    def add(self, ids) -> np.ndarray:
+        a = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 32)
+        out = np.zeros(a.shape[0], dtype=bool)
+        for i in range(a.shape[0]):
+            k = a[i].tobytes()
+            if k not in self.seen:
+                self.seen.add(k)
+                out[i] = True
+        return out
