@@ -339,6 +339,33 @@ def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_s
                                   "peak engine clock"},
              "chunk_plus_ids_ms": round(dt2 * 1e3, 3), "chunk_plus_ids_gib_s": round(n / dt2 / GIB, 2),
              "parity_probe_chunks": int(len(sel)), "parity_probe_ok": ok}
+        # dedup index (save_blob's index check, repository_v1.rs:169-180) over these IDs in HBM:
+        # into an empty index (all new) and again into the populated one (all duplicates)
+        try:
+            k = ctx.chunk_device_to_device(p, dp, n, d_out, cap)
+            ctx.chunk_ids(dp, n, (d_out, k), ids=d_ids)
+
+            def fresh():
+                with ctx.index_create() as ix:
+                    f = ix.add(None, d_ids=d_ids, n=k)
+                    return f, len(ix)
+            dtf, (ff, size) = _timed(fresh, steps, 1)
+            with ctx.index_create() as ix:
+                ix.add(None, d_ids=d_ids, n=k)
+                dtd, fd = _timed(lambda: ix.add(None, d_ids=d_ids, n=k), steps, 1)
+            idh = ctx.d2h_bytes(d_ids, 32 * k).reshape(k, 32)
+            t0 = time.perf_counter()
+            ref = O.DedupIndex().add(idh)
+            cdt = time.perf_counter() - t0
+            r["dedup"] = {"ids": int(k), "new_ms_per_step": round(dtf * 1e3, 3),
+                          "dup_ms_per_step": round(dtd * 1e3, 3), "new_ids_per_s": round(k / dtf),
+                          "parity_ok": bool(ff.all() and size == k and not fd.any() and (ff == ref).all()),
+                          "note": "mcdc_index_add of the headline's chunk IDs (device-resident): a fresh index "
+                                  "per step (all new), then the same IDs into the populated index (all seen)",
+                          "cpu_baseline": {"value": round(k / cdt), "unit": "IDs/s", "cores": 1, "kind": "port",
+                                           "sample": "oracle.DedupIndex (Python set) over the same IDs"}}
+        except Exception as ex:  # reported, never silently dropped
+            r["dedup"] = {"error": f"{type(ex).__name__}: {ex}"}
         if not no_cpu:
             m = int(cpu_sample_gib * GIB)
             sample = chunks[chunks["offset"] + chunks["length"] <= m]
