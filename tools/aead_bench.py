@@ -1,6 +1,8 @@
 """Seal/open microbenchmark (iteration tool; bench.py's `seal` leg is the
 reported one): the chunks of an N-GiB device stream as blobs, K timed calls
 each, per-call device time from the library's events."""
+import hashlib
+import os
 import sys
 import time
 
@@ -33,6 +35,9 @@ for name, fn in (("seal", lambda: ctx.seal(key, dp, n, ch["offset"], ch["length"
         fn()
         dev.append(ctx.timing()["aead_ms"])
     dt = (time.perf_counter() - t0) / steps
-    print(f"{name}: {k} blobs, {dt * 1e3:.2f} ms/call ({n / dt / 2**30:.1f} GiB/s), kernels {np.median(dev):.2f} ms",
+    dig = ""
+    if name == "seal":  # digest of a 256 MiB sample of the sealed output (compares builds)
+        dig = hashlib.sha256(ctx.d2h_bytes(ds, min(int(oo[-1]), 256 << 20)).tobytes()).hexdigest()[:16]
+    print(f"{os.path.basename(_lib.LIB_PATH)} {dig} {name}: {k} blobs, {dt * 1e3:.2f} ms/call ({n / dt / 2**30:.1f} GiB/s), kernels {np.median(dev):.2f} ms",
           flush=True)
 ctx.close()
