@@ -138,11 +138,25 @@ __device__ __forceinline__ uint4 aes256(const uint32_t *tl, const uint32_t *rk, 
 // banks are (addr / 4) mod 32, so the 32 lanes of a half hit 32 banks.
 // v_bitop3_b32 merges three terms per instruction.  ~500 VALU + 224 LDS reads
 // per block (the 32-replica version above: ~850 VALU).
+//
+// MCDC_AES_2T (default): ds_read_b32 serves 32-lane groups with banks
+// (a / 4) mod 32 (MI355X_MICROARCH.md, LDS table), so 32 replicas are
+// conflict-free too, and the same 64 KiB hold two tables: row x = Te0[x] for
+// lanes l mod 32 at 4 l, then Te2[x] = rotl16(Te0[x]) at 128 + 4 l.  A column
+// T0(a) ^ rotl8 T0(b) ^ rotl16 T0(c) ^ rotl24 T0(d) ^ k is then
+// [T0(a) ^ T2(c) ^ k] ^ rotl8[T0(b) ^ T2(d)]: one rotate instead of three
+// (8 VALU per column with the four address perms instead of 9).
+#ifndef MCDC_AES_2T
+#define MCDC_AES_2T 1
+#endif
 constexpr int kRepP = 64;
 constexpr int kTabPWords = 256 * kRepP;
 
 __device__ __forceinline__ void fill_table_p(uint32_t *tt) {
-  for (int k = threadIdx.x; k < kTabPWords; k += blockDim.x) tt[k] = kDevTab.te0[k / kRepP];
+  for (int k = threadIdx.x; k < kTabPWords; k += blockDim.x) {
+    const uint32_t t = kDevTab.te0[k / kRepP];
+    tt[k] = (MCDC_AES_2T && (k & 32)) ? __builtin_amdgcn_alignbit(t, t, 16) : t;
+  }
   __syncthreads();
 }
 
@@ -175,10 +189,16 @@ __device__ __forceinline__ void aes256p(const uint8_t *tb, uint32_t lane4, const
 #pragma unroll
     for (int j = 0; j < N; ++j) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c) {
+#if MCDC_AES_2T
+        const uint32_t w = tp<1>(tb, a[j][(c + 1) & 3], lane4) ^ tp<3>(tb, a[j][(c + 3) & 3], lane4 | 128u);
+        b[j][c] = xor3(tp<0>(tb, a[j][c], lane4), tp<2>(tb, a[j][(c + 2) & 3], lane4 | 128u), rk[4 * r + c]) ^ rl8(w);
+#else
         b[j][c] = xor3(xor3(tp<0>(tb, a[j][c], lane4), rl8(tp<1>(tb, a[j][(c + 1) & 3], lane4)),
                             rl16(tp<2>(tb, a[j][(c + 2) & 3], lane4))),
                        rl24(tp<3>(tb, a[j][(c + 3) & 3], lane4)), rk[4 * r + c]);
+#endif
+      }
     }
 #pragma unroll
     for (int j = 0; j < N; ++j)
@@ -680,7 +700,7 @@ __global__ __launch_bounds__(64 * kCtrWaves) void k_aead_ctr(int open, const Aea
   uint32_t tile = (MCDC_AEAD_PERSIST & 2) ? next_tile(ctr) : blockIdx.x * kCtrWaves + rfl(threadIdx.x >> 6);
   for (;;) {
     if (tile >= ntiles) break;
-    ctr_tile(open, rec, keys, owner, tb, lane, 4 * lane, tile);
+    ctr_tile(open, rec, keys, owner, tb, lane, MCDC_AES_2T ? 4 * (lane & 31) : 4 * lane, tile);
     if (!(MCDC_AEAD_PERSIST & 2)) break;
     tile = next_tile(ctr);
   }
