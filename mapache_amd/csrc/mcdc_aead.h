@@ -31,6 +31,7 @@ struct AeadKeys {
   uint32_t h[4];       // message-authentication key H
   uint32_t h4096[4];   // H^4096 (dot powers): tile combination
   uint32_t w[64][4];   // w[i] = H^(64 - i); w[0] = H^64 steps the row Horner
+  uint32_t bas[128][4];  // bas[j] = dot(x^j, w[0]) = x^j G x^-128: basis of the row step's nibble tables
 };
 
 // AES-256 key schedule on the host: 60 little-endian words (FIPS-197 §5.2 bytes).

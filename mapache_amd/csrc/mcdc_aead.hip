@@ -78,6 +78,9 @@ __constant__ Tables kDevTab = make_tables();
 #ifndef MCDC_CTR_WAVES
 #define MCDC_CTR_WAVES 12
 #endif
+#ifndef MCDC_PV_NIB  // POLYVAL row step from 32 nibble tables (1) or one byte table with x^-8 steps (0)
+#define MCDC_PV_NIB 1
+#endif
 #ifndef MCDC_AEAD_PERSIST  // bit 0: k_aead_polyval, bit 1: k_aead_ctr draw tiles from a counter (A/B: tools/dbg/build_persist_ab.sh)
 #define MCDC_AEAD_PERSIST 3
 #endif
@@ -461,6 +464,16 @@ __global__ __launch_bounds__(256) void k_aead_prep(int open, AeadMaster mk, cons
     w = dotb(w, H);
     *reinterpret_cast<uint4 *>(K.w[j]) = w;
   }
+#if MCDC_PV_NIB
+  {  // the row step U -> dot(U, G) is linear: its images of x^j, j = 0..127
+    uint4 b = dotb(w, make_uint4(1, 0, 0, 0));  // G x^-128
+    *reinterpret_cast<uint4 *>(K.bas[0]) = b;
+    for (int j = 1; j < 128; ++j) {
+      b = mulx(b);
+      *reinterpret_cast<uint4 *>(K.bas[j]) = b;
+    }
+  }
+#endif
   for (int j = 0; j < 6; ++j) w = dotb(w, w);  // (H^64)^64
   *reinterpret_cast<uint4 *>(K.h4096) = w;
 }
@@ -485,10 +498,62 @@ __device__ __forceinline__ uint32_t next_tile(uint32_t *ctr) {
   return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
 }
 
+// dot(y, G) = XOR over the 32 nibbles k of y of T_k[nibble], T_k[e] =
+// sum over the set bits i of e of bas[4 k + i] (AeadKeys::bas): 32 conflict-
+// free ds_read_b128 (a table's 16 entries cover the 64 banks once; lanes
+// reading one entry broadcast) and no shifts or reductions — the byte-table
+// form (m8mul) spent ~385 VALU per block on its x^-8 steps and read a 4 KiB
+// table at random (60 % of its LDS cycles bank conflicts).
+typedef uint32_t pv_u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(3))) pv_u32x4 *lds_u4;
+
+__device__ __forceinline__ uint4 nibmul(const uint4 *T, uint4 y) {
+  // the tables' LDS address (the low 32 bits of the generic pointer) is a
+  // multiple of 8 KiB, so a lookup's address is one v_and_or of the shifted
+  // word; the table number goes into the ds_read offset
+  const uint32_t lb = (uint32_t)reinterpret_cast<uintptr_t>(T);
+  const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t ka = 8 * d + j, kb = ka + 1;
+      const uint32_t oa = ((j == 0 ? yw[d] << 4 : yw[d] >> (4 * j - 4)) & 0xf0u) | lb;
+      const uint32_t ob = ((yw[d] >> (4 * j)) & 0xf0u) | lb;
+      const pv_u32x4 a = *reinterpret_cast<lds_u4>((uintptr_t)(oa + 256 * ka));
+      const pv_u32x4 b = *reinterpret_cast<lds_u4>((uintptr_t)(ob + 256 * kb));
+      z0 = xor3(z0, a.x, b.x);
+      z1 = xor3(z1, a.y, b.y);
+      z2 = xor3(z2, a.z, b.z);
+      z3 = xor3(z3, a.w, b.w);
+    }
+  }
+  return make_uint4(z0, z1, z2, z3);
+}
+
 // One POLYVAL tile: its sum, exponents relative to its end.
 __device__ __forceinline__ void polyval_tile(const AeadRec *__restrict__ rec, const AeadKeys *__restrict__ keys,
                                              uint4 *M, uint32_t lane, uint32_t i, uint32_t t, uint32_t tile,
                                              uint4 *__restrict__ tsum) {
+#if MCDC_PV_NIB
+  {  // the 32 nibble tables: lane builds entries 8 (lane & 1) .. + 8 of table lane >> 1
+    const uint32_t k = lane >> 1;
+    const uint4 *bs = reinterpret_cast<const uint4 *>(keys[i].bas[4 * k]);
+    const uint4 b0 = bs[0], b1 = bs[1], b2 = bs[2], b3 = bs[3];
+    const uint4 hi = (lane & 1) ? b3 : make_uint4(0, 0, 0, 0);
+    wave_sync();  // the previous tile's reads of the tables are done
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      uint4 v = hi;
+      if (e & 1) v = u4xor(v, b0);
+      if (e & 2) v = u4xor(v, b1);
+      if (e & 4) v = u4xor(v, b2);
+      M[16 * k + 8 * (lane & 1) + e] = v;
+    }
+    wave_sync();
+  }
+#else
   {  // M[b] = b(x) G, G = H^64: lane builds entries lane + 64 q
     uint4 base[8];
     base[0] = *reinterpret_cast<const uint4 *>(keys[i].w[0]);
@@ -508,6 +573,7 @@ __device__ __forceinline__ void polyval_tile(const AeadRec *__restrict__ rec, co
     }
     wave_sync();
   }
+#endif
   const AeadRec &R = rec[i];
   const uint64_t s = R.len, nblk = (s + 15) / 16, V = (nblk + 63) / 64 * 64, rows_all = V / 64;
   const uint64_t rows0 = rows_all - (uint64_t)kAeadRows * (R.ptiles - 1);
@@ -516,14 +582,18 @@ __device__ __forceinline__ void polyval_tile(const AeadRec *__restrict__ rec, co
   const uint64_t pad = V - nblk;
   const uint64_t lo = R.pv, hi = R.pv + s;
   const uint64_t a0 = R.pv - 16 * pad + 16 * (vstart + lane);  // (virtual block v at pv + 16 (v - pad))
-  const uint32_t e = (uint32_t)(R.pv & 15);
+  const uint32_t e = rfl((uint32_t)(R.pv & 15));  // (wave-uniform: scalar branches in load16)
   uint4 U = make_uint4(0, 0, 0, 0);
   uint4 X = load16(a0, lo, hi, e);
 #pragma unroll 1
   for (uint32_t r = 0; r < rows; ++r) {
     const uint4 Xc = X;
     if (r + 1 < rows) X = load16(a0 + 1024ull * (r + 1), lo, hi, e);
+#if MCDC_PV_NIB
+    U = u4xor(nibmul(M, U), Xc);  // U <- U G + X
+#else
     U = u4xor(m8mul(M, U), Xc);  // U <- U G + X
+#endif
   }
   U = dotb(U, *reinterpret_cast<const uint4 *>(keys[i].w[lane]));  // lane l's last block sits 64 - l from the end
 #pragma unroll
@@ -537,11 +607,15 @@ __device__ __forceinline__ void polyval_tile(const AeadRec *__restrict__ rec, co
 }
 
 // Persistent waves over the tiles; a tile past a blob's POLYVAL tiles is skipped.
+constexpr int kPvTab = MCDC_PV_NIB ? 512 : 256;  // uint4 per wave: 32 nibble tables of 16 (8 KiB) / 256 bytes
 __global__ __launch_bounds__(256) void k_aead_polyval(const AeadRec *__restrict__ rec,
                                                       const AeadKeys *__restrict__ keys,
                                                       const uint32_t *__restrict__ owner, uint64_t ntiles,
                                                       uint4 *__restrict__ tsum, uint32_t *ctr) {
-  __shared__ uint4 mt[4][256];
+  __shared__ __attribute__((aligned(256))) uint4 mt[4][kPvTab];  // (nibmul ORs offsets into the base)
+#if MCDC_PV_NIB
+  MCDC_VGPR_PAD(104);  // 104 used: not an exact fill (MCDC_VGPR_PAD)
+#endif
   const uint32_t wv = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint32_t tile = (MCDC_AEAD_PERSIST & 1) ? next_tile(ctr) : blockIdx.x * 4 + wv;
   for (;;) {
@@ -769,14 +843,14 @@ void launch_aead_sizes(int open, const uint64_t *ext, uint64_t n, uint64_t n_in,
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, tcnt, toff, (int)n + 1, stream);
 }
 
-// Persistent grids: as many blocks as fit at once (k_aead_polyval: 16 KiB LDS,
-// 4 waves -> 8 per CU; k_aead_ctr: 64 KiB LDS -> 2 per CU), never more than
+// Persistent grids: as many blocks as fit at once (k_aead_polyval: 32 KiB LDS,
+// 4 waves -> 5 per CU; k_aead_ctr: 64 KiB LDS -> 2 per CU), never more than
 // there are tiles; ctr[0], ctr[1]: the two launches' tile counters.
 static void launch_tiles(int open, const AeadRec *rec, const AeadKeys *keys, const uint32_t *owner, uint64_t ntiles,
                          uint4 *tsum, uint32_t *ctr, int num_cus, bool polyval, hipStream_t stream) {
   if (!ntiles) return;
   if (polyval) {
-    const uint64_t nb = (MCDC_AEAD_PERSIST & 1) ? std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)num_cus * 8)
+    const uint64_t nb = (MCDC_AEAD_PERSIST & 1) ? std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)num_cus * (160 / (4 * kPvTab * 16 / 1024)))
                                                 : (ntiles + 3) / 4;
     hipLaunchKernelGGL(k_aead_polyval, dim3((unsigned)nb), dim3(256), 0, stream, rec, keys, owner, ntiles, tsum, ctr);
   } else {
