@@ -504,31 +504,57 @@ __device__ __forceinline__ uint32_t next_tile(uint32_t *ctr) {
 // reading one entry broadcast) and no shifts or reductions — the byte-table
 // form (m8mul) spent ~385 VALU per block on its x^-8 steps and read a 4 KiB
 // table at random (60 % of its LDS cycles bank conflicts).
+// (nibble at bit S) << 4 | lb in two VALU ops (v_bfe_u32 + v_lshl_or_b32;
+// the compiler's own form of the same expression took 2.6)
+template <int S>
+__device__ __forceinline__ uint32_t nib_addr(uint32_t w, uint32_t lb) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, %2, 4\n\tv_lshl_or_b32 %0, %0, 4, %3" : "=&v"(r) : "v"(w), "i"(S), "v"(lb));
+  return r;
+}
+
 typedef uint32_t pv_u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(3))) pv_u32x4 *lds_u4;
+typedef const __attribute__((address_space(1))) pv_u32x4 *glb_u4;
+
+// 16 bytes at a 16-byte aligned global address (one global_load_dwordx4)
+__device__ __forceinline__ uint4 gld16(uint64_t a) {
+  const pv_u32x4 v = *reinterpret_cast<glb_u4>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// two nibbles (J, J + 1) of word w, tables 8 D + J and 8 D + J + 1
+template <int D, int J>
+__device__ __forceinline__ void nib2(uint32_t w, uint32_t lb, uint32_t &z0, uint32_t &z1, uint32_t &z2,
+                                     uint32_t &z3) {
+  const uint32_t oa = nib_addr<4 * J>(w, lb), ob = nib_addr<4 * J + 4>(w, lb);
+  const pv_u32x4 a = *reinterpret_cast<lds_u4>((uintptr_t)(oa + 256 * (8 * D + J)));
+  const pv_u32x4 b = *reinterpret_cast<lds_u4>((uintptr_t)(ob + 256 * (8 * D + J + 1)));
+  z0 = xor3(z0, a.x, b.x);
+  z1 = xor3(z1, a.y, b.y);
+  z2 = xor3(z2, a.z, b.z);
+  z3 = xor3(z3, a.w, b.w);
+}
+
+template <int D>
+__device__ __forceinline__ void nibword(uint32_t w, uint32_t lb, uint32_t &z0, uint32_t &z1, uint32_t &z2,
+                                        uint32_t &z3) {
+  nib2<D, 0>(w, lb, z0, z1, z2, z3);
+  nib2<D, 2>(w, lb, z0, z1, z2, z3);
+  nib2<D, 4>(w, lb, z0, z1, z2, z3);
+  nib2<D, 6>(w, lb, z0, z1, z2, z3);
+}
 
 __device__ __forceinline__ uint4 nibmul(const uint4 *T, uint4 y) {
   // the tables' LDS address (the low 32 bits of the generic pointer) is a
-  // multiple of 8 KiB, so a lookup's address is one v_and_or of the shifted
-  // word; the table number goes into the ds_read offset
+  // multiple of 8 KiB, so a lookup's address is the nibble ORed into it; the
+  // table number goes into the ds_read offset
   const uint32_t lb = (uint32_t)reinterpret_cast<uintptr_t>(T);
-  const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
   uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const uint32_t ka = 8 * d + j, kb = ka + 1;
-      const uint32_t oa = ((j == 0 ? yw[d] << 4 : yw[d] >> (4 * j - 4)) & 0xf0u) | lb;
-      const uint32_t ob = ((yw[d] >> (4 * j)) & 0xf0u) | lb;
-      const pv_u32x4 a = *reinterpret_cast<lds_u4>((uintptr_t)(oa + 256 * ka));
-      const pv_u32x4 b = *reinterpret_cast<lds_u4>((uintptr_t)(ob + 256 * kb));
-      z0 = xor3(z0, a.x, b.x);
-      z1 = xor3(z1, a.y, b.y);
-      z2 = xor3(z2, a.z, b.z);
-      z3 = xor3(z3, a.w, b.w);
-    }
-  }
+  nibword<0>(y.x, lb, z0, z1, z2, z3);
+  nibword<1>(y.y, lb, z0, z1, z2, z3);
+  nibword<2>(y.z, lb, z0, z1, z2, z3);
+  nibword<3>(y.w, lb, z0, z1, z2, z3);
   return make_uint4(z0, z1, z2, z3);
 }
 
@@ -585,10 +611,24 @@ __device__ __forceinline__ void polyval_tile(const AeadRec *__restrict__ rec, co
   const uint32_t e = rfl((uint32_t)(R.pv & 15));  // (wave-uniform: scalar branches in load16)
   uint4 U = make_uint4(0, 0, 0, 0);
   uint4 X = load16(a0, lo, hi, e);
+  // a row whose 1 KiB lies inside [lo, hi) needs no per-lane bounds (wave-uniform test)
+  const uint64_t rb = ((uint64_t)rfl((uint32_t)((a0 - 16 * lane) >> 32)) << 32) | rfl((uint32_t)(a0 - 16 * lane));
+  const uint64_t lo_u = ((uint64_t)rfl((uint32_t)(lo >> 32)) << 32) | rfl((uint32_t)lo);
+  const uint64_t hi_u = ((uint64_t)rfl((uint32_t)(hi >> 32)) << 32) | rfl((uint32_t)hi);
 #pragma unroll 1
   for (uint32_t r = 0; r < rows; ++r) {
     const uint4 Xc = X;
-    if (r + 1 < rows) X = load16(a0 + 1024ull * (r + 1), lo, hi, e);
+    if (r + 1 < rows) {
+      const uint64_t ra = rb + 1024ull * (r + 1);
+      if (ra >= lo_u && ra + 1024 <= hi_u) {
+        const uint64_t q = a0 + 1024ull * (r + 1) - e;
+        const uint4 l0 = gld16(q);
+        const uint4 l1 = e ? gld16(q + 16) : make_uint4(0, 0, 0, 0);
+        X = shift16(l0, l1, e);
+      } else {
+        X = load16(a0 + 1024ull * (r + 1), lo, hi, e);
+      }
+    }
 #if MCDC_PV_NIB
     U = u4xor(nibmul(M, U), Xc);  // U <- U G + X
 #else

@@ -8,7 +8,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mapache_amd import _lib  # noqa: E402
 
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 64
