@@ -346,9 +346,14 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
   return (w >> (8 * (k & 3))) & 0xffu;
 }
 
+// POLYVAL tiles: the last ones hold kAeadRows rows each, the first the rest;
+// a first tile under half that joins the next (up to 1.5 x kAeadRows rows):
+// every tile ends with one per-lane H^(64 - l) multiply (~1.5 K VALU per lane)
+// and a wave reduction, which cost as much as ~11 rows' lookups.
 __device__ __forceinline__ uint64_t ptiles_of(uint64_t s) {
   const uint64_t nblk = (s + 15) / 16, rows = (nblk + 63) / 64;
-  return (rows + kAeadRows - 1) / kAeadRows;
+  const uint64_t pt = (rows + kAeadRows - 1) / kAeadRows;
+  return pt > 1 && rows - kAeadRows * (pt - 1) < kAeadRows / 2 ? pt - 1 : pt;
 }
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
