@@ -504,6 +504,15 @@ class Index:
     def __len__(self) -> int:
         return int(load().mcdc_index_size(ctypes.c_void_p(self._h)))
 
+    def add_device(self, d_ids: int, n: int, d_chunks: int, d_new: int) -> int:
+        """Device-resident form: IDs and chunk records in HBM, the new chunks
+        compacted into d_new (HBM); returns their number (no flags copied back)."""
+        nn = ctypes.c_size_t()
+        with self._ctx._lock:
+            check(load().mcdc_index_add(self._ctx._h, ctypes.c_void_p(self._h), ctypes.c_void_p(d_ids), n, None,
+                                        ctypes.c_void_p(d_chunks), ctypes.c_void_p(d_new), ctypes.byref(nn)))
+        return nn.value
+
     def add(self, ids, chunks=None, d_ids: int = None, n: int = None):
         """Mark which IDs of a batch are new (mcdc_index_add) and add them.
         ids: (n, 32) uint8 host array, or d_ids (device pointer) with n.
