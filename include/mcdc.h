@@ -211,6 +211,27 @@ int mcdc_open_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_
                      const mcdc_blob *sealed, size_t nblobs, void *d_out, size_t out_cap,
                      uint64_t *out_offsets, int32_t *status);
 
+/* SecureStorage::encode / decode for many blobs held in host memory
+ * (storage.rs:61-69): zstd (level 3, window log 20 = log2(AVG_CHUNK_SIZE), no
+ * checksum: :31, :74-84) on host threads with the system libzstd.so.1, then
+ * encrypt_with_key on the GPU (as mcdc_seal_device); decode = decrypt on the
+ * GPU, then zstd decompression with window_log_max 20 (:87-94).
+ * encode: blob i = h_in[blobs[i].offset, + length); result i = nonce ||
+ * AES-256-GCM-SIV(zstd(blob i)) || tag, packed back to back into h_out in
+ * blob order; out_offsets (optional, nblobs + 1): offsets and total.
+ * decode: sealed extents of h_in -> the original blobs packed into h_out;
+ * status (optional): 0, -1 (authentication failed) or -2 (not a zstd frame
+ * within the window); any failure -> MCDC_E_AUTH.  Too small an out_cap ->
+ * MCDC_E_CAPACITY (out_offsets still filled).  The compressed bytes depend on
+ * the libzstd version; decoding is what is compatible.  No libzstd.so.1 ->
+ * MCDC_E_INTERNAL. */
+int mcdc_encode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, size_t n_in,
+                      const mcdc_blob *blobs, size_t nblobs, const uint8_t *nonces, void *h_out,
+                      size_t out_cap, uint64_t *out_offsets);
+int mcdc_decode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, size_t n_in,
+                      const mcdc_blob *sealed, size_t nblobs, void *h_out, size_t out_cap,
+                      uint64_t *out_offsets, int32_t *status);
+
 /* ------------------------------------------------------------- dedup index
  * Repository::save_blob stores a blob only when its ID is neither in the
  * index nor already pending (/root/reference/src/repository/repository_v1.rs:

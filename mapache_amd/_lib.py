@@ -37,6 +37,7 @@ EXPORTS = (
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
+    "mcdc_encode_blobs", "mcdc_decode_blobs",
 )
 
 
@@ -120,6 +121,8 @@ def load():
     L.mcdc_index_size.argtypes = [vp]
     L.mcdc_index_size.restype = sz
     L.mcdc_index_add.argtypes = [vp, vp, vp, sz, vp, vp, vp, P(sz)]
+    L.mcdc_encode_blobs.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
+    L.mcdc_decode_blobs.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -306,6 +309,45 @@ class Context:
         check(load().mcdc_chunk_ids_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(cptr), count,
                                            out.ctypes.data))
         return out[:count]
+
+    # ------------------------------------------- SecureStorage encode/decode --
+    @_locked
+    def encode_blobs(self, key, data, offsets, lengths, nonces):
+        """SecureStorage::encode of every blob data[offsets[i], +lengths[i]) (host
+        bytes): zstd on host threads, AES-256-GCM-SIV on the GPU
+        (mcdc_encode_blobs).  Returns (packed bytes, nblobs + 1 offsets)."""
+        a = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        ext = self._extents(offsets, lengths)
+        nz = np.ascontiguousarray(nonces, dtype=np.uint8).reshape(-1)
+        if nz.size != NONCE_BYTES * len(ext):
+            raise ValueError("need 12 nonce bytes per blob")
+        oo = np.zeros(len(ext) + 1, dtype=np.uint64)
+        cap = int(a.size + (a.size >> 7) + 64 * len(ext) + 64)  # zstd's bound + 28 per blob
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        rc = load().mcdc_encode_blobs(self._h, self._key(key), a.ctypes.data, a.size, ext.ctypes.data, len(ext),
+                                      nz.ctypes.data, out.ctypes.data, cap, oo.ctypes.data)
+        if rc == MCDC_E_CAPACITY:
+            out = np.empty(int(oo[-1]), dtype=np.uint8)
+            rc = load().mcdc_encode_blobs(self._h, self._key(key), a.ctypes.data, a.size, ext.ctypes.data,
+                                          len(ext), nz.ctypes.data, out.ctypes.data, out.size, oo.ctypes.data)
+        check(rc)
+        return out[:int(oo[-1])], oo
+
+    @_locked
+    def decode_blobs(self, key, data, offsets, lengths, cap: int):
+        """SecureStorage::decode of every sealed extent (mcdc_decode_blobs).
+        Returns (packed plaintexts, nblobs + 1 offsets, status); status -1 / -2
+        marks blobs that failed (no exception for those)."""
+        a = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        ext = self._extents(offsets, lengths)
+        oo = np.zeros(len(ext) + 1, dtype=np.uint64)
+        st = np.zeros(max(len(ext), 1), dtype=np.int32)
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        rc = load().mcdc_decode_blobs(self._h, self._key(key), a.ctypes.data, a.size, ext.ctypes.data, len(ext),
+                                      out.ctypes.data, cap, oo.ctypes.data, st.ctypes.data)
+        if rc != MCDC_E_AUTH:
+            check(rc)
+        return out[:int(oo[-1])], oo, st[:len(ext)]
 
     # ------------------------------------------------------- dedup index --
     @_locked

@@ -28,6 +28,7 @@
 #include "mcdc_blake3.h"
 #include "mcdc_index.h"
 #include "mcdc_internal.h"
+#include "../host/zstd_stage.hpp"
 
 using namespace mcdc;
 
@@ -219,7 +220,7 @@ struct mcdc_ctx {
   DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist,
+      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
@@ -873,7 +874,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
                     &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->tile_ctr, &ctx->b3_chunks, &ctx->b3_gcnt,
-                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp, &ctx->b3_hist,
+                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp, &ctx->b3_hist, &ctx->enc_in, &ctx->enc_out,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status};
   for (DevBuf *b : bufs)
@@ -1305,6 +1306,114 @@ int mcdc_index_add(mcdc_ctx *ctx, mcdc_index *ix, const uint8_t *ids, size_t n, 
   ctx->timing.device_ms = ms;
   ctx->timing.chunks = n;
   ctx->timing.total_ms = now_ms() - t0;
+  return MCDC_OK;
+}
+
+// ------------------------------------------------------ SecureStorage ---
+// encode / decode of many host blobs: zstd on host threads (host/zstd_stage.hpp),
+// AES-256-GCM-SIV on the GPU (aead_run).
+static int zstd_threads() {
+  const unsigned hw = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+}
+
+static int check_extents(const mcdc_blob *b, size_t n, size_t n_in) {
+  for (size_t i = 0; i < n; ++i)
+    if (b[i].offset > n_in || b[i].length > n_in - b[i].offset)
+      return fail(MCDC_E_INVALID, "blob %zu lies outside the %zu-byte input", i, n_in);
+  return MCDC_OK;
+}
+
+int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, size_t n_in, const mcdc_blob *blobs,
+                      size_t nblobs, const uint8_t *nonces, void *h_out, size_t out_cap, uint64_t *out_offsets) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!key || (!h_in && n_in) || (nblobs && (!blobs || !nonces))) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((h_in && is_device_ptr(h_in)) || (h_out && is_device_ptr(h_out)))
+    return fail(MCDC_E_INVALID, "h_in / h_out must be host memory");
+  if ((rc = check_extents(blobs, nblobs, n_in))) return rc;
+  const double t0 = now_ms();
+  std::vector<uint64_t> off(nblobs), len(nblobs);
+  for (size_t i = 0; i < nblobs; ++i) off[i] = blobs[i].offset, len[i] = blobs[i].length;
+  std::vector<std::vector<uint8_t>> comp;
+  const std::string zerr =
+      mcdc::host::zstd_compress_all((const uint8_t *)h_in, off.data(), len.data(), nblobs, zstd_threads(), comp);
+  if (!zerr.empty()) return fail(MCDC_E_INTERNAL, "%s", zerr.c_str());
+  std::vector<mcdc_blob> ext(nblobs);
+  size_t total = 0;
+  for (size_t i = 0; i < nblobs; ++i) ext[i] = mcdc_blob{total, comp[i].size()}, total += comp[i].size();
+  std::vector<uint8_t> arena(std::max<size_t>(total, 1));
+  for (size_t i = 0; i < nblobs; ++i)
+    if (!comp[i].empty()) std::memcpy(arena.data() + ext[i].offset, comp[i].data(), comp[i].size());
+  comp.clear();
+  const size_t cap = total + (size_t)kAeadOverhead * nblobs;
+  if ((rc = ensure(ctx, ctx->enc_in, total)) || (rc = ensure(ctx, ctx->enc_out, cap))) return rc;
+  if (total) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, arena.data(), total, hipMemcpyHostToDevice, ctx->stream));
+  std::vector<uint64_t> oo(nblobs + 1);
+  if ((rc = aead_run(ctx, 0, key, ctx->enc_in.p, total, ext.data(), nblobs, nonces, ctx->enc_out.p, cap, oo.data(),
+                     nullptr)))
+    return rc;
+  const mcdc_timing tm = ctx->timing;
+  if (out_offsets) std::memcpy(out_offsets, oo.data(), (nblobs + 1) * 8);
+  if (oo[nblobs] > out_cap || (oo[nblobs] && !h_out))
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", out_cap, (unsigned long long)oo[nblobs]);
+  if (oo[nblobs]) {
+    HIP_TRY(hipMemcpyAsync(h_out, ctx->enc_out.p, oo[nblobs], hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  ctx->timing = tm;
+  ctx->timing.bytes = n_in;
+  ctx->timing.total_ms = now_ms() - t0;
+  return MCDC_OK;
+}
+
+int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, size_t n_in, const mcdc_blob *sealed,
+                      size_t nblobs, void *h_out, size_t out_cap, uint64_t *out_offsets, int32_t *status) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!key || (!h_in && n_in) || (nblobs && !sealed)) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((h_in && is_device_ptr(h_in)) || (h_out && is_device_ptr(h_out)))
+    return fail(MCDC_E_INVALID, "h_in / h_out must be host memory");
+  if ((rc = check_extents(sealed, nblobs, n_in))) return rc;
+  const double t0 = now_ms();
+  if ((rc = ensure(ctx, ctx->enc_in, n_in)) || (rc = ensure(ctx, ctx->enc_out, n_in))) return rc;
+  if (n_in) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_in, n_in, hipMemcpyHostToDevice, ctx->stream));
+  std::vector<uint64_t> oo(nblobs + 1);
+  std::vector<int32_t> st(std::max<size_t>(nblobs, 1));
+  rc = aead_run(ctx, 1, key, ctx->enc_in.p, n_in, sealed, nblobs, nullptr, ctx->enc_out.p, n_in, oo.data(),
+                st.data());
+  if (rc && rc != MCDC_E_AUTH) return rc;
+  const mcdc_timing tm = ctx->timing;
+  std::vector<uint8_t> plain(std::max<uint64_t>(oo[nblobs], 1));
+  if (oo[nblobs]) {
+    HIP_TRY(hipMemcpyAsync(plain.data(), ctx->enc_out.p, oo[nblobs], hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  std::vector<uint64_t> poff(nblobs), plen(nblobs);
+  for (size_t i = 0; i < nblobs; ++i) poff[i] = oo[i], plen[i] = oo[i + 1] - oo[i];
+  std::vector<std::vector<uint8_t>> dec;
+  std::vector<int32_t> zok;
+  const std::string zerr = mcdc::host::zstd_decompress_all(plain.data(), poff.data(), plen.data(), st.data(),
+                                                           nblobs, zstd_threads(), dec, zok);
+  if (!zerr.empty()) return fail(MCDC_E_INTERNAL, "%s", zerr.c_str());
+  size_t total = 0, bad = 0;
+  std::vector<uint64_t> doff(nblobs + 1);
+  for (size_t i = 0; i < nblobs; ++i) {
+    const int32_t s = st[i] ? -1 : zok[i];
+    if (status) status[i] = s;
+    bad += s != 0;
+    doff[i] = total;
+    total += dec[i].size();
+  }
+  doff[nblobs] = total;
+  if (out_offsets) std::memcpy(out_offsets, doff.data(), (nblobs + 1) * 8);
+  if (total > out_cap || (total && !h_out))
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
+  for (size_t i = 0; i < nblobs; ++i)
+    if (!dec[i].empty()) std::memcpy((uint8_t *)h_out + doff[i], dec[i].data(), dec[i].size());
+  ctx->timing = tm;
+  ctx->timing.total_ms = now_ms() - t0;
+  if (bad) return fail(MCDC_E_AUTH, "%zu of %zu blobs failed to decode", bad, nblobs);
   return MCDC_OK;
 }
 
