@@ -31,6 +31,8 @@ Prints ONE JSON line (rank 0).  Extra objects:
   chunk_ids       - SURVEY.md §8(f) next stage: BLAKE3 chunk IDs of the same 64 GiB
                     boundary list in HBM (ID::from_content, processor.rs:184), and
                     the chunk + ID pipeline
+  encode          - SecureStorage::encode / decode of host blobs: zstd on host threads +
+                    sealing on the GPU (1 GiB of synthetic text)
   seal            - SURVEY.md §8(f) rank 3: SecureStorage encryption (AES-256-GCM-SIV,
                     storage.rs:97-118) of every chunk of the same stream as a blob
                     (mcdc_seal_device), its inverse (mcdc_open_device), parity probe
@@ -472,6 +474,39 @@ def incremental(ctx, p, dp: int, n: int, d_ch: int, cap_c: int, d_ids: int, key:
                     "snapshot's IDs"}
 
 
+def encode(ctx, gib: float, steps: int) -> dict:
+    """SecureStorage::encode / decode (storage.rs:61-94) of the chunks of a
+    compressible host buffer: zstd on host threads + AES-256-GCM-SIV on the GPU
+    (mcdc_encode_blobs / mcdc_decode_blobs), PCIe both ways included.  Data:
+    synthetic text (a 2 000-word vocabulary), chunked at 16/64/256 KiB."""
+    from mapache_amd import _lib
+    from oracle import oracle as O
+    rng = np.random.default_rng(21)
+    vocab = [bytes(rng.integers(97, 123, int(k))) for k in rng.integers(2, 11, 2000)]
+    base = b" ".join(vocab[i] for i in rng.integers(0, 2000, 12_000_000))[:64 << 20]
+    n = int(gib * GIB) // len(base) * len(base)
+    data = np.frombuffer(base * (n // len(base)), np.uint8)
+    ch = ctx.chunk_host(_lib.params(*PARAMS), data)
+    nz = np.zeros((len(ch), 12), np.uint8)
+    nz[:, :4] = np.arange(len(ch), dtype=np.uint32).view(np.uint8).reshape(-1, 4)
+    dte, (enc, oo) = _timed(lambda: ctx.encode_blobs(bytes(range(32)), data, ch["offset"], ch["length"], nz),
+                            steps, 1)
+    dtd, (dec, do, st) = _timed(lambda: ctx.decode_blobs(bytes(range(32)), enc, oo[:-1], np.diff(oo), n + 64),
+                                steps, 1)
+    ok = bool((st == 0).all() and dec.size == n and (dec == data).all())
+    pick = rng.integers(0, len(ch), 8)  # sealed bytes open with the oracle
+    ok_o = all(O.decrypt_with_key(bytes(range(32)), enc[int(oo[i]):int(oo[i + 1])].tobytes()) is not None
+               for i in pick)
+    return {"bytes": n, "blobs": int(len(ch)), "sealed_bytes": int(oo[-1]), "ratio": round(n / int(oo[-1]), 3),
+            "encode_ms": round(dte * 1e3, 2), "encode_gib_s": round(n / dte / GIB, 3),
+            "decode_ms": round(dtd * 1e3, 2), "decode_gib_s": round(n / dtd / GIB, 3),
+            "round_trip_ok": ok, "oracle_open_ok": ok_o,
+            "note": "host bytes in and out: zstd level 3 / window 20 on up to 16 host threads (system libzstd), "
+                    "sealing on the GPU, H2D and D2H included",
+            "data": "synthetic text, 2 000-word vocabulary, 64 MiB pattern repeated (repeats lie beyond the "
+                    "1 MiB window)"}
+
+
 def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> dict:
     """Every chunk of the headline stream sealed as one blob (random data: zstd
     would store it raw, so the blobs stand in for the compressed chunks), device
@@ -633,6 +668,7 @@ def main() -> int:
     ap.add_argument("--cpu-batch-files", type=int, default=4096, help="files in the multi-thread CPU sample")
     ap.add_argument("--no-ids", action="store_true", help="skip the chunk-ID (BLAKE3) stage")
     ap.add_argument("--no-seal", action="store_true", help="skip the SecureStorage sealing stage")
+    ap.add_argument("--encode-gib", type=float, default=1.0, help="host encode/decode sample (GiB, 0: skip)")
     a = ap.parse_args()
 
     world, rank, local = _dist()
@@ -803,6 +839,11 @@ def main() -> int:
                                        "parity_probe_chunks": int(len(g5)),
                                        "parity_probe_ok": bool(len(g5) > 0 and _same(g5, r5[:len(g5)])),
                                        "note": "same 64 GiB buffer, device-resident in and out, mapache defaults"}
+        if not a.no_seal and a.encode_gib > 0:
+            try:
+                result["encode"] = encode(ctx, a.encode_gib, 2)
+            except Exception as ex:  # reported, never silently dropped
+                result["encode"] = {"error": f"{type(ex).__name__}: {ex}"}
         if not a.no_seal:  # (last: its 128 GiB of buffers are freed before nothing else is allocated)
             try:
                 result["seal"] = seal(ctx, dp, n, chunks, max(3, a.steps // 2), a.no_cpu)

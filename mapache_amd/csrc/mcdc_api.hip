@@ -1343,8 +1343,9 @@ int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   size_t total = 0;
   for (size_t i = 0; i < nblobs; ++i) ext[i] = mcdc_blob{total, comp[i].size()}, total += comp[i].size();
   std::vector<uint8_t> arena(std::max<size_t>(total, 1));
-  for (size_t i = 0; i < nblobs; ++i)
+  mcdc::host::parallel_items(nblobs, zstd_threads(), [&](size_t i, int) {
     if (!comp[i].empty()) std::memcpy(arena.data() + ext[i].offset, comp[i].data(), comp[i].size());
+  });
   comp.clear();
   const size_t cap = total + (size_t)kAeadOverhead * nblobs;
   if ((rc = ensure(ctx, ctx->enc_in, total)) || (rc = ensure(ctx, ctx->enc_out, cap))) return rc;
@@ -1409,8 +1410,9 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   if (out_offsets) std::memcpy(out_offsets, doff.data(), (nblobs + 1) * 8);
   if (total > out_cap || (total && !h_out))
     return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
-  for (size_t i = 0; i < nblobs; ++i)
+  mcdc::host::parallel_items(nblobs, zstd_threads(), [&](size_t i, int) {
     if (!dec[i].empty()) std::memcpy((uint8_t *)h_out + doff[i], dec[i].data(), dec[i].size());
+  });
   ctx->timing = tm;
   ctx->timing.total_ms = now_ms() - t0;
   if (bad) return fail(MCDC_E_AUTH, "%zu of %zu blobs failed to decode", bad, nblobs);
