@@ -232,6 +232,33 @@ int mcdc_decode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h
                       const mcdc_blob *sealed, size_t nblobs, void *h_out, size_t out_cap,
                       uint64_t *out_offsets, int32_t *status);
 
+/* Packer::add_blob + flush (/root/reference/src/repository/packer.rs:101-186;
+ * flushed when the packer holds more than max_pack_size bytes,
+ * repository_v1.rs:185-193, and once more at the end) over a run of encoded
+ * blobs in host memory: pack = blobs back to back || encode(header) ||
+ * le32(len(encode(header))); header = per blob ID (32 B) || le32 length ||
+ * type (1 B: 0 data, 1 tree), padded to a multiple of 64 entries with entries
+ * of 36 random bytes + type 0xff (generate_header).  The randomness is the
+ * caller's (OsRng in the crate): header_nonces (12 B per pack) and padding (36
+ * B per padding entry, npadding entries; at most 63 per pack are used).
+ * The header is encoded with mcdc_encode_blobs; the pack ID is BLAKE3 of the
+ * pack (utils::calculate_hash), computed on the GPU.  Output: the packs back
+ * to back in h_out; *out_bytes their total and *npacks their number (also on
+ * MCDC_E_CAPACITY); packs[k] = {offset, length, blobs, meta_size (encoded
+ * header + 4), id}. */
+typedef struct {
+  uint64_t offset;
+  uint64_t length;
+  uint64_t nblobs;
+  uint64_t meta_size;
+  uint8_t id[32];
+} mcdc_pack;
+int mcdc_pack_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, size_t n_in,
+                    const mcdc_blob *blobs, const uint8_t *ids, const uint8_t *types, size_t nblobs,
+                    uint64_t max_pack_size, const uint8_t *header_nonces, size_t nnonces,
+                    const uint8_t *padding, size_t npadding, void *h_out, size_t out_cap,
+                    size_t *out_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks);
+
 /* ------------------------------------------------------------- dedup index
  * Repository::save_blob stores a blob only when its ID is neither in the
  * index nor already pending (/root/reference/src/repository/repository_v1.rs:

@@ -37,8 +37,12 @@ EXPORTS = (
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
-    "mcdc_encode_blobs", "mcdc_decode_blobs",
+    "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs",
 )
+
+
+PACK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("nblobs", "<u8"), ("meta_size", "<u8"),
+                       ("id", "u1", (32,))])
 
 
 class McdcParams(ctypes.Structure):
@@ -123,6 +127,8 @@ def load():
     L.mcdc_index_add.argtypes = [vp, vp, vp, sz, vp, vp, vp, P(sz)]
     L.mcdc_encode_blobs.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
     L.mcdc_decode_blobs.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp]
+    L.mcdc_pack_blobs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, u64, vp, sz, vp, sz, vp, sz, P(sz), vp, sz,
+                                  P(sz)]
     for name in EXPORTS:  # fail loudly if the build is stale
         getattr(L, name)
     _lib = L
@@ -348,6 +354,32 @@ class Context:
         if rc != MCDC_E_AUTH:
             check(rc)
         return out[:int(oo[-1])], oo, st[:len(ext)]
+
+    @_locked
+    def pack_blobs(self, key, data, offsets, lengths, ids, types, max_pack_size: int, header_nonces, padding):
+        """Packer::add_blob + flush over encoded host blobs (mcdc_pack_blobs).
+        Returns (packed bytes, PACK_DTYPE records)."""
+        a = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        ext = self._extents(offsets, lengths)
+        iv = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1)
+        ty = np.ascontiguousarray(types, dtype=np.uint8).reshape(-1)
+        hn = np.ascontiguousarray(header_nonces, dtype=np.uint8).reshape(-1)
+        pd = np.ascontiguousarray(padding, dtype=np.uint8).reshape(-1)
+        nb, np_, cap = ctypes.c_size_t(), ctypes.c_size_t(), 0
+        packs = np.zeros(1, dtype=PACK_DTYPE)
+        out = np.empty(1, dtype=np.uint8)
+        for _ in range(2):  # size query, then the call
+            rc = load().mcdc_pack_blobs(self._h, self._key(key), a.ctypes.data, a.size, ext.ctypes.data,
+                                        iv.ctypes.data, ty.ctypes.data, len(ext), max_pack_size, hn.ctypes.data,
+                                        hn.size // NONCE_BYTES, pd.ctypes.data, pd.size // 36, out.ctypes.data, cap,
+                                        ctypes.byref(nb), packs.ctypes.data, packs.size, ctypes.byref(np_))
+            if rc != MCDC_E_CAPACITY:
+                break
+            cap = nb.value
+            out = np.empty(max(cap, 1), dtype=np.uint8)
+            packs = np.zeros(max(np_.value, 1), dtype=PACK_DTYPE)
+        check(rc)
+        return out[:nb.value], packs[:np_.value]
 
     # ------------------------------------------------------- dedup index --
     @_locked

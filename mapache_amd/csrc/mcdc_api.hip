@@ -1419,6 +1419,121 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   return MCDC_OK;
 }
 
+// --------------------------------------------------------------- packer --
+// Packer::add_blob / flush for a run of encoded blobs (packer.rs:101-186,
+// repository_v1.rs:182-193): packs on the host, their headers encoded by
+// mcdc_encode_blobs, pack IDs (BLAKE3 of each pack) by mcdc_chunk_ids_device.
+static constexpr size_t kHeaderEntry = 37, kHeaderMultiple = 64;  // packer.rs:30, defaults.rs:32
+
+int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, size_t n_in, const mcdc_blob *blobs,
+                    const uint8_t *ids, const uint8_t *types, size_t nblobs, uint64_t max_pack_size,
+                    const uint8_t *header_nonces, size_t nnonces, const uint8_t *padding, size_t npadding,
+                    void *h_out, size_t out_cap, size_t *out_bytes, mcdc_pack *packs, size_t packs_cap,
+                    size_t *npacks) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!key || (!h_blobs && n_in) || (nblobs && (!blobs || !ids || !types)) || !npacks)
+    return fail(MCDC_E_INVALID, "NULL argument");
+  if ((h_blobs && is_device_ptr(h_blobs)) || (h_out && is_device_ptr(h_out)))
+    return fail(MCDC_E_INVALID, "h_blobs / h_out must be host memory");
+  if ((rc = check_extents(blobs, nblobs, n_in))) return rc;
+  *npacks = 0;
+  if (out_bytes) *out_bytes = 0;
+  const double t0 = now_ms();
+  // plan: add, then flush once the packer holds more than max_pack_size bytes;
+  // the rest is flushed last
+  std::vector<size_t> first;  // first blob of each pack (+ nblobs at the end)
+  uint64_t size = 0;
+  bool open = false;
+  for (size_t i = 0; i < nblobs; ++i) {
+    if (!open) first.push_back(i), open = true;
+    size += blobs[i].length;
+    if (size > max_pack_size) size = 0, open = false;
+  }
+  const size_t np = first.size();
+  first.push_back(nblobs);
+  if (np > nnonces) return fail(MCDC_E_INVALID, "%zu packs need %zu header nonces (%zu given)", np, np, nnonces);
+  // headers: 37-byte entries (ID, le32 length, type), padded with random entries
+  // (36 random bytes + BlobType::Padding) to a multiple of 64 (generate_header)
+  std::vector<uint8_t> hdr;
+  std::vector<mcdc_blob> hext(np);
+  size_t pad_used = 0;
+  for (size_t k = 0; k < np; ++k) {
+    const size_t cnt = first[k + 1] - first[k];
+    const size_t pad = cnt % kHeaderMultiple ? kHeaderMultiple - cnt % kHeaderMultiple : 0;
+    if (pad_used + pad > npadding)
+      return fail(MCDC_E_INVALID, "the padding pool holds %zu entries, the headers need more", npadding);
+    hext[k] = mcdc_blob{hdr.size(), (cnt + pad) * kHeaderEntry};
+    for (size_t i = first[k]; i < first[k + 1]; ++i) {
+      const uint32_t len = (uint32_t)blobs[i].length;
+      hdr.insert(hdr.end(), ids + 32 * i, ids + 32 * i + 32);
+      for (int b = 0; b < 4; ++b) hdr.push_back((uint8_t)(len >> (8 * b)));
+      hdr.push_back(types[i]);
+    }
+    for (size_t j = 0; j < pad; ++j, ++pad_used) {
+      hdr.insert(hdr.end(), padding + 36 * pad_used, padding + 36 * pad_used + 36);
+      hdr.push_back(0xff);
+    }
+  }
+  // SecureStorage::encode of every header (zstd on host threads, sealing on the GPU)
+  size_t enc_cap = hdr.size() + hdr.size() / 64 + 1024 * np + 64;
+  std::vector<uint8_t> enc(enc_cap);
+  std::vector<uint64_t> eo(np + 1);
+  if (np) {
+    rc = mcdc_encode_blobs(ctx, key, hdr.data(), hdr.size(), hext.data(), np, header_nonces, enc.data(), enc_cap,
+                           eo.data());
+    if (rc == MCDC_E_CAPACITY) {
+      enc.resize(eo[np]);
+      enc_cap = enc.size();
+      rc = mcdc_encode_blobs(ctx, key, hdr.data(), hdr.size(), hext.data(), np, header_nonces, enc.data(), enc_cap,
+                             eo.data());
+    }
+    if (rc) return rc;
+  }
+  // layout: blobs || encoded header || le32(len)
+  std::vector<mcdc_chunk> pk(np);
+  size_t total = 0;
+  for (size_t k = 0; k < np; ++k) {
+    uint64_t body = 0;
+    for (size_t i = first[k]; i < first[k + 1]; ++i) body += blobs[i].length;
+    const uint64_t meta = (eo[k + 1] - eo[k]) + 4;
+    pk[k] = mcdc_chunk{total, body + meta, 0};
+    total += body + meta;
+  }
+  *npacks = np;
+  if (out_bytes) *out_bytes = total;
+  if (np > packs_cap || (packs_cap && !packs)) return fail(MCDC_E_CAPACITY, "%zu packs, capacity %zu", np, packs_cap);
+  if (total > out_cap || (total && !h_out))
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
+  uint8_t *o = (uint8_t *)h_out;
+  mcdc::host::parallel_items(np, zstd_threads(), [&](size_t k, int) {
+    uint8_t *d = o + pk[k].offset;
+    for (size_t i = first[k]; i < first[k + 1]; ++i) {
+      std::memcpy(d, (const uint8_t *)h_blobs + blobs[i].offset, blobs[i].length);
+      d += blobs[i].length;
+    }
+    const uint32_t hl = (uint32_t)(eo[k + 1] - eo[k]);
+    std::memcpy(d, enc.data() + eo[k], hl);
+    for (int b = 0; b < 4; ++b) d[hl + b] = (uint8_t)(hl >> (8 * b));
+  });
+  // pack IDs: BLAKE3 of each pack (flush: utils::calculate_hash(&data)), on the GPU
+  std::vector<uint8_t> pid(32 * std::max<size_t>(np, 1));
+  if (np) {
+    if ((rc = ensure(ctx, ctx->enc_in, total))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_out, total, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = mcdc_chunk_ids_device(ctx, ctx->enc_in.p, total, pk.data(), np, pid.data()))) return rc;
+  }
+  for (size_t k = 0; k < np; ++k) {
+    packs[k].offset = pk[k].offset;
+    packs[k].length = pk[k].length;
+    packs[k].nblobs = first[k + 1] - first[k];
+    packs[k].meta_size = (eo[k + 1] - eo[k]) + 4;
+    std::memcpy(packs[k].id, pid.data() + 32 * k, 32);
+  }
+  ctx->timing.total_ms = now_ms() - t0;
+  return MCDC_OK;
+}
+
 // ------------------------------------------------------------ batcher --
 // C ABI of the cross-worker batching front-end (mapache_amd/host/batcher.hpp)
 // over this library's mcdc_chunk_batch on a context of its own.

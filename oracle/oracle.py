@@ -478,3 +478,36 @@ class DedupIndex:
                 self.seen.add(k)
                 out[i] = True
         return out
+
+
+# ----------------------------------------------------------------- packer --
+HEADER_BLOB_LEN, HEADER_BLOB_MULTIPLE = 37, 64  # packer.rs:30, defaults.rs:32
+
+
+def pack_plan(lengths, max_pack_size: int):
+    """Restates Repository::save_blob's flush rule (repository_v1.rs:185-193:
+    add the blob, then flush once the packer holds more than max_pack_size
+    bytes) plus the final flush: [(first, end)) blob ranges per pack."""
+    plan, size, first = [], 0, None
+    for i, n in enumerate(lengths):
+        if first is None:
+            first = i
+        size += int(n)
+        if size > max_pack_size:
+            plan.append((first, i + 1))
+            size, first = 0, None
+    if first is not None:
+        plan.append((first, len(lengths)))
+    return plan
+
+
+def pack_header(ids, lengths, types, padding36) -> bytes:
+    """Packer::generate_header (packer.rs:156-186): per blob ID || le32 length ||
+    type, padded to a multiple of 64 entries with (36 random bytes, 0xff);
+    padding36: the random bytes of the padding entries, in order."""
+    out = bytearray()
+    for i in range(len(lengths)):
+        out += bytes(ids[i]) + int(lengths[i]).to_bytes(4, "little") + bytes([int(types[i])])
+    for p in padding36:
+        out += bytes(p) + b"\xff"
+    return bytes(out)
