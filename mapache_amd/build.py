@@ -123,6 +123,12 @@ def build_cpu_tests(force: bool = False) -> None:
                 objs.append(o)
             _run(["g++", *flags, "-std=c++17", "-Wall", "-Imapache_amd/host", "-o", out, src, *objs, "-lpthread",
                   "-lm"], ROOT)
+    zsrc = os.path.join(cpp, "test_zstd_stage.cpp")
+    for suffix, flags in SANITIZERS.items():  # the zstd host stage (system libzstd.so.1, dlopen'd)
+        out = os.path.join(cpp, "test_zstd_stage" + suffix)
+        if os.path.exists(zsrc) and (force or _stale(out, [zsrc, os.path.join(HERE, "host", "zstd_stage.hpp")])):
+            _run(["g++", *flags, "-std=c++17", "-Wall", "-Imapache_amd/host", "-o", out, zsrc, "-lpthread", "-ldl"],
+                 ROOT)
     out = os.path.join(cpp, "test_host_api_asan")
     src = os.path.join(cpp, "test_host_api.cpp")
     if force or _stale(out, deps + [src, os.path.join(HERE, "libmcdc.so")]):

@@ -42,3 +42,17 @@ def test_host_mirror_and_oracle_asan_ubsan():
     # (the HIP runtime it links is not instrumented; its allocations are not leak-checked)
     r = _run("test_host_api_asan", "cpu", env={"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=1"})
     assert "runtime error" not in r.stderr
+
+
+def test_zstd_stage_threads():
+    _run("test_zstd_stage", 8)
+
+
+def test_zstd_stage_asan_ubsan():
+    r = _run("test_zstd_stage_asan", 4, env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"})
+    assert "runtime error" not in r.stderr
+
+
+def test_zstd_stage_tsan():
+    r = _run("test_zstd_stage_tsan", 4, env={"TSAN_OPTIONS": "halt_on_error=1"})
+    assert "WARNING: ThreadSanitizer" not in r.stderr
