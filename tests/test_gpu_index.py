@@ -100,3 +100,54 @@ def test_device_pipeline_repeated_content(ctx):
     ref = O.DedupIndex().add(O.chunk_ids(data, rc, threads=8))
     assert (f == ref).all()
     assert ref.sum() < 0.5 * k  # the repeats were found
+
+
+def test_incremental_save_path_in_hbm(ctx):
+    """Second snapshot with a few changed bytes: chunk -> IDs -> dedup against
+    the first snapshot's index -> seal only the new chunks, all in HBM; the new
+    chunks are those the oracle's chunks/IDs/index give, sealed as the RFC 8452
+    oracle seals them."""
+    n = 40 << 20
+    data = O.random_bytes(n, SEED + 4)
+    changed = data.copy()
+    pos = np.array([3 << 20, (17 << 20) + 5, (33 << 20) + 77])
+    changed[pos] ^= 0x5A
+    p = _lib.params(16384, 65536, 262144, 1)
+    cap = n // (16384 - 1) + 2
+    dp = ctx.device_alloc(n + 16)
+    d_ch = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    d_new = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+    d_ids = ctx.device_alloc(cap * 32)
+    key = bytes(range(32))
+    try:
+        with ctx.index_create() as ix:
+            ctx.h2d(dp, data)
+            k0 = ctx.chunk_device_to_device(p, dp, n, d_ch, cap)
+            ctx.chunk_ids(dp, n, (d_ch, k0), ids=d_ids)
+            assert ix.add_device(d_ids, k0, d_ch, d_new) == k0
+            ctx.h2d(dp, changed)
+            k1 = ctx.chunk_device_to_device(p, dp, n, d_ch, cap)
+            ctx.chunk_ids(dp, n, (d_ch, k1), ids=d_ids)
+            m = ix.add_device(d_ids, k1, d_ch, d_new)
+            new = ctx.d2h_chunks(d_new, m)
+            nonces = np.arange(12 * m, dtype=np.uint32).astype(np.uint8).reshape(m, 12)
+            cap_s = int(new["length"].sum()) + 28 * m
+            d_s = ctx.device_alloc(cap_s)
+            try:
+                oo = ctx.seal_chunks(key, dp, n, new, nonces, d_s, cap_s)
+                sealed = ctx.d2h_bytes(d_s, int(oo[-1]))
+            finally:
+                ctx.device_free(d_s)
+    finally:
+        for x in (d_ids, d_new, d_ch, dp):
+            ctx.device_free(x)
+    P = O.Params(16384, 65536, 262144, 1)
+    r0, r1 = O.chunk(P, data), O.chunk(P, changed)
+    ix_ref = O.DedupIndex()
+    ix_ref.add(O.chunk_ids(data, r0, threads=8))
+    flags = ix_ref.add(O.chunk_ids(changed, r1, threads=8))
+    ref_new = r1[flags]
+    assert 0 < m == len(ref_new) and (new["offset"] == ref_new["offset"]).all()
+    assert (new["length"] == ref_new["length"]).all()
+    ref, _ = O.seal_blobs(key, changed, ref_new["offset"], ref_new["length"], nonces)
+    assert sealed.tobytes() == ref.tobytes()
