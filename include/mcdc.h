@@ -232,6 +232,18 @@ int mcdc_decode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h
                       const mcdc_blob *sealed, size_t nblobs, void *h_out, size_t out_cap,
                       uint64_t *out_offsets, int32_t *status);
 
+/* zstd frames of every chunk of a boundary list, in HBM, in raw-block
+ * ("store") mode: the format of SecureStorage::compress (storage.rs:74-84;
+ * window 2^20, no checksum) without entropy coding — what zstd itself emits
+ * for incompressible data — so chunk -> frame -> seal stays on the GPU and the
+ * blobs stay readable by mapache's decoder (storage.rs:87-94).  Frame i is
+ * written at a 16-byte aligned offset of d_out; frames[i] (host or device)
+ * receives its (offset, length), ready for mcdc_seal_device.  *out_bytes: the
+ * output span (also on MCDC_E_CAPACITY).  chunks: host or device. */
+int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
+                            size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,
+                            mcdc_blob *frames);
+
 /* Packer::add_blob + flush (/root/reference/src/repository/packer.rs:101-186;
  * flushed when the packer holds more than max_pack_size bytes,
  * repository_v1.rs:185-193, and once more at the end) over a run of encoded

@@ -37,7 +37,7 @@ EXPORTS = (
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
-    "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs",
+    "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device",
 )
 
 
@@ -127,6 +127,7 @@ def load():
     L.mcdc_index_add.argtypes = [vp, vp, vp, sz, vp, vp, vp, P(sz)]
     L.mcdc_encode_blobs.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
     L.mcdc_decode_blobs.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, vp]
+    L.mcdc_zstd_frames_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, P(sz), vp]
     L.mcdc_pack_blobs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, u64, vp, sz, vp, sz, vp, sz, P(sz), vp, sz,
                                   P(sz)]
     for name in EXPORTS:  # fail loudly if the build is stale
@@ -354,6 +355,26 @@ class Context:
         if rc != MCDC_E_AUTH:
             check(rc)
         return out[:int(oo[-1])], oo, st[:len(ext)]
+
+    @_locked
+    def zstd_frames(self, d_data: int, n: int, chunks, d_out: int, out_cap: int, frames_out=None):
+        """zstd raw-block frames of every chunk (mcdc_zstd_frames_device).  chunks:
+        CHUNK_DTYPE array or (device pointer, count).  Returns (frames as an
+        (count, 2) uint64 array of (offset, length), output span), or writes the
+        extents to the device pointer frames_out and returns (None, span)."""
+        if isinstance(chunks, tuple):
+            cptr, count = chunks
+        else:
+            arr = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+            cptr, count = arr.ctypes.data, arr.size
+            keep = arr  # noqa: F841
+        span = ctypes.c_size_t()
+        fr = None if frames_out is not None else np.zeros((max(count, 1), 2), dtype=np.uint64)
+        fptr = frames_out if frames_out is not None else fr.ctypes.data
+        check(load().mcdc_zstd_frames_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(cptr), count,
+                                             ctypes.c_void_p(d_out), out_cap, ctypes.byref(span),
+                                             ctypes.c_void_p(fptr)))
+        return (None if fr is None else fr[:count]), span.value
 
     @_locked
     def pack_blobs(self, key, data, offsets, lengths, ids, types, max_pack_size: int, header_nonces, padding):

@@ -22,8 +22,8 @@ ARCH = os.environ.get("MCDC_ARCH", "gfx950")
 CXXFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 LIB_SRCS = ["csrc/mcdc_kernels.hip", "csrc/mcdc_blake3.hip", "csrc/mcdc_aead.hip", "csrc/mcdc_index.hip",
-            "csrc/mcdc_api.hip"]
-LIB_DEPS = LIB_SRCS + ["csrc/mcdc_internal.h", "csrc/mcdc_blake3.h", "csrc/mcdc_aead.h", "csrc/mcdc_index.h", "csrc/gear_table.h", "../include/mcdc.h",
+            "csrc/mcdc_zframe.hip", "csrc/mcdc_api.hip"]
+LIB_DEPS = LIB_SRCS + ["csrc/mcdc_internal.h", "csrc/mcdc_blake3.h", "csrc/mcdc_aead.h", "csrc/mcdc_index.h", "csrc/mcdc_zframe.h", "csrc/gear_table.h", "../include/mcdc.h",
                        "host/batcher.hpp", "host/zstd_stage.hpp"]
 
 

@@ -27,6 +27,7 @@
 #include "mcdc_aead.h"
 #include "mcdc_blake3.h"
 #include "mcdc_index.h"
+#include "mcdc_zframe.h"
 #include "mcdc_internal.h"
 #include "../host/zstd_stage.hpp"
 
@@ -220,7 +221,7 @@ struct mcdc_ctx {
   DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
-      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out,
+      scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
@@ -874,7 +875,8 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
                     &ctx->seg_true, &ctx->entry_idx, &ctx->seg_count, &ctx->seg_off, &ctx->out,
                     &ctx->err, &ctx->scan_tmp, &ctx->seg_incl, &ctx->irr, &ctx->tile_ctr, &ctx->b3_chunks, &ctx->b3_gcnt,
-                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp, &ctx->b3_hist, &ctx->enc_in, &ctx->enc_out,
+                    &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp, &ctx->b3_hist, &ctx->enc_in, &ctx->enc_out, &ctx->zf_sz,
+                    &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status};
   for (DevBuf *b : bufs)
@@ -1416,6 +1418,61 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   ctx->timing = tm;
   ctx->timing.total_ms = now_ms() - t0;
   if (bad) return fail(MCDC_E_AUTH, "%zu of %zu blobs failed to decode", bad, nblobs);
+  return MCDC_OK;
+}
+
+// ------------------------------------------------------- zstd raw frames --
+int mcdc_zstd_frames_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks, size_t nchunks,
+                            void *d_out, size_t out_cap, size_t *out_bytes, mcdc_blob *frames) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if ((!d_data && n) || (nchunks && (!chunks || !frames))) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((d_data && !is_device_ptr(d_data)) || (d_out && !is_device_ptr(d_out)))
+    return fail(MCDC_E_INVALID, "d_data / d_out must be device pointers");
+  if (out_bytes) *out_bytes = 0;
+  if (nchunks == 0) return MCDC_OK;
+  if (nchunks >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many chunks (%zu)", nchunks);
+  const double t0 = now_ms();
+  hipStream_t st = ctx->stream;
+  const size_t tmpb = zframe_tmp_bytes(nchunks);
+  if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, nchunks * sizeof(mcdc_chunk))) ||
+      (rc = ensure(ctx, ctx->zf_sz, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->zf_off, (nchunks + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->zf_tmp, tmpb)) || (rc = ensure(ctx, ctx->err, 32)))
+    return rc;
+  uint32_t *err = (uint32_t *)ctx->err.p + 6;
+  HIP_TRY(hipMemsetAsync(err, 0, 4, st));
+  HIP_TRY(hipEventRecord(ctx->ev_start, st));
+  launch_zframe_sizes((const DevChunk *)ctx->b3_chunks.p, nchunks, n, (uint64_t *)ctx->zf_sz.p,
+                      (uint64_t *)ctx->zf_off.p, err, ctx->zf_tmp.p, tmpb, st);
+  HIP_TRY(hipGetLastError());
+  uint32_t herr = 0;
+  uint64_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&total, (uint64_t *)ctx->zf_off.p + nchunks, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (herr) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer", n);
+  if (out_bytes) *out_bytes = total;
+  if (total > out_cap || !d_out) return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", out_cap,
+                                             (unsigned long long)total);
+  uint64_t *ext = (uint64_t *)direct_out(ctx, frames);
+  if (!ext && is_device_ptr(frames)) return fail(MCDC_E_INVALID, "frames is a device pointer of another device");
+  if (!ext) {
+    if ((rc = ensure(ctx, ctx->zf_ext, nchunks * 16))) return rc;
+    ext = (uint64_t *)ctx->zf_ext.p;
+  }
+  launch_zframe_write((const uint8_t *)d_data, (const DevChunk *)ctx->b3_chunks.p, nchunks,
+                      (const uint64_t *)ctx->zf_off.p, (uint8_t *)d_out, ext, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev_end, st));
+  if (ext == ctx->zf_ext.p) HIP_TRY(hipMemcpyAsync(frames, ext, nchunks * 16, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_end));
+  ctx->timing = mcdc_timing{};
+  ctx->timing.device_ms = ms;
+  ctx->timing.bytes = n;
+  ctx->timing.chunks = nchunks;
+  ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
 }
 

@@ -1,0 +1,133 @@
+// mcdc_zframe.hip — CDNA4 (gfx950) zstd frames in raw-block ("store") mode
+// for every chunk of a boundary list, in HBM: the format half of
+// SecureStorage::compress (/root/reference/src/repository/storage.rs:74-84)
+// without the entropy coding, so chunk -> frame -> seal stays on the GPU and
+// the stored blobs remain readable by mapache's decoder (storage.rs:87-94:
+// zstd Decoder, window_log_max 20).
+//
+// Frame (RFC 8878): magic 28 B5 2F FD; Frame_Header_Descriptor 0x00 (no
+// content size, multi-segment, no checksum, no dictionary); Window_Descriptor
+// 0x50 (2^20 bytes: storage.rs:31 WindowLog(log2 AVG_CHUNK_SIZE)); then raw
+// blocks of at most 128 KiB, each a 3-byte little-endian header
+// (Last_Block | Block_Type 0 << 1 | Block_Size << 3) and the bytes; an empty
+// chunk is one empty last block.  Raw blocks are what zstd itself emits for
+// data it cannot compress; for compressible data the host stage
+// (host/zstd_stage.hpp) gives the reference's compression.
+//
+// Layout: frame i starts at a 16-byte aligned output offset (aligned stores;
+// the sealing entry points take the frames as (offset, length) extents, so
+// the gaps are never read).  One workgroup per chunk; each thread writes
+// whole 16-byte output quads: inside a block's data a quad is one misaligned
+// 16-byte load (gfx950 reads it as the bytes at that address,
+// tools/dbg/unaligned_probe.hip), quads touching a header are assembled byte
+// by byte.  HBM-bound: each input byte read once, written once.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "mcdc_zframe.h"
+
+namespace mcdc {
+
+namespace {
+
+constexpr uint64_t kZBlock = 131072, kZHdr = 6, kZBlkHdr = 3;
+
+__device__ __host__ __forceinline__ uint64_t zblocks(uint64_t len) { return len ? (len + kZBlock - 1) / kZBlock : 1; }
+__device__ __host__ __forceinline__ uint64_t zframe_len(uint64_t len) { return kZHdr + kZBlkHdr * zblocks(len) + len; }
+
+// byte p of the frame of a len-byte chunk at src
+__device__ __forceinline__ uint8_t zbyte(const uint8_t *src, uint64_t len, uint64_t p) {
+  if (p < kZHdr) {
+    const uint8_t h[6] = {0x28, 0xB5, 0x2F, 0xFD, 0x00, 0x50};
+    return h[p];
+  }
+  const uint64_t q = p - kZHdr, k = q / (kZBlock + kZBlkHdr), r = q % (kZBlock + kZBlkHdr);
+  const uint64_t nb = zblocks(len);
+  if (r < kZBlkHdr) {
+    const uint64_t bsz = k + 1 < nb ? kZBlock : len - k * kZBlock;
+    const uint32_t h = (uint32_t)(k + 1 == nb) | (uint32_t)(bsz << 3);
+    return (uint8_t)(h >> (8 * r));
+  }
+  return src[k * kZBlock + (r - kZBlkHdr)];
+}
+
+__global__ void k_zframe_sizes(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *sz, uint32_t *err) {
+  MCDC_VGPR_PAD(8);  // 8 used: not an exact fill (MCDC_VGPR_PAD)
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const DevChunk c = chunks[i];
+    const bool ok = c.offset <= nbytes && c.length <= nbytes - c.offset;
+    if (!ok) atomicOr(err, 1u);
+    sz[i] = ok ? (zframe_len(c.length) + 15) / 16 * 16 : 0;  // (16-byte aligned starts)
+  } else if (i == n) {
+    sz[i] = 0;
+  }
+}
+
+typedef uint32_t zf_u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) zf_u32x4 *zf_gq;
+
+__global__ __launch_bounds__(256) void k_zframe_write(const uint8_t *base, const DevChunk *chunks, uint64_t n,
+                                                      const uint64_t *off, uint8_t *out, uint64_t *ext) {
+  const uint64_t i = blockIdx.x;
+  if (i >= n) return;
+  const DevChunk c = chunks[i];
+  const uint64_t fl = zframe_len(c.length), o = off[i];
+  if (threadIdx.x == 0) {
+    ext[2 * i] = o;
+    ext[2 * i + 1] = fl;
+  }
+  const uint8_t *src = base + c.offset;
+  uint8_t *dst = out + o;
+  for (uint64_t q = threadIdx.x; 16 * q < fl; q += blockDim.x) {
+    const uint64_t p = 16 * q;
+    // a quad wholly inside one block's data: one misaligned 16-byte load
+    bool inside = false;
+    uint64_t s = 0;
+    if (p >= kZHdr && p + 16 <= fl) {
+      const uint64_t a = p - kZHdr, k = a / (kZBlock + kZBlkHdr), r = a % (kZBlock + kZBlkHdr);
+      if (r >= kZBlkHdr && r + 16 <= kZBlock + kZBlkHdr) {
+        inside = true;
+        s = k * kZBlock + (r - kZBlkHdr);
+      }
+    }
+    uint4 v;
+    if (inside) {
+      const zf_u32x4 x = *reinterpret_cast<zf_gq>(reinterpret_cast<uintptr_t>(src + s));
+      v = make_uint4(x.x, x.y, x.z, x.w);
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t b = 0; b < 16 && p + b < fl; ++b) w[b >> 2] |= (uint32_t)zbyte(src, c.length, p + b) << (8 * (b & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (p + 16 <= fl) {
+      *reinterpret_cast<uint4 *>(dst + p) = v;
+    } else {  // the frame's last, partial quad: its own bytes only (the rest is the alignment gap)
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      for (uint32_t b = 0; p + b < fl; ++b) dst[p + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
+}  // namespace
+
+size_t zframe_tmp_bytes(uint64_t n) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n + 1);
+  return b;
+}
+
+void launch_zframe_sizes(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *sz, uint64_t *off,
+                         uint32_t *err, void *tmp, size_t tmp_bytes, hipStream_t st) {
+  hipLaunchKernelGGL(k_zframe_sizes, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, chunks, n, nbytes, sz,
+                     err);
+  size_t b = tmp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, sz, off, (int)n + 1, st);
+}
+
+void launch_zframe_write(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *off, uint8_t *out,
+                         uint64_t *ext, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_zframe_write, dim3((unsigned)n), dim3(256), 0, st, base, chunks, n, off, out, ext);
+}
+
+}  // namespace mcdc

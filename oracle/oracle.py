@@ -511,3 +511,19 @@ def pack_header(ids, lengths, types, padding36) -> bytes:
     for p in padding36:
         out += bytes(p) + b"\xff"
     return bytes(out)
+
+
+# ------------------------------------------------------- zstd raw frames --
+def zstd_raw_frame(data) -> bytes:
+    """RFC 8878 frame in raw-block mode, as mcdc_zstd_frames_device writes it:
+    magic, Frame_Header_Descriptor 0 (no content size, not single-segment, no
+    checksum, no dictionary), Window_Descriptor 0x50 (2^20, storage.rs:31),
+    raw blocks of <= 128 KiB with 3-byte headers (Last_Block | Raw << 1 |
+    Block_Size << 3); an empty input is one empty last block."""
+    data = bytes(data)
+    out = bytearray(b"\x28\xb5\x2f\xfd\x00\x50")
+    blocks = [data[i:i + 131072] for i in range(0, len(data), 131072)] or [b""]
+    for k, b in enumerate(blocks):
+        h = (1 if k + 1 == len(blocks) else 0) | (len(b) << 3)
+        out += h.to_bytes(3, "little") + b
+    return bytes(out)
