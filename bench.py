@@ -523,13 +523,21 @@ def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> 
     nonces[:, 1:] = np.frombuffer(b"mapache!", np.uint32)
     nonces = nonces.view(np.uint8).reshape(k, 12)
     cap = n + 28 * k
-    d_seal = ctx.device_alloc(cap)
-    d_open = ctx.device_alloc(n)
+    d_seal = ctx.device_alloc(cap + (64 << 20))  # (+ room for the store-mode frames' headers, below)
+    d_open = ctx.device_alloc(n + (64 << 20))
     try:
         dt, oo = _timed(lambda: ctx.seal(key, dp, n, offs, lens, nonces, d_seal, cap), steps, 1)
         ts = ctx.timing()
         dto, (po, st) = _timed(lambda: ctx.open(key, d_seal, int(oo[-1]), oo[:-1], np.diff(oo), d_open, n), steps, 1)
         to = ctx.timing()
+        # parity probe and round trip now (the store-mode path below reuses d_seal / d_open)
+        rng = np.random.default_rng(3)
+        pick = np.unique(np.concatenate([np.arange(32), rng.integers(0, k, 64)]))
+        got = [ctx.d2h_bytes(d_seal + int(oo[i]), int(lens[i]) + 28).tobytes() for i in pick]
+        ref = [O.encrypt_with_key(key, nonces[i], O.random_bytes(int(lens[i]), SEED, pos=int(offs[i]))) for i in pick]
+        windows = [int(x) for x in rng.integers(0, n - (1 << 20), 16)]
+        rt_ok = bool((st == 0).all()) and all(
+            (ctx.d2h_bytes(d_open + w, 1 << 20) == O.random_bytes(1 << 20, SEED, pos=w)).all() for w in windows)
         # the save path's GPU stages back to back, all in HBM: chunk -> IDs -> seal
         p = _lib.params(*PARAMS)
         cap_c = n // (p.min_size - 1) + 2
@@ -546,16 +554,31 @@ def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> 
                 ctx.seal_chunks(key, dp, n, (d_ch, kk), d_nonce, d_seal, cap, offsets_out=d_offs)
             dtp, _ = _timed(save_path, steps, 1)  # (rewrites d_seal with the same bytes: same list, nonces, key)
             incr = incremental(ctx, p, dp, n, d_ch, cap_c, d_ids, key, d_nonce, d_offs)
+            # the whole GPU encode in store mode: chunk -> IDs -> zstd raw frames -> seal,
+            # every array in HBM (blobs mapache's decoder reads; no compression)
+            d_fr = ctx.device_alloc(16 * cap_c)
+            try:
+                def store_path():
+                    kk = ctx.chunk_device_to_device(p, dp, n, d_ch, cap_c)
+                    ctx.chunk_ids(dp, n, (d_ch, kk), ids=d_ids)
+                    _, span = ctx.zstd_frames(dp, n, (d_ch, kk), d_open, n + (64 << 20), frames_out=d_fr)
+                    t_fr = ctx.timing()["device_ms"]
+                    ctx.seal_device_ext(key, d_open, span, d_fr, kk, d_nonce, d_seal, cap + (64 << 20), d_offs)
+                    return span, t_fr
+                dts, (span_s, t_fr) = _timed(store_path, steps, 1)
+                fr_probe = ctx.d2h_bytes(d_fr, 16 * 4).view(np.uint64).reshape(4, 2)
+                probe_ok = all(ctx.d2h_bytes(d_open + int(fr_probe[i, 0]), int(fr_probe[i, 1])).tobytes()
+                               == O.zstd_raw_frame(O.random_bytes(int(lens[i]), SEED, pos=int(offs[i])))
+                               for i in range(4))
+                store = {"ms_per_step": round(dts * 1e3, 3), "gib_s": round(n / dts / GIB, 2),
+                         "frames_ms": round(t_fr, 3), "frame_bytes": int(span_s), "frames_probe_ok": probe_ok,
+                         "note": "mcdc_chunk_device + mcdc_chunk_ids_device + mcdc_zstd_frames_device + "
+                                 "mcdc_seal_device per step, all in HBM: zstd frames in raw-block mode"}
+            finally:
+                ctx.device_free(d_fr)
         finally:
             for ptr in (d_offs, d_nonce, d_ids, d_ch):
                 ctx.device_free(ptr)
-        rng = np.random.default_rng(3)
-        pick = np.unique(np.concatenate([np.arange(32), rng.integers(0, k, 64)]))
-        got = [ctx.d2h_bytes(d_seal + int(oo[i]), int(lens[i]) + 28).tobytes() for i in pick]
-        ref = [O.encrypt_with_key(key, nonces[i], O.random_bytes(int(lens[i]), SEED, pos=int(offs[i]))) for i in pick]
-        windows = [int(x) for x in rng.integers(0, n - (1 << 20), 16)]
-        rt_ok = bool((st == 0).all()) and all(
-            (ctx.d2h_bytes(d_open + w, 1 << 20) == O.random_bytes(1 << 20, SEED, pos=w)).all() for w in windows)
         r = {"blobs": k, "bytes": n, "steps": steps,
              "seal_ms_per_step": round(dt * 1e3, 3), "seal_gib_s": round(n / dt / GIB, 2),
              "seal_device_ms": round(ts["device_ms"], 3), "seal_kernels_ms": round(ts["aead_ms"], 3),
@@ -565,7 +588,7 @@ def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> 
              "chunk_ids_seal": "mcdc_chunk_device + mcdc_chunk_ids_device + mcdc_seal_chunks_device per step, "
                                "boundary list, IDs, nonces and output offsets in HBM",
              "parity_probe_blobs": int(len(pick)), "parity_probe_ok": got == ref,
-             "round_trip_ok": rt_ok, "incremental_save_path": incr,
+             "round_trip_ok": rt_ok, "incremental_save_path": incr, "store_mode_encode_path": store,
              "output": "nonce || ciphertext || tag per blob, packed in blob order (the pack body)",
              "data": "synthetic: the chunks of the 64 GiB headline stream as blobs, nonce i = le32(i) || 'mapache!'"}
         if not no_cpu:

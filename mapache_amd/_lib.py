@@ -426,6 +426,15 @@ class Context:
         return key
 
     @_locked
+    def seal_device_ext(self, key, d_in: int, n_in: int, d_ext: int, count: int, d_nonces: int, d_out: int,
+                        out_cap: int, d_offsets: int) -> None:
+        """mcdc_seal_device with every array in HBM: (offset, length) extents,
+        nonces and the nblobs + 1 output offsets."""
+        check(load().mcdc_seal_device(self._h, self._key(key), ctypes.c_void_p(d_in), n_in, ctypes.c_void_p(d_ext),
+                                      count, ctypes.c_void_p(d_nonces), ctypes.c_void_p(d_out), out_cap,
+                                      ctypes.c_void_p(d_offsets)))
+
+    @_locked
     def seal(self, key, d_in: int, n_in: int, offsets, lengths, nonces, d_out: int, out_cap: int) -> np.ndarray:
         """SecureStorage::encrypt_with_key for every blob d_in[offsets[i], +lengths[i])
         (mcdc_seal_device): results nonce || ct || tag packed from d_out.  Returns the
