@@ -239,7 +239,8 @@ int mcdc_decode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h
  * blobs stay readable by mapache's decoder (storage.rs:87-94).  Frame i is
  * written at a 16-byte aligned offset of d_out; frames[i] (host or device)
  * receives its (offset, length), ready for mcdc_seal_device.  *out_bytes: the
- * output span (also on MCDC_E_CAPACITY).  chunks: host or device. */
+ * output span (also on MCDC_E_CAPACITY).  chunks: host or device; a chunk
+ * outside [0, n) or of 2 GiB or more -> MCDC_E_INVALID. */
 int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
                             size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,
                             mcdc_blob *frames);

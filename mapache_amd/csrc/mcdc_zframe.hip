@@ -56,7 +56,7 @@ __global__ void k_zframe_sizes(const DevChunk *chunks, uint64_t n, uint64_t nbyt
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const DevChunk c = chunks[i];
-    const bool ok = c.offset <= nbytes && c.length <= nbytes - c.offset;
+    const bool ok = c.offset <= nbytes && c.length <= nbytes - c.offset && c.length < (1ull << 31);
     if (!ok) atomicOr(err, 1u);
     sz[i] = ok ? (zframe_len(c.length) + 15) / 16 * 16 : 0;  // (16-byte aligned starts)
   } else if (i == n) {
@@ -79,16 +79,18 @@ __global__ __launch_bounds__(256) void k_zframe_write(const uint8_t *base, const
   }
   const uint8_t *src = base + c.offset;
   uint8_t *dst = out + o;
-  for (uint64_t q = threadIdx.x; 16 * q < fl; q += blockDim.x) {
-    const uint64_t p = 16 * q;
+  // (32-bit positions: chunks of 2 GiB and more are rejected by k_zframe_sizes)
+  const uint32_t fl32 = (uint32_t)fl;
+  for (uint32_t p = 16 * threadIdx.x; p < fl32; p += 16 * blockDim.x) {
     // a quad wholly inside one block's data: one misaligned 16-byte load
     bool inside = false;
-    uint64_t s = 0;
-    if (p >= kZHdr && p + 16 <= fl) {
-      const uint64_t a = p - kZHdr, k = a / (kZBlock + kZBlkHdr), r = a % (kZBlock + kZBlkHdr);
+    uint32_t s = 0;
+    if (p >= kZHdr && p + 16 <= fl32) {
+      const uint32_t a = p - (uint32_t)kZHdr, k = a / (uint32_t)(kZBlock + kZBlkHdr),
+                     r = a - k * (uint32_t)(kZBlock + kZBlkHdr);
       if (r >= kZBlkHdr && r + 16 <= kZBlock + kZBlkHdr) {
         inside = true;
-        s = k * kZBlock + (r - kZBlkHdr);
+        s = k * (uint32_t)kZBlock + (r - (uint32_t)kZBlkHdr);
       }
     }
     uint4 v;
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256) void k_zframe_write(const uint8_t *base, const
       for (uint32_t b = 0; b < 16 && p + b < fl; ++b) w[b >> 2] |= (uint32_t)zbyte(src, c.length, p + b) << (8 * (b & 3));
       v = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    if (p + 16 <= fl) {
+    if (p + 16 <= fl32) {
       *reinterpret_cast<uint4 *>(dst + p) = v;
     } else {  // the frame's last, partial quad: its own bytes only (the rest is the alignment gap)
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
