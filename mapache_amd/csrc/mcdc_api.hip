@@ -1494,6 +1494,8 @@ int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, s
   if ((h_blobs && is_device_ptr(h_blobs)) || (h_out && is_device_ptr(h_out)))
     return fail(MCDC_E_INVALID, "h_blobs / h_out must be host memory");
   if ((rc = check_extents(blobs, nblobs, n_in))) return rc;
+  for (size_t i = 0; i < nblobs; ++i)
+    if (blobs[i].length > 0xffffffffull) return fail(MCDC_E_INVALID, "blob %zu exceeds the header's u32 length", i);
   *npacks = 0;
   if (out_bytes) *out_bytes = 0;
   const double t0 = now_ms();

@@ -106,9 +106,16 @@ inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, con
   parallel_items(n, threads, [&](size_t i, int w) {
     if (!cctx[w]) {
       cctx[w] = z.createCCtx();
-      z.cctxSetParameter(cctx[w], kZstdCLevel, kZstdLevel);
-      z.cctxSetParameter(cctx[w], kZstdCWindowLog, kZstdWindowLog);
-      z.cctxSetParameter(cctx[w], kZstdCChecksum, 0);
+      const bool ok = cctx[w] && !z.isError(z.cctxSetParameter(cctx[w], kZstdCLevel, kZstdLevel)) &&
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCWindowLog, kZstdWindowLog)) &&
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCChecksum, 0));
+      if (!ok) {  // never compress with other settings than the reference's
+        std::lock_guard<std::mutex> lk(emu);
+        err = "zstd rejected level 3 / window log 20 / no checksum";
+        if (cctx[w]) z.freeCCtx(cctx[w]);
+        cctx[w] = nullptr;
+        return;
+      }
     }
     std::vector<uint8_t> &o = out[i];
     o.resize(z.compressBound(len[i]));
@@ -149,7 +156,12 @@ inline std::string zstd_decompress_all(const uint8_t *in, const uint64_t *off, c
     if ((skip && skip[i]) || len[i] == 0) return;  // (no frame: no bytes, as read_to_end of an empty reader)
     if (!dctx[w]) {
       dctx[w] = z.createDCtx();
-      z.dctxSetParameter(dctx[w], kZstdDWindowLogMax, kZstdWindowLog);
+      if (!dctx[w] || z.isError(z.dctxSetParameter(dctx[w], kZstdDWindowLogMax, kZstdWindowLog))) {
+        if (dctx[w]) z.freeDCtx(dctx[w]);
+        dctx[w] = nullptr;
+        ok[i] = -2;
+        return;
+      }
     }
     std::vector<uint8_t> &o = out[i];
     const size_t step = z.dStreamOutSize();
