@@ -1161,7 +1161,7 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   launch_b3_prepare(dch, nchunks, n, (uint64_t *)ctx->b3_gcnt.p, (uint64_t *)ctx->b3_goff.p, hist, err, ctx->b3_tmp.p,
                     tmpb, st);
   launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, hist, (uint32_t *)ctx->b3_owner.p,
-                 (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
+                 (uint32_t *)ctx->b3_nodes.p, ids_dev, (uint64_t *)ctx->b3_gcnt.p, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
   uint32_t herr = 0;
@@ -1176,7 +1176,7 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
     if ((rc = ensure(ctx, ctx->b3_owner, bound * 4)) || (rc = ensure(ctx, ctx->b3_nodes, bound * 32))) return rc;
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
     launch_b3_hash((const uint8_t *)d_data, dch, nchunks, goff, bound, hist, (uint32_t *)ctx->b3_owner.p,
-                   (uint32_t *)ctx->b3_nodes.p, ids_dev, st);
+                   (uint32_t *)ctx->b3_nodes.p, ids_dev, (uint64_t *)ctx->b3_gcnt.p, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_end, st));
     HIP_TRY(hipStreamSynchronize(st));

@@ -13,7 +13,7 @@ size_t b3_tmp_bytes(uint64_t nchunks);
 // upper bound of the 16-KiB leaf groups of a boundary list covering total_bytes
 uint64_t b3_group_bound(uint64_t total_bytes, uint64_t nchunks);
 // device words of the tail-group histogram and bin cursors (hist argument)
-constexpr size_t kB3HistWords = 512;
+constexpr size_t kB3HistWords = 520;  // tail bins, bin cursors, wide-tree list count and draw counter
 // gcnt[0..n] (n + 1 entries), goff[0..n] = exclusive prefix of the packed
 // counts (low 32 bits full groups, high 32 bits tail groups);
 // b3_groups_total(goff[n]) = groups.  Chunks outside [0, nbytes) set *err and
@@ -26,8 +26,10 @@ uint64_t b3_groups_total(uint64_t packed);
 // sizes the grid (b3_group_bound, exact for disjoint chunks).  When the group
 // total exceeds it (overlapping or repeated chunks) the kernels write nothing
 // and the caller re-runs with group_bound = the total.  hist: as prepared.
+// gcnt: the prepare step's count buffer (free after its scan; reused for the
+// list of chunks the wave-parallel tree takes).
 void launch_b3_hash(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *goff,
                     uint64_t group_bound, uint32_t *hist, uint32_t *owner, uint32_t *nodes, uint8_t *ids,
-                    hipStream_t stream);
+                    uint64_t *gcnt, hipStream_t stream);
 
 }  // namespace mcdc

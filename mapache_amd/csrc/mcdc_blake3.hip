@@ -20,12 +20,15 @@
 //                 quad-coalesced loads transposed through LDS, the group's
 //                 subtree reduced on the fly (completed subtrees in registers);
 //                 a chunk of <= 16 leaves finishes its ID here (ROOT)
-//   k_b3_tree     one lane per larger chunk: level-by-level pairing of its
+//   k_b3_tree_wide one wave per chunk of more than 16 groups (nodes in LDS)
+//   k_b3_tree     one lane per chunk of 2-16 groups: level-by-level pairing of its
 //                 group nodes (the last node of an odd level moves up
 //                 unchanged — the same tree as the specification's stack rule)
 // Integer VALU work (~11 32-bit ops per input byte), no MFMA.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+
+#include <algorithm>
 
 #include "mcdc_blake3.h"
 
@@ -156,6 +159,8 @@ using namespace b3;
 // its lane-cycles idle on the 64 GiB stream).
 constexpr uint32_t kGroupBytes = kGroupLeaves * kLeaf;
 constexpr int kTailBins = 256;
+// chunks of kTreeLaneMax < groups <= kTreeWaveMax: the wave-parallel tree
+constexpr uint64_t kTreeLaneMax = 16, kTreeWaveMax = 512;
 
 __device__ __forceinline__ uint64_t gtotal(uint64_t x) { return (x & 0xffffffffull) + (x >> 32); }
 
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(256) void k_b3_groups(const DevChunk *chunks, uint6
 // F + (start of their bin) + (arrival order within the bin).
 __global__ __launch_bounds__(256) void k_b3_owner(const DevChunk *chunks, const uint64_t *goff, uint64_t n,
                                                   uint64_t bound, const uint32_t *hist, uint32_t *cur,
-                                                  uint32_t *owner) {
+                                                  uint32_t *owner, uint32_t *wide, uint32_t *wide_cnt) {
   __shared__ uint32_t bs[kTailBins], lc[kTailBins];
   const uint32_t t = threadIdx.x;
   bs[t] = hist[t];
@@ -209,6 +214,10 @@ __global__ __launch_bounds__(256) void k_b3_owner(const DevChunk *chunks, const 
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
   const uint64_t last = goff[n];
   const bool ok = i < n && gtotal(last) <= bound;
+  if (ok) {  // chunks for the wave-parallel tree
+    const uint64_t m = gtotal(goff[i + 1]) - gtotal(goff[i]);
+    if (m > kTreeLaneMax && m <= kTreeWaveMax) wide[atomicAdd(wide_cnt, 1u)] = (uint32_t)i;
+  }
   uint64_t a = 0, b = 0;
   uint32_t bin = 0, rank = 0;
   bool tl = false;
@@ -442,6 +451,74 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
 // One lane per chunk of more than one group: level-by-level pairing of its
 // group nodes in place (nodes [goff[i], goff[i+1]) belong to this lane only).
+// Chunks of more than kTreeLaneMax groups (over 256 KiB: mapache's own
+// 512K/1M/8M chunks, up to 512 groups) are paired by a whole wave
+// (k_b3_tree_wide): per level, lanes take pairs, the nodes live in LDS, so a
+// 512-group chunk costs 13 wave-steps instead of 511 serial compressions on
+// one lane (the tree was 11 % of a 512K/1M/8M ID pass).  k_b3_owner lists
+// these chunks; persistent waves draw them from a counter.  Longer chunks (the
+// packer's ~16 MiB packs) keep the lane path.
+
+// order the wave's LDS accesses (fences keep the compiler from moving a
+// lane's write above another lane's read of the same node)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(64) void k_b3_tree_wide(const uint64_t *goff, uint64_t n, uint64_t bound,
+                                                     const uint32_t *nodes, uint8_t *ids, const uint32_t *wide,
+                                                     uint32_t *cnt) {
+  __shared__ uint4 nd[2 * kTreeWaveMax];  // node j = nd[2 j], nd[2 j + 1] (16 KiB)
+  const uint32_t lane = threadIdx.x;
+  if (gtotal(goff[n]) > bound) return;
+  const uint32_t total = cnt[0];
+  // persistent waves draw chunks from the list (drawn before the loop and at
+  // its end, lane 0's value read explicitly: see next_tile in mcdc_aead.hip)
+  auto draw = [&]() {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(cnt + 1, 1u);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  };
+  uint32_t k = draw();
+  while (k < total) {
+    const uint64_t i = wide[k];
+    const uint64_t g0 = gtotal(goff[i]);
+    uint32_t m = (uint32_t)(gtotal(goff[i + 1]) - g0);
+    const uint4 *src = reinterpret_cast<const uint4 *>(nodes + 8 * g0);
+    for (uint32_t t = lane; t < 2 * m; t += 64) nd[t] = src[t];
+    wave_lds_sync();
+    while (m > 1) {
+      const uint32_t pairs = m / 2;
+      for (uint32_t t0 = 0; t0 < pairs; t0 += 64) {  // (batch t0 reads nodes >= 2 t0, writes nodes < t0 + 64)
+        const uint32_t t = t0 + lane;
+        uint32_t l[8], r[8], o[8];
+        if (t < pairs) {
+          const uint4 a = nd[4 * t], bb = nd[4 * t + 1], c = nd[4 * t + 2], d = nd[4 * t + 3];
+          l[0] = a.x; l[1] = a.y; l[2] = a.z; l[3] = a.w; l[4] = bb.x; l[5] = bb.y; l[6] = bb.z; l[7] = bb.w;
+          r[0] = c.x; r[1] = c.y; r[2] = c.z; r[3] = c.w; r[4] = d.x; r[5] = d.y; r[6] = d.z; r[7] = d.w;
+          parent(l, r, m == 2 ? kRoot : 0, o);
+        }
+        wave_lds_sync();  // (every read of the batch before any write)
+        if (t < pairs) {
+          nd[2 * t] = make_uint4(o[0], o[1], o[2], o[3]);
+          nd[2 * t + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+        }
+        wave_lds_sync();
+      }
+      if (m & 1) {  // the last node of an odd level moves up unchanged
+        if (lane < 2) nd[2 * pairs + lane] = nd[2 * (m - 1) + lane];
+        wave_lds_sync();
+      }
+      m = pairs + (m & 1);
+    }
+    if (lane < 2) reinterpret_cast<uint4 *>(ids + 32ull * i)[lane] = nd[lane];
+    wave_lds_sync();
+    k = draw();
+  }
+}
+
 __global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t n, uint64_t bound, uint32_t *nodes,
                           uint8_t *ids) {
   MCDC_VGPR_PAD(48);  // 48 used: not an exact fill (MCDC_VGPR_PAD)
@@ -449,6 +526,7 @@ __global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t
   if (i >= n || gtotal(goff[n]) > bound) return;
   uint64_t m = gtotal(goff[i + 1]) - gtotal(goff[i]);
   if (m < 2) return;  // finished by k_b3_leaves
+  if (m > kTreeLaneMax && m <= kTreeWaveMax) return;  // k_b3_tree_wide
   uint32_t *nd = nodes + 8 * gtotal(goff[i]);
   uint32_t l[8], r[8], o[8];
   while (m > 1) {
@@ -490,13 +568,18 @@ void launch_b3_prepare(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 
 void launch_b3_hash(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *goff,
                     uint64_t group_bound, uint32_t *hist, uint32_t *owner, uint32_t *nodes, uint8_t *ids,
-                    hipStream_t stream) {
+                    uint64_t *gcnt, hipStream_t stream) {
   if (n == 0) return;
-  (void)hipMemsetAsync(hist + kTailBins, 0, kTailBins * sizeof(uint32_t), stream);  // bin cursors
+  // bin cursors, the wide-tree list count and draw counter
+  (void)hipMemsetAsync(hist + kTailBins, 0, (kB3HistWords - kTailBins) * sizeof(uint32_t), stream);
+  uint32_t *wide = reinterpret_cast<uint32_t *>(gcnt), *wcnt = hist + 2 * kTailBins;
   hipLaunchKernelGGL(k_b3_owner, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n,
-                     group_bound, (const uint32_t *)hist, hist + kTailBins, owner);
+                     group_bound, (const uint32_t *)hist, hist + kTailBins, owner, wide, wcnt);
   hipLaunchKernelGGL(k_b3_leaves, dim3((unsigned)((group_bound + 255) / 256)), dim3(256), 0, stream, base, chunks,
                      goff, (const uint32_t *)owner, n, group_bound, nodes, ids);
+  // (at most as many waves as fit: 16 KiB of LDS each)
+  hipLaunchKernelGGL(k_b3_tree_wide, dim3((unsigned)std::min<uint64_t>(n, 2048)), dim3(64), 0, stream, goff, n,
+                     group_bound, (const uint32_t *)nodes, ids, (const uint32_t *)wide, wcnt);
   hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n, group_bound,
                      nodes, ids);
 }

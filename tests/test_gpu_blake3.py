@@ -166,3 +166,24 @@ def test_many_tail_lengths_in_list_order(ctx):
     ref = O.chunk_ids(data, c, threads=8)
     bad = np.nonzero(~(got == ref).all(axis=1))[0]
     assert bad.size == 0, [(int(c["offset"][i]), int(c["length"][i])) for i in bad[:10]]
+
+
+def test_large_chunks_tree_paths(ctx):
+    """Chunks of 17-1536 groups go to the wave-parallel tree (k_b3_tree_wide),
+    longer ones to the lane path: 256 KiB + 1, 1 MiB, 8 MiB (mapache's max),
+    16 MiB + 1 (a pack's size), 24 MiB (the wave path's limit), 24 MiB + 1 and
+    40 MiB + 3 (the lane path), at odd offsets."""
+    lens = [(256 << 10) + 1, 1 << 20, 8 << 20, (16 << 20) + 1, 24 << 20, (24 << 20) + 1, (40 << 20) + 3]
+    pairs, pos = [], 5
+    for n_ in lens:
+        pairs.append((pos, n_))
+        pos += n_ + 3
+    data = O.random_bytes(pos, SEED + 12)
+    dp = _device_bytes(ctx, data)
+    try:
+        got = ctx.chunk_ids(dp, data.size, _chunks(pairs))
+    finally:
+        ctx.device_free(dp)
+    ref = O.chunk_ids(data, _chunks(pairs), threads=8)
+    bad = [lens[i] for i in range(len(pairs)) if not (got[i] == ref[i]).all()]
+    assert not bad, bad
