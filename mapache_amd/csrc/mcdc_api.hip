@@ -1122,6 +1122,8 @@ int mcdc_chunk_ids_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcd
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if ((!d_data && n) || (nchunks && (!chunks || !ids))) return fail(MCDC_E_INVALID, "NULL argument");
+  // (chunk indices are 32-bit in the group owners and the wide-tree list; the scan counts in int)
+  if (nchunks >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many chunks (%zu)", nchunks);
   const double t0 = now_ms();
   hipStream_t st = ctx->stream;
   ctx->timing = mcdc_timing{};
