@@ -67,8 +67,55 @@ __global__ void k_zframe_sizes(const DevChunk *chunks, uint64_t n, uint64_t nbyt
 typedef uint32_t zf_u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) zf_u32x4 *zf_gq;
 
-__global__ __launch_bounds__(256) void k_zframe_write(const uint8_t *base, const DevChunk *chunks, uint64_t n,
-                                                      const uint64_t *off, uint8_t *out, uint64_t *ext) {
+// Same-box A/B (tools/zf_ab.sh, 16 GiB, 215 074 chunks): non-temporal frame
+// stores 7.07 ms vs 7.40-7.56 ms plain; non-temporal loads, 2-4 quads per
+// thread per step and 512/1024-thread workgroups gave nothing repeatable.
+#ifndef MCDC_ZF_NT  // non-temporal stores of the frames (bit 0), loads of the chunk bytes (bit 1)
+#define MCDC_ZF_NT 1
+#endif
+#ifndef MCDC_ZF_THREADS  // threads per chunk's workgroup
+#define MCDC_ZF_THREADS 256
+#endif
+
+// the 16 bytes of output quad p of the frame of a len-byte chunk at src
+__device__ __forceinline__ uint4 zquad(const uint8_t *__restrict__ src, uint64_t len, uint32_t fl32, uint32_t p) {
+  // a quad wholly inside one block's data: one misaligned 16-byte load
+  if (p >= kZHdr && p + 16 <= fl32) {
+    const uint32_t a = p - (uint32_t)kZHdr, k = a / (uint32_t)(kZBlock + kZBlkHdr),
+                   r = a - k * (uint32_t)(kZBlock + kZBlkHdr);
+    if (r >= kZBlkHdr && r + 16 <= kZBlock + kZBlkHdr) {
+      const uint32_t s = k * (uint32_t)kZBlock + (r - (uint32_t)kZBlkHdr);
+#if MCDC_ZF_NT & 2
+      const zf_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<zf_gq>(reinterpret_cast<uintptr_t>(src + s)));
+#else
+      const zf_u32x4 x = *reinterpret_cast<zf_gq>(reinterpret_cast<uintptr_t>(src + s));
+#endif
+      return make_uint4(x.x, x.y, x.z, x.w);
+    }
+  }
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t b = 0; b < 16 && p + b < fl32; ++b) w[b >> 2] |= (uint32_t)zbyte(src, len, p + b) << (8 * (b & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void zstore(uint8_t *__restrict__ dst, uint32_t fl32, uint32_t p, uint4 v) {
+  if (p + 16 <= fl32) {
+#if MCDC_ZF_NT & 1
+    zf_u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<zf_u32x4 *>(dst + p));
+#else
+    *reinterpret_cast<uint4 *>(dst + p) = v;
+#endif
+  } else {  // the frame's last, partial quad: its own bytes only (the rest is the alignment gap)
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t b = 0; p + b < fl32; ++b) dst[p + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+  }
+}
+
+__global__ __launch_bounds__(MCDC_ZF_THREADS) void k_zframe_write(const uint8_t *__restrict__ base,
+                                                                  const DevChunk *chunks, uint64_t n,
+                                                                  const uint64_t *off, uint8_t *__restrict__ out,
+                                                                  uint64_t *ext) {
   const uint64_t i = blockIdx.x;
   if (i >= n) return;
   const DevChunk c = chunks[i];
@@ -80,35 +127,8 @@ __global__ __launch_bounds__(256) void k_zframe_write(const uint8_t *base, const
   const uint8_t *src = base + c.offset;
   uint8_t *dst = out + o;
   // (32-bit positions: chunks of 2 GiB and more are rejected by k_zframe_sizes)
-  const uint32_t fl32 = (uint32_t)fl;
-  for (uint32_t p = 16 * threadIdx.x; p < fl32; p += 16 * blockDim.x) {
-    // a quad wholly inside one block's data: one misaligned 16-byte load
-    bool inside = false;
-    uint32_t s = 0;
-    if (p >= kZHdr && p + 16 <= fl32) {
-      const uint32_t a = p - (uint32_t)kZHdr, k = a / (uint32_t)(kZBlock + kZBlkHdr),
-                     r = a - k * (uint32_t)(kZBlock + kZBlkHdr);
-      if (r >= kZBlkHdr && r + 16 <= kZBlock + kZBlkHdr) {
-        inside = true;
-        s = k * (uint32_t)kZBlock + (r - (uint32_t)kZBlkHdr);
-      }
-    }
-    uint4 v;
-    if (inside) {
-      const zf_u32x4 x = *reinterpret_cast<zf_gq>(reinterpret_cast<uintptr_t>(src + s));
-      v = make_uint4(x.x, x.y, x.z, x.w);
-    } else {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t b = 0; b < 16 && p + b < fl; ++b) w[b >> 2] |= (uint32_t)zbyte(src, c.length, p + b) << (8 * (b & 3));
-      v = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    if (p + 16 <= fl32) {
-      *reinterpret_cast<uint4 *>(dst + p) = v;
-    } else {  // the frame's last, partial quad: its own bytes only (the rest is the alignment gap)
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      for (uint32_t b = 0; p + b < fl; ++b) dst[p + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-    }
-  }
+  const uint32_t fl32 = (uint32_t)fl, step = 16 * blockDim.x;
+  for (uint32_t p = 16 * threadIdx.x; p < fl32; p += step) zstore(dst, fl32, p, zquad(src, c.length, fl32, p));
 }
 
 }  // namespace
@@ -129,7 +149,9 @@ void launch_zframe_sizes(const DevChunk *chunks, uint64_t n, uint64_t nbytes, ui
 
 void launch_zframe_write(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *off, uint8_t *out,
                          uint64_t *ext, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_zframe_write, dim3((unsigned)n), dim3(256), 0, st, base, chunks, n, off, out, ext);
+  if (n)
+    hipLaunchKernelGGL(k_zframe_write, dim3((unsigned)n), dim3(MCDC_ZF_THREADS), 0, st, base, chunks, n, off, out,
+                       ext);
 }
 
 }  // namespace mcdc
