@@ -614,7 +614,7 @@ def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> 
 
 
 def corpus_sharded(ctx, p, files_per_gpu: int, file_bytes: int, steps: int, warmup: int, world: int, rank: int,
-                   barrier, allreduce_max, gather) -> dict:
+                   barrier, allreduce_max, gather, oracle_threads: int = 16) -> dict:
     """BASELINE configs[4]: a corpus of world x files_per_gpu files of file_bytes
     (file i = the counter-based stream of seed SEED ^ (i + 1)), assigned to
     ranks by shard.assign_files (no data exchange); each rank chunks its files
@@ -643,32 +643,42 @@ def corpus_sharded(ctx, p, files_per_gpu: int, file_bytes: int, steps: int, warm
         mine_s = time.perf_counter() - t0
         elapsed = allreduce_max(mine_s)
         # gathered result: per-file counts and an order-sensitive digest of the
-        # whole corpus's boundary lists (file order); parity probe: the rank's
-        # first and last files against the oracle
+        # whole corpus's boundary lists (file order).  Parity (after timing):
+        # every file of this rank against the oracle regenerating it on
+        # `oracle_threads` host threads (oracle.random_files_digest), and the
+        # gathered corpus digest against the fold of the oracle's digests.
         chunks = ctx.d2h_chunks(d_out, total)
         starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
         per_file = [(i, int(counts[k]), _lib.digest(chunks[starts[k]:starts[k + 1]])) for k, i in enumerate(mine)]
         from oracle import oracle as O
-        ok = True
-        for k in sorted({0, len(mine) - 1}):
-            ref = O.chunk(O.Params(*PARAMS), O.random_bytes(file_bytes, SEED ^ (mine[k] + 1)))
-            ok &= _same(chunks[starts[k]:starts[k + 1]], ref)
-        parts = gather((per_file, bool(ok), mine_s))
+        t0 = time.perf_counter()
+        rc, rd, _ = O.random_files_digest(O.Params(*PARAMS), [SEED ^ (i + 1) for i in mine], 0,
+                                          [file_bytes] * len(mine), threads=oracle_threads)
+        oracle_s = time.perf_counter() - t0
+        ref_file = [(i, int(rc[k]), int(rd[k])) for k, i in enumerate(mine)]
+        parts = gather((per_file, ref_file, mine_s, oracle_s))
     finally:
         ctx.device_free(d_out)
         ctx.device_free(arena)
     if parts is None:
         return {}
     allf = sorted(x for part in parts for x in part[0])
-    dig = 0
-    for _, c, d in allf:
-        dig = (dig * 0x100000001b3 ^ d ^ c) & ((1 << 64) - 1)
+    allr = sorted(x for part in parts for x in part[1])
+    dig = shard.corpus_digest([c for _, c, _ in allf], [d for _, _, d in allf])
+    rdig = shard.corpus_digest([c for _, c, _ in allr], [d for _, _, d in allr])
+    bad = [i for (i, c, d), (_, rc_, rd_) in zip(allf, allr) if (c, d) != (rc_, rd_)]
     total_bytes = nfiles * file_bytes
     return {"files": nfiles, "file_bytes": file_bytes, "bytes": total_bytes, "steps": steps,
             "ms_per_step": round(elapsed / steps * 1e3, 3), "gib_s": round(total_bytes * steps / elapsed / GIB, 2),
             "per_rank_gib_s": [round(nbytes * steps / part[2] / GIB, 2) for part in parts],
             "chunks": int(sum(c for _, c, _ in allf)), "corpus_digest": f"{dig:016x}",
-            "parity_probe_files": 2 * len(parts), "parity_probe_ok": bool(all(part[1] for part in parts)),
+            "oracle_corpus_digest": f"{rdig:016x}",
+            "parity_ok": bool(len(allf) == nfiles and [x[0] for x in allf] == list(range(nfiles))
+                              and not bad and dig == rdig),
+            "parity_files_checked": len(allr), "parity_bad_files": bad[:8],
+            "oracle_seconds_per_rank": [round(part[3], 2) for part in parts],
+            "parity": f"every file against oracle.random_files_digest ({oracle_threads} host threads per rank, "
+                      f"after the timed steps); corpus digest = shard.corpus_digest",
             "assignment": "shard.assign_files (LPT by bytes; equal sizes -> round robin), no data exchange",
             "data": "synthetic uniform-random files (device PRNG, per-file seeds)"}
 
@@ -692,6 +702,9 @@ def main() -> int:
     ap.add_argument("--no-ids", action="store_true", help="skip the chunk-ID (BLAKE3) stage")
     ap.add_argument("--no-seal", action="store_true", help="skip the SecureStorage sealing stage")
     ap.add_argument("--encode-gib", type=float, default=1.0, help="host encode/decode sample (GiB, 0: skip)")
+    ap.add_argument("--parity", action="store_true",
+                    help="after timing, gather every rank's exact chunks of the split stream and compare the "
+                         "whole list with the oracle's (small --gib; tests/test_gpu_multirank.py)")
     a = ap.parse_args()
 
     world, rank, local = _dist()
@@ -819,6 +832,21 @@ def main() -> int:
                         "gib_s": round((hi - s) / (float(np.mean(dev_ms)) * 1e-3) / GIB, 2),
                         "call_ms": round(float(np.mean(total_ms)), 3)},
     }
+    if a.parity:  # the whole stream's boundary list against the oracle (after timing)
+        if world == 1:
+            mine = ctx.d2h_chunks(d_out, ctx.chunk_device_to_device(p, dp, n, d_out, cap))
+        else:
+            spec = shard.DeviceChunks(ctx, d_out, ctx.chunk_device_to_device(p, dp, hi - s, d_out, cap), base=s)
+            mine, _ = shard.split_stream(lambda x, y: ctx.chunk_device(p, dp + (x - s), y - x), allgather, s, e,
+                                         total, PARAMS[2], rank, world, spec=spec)
+        parts = gather(mine)
+        if parts is not None:
+            from oracle import oracle as O
+            allc = np.concatenate(parts)
+            rk, rdig, rsum = O.random_stream_digest(O.Params(*PARAMS), SEED, total)
+            result["stream_parity"] = {"chunks": int(len(allc)), "oracle_chunks": int(rk),
+                                       "digest": f"{_lib.digest(allc):016x}", "oracle_digest": f"{rdig:016x}",
+                                       "ok": bool(len(allc) == rk and _lib.digest(allc) == rdig and rsum == total)}
     if world > 1:
         st = gather(dict(split_stats))
         if st:
@@ -877,7 +905,7 @@ def main() -> int:
     if a.corpus_files_per_gpu > 0:
         try:
             r = corpus_sharded(ctx, p, a.corpus_files_per_gpu, 8 << 20, max(3, a.steps // 2), 1, world, rank,
-                               barrier, allreduce_max, gather)
+                               barrier, allreduce_max, gather, max(1, min(a.cpu_threads, _cpus())))
             if r:
                 result["corpus_sharded"] = r
         except Exception as ex:  # reported, never silently dropped

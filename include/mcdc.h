@@ -236,7 +236,8 @@ int mcdc_decode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h
  * ("store") mode: the format of SecureStorage::compress (storage.rs:74-84;
  * window 2^20, no checksum) without entropy coding — what zstd itself emits
  * for incompressible data — so chunk -> frame -> seal stays on the GPU and the
- * blobs stay readable by mapache's decoder (storage.rs:87-94).  Frame i is
+ * blobs stay readable by mapache's decoder (storage.rs:87-94).  d_out must be
+ * 16-byte aligned (else MCDC_E_INVALID).  Frame i is
  * written at a 16-byte aligned offset of d_out; frames[i] (host or device)
  * receives its (offset, length), ready for mcdc_seal_device.  *out_bytes: the
  * output span (also on MCDC_E_CAPACITY).  chunks: host or device; a chunk

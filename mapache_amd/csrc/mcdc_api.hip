@@ -1431,6 +1431,8 @@ int mcdc_zstd_frames_device(mcdc_ctx *ctx, const void *d_data, size_t n, const m
   if ((!d_data && n) || (nchunks && (!chunks || !frames))) return fail(MCDC_E_INVALID, "NULL argument");
   if ((d_data && !is_device_ptr(d_data)) || (d_out && !is_device_ptr(d_out)))
     return fail(MCDC_E_INVALID, "d_data / d_out must be device pointers");
+  // k_zframe_write stores whole 16-byte quads at d_out + off[i]
+  if ((uintptr_t)d_out & 15) return fail(MCDC_E_INVALID, "d_out must be 16-byte aligned");
   if (out_bytes) *out_bytes = 0;
   if (nchunks == 0) return MCDC_OK;
   if (nchunks >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many chunks (%zu)", nchunks);

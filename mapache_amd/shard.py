@@ -95,6 +95,17 @@ def chunk_sharded(sizes: Sequence[int], chunk_indices: Callable[[list], "tuple[n
     return result
 
 
+def corpus_digest(counts: Sequence[int], digests: Sequence[int]) -> int:
+    """Order-sensitive digest of a whole corpus's boundary lists, in file order:
+    a fold of each file's chunk count and boundary-list digest (mcdc_digest of
+    its file-relative records).  The bench gathers it across ranks; the oracle
+    side folds oracle.random_files_digest the same way."""
+    d = 0
+    for c, x in zip(counts, digests):
+        d = (d * 0x100000001b3 ^ int(x) ^ int(c)) & ((1 << 64) - 1)
+    return d
+
+
 def chunk_files_sharded(files: Sequence, chunk: ChunkFn, group=None, dst: int | None = None) -> list[np.ndarray] | None:
     """Chunk `files` (byte buffers, identical on every rank) across the ranks of
     `group`: ``chunk(list_of_buffers) -> (chunks, counts)`` is this rank's batch

@@ -402,3 +402,74 @@ void oc_fill_random(uint8_t *dst, uint64_t pos, size_t n, uint64_t seed) {
 uint64_t oc_file_seed(uint64_t seed, uint64_t file_index) {
   return mix64(seed ^ ((file_index + 1) * 0xd1b54a32d192ed03ULL));
 }
+
+/* Many files of the counter-based streams, each regenerated in its own buffer
+ * and chunked as one file (a new StreamCDC per file, processor.rs:173), on
+ * `threads` threads: file i = bytes [pos[i], pos[i] + len[i]) of the stream of
+ * seeds[i].  Per file: its chunk count, oc_chunk_digest of its boundary list
+ * (offsets relative to the file) and oc_hash_digest of its hashes.  The host
+ * never holds more than threads x max(len) bytes: full-size parity for the
+ * many-file configs.  Returns 0, or -1 on allocation failure. */
+typedef struct {
+  const oc_params *p;
+  const uint64_t *seeds, *pos, *len;
+  size_t nfiles, next;
+  pthread_mutex_t mu;
+  uint64_t *counts, *digests, *hdigests;
+  int failed;
+} rfiles_job;
+
+static void *rfiles_worker(void *arg) {
+  rfiles_job *j = (rfiles_job *)arg;
+  uint8_t *buf = NULL;
+  size_t bcap = 0;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    size_t i = j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (i >= j->nfiles) break;
+    const size_t n = (size_t)j->len[i];
+    if (n > bcap) {
+      free(buf);
+      buf = (uint8_t *)malloc(n ? n : 1);
+      bcap = buf ? n : 0;
+      if (!buf) { j->failed = 1; continue; }
+    }
+    oc_fill_random(buf, j->pos[i], n, j->seeds[i]);
+    size_t off = 0, k = 0;
+    uint64_t d = 0, hd = 0;
+    while (off < n) {
+      uint64_t h;
+      size_t c;
+      oc_cut_gear(j->p, buf + off, n - off, &h, &c);
+      if (c == 0) break;
+      d = oc_digest_step(d, off, c);
+      hd = oc_digest_step(hd, k, h);
+      ++k;
+      off += c;
+    }
+    j->counts[i] = k;
+    j->digests[i] = d;
+    if (j->hdigests) j->hdigests[i] = hd;
+  }
+  free(buf);
+  return NULL;
+}
+
+int oc_random_files_digest(const oc_params *p, const uint64_t *seeds, const uint64_t *pos, const uint64_t *len,
+                           size_t nfiles, int threads, uint64_t *counts, uint64_t *digests, uint64_t *hdigests) {
+  pthread_once(&gear_once, gear_init);
+  rfiles_job j;
+  memset(&j, 0, sizeof j);
+  j.p = p; j.seeds = seeds; j.pos = pos; j.len = len; j.nfiles = nfiles;
+  j.counts = counts; j.digests = digests; j.hdigests = hdigests;
+  pthread_mutex_init(&j.mu, NULL);
+  if (threads < 1) threads = 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+  if (!th) return -1;
+  for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, rfiles_worker, &j);
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  pthread_mutex_destroy(&j.mu);
+  return j.failed ? -1 : 0;
+}

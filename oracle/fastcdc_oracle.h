@@ -117,6 +117,14 @@ size_t oc_random_stream_digest_h(const oc_params *p, uint64_t seed, uint64_t n, 
  * oc_digest_step(d, index, hash). */
 uint64_t oc_hash_digest(const uint64_t *hashes, size_t n);
 
+/* Many files of counter-based streams (file i = [pos[i], pos[i] + len[i]) of
+ * the stream of seeds[i]), each chunked as one file on `threads` threads:
+ * per-file count, oc_chunk_digest-style boundary digest (file-relative
+ * offsets) and hash digest (hdigests may be NULL).  0 ok, -1 allocation. */
+int oc_random_files_digest(const oc_params *p, const uint64_t *seeds, const uint64_t *pos,
+                           const uint64_t *len, size_t nfiles, int threads, uint64_t *counts,
+                           uint64_t *digests, uint64_t *hdigests);
+
 /* Counter-based byte generator shared with the device fill kernel and the
  * bench: byte i = (splitmix64_at(seed, i/8) >> 8*(i%8)) & 0xff. */
 void oc_fill_random(uint8_t *dst, uint64_t pos, size_t n, uint64_t seed);

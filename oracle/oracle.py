@@ -88,6 +88,10 @@ def lib():
         L.oc_random_stream_digest_h.argtypes = [ctypes.POINTER(OcParams), ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_size_t, u64p, u64p, u64p]
         L.oc_random_stream_digest_h.restype = ctypes.c_size_t
+        L.oc_random_files_digest.argtypes = [ctypes.POINTER(OcParams), ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        L.oc_random_files_digest.restype = ctypes.c_int
         L.oc_hash_digest.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
         L.oc_hash_digest.restype = ctypes.c_uint64
         L.oc_fill_random.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint64]
@@ -217,6 +221,23 @@ def random_stream_digest(params: Params, seed: int, n: int, slab: int = 256 << 2
     k = lib().oc_random_stream_digest_h(ctypes.byref(params.c()), seed, n, slab, ctypes.byref(d), ctypes.byref(sm),
                                         ctypes.byref(hd))
     return (k, d.value, sm.value, hd.value) if hashes else (k, d.value, sm.value)
+
+
+def random_files_digest(params: Params, seeds, pos, lens, threads: int = 16):
+    """(counts, digests, hash digests) per file; file i = bytes [pos[i], pos[i] +
+    lens[i]) of the counter-based stream of seeds[i], chunked as one file
+    (oc_random_files_digest: regenerated per file on `threads` threads, so the
+    host never holds the corpus).  digests[i] == mcdc digest of the file's
+    boundary list (file-relative offsets), hash digests == hash_digest."""
+    n = len(lens)
+    a = [np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=np.uint64), (n,))) for x in (seeds, pos, lens)]
+    counts, dig, hd = (np.zeros(max(n, 1), np.uint64) for _ in range(3))
+    rc = lib().oc_random_files_digest(ctypes.byref(params.c()), a[0].ctypes.data, a[1].ctypes.data,
+                                      a[2].ctypes.data, n, threads, counts.ctypes.data, dig.ctypes.data,
+                                      hd.ctypes.data)
+    if rc:
+        raise RuntimeError("oc_random_files_digest failed")
+    return counts[:n], dig[:n], hd[:n]
 
 
 def hash_digest(chunks: np.ndarray) -> int:

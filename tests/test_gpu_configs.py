@@ -10,6 +10,15 @@
   checks, and four more calls (device and pinned-host output) identical to
   the first, record for record (the k_emit VGPR item, DESIGN.md §3a, changed
   ~3 % of the hashes of some calls).
+* configs[2]: 10 000 independent 8 MiB files (78 GiB) in one batched device
+  call (bench.py batch_files' arena: file i = bytes [8 MiB i, 8 MiB (i+1)) of
+  the stream of SEED ^ 0xB0): every file's count, boundary digest and hash
+  digest against oracle.random_files_digest, which regenerates each file on 16
+  host threads (the host never holds the 78 GiB).
+* configs[4], one rank's slice: 8192 files of 8 MiB (file i = the stream of
+  SEED ^ (i + 1), bench.py corpus_sharded) through shard.chunk_sharded at
+  world 1, every file and the corpus digest (shard.corpus_digest) against the
+  oracle's.
 * configs[3] stand-in: the bench's 80 000-file log-normal mix (median 8 KiB,
   1.34 GB; bench.py small_files), one batched device call, every file's
   boundary list and count against oracle.chunk_files.
@@ -17,7 +26,7 @@
 import numpy as np
 import pytest
 
-from mapache_amd import _lib
+from mapache_amd import _lib, shard
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -89,3 +98,75 @@ def test_configs3_80k_small_files(ctx):
     bad = np.nonzero((got["offset"] != ref["offset"]) | (got["length"] != ref["length"]) |
                      (got["hash"] != ref["hash"]))[0]
     assert bad.size == 0, f"first mismatch at chunk {bad[0]}"
+
+
+def _per_file(g, counts):
+    """(count, boundary digest, hash digest) of every file of a batch result."""
+    starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    return [(int(counts[k]), _lib.digest(g[starts[k]:starts[k + 1]]), O.hash_digest(g[starts[k]:starts[k + 1]]))
+            for k in range(len(counts))]
+
+
+def test_configs2_10000_files_full(ctx):
+    nfiles, size = 10_000, 8 << 20
+    n = nfiles * size
+    p = _lib.params(*P16)
+    offs = np.arange(nfiles, dtype=np.uint64) * np.uint64(size)
+    lens = np.full(nfiles, size, dtype=np.uint64)
+    big = _lib.Context(0, 1 << 30)
+    try:
+        arena = big.device_alloc(n)
+        cap = nfiles * (size // (P16[0] - 1) + 2)
+        d_out = big.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+        try:
+            big.fill_random(arena, n, SEED ^ 0xB0)
+            total, counts = big.chunk_batch_device_to_device(p, arena, offs, lens, d_out, cap)
+            g = big.d2h_chunks(d_out, total)
+        finally:
+            big.device_free(d_out)
+            big.device_free(arena)
+    finally:
+        big.close()
+    assert counts.size == nfiles and int(counts.sum()) == total
+    got = _per_file(g, counts)
+    rc, rd, rh = O.random_files_digest(O.Params(*P16), SEED ^ 0xB0, offs, lens, threads=16)
+    bad = [i for i in range(nfiles) if got[i] != (int(rc[i]), int(rd[i]), int(rh[i]))]
+    assert not bad, (len(bad), bad[:8])
+    # size-independent invariants over the whole list
+    starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    assert (g["offset"][starts[:-1]] == 0).all()
+    assert int(g["length"].sum()) == n
+
+
+def test_configs4_rank_slice_8192_files(ctx):
+    nfiles, size = 8192, 8 << 20
+    p = _lib.params(*P16)
+    sizes = [size] * nfiles
+    big = _lib.Context(0, 1 << 30)
+    try:
+        arena = big.device_alloc(nfiles * size)
+        cap = nfiles * (size // (P16[0] - 1) + 2)
+        d_out = big.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+        try:
+            def chunk_indices(idx):
+                for k, i in enumerate(idx):
+                    big.fill_random(arena + k * size, size, SEED ^ (i + 1))
+                offs = np.arange(len(idx), dtype=np.uint64) * np.uint64(size)
+                total, counts = big.chunk_batch_device_to_device(p, arena, offs, np.full(len(idx), size, np.uint64),
+                                                                 d_out, cap)
+                return big.d2h_chunks(d_out, total), counts
+            per_file = shard.chunk_sharded(sizes, chunk_indices)
+        finally:
+            big.device_free(d_out)
+            big.device_free(arena)
+    finally:
+        big.close()
+    assert len(per_file) == nfiles
+    cnt = [len(c) for c in per_file]
+    dig = [_lib.digest(c) for c in per_file]
+    rc, rd, rh = O.random_files_digest(O.Params(*P16), [SEED ^ (i + 1) for i in range(nfiles)], 0, sizes,
+                                       threads=16)
+    assert shard.corpus_digest(cnt, dig) == shard.corpus_digest(rc, rd)
+    bad = [i for i in range(nfiles) if (cnt[i], dig[i], O.hash_digest(per_file[i])) !=
+           (int(rc[i]), int(rd[i]), int(rh[i]))]
+    assert not bad, (len(bad), bad[:8])

@@ -154,3 +154,31 @@ def test_rehearsal_file_sharded_corpus(world):
 def test_rehearsal_split_stream(world):
     res = _launch(world, "split")
     assert all(r[1] for r in res), res
+
+
+def test_bench_two_ranks_rehearsal():
+    """bench.py's own N > 1 path (the split stream with its exit exchange and the
+    file-sharded corpus), launched as the driver launches it (torch.distributed.run,
+    one fresh process per rank) in rehearsal mode (MCDC_BENCH_ONE_DEVICE=1: both
+    ranks on device 0, the exchange and barriers over gloo), at a small size: the
+    gathered split-stream boundary list (--parity) and every file of the sharded
+    corpus must equal the oracle's."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MCDC_BENCH_ONE_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--gib", "0.75", "--corpus-files-per-gpu", "24", "--parity", "--no-cpu", "--cpu-threads",
+           "8"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["config"]["bytes_per_gpu"] == int(0.75 * (1 << 30))
+    sp = d["stream_parity"]
+    assert sp["ok"], sp
+    assert d["config"]["chunks_per_step"] == sp["oracle_chunks"]
+    cs = d["corpus_sharded"]
+    assert cs["parity_ok"] and cs["files"] == 48 and cs["corpus_digest"] == cs["oracle_corpus_digest"], cs

@@ -112,3 +112,25 @@ def test_capacity_error(ctx):
     finally:
         ctx.device_free(d_out)
         ctx.device_free(dp)
+
+
+def test_misaligned_output_rejected(ctx):
+    """k_zframe_write stores 16-byte quads: an output pointer off the 16-byte
+    grid is refused up front (MCDC_E_INVALID), an aligned sub-buffer works."""
+    data = O.random_bytes(100_003, 2)
+    ch = np.zeros(1, dtype=_lib.CHUNK_DTYPE)
+    ch["length"] = data.size
+    dp = ctx.device_alloc(data.size)
+    d_out = ctx.device_alloc(data.size + 4096)
+    try:
+        ctx.h2d(dp, data)
+        for shift in (1, 4, 8):
+            with pytest.raises(_lib.McdcError) as ei:
+                ctx.zstd_frames(dp, data.size, ch, d_out + shift, data.size + 1024)
+            assert ei.value.code == _lib.MCDC_E_INVALID
+        fr, _ = ctx.zstd_frames(dp, data.size, ch, d_out + 32, data.size + 1024)
+        got = ctx.d2h_bytes(d_out + 32 + int(fr[0, 0]), int(fr[0, 1]))
+        assert got.tobytes() == O.zstd_raw_frame(data.tobytes())
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(dp)

@@ -148,3 +148,22 @@ def test_streamed_random_digest_equals_in_memory(p):
     for slab in (4096, 1 << 20, 5_000_000, 64 << 20):
         assert O.random_stream_digest(O.Params(*p), 77, n, slab) == (k, dig, n)
         assert O.random_stream_digest(O.Params(*p), 77, n, slab, hashes=True) == (k, dig, n, hd)
+
+
+def test_random_files_digest_equals_in_memory():
+    """oracle.random_files_digest (files regenerated per thread, the full-size
+    many-file parity of tests/test_gpu_configs.py) equals chunking each file in
+    memory: counts, boundary digests (the library's mcdc_digest over
+    file-relative records) and hash digests; positional and per-file seeds,
+    empty and sub-min files, several threads."""
+    from mapache_amd import _lib, shard
+    p = O.Params(16384, 65536, 262144, 1)
+    seeds = [0x5EED ^ (i + 1) for i in range(12)]
+    lens = [0, 1, 16383, 16384, 16385, 3 << 20, (1 << 20) + 7, 262145, 5, 2 << 20, 777_777, 1 << 16]
+    pos = [i * 1000 + (i % 3) for i in range(12)]
+    c, d, h = O.random_files_digest(p, seeds, pos, lens, threads=3)
+    for i in range(12):
+        ch = O.chunk(p, O.random_bytes(lens[i], seeds[i], pos=pos[i]))
+        assert (int(c[i]), int(d[i]), int(h[i])) == (len(ch), _lib.digest(ch), O.hash_digest(ch)), i
+    assert shard.corpus_digest(c, d) == shard.corpus_digest([int(x) for x in c], [int(x) for x in d])
+    assert shard.corpus_digest(c, d) != shard.corpus_digest(c[::-1], d[::-1])
