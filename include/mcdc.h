@@ -224,7 +224,12 @@ int mcdc_open_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_
  * within the window); any failure -> MCDC_E_AUTH.  Too small an out_cap ->
  * MCDC_E_CAPACITY (out_offsets still filled).  The compressed bytes depend on
  * the libzstd version; decoding is what is compatible.  No libzstd.so.1 ->
- * MCDC_E_INTERNAL. */
+ * MCDC_E_INTERNAL.  Frames carry no content size (the crate's streaming
+ * encoder pledges none), so their header is magic || 0x00 || window byte.
+ * key == NULL is SecureStorage::build() (storage.rs:40-46: no key; level 0 =
+ * zstd's default 3): encode only compresses, decode only decompresses
+ * (encrypt / decrypt are the identity, :120-125, :146-151) and nonces may be
+ * NULL. */
 int mcdc_encode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, size_t n_in,
                       const mcdc_blob *blobs, size_t nblobs, const uint8_t *nonces, void *h_out,
                       size_t out_cap, uint64_t *out_offsets);
@@ -255,7 +260,9 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
  * of 36 random bytes + type 0xff (generate_header).  The randomness is the
  * caller's (OsRng in the crate): header_nonces (12 B per pack) and padding (36
  * B per padding entry, npadding entries; at most 63 per pack are used).
- * The header is encoded with mcdc_encode_blobs; the pack ID is BLAKE3 of the
+ * The header is encoded with mcdc_encode_blobs (key == NULL: compressed only,
+ * as with SecureStorage::build() in packer.rs's own tests; no header nonces
+ * needed); the pack ID is BLAKE3 of the
  * pack (utils::calculate_hash), computed on the GPU.  Output: the packs back
  * to back in h_out; *out_bytes their total and *npacks their number (also on
  * MCDC_E_CAPACITY); packs[k] = {offset, length, blobs, meta_size (encoded

@@ -322,11 +322,12 @@ class Context:
     def encode_blobs(self, key, data, offsets, lengths, nonces):
         """SecureStorage::encode of every blob data[offsets[i], +lengths[i]) (host
         bytes): zstd on host threads, AES-256-GCM-SIV on the GPU
-        (mcdc_encode_blobs).  Returns (packed bytes, nblobs + 1 offsets)."""
+        (mcdc_encode_blobs).  key=None: SecureStorage::build() (compress only,
+        nonces unused).  Returns (packed bytes, nblobs + 1 offsets)."""
         a = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
         ext = self._extents(offsets, lengths)
-        nz = np.ascontiguousarray(nonces, dtype=np.uint8).reshape(-1)
-        if nz.size != NONCE_BYTES * len(ext):
+        nz = np.ascontiguousarray(np.zeros(0, np.uint8) if nonces is None else nonces, dtype=np.uint8).reshape(-1)
+        if key is not None and nz.size != NONCE_BYTES * len(ext):
             raise ValueError("need 12 nonce bytes per blob")
         oo = np.zeros(len(ext) + 1, dtype=np.uint64)
         cap = int(a.size + (a.size >> 7) + 64 * len(ext) + 64)  # zstd's bound + 28 per blob
@@ -384,7 +385,8 @@ class Context:
         ext = self._extents(offsets, lengths)
         iv = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1)
         ty = np.ascontiguousarray(types, dtype=np.uint8).reshape(-1)
-        hn = np.ascontiguousarray(header_nonces, dtype=np.uint8).reshape(-1)
+        hn = np.ascontiguousarray(np.zeros(0, np.uint8) if header_nonces is None else header_nonces,
+                                  dtype=np.uint8).reshape(-1)
         pd = np.ascontiguousarray(padding, dtype=np.uint8).reshape(-1)
         nb, np_, cap = ctypes.c_size_t(), ctypes.c_size_t(), 0
         packs = np.zeros(1, dtype=PACK_DTYPE)
@@ -419,7 +421,10 @@ class Context:
         return ext
 
     @staticmethod
-    def _key(key) -> bytes:
+    def _key(key):
+        """32 key bytes, or None (SecureStorage::build(): no encryption)."""
+        if key is None:
+            return None
         key = bytes(key)
         if len(key) != 32:
             raise ValueError("AES-256-GCM-SIV key must be 32 bytes")

@@ -1332,7 +1332,7 @@ int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
                       size_t nblobs, const uint8_t *nonces, void *h_out, size_t out_cap, uint64_t *out_offsets) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  if (!key || (!h_in && n_in) || (nblobs && (!blobs || !nonces))) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((!h_in && n_in) || (nblobs && (!blobs || (key && !nonces)))) return fail(MCDC_E_INVALID, "NULL argument");
   if ((h_in && is_device_ptr(h_in)) || (h_out && is_device_ptr(h_out)))
     return fail(MCDC_E_INVALID, "h_in / h_out must be host memory");
   if ((rc = check_extents(blobs, nblobs, n_in))) return rc;
@@ -1351,6 +1351,19 @@ int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
     if (!comp[i].empty()) std::memcpy(arena.data() + ext[i].offset, comp[i].data(), comp[i].size());
   });
   comp.clear();
+  if (!key) {  // SecureStorage::build(): no key, encrypt() returns the compressed bytes (storage.rs:120-125)
+    if (out_offsets) {
+      for (size_t i = 0; i < nblobs; ++i) out_offsets[i] = ext[i].offset;
+      out_offsets[nblobs] = total;
+    }
+    if (total > out_cap || (total && !h_out))
+      return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
+    if (total) std::memcpy(h_out, arena.data(), total);
+    ctx->timing = mcdc_timing{};
+    ctx->timing.bytes = n_in;
+    ctx->timing.total_ms = now_ms() - t0;
+    return MCDC_OK;
+  }
   const size_t cap = total + (size_t)kAeadOverhead * nblobs;
   if ((rc = ensure(ctx, ctx->enc_in, total)) || (rc = ensure(ctx, ctx->enc_out, cap))) return rc;
   if (total) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, arena.data(), total, hipMemcpyHostToDevice, ctx->stream));
@@ -1376,29 +1389,37 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
                       size_t nblobs, void *h_out, size_t out_cap, uint64_t *out_offsets, int32_t *status) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  if (!key || (!h_in && n_in) || (nblobs && !sealed)) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((!h_in && n_in) || (nblobs && !sealed)) return fail(MCDC_E_INVALID, "NULL argument");
   if ((h_in && is_device_ptr(h_in)) || (h_out && is_device_ptr(h_out)))
     return fail(MCDC_E_INVALID, "h_in / h_out must be host memory");
   if ((rc = check_extents(sealed, nblobs, n_in))) return rc;
   const double t0 = now_ms();
-  if ((rc = ensure(ctx, ctx->enc_in, n_in)) || (rc = ensure(ctx, ctx->enc_out, n_in))) return rc;
-  if (n_in) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_in, n_in, hipMemcpyHostToDevice, ctx->stream));
-  std::vector<uint64_t> oo(nblobs + 1);
-  std::vector<int32_t> st(std::max<size_t>(nblobs, 1));
-  rc = aead_run(ctx, 1, key, ctx->enc_in.p, n_in, sealed, nblobs, nullptr, ctx->enc_out.p, n_in, oo.data(),
-                st.data());
-  if (rc && rc != MCDC_E_AUTH) return rc;
-  const mcdc_timing tm = ctx->timing;
-  std::vector<uint8_t> plain(std::max<uint64_t>(oo[nblobs], 1));
-  if (oo[nblobs]) {
-    HIP_TRY(hipMemcpyAsync(plain.data(), ctx->enc_out.p, oo[nblobs], hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-  }
   std::vector<uint64_t> poff(nblobs), plen(nblobs);
-  for (size_t i = 0; i < nblobs; ++i) poff[i] = oo[i], plen[i] = oo[i + 1] - oo[i];
+  std::vector<int32_t> st(std::max<size_t>(nblobs, 1), 0);
+  std::vector<uint8_t> plain;
+  const uint8_t *zin = (const uint8_t *)h_in;
+  mcdc_timing tm{};
+  if (key) {
+    if ((rc = ensure(ctx, ctx->enc_in, n_in)) || (rc = ensure(ctx, ctx->enc_out, n_in))) return rc;
+    if (n_in) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_in, n_in, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<uint64_t> oo(nblobs + 1);
+    rc = aead_run(ctx, 1, key, ctx->enc_in.p, n_in, sealed, nblobs, nullptr, ctx->enc_out.p, n_in, oo.data(),
+                  st.data());
+    if (rc && rc != MCDC_E_AUTH) return rc;
+    tm = ctx->timing;
+    plain.resize(std::max<uint64_t>(oo[nblobs], 1));
+    if (oo[nblobs]) {
+      HIP_TRY(hipMemcpyAsync(plain.data(), ctx->enc_out.p, oo[nblobs], hipMemcpyDeviceToHost, ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    for (size_t i = 0; i < nblobs; ++i) poff[i] = oo[i], plen[i] = oo[i + 1] - oo[i];
+    zin = plain.data();
+  } else {  // SecureStorage::build(): decrypt() is the identity, only decompress (storage.rs:67-69)
+    for (size_t i = 0; i < nblobs; ++i) poff[i] = sealed[i].offset, plen[i] = sealed[i].length;
+  }
   std::vector<std::vector<uint8_t>> dec;
   std::vector<int32_t> zok;
-  const std::string zerr = mcdc::host::zstd_decompress_all(plain.data(), poff.data(), plen.data(), st.data(),
+  const std::string zerr = mcdc::host::zstd_decompress_all(zin, poff.data(), plen.data(), st.data(),
                                                            nblobs, zstd_threads(), dec, zok);
   if (!zerr.empty()) return fail(MCDC_E_INTERNAL, "%s", zerr.c_str());
   size_t total = 0, bad = 0;
@@ -1493,7 +1514,7 @@ int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, s
                     size_t *npacks) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  if (!key || (!h_blobs && n_in) || (nblobs && (!blobs || !ids || !types)) || !npacks)
+  if ((!h_blobs && n_in) || (nblobs && (!blobs || !ids || !types)) || !npacks)
     return fail(MCDC_E_INVALID, "NULL argument");
   if ((h_blobs && is_device_ptr(h_blobs)) || (h_out && is_device_ptr(h_out)))
     return fail(MCDC_E_INVALID, "h_blobs / h_out must be host memory");
@@ -1515,7 +1536,8 @@ int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, s
   }
   const size_t np = first.size();
   first.push_back(nblobs);
-  if (np > nnonces) return fail(MCDC_E_INVALID, "%zu packs need %zu header nonces (%zu given)", np, np, nnonces);
+  if (key && np > nnonces)  // (without a key the headers are only compressed: no nonces)
+    return fail(MCDC_E_INVALID, "%zu packs need %zu header nonces (%zu given)", np, np, nnonces);
   // headers: 37-byte entries (ID, le32 length, type), padded with random entries
   // (36 random bytes + BlobType::Padding) to a multiple of 64 (generate_header)
   std::vector<uint8_t> hdr;

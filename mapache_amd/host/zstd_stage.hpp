@@ -27,12 +27,21 @@
 namespace mcdc {
 namespace host {
 
+struct ZInBuf {
+  const void *src;
+  size_t size, pos;
+};
+struct ZOutBuf {
+  void *dst;
+  size_t size, pos;
+};
+
 // The libzstd entry points used (stable API since zstd 1.4.0).
 struct ZstdApi {
   void *(*createCCtx)() = nullptr;
   size_t (*freeCCtx)(void *) = nullptr;
   size_t (*cctxSetParameter)(void *, int, int) = nullptr;
-  size_t (*compress2)(void *, void *, size_t, const void *, size_t) = nullptr;
+  size_t (*compressStream2)(void *, ZOutBuf *, ZInBuf *, int) = nullptr;
   size_t (*compressBound)(size_t) = nullptr;
   unsigned (*isError)(size_t) = nullptr;
   const char *(*getErrorName)(size_t) = nullptr;
@@ -46,8 +55,10 @@ struct ZstdApi {
 };
 
 // ZSTD_cParameter / ZSTD_dParameter values (zstd.h, stable)
-constexpr int kZstdCLevel = 100, kZstdCWindowLog = 101, kZstdCChecksum = 201, kZstdDWindowLogMax = 100;
-constexpr int kZstdLevel = 3, kZstdWindowLog = 20;  // storage.rs:31,76-79 (zstd crate default level 3)
+constexpr int kZstdCLevel = 100, kZstdCWindowLog = 101, kZstdCContentSize = 200, kZstdCChecksum = 201,
+              kZstdDWindowLogMax = 100;
+constexpr int kZstdLevel = 3, kZstdWindowLog = 20;
+constexpr int kZstdEContinue = 0, kZstdEEnd = 2;  // ZSTD_EndDirective  // storage.rs:31,76-79 (zstd crate default level 3)
 
 inline const ZstdApi &zstd_api() {
   static ZstdApi api;
@@ -62,7 +73,7 @@ inline const ZstdApi &zstd_api() {
     api.createCCtx = (void *(*)())sym("ZSTD_createCCtx");
     api.freeCCtx = (size_t(*)(void *))sym("ZSTD_freeCCtx");
     api.cctxSetParameter = (size_t(*)(void *, int, int))sym("ZSTD_CCtx_setParameter");
-    api.compress2 = (size_t(*)(void *, void *, size_t, const void *, size_t))sym("ZSTD_compress2");
+    api.compressStream2 = (size_t(*)(void *, ZOutBuf *, ZInBuf *, int))sym("ZSTD_compressStream2");
     api.compressBound = (size_t(*)(size_t))sym("ZSTD_compressBound");
     api.isError = (unsigned (*)(size_t))sym("ZSTD_isError");
     api.getErrorName = (const char *(*)(size_t))sym("ZSTD_getErrorName");
@@ -71,7 +82,7 @@ inline const ZstdApi &zstd_api() {
     api.dctxSetParameter = (size_t(*)(void *, int, int))sym("ZSTD_DCtx_setParameter");
     api.decompressStream = (size_t(*)(void *, void *, void *))sym("ZSTD_decompressStream");
     api.dStreamOutSize = (size_t(*)())sym("ZSTD_DStreamOutSize");
-    api.ok = api.createCCtx && api.freeCCtx && api.cctxSetParameter && api.compress2 && api.compressBound &&
+    api.ok = api.createCCtx && api.freeCCtx && api.cctxSetParameter && api.compressStream2 && api.compressBound &&
              api.isError && api.getErrorName && api.createDCtx && api.freeDCtx && api.dctxSetParameter &&
              api.decompressStream && api.dStreamOutSize;
     if (!api.ok) api.why = "libzstd.so.1 lacks the zstd 1.4 advanced API";
@@ -108,39 +119,45 @@ inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, con
       cctx[w] = z.createCCtx();
       const bool ok = cctx[w] && !z.isError(z.cctxSetParameter(cctx[w], kZstdCLevel, kZstdLevel)) &&
                       !z.isError(z.cctxSetParameter(cctx[w], kZstdCWindowLog, kZstdWindowLog)) &&
-                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCChecksum, 0));
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCChecksum, 0)) &&
+                      // the crate's streaming encoder (write_all + finish) never pledges a
+                      // size, so its frames carry no content size and keep the window
+                      // descriptor: the same 6-byte frame header here
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCContentSize, 0));
       if (!ok) {  // never compress with other settings than the reference's
         std::lock_guard<std::mutex> lk(emu);
-        err = "zstd rejected level 3 / window log 20 / no checksum";
+        err = "zstd rejected level 3 / window log 20 / no checksum / no content size";
         if (cctx[w]) z.freeCCtx(cctx[w]);
         cctx[w] = nullptr;
         return;
       }
     }
+    // as the crate's ZstdEncoder: write_all (ZSTD_e_continue), then finish
+    // (ZSTD_e_end until flushed); the size is never pledged
     std::vector<uint8_t> &o = out[i];
-    o.resize(z.compressBound(len[i]));
-    const size_t r = z.compress2(cctx[w], o.data(), o.size(), in + off[i], len[i]);
-    if (z.isError(r)) {
+    o.resize(z.compressBound(len[i]) + 64);
+    ZInBuf ib{in + off[i], (size_t)len[i], 0};
+    ZOutBuf ob{o.data(), o.size(), 0};
+    size_t r = z.compressStream2(cctx[w], &ob, &ib, kZstdEContinue);
+    if (!z.isError(r)) {
+      do {
+        r = z.compressStream2(cctx[w], &ob, &ib, kZstdEEnd);
+      } while (!z.isError(r) && r != 0 && ob.pos < ob.size);
+    }
+    if (z.isError(r) || r != 0) {  // (the context is mid-frame: drop it)
       std::lock_guard<std::mutex> lk(emu);
-      err = std::string("zstd compression failed: ") + z.getErrorName(r);
+      err = std::string("zstd compression failed: ") + (z.isError(r) ? z.getErrorName(r) : "output bound");
+      z.freeCCtx(cctx[w]);
+      cctx[w] = nullptr;
       o.clear();
       return;
     }
-    o.resize(r);
+    o.resize(ob.pos);
   });
   for (void *c : cctx)
     if (c) z.freeCCtx(c);
   return err;
 }
-
-struct ZInBuf {
-  const void *src;
-  size_t size, pos;
-};
-struct ZOutBuf {
-  void *dst;
-  size_t size, pos;
-};
 
 // decompress frame i = in[off[i], + len[i]) into out[i] (window_log_max 20,
 // as storage.rs:87-94); ok[i] = 0 or -2 (not a valid frame within the window)

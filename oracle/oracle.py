@@ -548,3 +548,149 @@ def zstd_raw_frame(data) -> bytes:
         h = (1 if k + 1 == len(blocks) else 0) | (len(b) << 3)
         out += h.to_bytes(3, "little") + b
     return bytes(out)
+
+
+# ------------------------------------------------------------ zstd codec --
+class Zstd:
+    """The system libzstd (1.4.8 here; the crate links 1.5.7) through ctypes:
+    the test-side reference codec for SecureStorage's compression
+    (storage.rs:74-94: level 3, window log 20, no checksum; decoded with
+    window_log_max 20).  Compressed bytes depend on the version: parity on
+    compressed data is decode-equality."""
+
+    def __init__(self):
+        import ctypes
+        z = ctypes.CDLL("libzstd.so.1")
+        z.ZSTD_createCCtx.restype = ctypes.c_void_p
+        z.ZSTD_createDCtx.restype = ctypes.c_void_p
+        z.ZSTD_compressBound.restype = ctypes.c_size_t
+        z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+        z.ZSTD_compress2.restype = ctypes.c_size_t
+        z.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                     ctypes.c_size_t]
+        z.ZSTD_CCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        z.ZSTD_DCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        z.ZSTD_decompressDCtx.restype = ctypes.c_size_t
+        z.ZSTD_decompressDCtx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.c_size_t]
+        z.ZSTD_compressStream2.restype = ctypes.c_size_t
+        z.ZSTD_compressStream2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        z.ZSTD_getFrameContentSize.restype = ctypes.c_ulonglong
+        z.ZSTD_getFrameContentSize.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        z.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
+        z.ZSTD_freeDCtx.argtypes = [ctypes.c_void_p]
+        self.z, self.ct = z, ctypes
+
+    def compress(self, data: bytes, content_size: bool, level: int = 3) -> bytes:
+        """content_size=True: one-shot ZSTD_compress2 (size known: content size in
+        the frame, window fitted to the input).  False: the crate's streaming
+        encoder (ZstdEncoder::write_all + finish, storage.rs:75-83): the data
+        is passed with ZSTD_e_continue, then ZSTD_e_end flushes -- the size is
+        never pledged, so the frame has no content size and keeps the 2^20
+        window descriptor."""
+        z, ct = self.z, self.ct
+        c = z.ZSTD_createCCtx()
+        z.ZSTD_CCtx_setParameter(c, 100, level)  # level (0: zstd's default, 3)
+        z.ZSTD_CCtx_setParameter(c, 101, 20)  # window log
+        z.ZSTD_CCtx_setParameter(c, 201, 0)  # checksum off
+        z.ZSTD_CCtx_setParameter(c, 200, 1 if content_size else 0)  # content size flag
+        out = ct.create_string_buffer(z.ZSTD_compressBound(len(data)) + 64)
+        if content_size:
+            r = z.ZSTD_compress2(c, out, len(out), data, len(data))
+            z.ZSTD_freeCCtx(c)
+            assert not z.ZSTD_isError(r)
+            return out.raw[:r]
+
+        class Buf(ct.Structure):
+            _fields_ = [("ptr", ct.c_void_p), ("size", ct.c_size_t), ("pos", ct.c_size_t)]
+        src = ct.create_string_buffer(bytes(data), max(len(data), 1))
+        ib, ob = Buf(ct.addressof(src), len(data), 0), Buf(ct.addressof(out), len(out), 0)
+        r = z.ZSTD_compressStream2(c, ct.byref(ob), ct.byref(ib), 0)  # ZSTD_e_continue
+        assert not z.ZSTD_isError(r) and ib.pos == len(data)
+        while True:
+            r = z.ZSTD_compressStream2(c, ct.byref(ob), ct.byref(ib), 2)  # ZSTD_e_end
+            assert not z.ZSTD_isError(r)
+            if r == 0:
+                break
+        z.ZSTD_freeCCtx(c)
+        return out.raw[:ob.pos]
+
+    def decompress(self, frame: bytes, size: int) -> bytes:
+        z = self.z
+        d = z.ZSTD_createDCtx()
+        z.ZSTD_DCtx_setParameter(d, 100, 20)  # window_log_max 20 (storage.rs:90)
+        out = self.ct.create_string_buffer(max(size, 1))
+        r = z.ZSTD_decompressDCtx(d, out, len(out), frame, len(frame))
+        z.ZSTD_freeDCtx(d)
+        assert not z.ZSTD_isError(r), "not a zstd frame within a 2^20 window"
+        return out.raw[:r]
+
+
+# ------------------------------------------------- SecureStorage + Packer --
+def storage_encode(data: bytes, key=None, nonce=None, level: int = 0) -> bytes:
+    """SecureStorage::encode (storage.rs:61-65): compress as the crate's
+    streaming encoder does (:74-84; no content size in the frame), then
+    encrypt_with_key when there is a key (:120-125; the identity without one:
+    SecureStorage::build())."""
+    c = Zstd().compress(bytes(data), content_size=False, level=level)
+    return c if key is None else encrypt_with_key(key, nonce, c)
+
+
+def storage_decode(blob: bytes, key=None, size_hint: int = 1 << 24) -> bytes:
+    """SecureStorage::decode (storage.rs:67-69): decrypt (identity without a
+    key), then decompress within a 2^20 window."""
+    if key is not None:
+        blob = decrypt_with_key(key, blob)
+        if blob is None:
+            raise ValueError("Decryption failed")
+    return Zstd().decompress(bytes(blob), size_hint)
+
+
+def pack_flush(blobs, ids, types, padding, key=None, nonce=None):
+    """Packer::flush (packer.rs:113-153) of the blobs added in order:
+    None for an empty packer (:114-116); else (data, descriptors) with
+    data = blobs back to back || encode(generate_header) || le32(len) and
+    descriptors = (id, type, offset, length) of the blobs followed by the
+    padding descriptors generate_header appends (:160-171).  padding: one
+    (id32, offset, length) per padding entry the header needs (the crate
+    draws them from its RNG)."""
+    if not blobs:
+        return None
+    data, desc, off = bytearray(), [], 0
+    for b, i, t in zip(blobs, ids, types):
+        desc.append((bytes(i), int(t), off, len(b)))
+        data += bytes(b)
+        off += len(b)
+    npad = (HEADER_BLOB_MULTIPLE - len(desc) % HEADER_BLOB_MULTIPLE) % HEADER_BLOB_MULTIPLE
+    for j in range(npad):
+        pid, poff, plen = padding[j]
+        desc.append((bytes(pid), 0xFF, int(poff), int(plen)))
+    header = b"".join(d[0] + (d[3] & 0xFFFFFFFF).to_bytes(4, "little") + bytes([d[1]]) for d in desc)
+    enc = storage_encode(header, key, nonce)
+    data += enc + len(enc).to_bytes(4, "little")
+    return bytes(data), desc
+
+
+def parse_header(header_data: bytes, key=None):
+    """Packer::parse_header (packer.rs:214-285): the le32 length at the end, the
+    encoded header before it, decoded; 37-byte entries; padding entries
+    (type 0xff) skipped; offsets are the running sum of the real entries'
+    lengths.  Returns [(id, type, offset, length)]."""
+    if len(header_data) < 4:
+        raise ValueError("Pack header is invalid: data too short for header length")
+    hl = int.from_bytes(header_data[-4:], "little")
+    if len(header_data) < hl:
+        raise ValueError("Pack header is invalid: declared header_length exceeds total data length")
+    info = storage_decode(header_data[len(header_data) - hl - 4:len(header_data) - 4], key)
+    if len(info) % HEADER_BLOB_LEN:
+        raise ValueError("Pack header is invalid: not a multiple of the descriptor size")
+    out, cur = [], 0
+    for j in range(len(info) // HEADER_BLOB_LEN):
+        e = info[j * HEADER_BLOB_LEN:(j + 1) * HEADER_BLOB_LEN]
+        if e[36] == 0xFF:
+            continue
+        ln = int.from_bytes(e[32:36], "little")
+        out.append((bytes(e[:32]), e[36], cur, ln))
+        cur += ln
+    return out

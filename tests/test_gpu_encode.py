@@ -7,8 +7,6 @@ checksum).  The compressed bytes depend on the libzstd version (the crate's is
 opened by the oracle and decompressed within a 2^20 window equals its input,
 frames carry no checksum, and frames the library did not write (no content
 size, as the crate's streaming encoder leaves them) decode too."""
-import ctypes
-
 import numpy as np
 import pytest
 
@@ -19,50 +17,7 @@ pytestmark = pytest.mark.gpu
 KEY = bytes(range(0x20, 0x40))
 
 
-class Zstd:
-    """The system libzstd through ctypes (test-side reference codec)."""
-
-    def __init__(self):
-        z = ctypes.CDLL("libzstd.so.1")
-        z.ZSTD_createCCtx.restype = ctypes.c_void_p
-        z.ZSTD_createDCtx.restype = ctypes.c_void_p
-        z.ZSTD_compressBound.restype = ctypes.c_size_t
-        z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
-        z.ZSTD_compress2.restype = ctypes.c_size_t
-        z.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                                     ctypes.c_size_t]
-        z.ZSTD_CCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        z.ZSTD_DCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        z.ZSTD_decompressDCtx.restype = ctypes.c_size_t
-        z.ZSTD_decompressDCtx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                                          ctypes.c_size_t]
-        z.ZSTD_isError.argtypes = [ctypes.c_size_t]
-        z.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
-        z.ZSTD_freeDCtx.argtypes = [ctypes.c_void_p]
-        self.z = z
-
-    def compress(self, data: bytes, content_size: bool) -> bytes:
-        z = self.z
-        c = z.ZSTD_createCCtx()
-        z.ZSTD_CCtx_setParameter(c, 100, 3)  # level
-        z.ZSTD_CCtx_setParameter(c, 101, 20)  # window log
-        z.ZSTD_CCtx_setParameter(c, 201, 0)  # checksum off
-        z.ZSTD_CCtx_setParameter(c, 200, 1 if content_size else 0)  # content size flag
-        out = ctypes.create_string_buffer(z.ZSTD_compressBound(len(data)))
-        r = z.ZSTD_compress2(c, out, len(out), data, len(data))
-        z.ZSTD_freeCCtx(c)
-        assert not z.ZSTD_isError(r)
-        return out.raw[:r]
-
-    def decompress(self, frame: bytes, size: int) -> bytes:
-        z = self.z
-        d = z.ZSTD_createDCtx()
-        z.ZSTD_DCtx_setParameter(d, 100, 20)  # window_log_max 20 (storage.rs:90)
-        out = ctypes.create_string_buffer(max(size, 1))
-        r = z.ZSTD_decompressDCtx(d, out, len(out), frame, len(frame))
-        z.ZSTD_freeDCtx(d)
-        assert not z.ZSTD_isError(r), "not a zstd frame within a 2^20 window"
-        return out.raw[:r]
+Zstd = O.Zstd  # the system libzstd through ctypes (oracle/oracle.py)
 
 
 def _blobs():
@@ -163,3 +118,23 @@ def test_encode_capacity_and_range_errors(ctx):
     rc = load().mcdc_encode_blobs(ctx._h, KEY, data.ctypes.data, data.size, ext.ctypes.data, len(parts),
                                   nz.ctypes.data, out.ctypes.data, out.size, oo.ctypes.data)
     assert rc == _lib.MCDC_E_INVALID
+
+
+def test_keyless_storage_is_the_crates_bytes(ctx):
+    """SecureStorage::build() (key None: storage.rs:40-46, encrypt / decrypt the
+    identity): every encoded blob is byte-for-byte the frame the crate's
+    streaming encoder writes with this libzstd (oracle.storage_encode: no
+    content size, 2^20 window descriptor), and decode(None) returns the blobs.
+    With a key, the opened frames are the same bytes."""
+    data, offs, lens, parts = _blobs()
+    enc, oo = ctx.encode_blobs(None, data, offs, lens, None)
+    got = [enc[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(len(parts))]
+    assert got == [O.storage_encode(p) for p in parts]
+    for g in got:
+        assert g[4] == 0x00 and g[5] == 0x50  # no content size / checksum; window 2^20
+    dec, do, st = ctx.decode_blobs(None, enc, oo[:-1], np.diff(oo), int(lens.sum()) + 16)
+    assert (st == 0).all()
+    assert [dec[int(do[i]):int(do[i + 1])].tobytes() for i in range(len(parts))] == parts
+    nz = _nonces(len(parts))
+    enc_k, ok = ctx.encode_blobs(KEY, data, offs, lens, nz)
+    assert [O.decrypt_with_key(KEY, enc_k[int(ok[i]):int(ok[i + 1])].tobytes()) for i in range(len(parts))] == got

@@ -7,7 +7,6 @@ import pytest
 
 from mapache_amd import _lib
 from oracle import oracle as O
-from tests.test_gpu_encode import Zstd
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +32,7 @@ def test_frames_of_a_stream(ctx, p):
     data = O.random_bytes((48 << 20) + 11, 0xF7)
     ch = O.chunk(O.Params(*p), data)
     fr, out = _frames(ctx, data, ch)
-    z = Zstd()
+    z = O.Zstd()
     for i in range(len(ch)):
         o, n = int(fr[i, 0]), int(fr[i, 1])
         assert o % 16 == 0
@@ -55,7 +54,7 @@ def test_edge_lengths_and_alignments(ctx):
     ch = np.zeros(len(pairs), dtype=_lib.CHUNK_DTYPE)
     ch["offset"], ch["length"] = [x[0] for x in pairs], [x[1] for x in pairs]
     fr, out = _frames(ctx, data, ch)
-    z = Zstd()
+    z = O.Zstd()
     for i, (o_, n_) in enumerate(pairs):
         frame = out[int(fr[i, 0]):int(fr[i, 0] + fr[i, 1])].tobytes()
         chunk = data[o_:o_ + n_].tobytes()
