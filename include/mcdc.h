@@ -280,6 +280,52 @@ int mcdc_pack_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_b
                     const uint8_t *padding, size_t npadding, void *h_out, size_t out_cap,
                     size_t *out_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks);
 
+/* ------------------------------------------------------------ save path
+ * The Archiver's save path for a run of files in one call -- what
+ * processor::save_file / chunk_and_save_blobs do per file
+ * (/root/reference/src/archiver/processor.rs:138-205) and
+ * Repository::save_blob per blob (repository_v1.rs:155-195), in file order:
+ *   - a file smaller than params->min_size (MIN_CHUNK_SIZE, :144) is one blob
+ *     whose ID is ID::from_content of the whole file (SaveID::CalculateID);
+ *     any other file is chunked (StreamCDC, :173-179) and each chunk is a
+ *     blob with ID::from_content (:184);
+ *   - each blob is stored unless its ID is in the index or already pending
+ *     (:173-180: the dedup index `ix`, which keeps the IDs across calls);
+ *   - a stored blob is SecureStorage::encode'd (:182; store->key NULL =
+ *     SecureStorage::build()) and added to the packer, which is flushed once
+ *     it holds more than store->max_pack_size bytes (:185-192) and once at the
+ *     end of the call (the end of the snapshot: Repository::flush).
+ * data: host memory or a device pointer (n bytes); files: extents in it (the
+ * chunked ones must not overlap).  Randomness is the caller's (OsRng in the
+ * crate): store->nonces, 12 bytes per stored blob in storing order (unused
+ * without a key), header_nonces per pack, padding (36 bytes per padding
+ * header entry, drawn in order).
+ * Outputs (host memory): file_blobs[nfiles + 1], the blob index where each
+ * file's ID list starts (the Vec<ID> save_file returns is ids[32 *
+ * file_blobs[f], 32 * file_blobs[f + 1])); ids (32 B per blob, blobs_cap
+ * entries); is_new (optional, 1 B per blob: stored by this call); the packs
+ * back to back in packs_out and their records (as mcdc_pack_blobs).  Too
+ * small a blobs_cap / packs_out_cap / packs_cap -> MCDC_E_CAPACITY with
+ * *nblobs / *packs_bytes / *npacks set and the index unchanged: call again
+ * with larger outputs.  Input larger than the context's max_bytes ->
+ * MCDC_E_TOOBIG. */
+typedef struct {
+  const uint8_t *key;           /* 32-byte key, or NULL (SecureStorage::build()) */
+  uint64_t max_pack_size;       /* the repository's max_packer_size (16 MiB) */
+  const uint8_t *nonces;        /* 12 B per stored blob */
+  size_t nnonces;
+  const uint8_t *header_nonces; /* 12 B per pack */
+  size_t nheader_nonces;
+  const uint8_t *padding;       /* 36 B per padding header entry */
+  size_t npadding;
+} mcdc_store;
+struct mcdc_index;
+int mcdc_save_files(struct mcdc_ctx *ctx, const mcdc_params *params, struct mcdc_index *ix,
+                    const mcdc_store *store, const void *data, size_t n, const mcdc_blob *files,
+                    size_t nfiles, uint64_t *file_blobs, uint8_t *ids, uint8_t *is_new, size_t blobs_cap,
+                    size_t *nblobs, void *packs_out, size_t packs_out_cap, size_t *packs_bytes,
+                    mcdc_pack *packs, size_t packs_cap, size_t *npacks);
+
 /* ------------------------------------------------------------- dedup index
  * Repository::save_blob stores a blob only when its ID is neither in the
  * index nor already pending (/root/reference/src/repository/repository_v1.rs:

@@ -37,8 +37,16 @@ EXPORTS = (
     "mcdc_abi_version", "mcdc_chunk_ids_device", "mcdc_batcher_create", "mcdc_batcher_destroy",
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
-    "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device",
+    "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device", "mcdc_save_files",
 )
+
+
+class McdcStore(ctypes.Structure):
+    """mcdc_store (include/mcdc.h): SecureStorage key (None = build()), the
+    repository's max pack size and the caller's randomness."""
+    _fields_ = [("key", ctypes.c_void_p), ("max_pack_size", ctypes.c_uint64), ("nonces", ctypes.c_void_p),
+                ("nnonces", ctypes.c_size_t), ("header_nonces", ctypes.c_void_p), ("nheader_nonces", ctypes.c_size_t),
+                ("padding", ctypes.c_void_p), ("npadding", ctypes.c_size_t)]
 
 
 PACK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("nblobs", "<u8"), ("meta_size", "<u8"),
@@ -130,8 +138,13 @@ def load():
     L.mcdc_zstd_frames_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, P(sz), vp]
     L.mcdc_pack_blobs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, u64, vp, sz, vp, sz, vp, sz, P(sz), vp, sz,
                                   P(sz)]
-    for name in EXPORTS:  # fail loudly if the build is stale
-        getattr(L, name)
+    # (an A/B library of older sources, MCDC_LIBRARY, may predate the save path)
+    if hasattr(L, "mcdc_save_files"):
+        L.mcdc_save_files.argtypes = [vp, P(McdcParams), vp, P(McdcStore), vp, sz, vp, sz, vp, vp, vp, sz, P(sz), vp,
+                                      sz, P(sz), vp, sz, P(sz)]
+    for name in EXPORTS:  # fail loudly if the build is stale (the in-tree build)
+        if not os.environ.get("MCDC_LIBRARY") or name != "mcdc_save_files":
+            getattr(L, name)
     _lib = L
     return L
 
@@ -403,6 +416,56 @@ class Context:
             packs = np.zeros(max(np_.value, 1), dtype=PACK_DTYPE)
         check(rc)
         return out[:nb.value], packs[:np_.value]
+
+    # --------------------------------------------------------- save path --
+    @_locked
+    def save_files(self, p: "McdcParams", index: "Index", data, offsets, lengths, key=None, nonces=None,
+                   header_nonces=None, padding=None, max_pack_size: int = 16 << 20, n: int | None = None):
+        """The Archiver's save path for a run of files (mcdc_save_files): data is
+        a host array (or a device pointer with n bytes); file f = data[offsets[f],
+        + lengths[f]).  Returns (ids_per_file: list of (k, 32) uint8 arrays,
+        is_new per blob, packed bytes, PACK_DTYPE records)."""
+        if isinstance(data, int):
+            dptr, nbytes, keep = data, int(n), None
+        else:
+            keep = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+            dptr, nbytes = keep.ctypes.data, keep.size
+        ext = self._extents(offsets, lengths)
+        nf = len(ext)
+        k = self._key(key)
+        arrs = [np.ascontiguousarray(np.zeros(0, np.uint8) if x is None else x, dtype=np.uint8).reshape(-1)
+                for x in (nonces, header_nonces, padding)]
+        kbuf = ctypes.create_string_buffer(k, len(k)) if k else None
+        st = McdcStore(ctypes.addressof(kbuf) if k else None, max_pack_size,
+                       arrs[0].ctypes.data, arrs[0].size // NONCE_BYTES, arrs[1].ctypes.data,
+                       arrs[1].size // NONCE_BYTES, arrs[2].ctypes.data, arrs[2].size // 36)
+        fb = np.zeros(nf + 1, np.uint64)
+        bcap = int(sum(int(x) // max(p.min_size - 1, 1) + 2 for x in ext[:, 1])) if nf else 1
+        ids = np.zeros((max(bcap, 1), 32), np.uint8)
+        nw = np.zeros(max(bcap, 1), np.uint8)
+        ocap = int(ext[:, 1].sum() * 1.01) + 4096 * nf + (1 << 16) if nf else 1
+        out = np.empty(max(ocap, 1), np.uint8)
+        packs = np.zeros(max(1, ocap // max(max_pack_size, 1) + 2), PACK_DTYPE)
+        nb, pb, np_ = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        for _ in range(3):
+            rc = load().mcdc_save_files(self._h, ctypes.byref(p), ctypes.c_void_p(index._h), ctypes.byref(st),
+                                        ctypes.c_void_p(dptr), nbytes, ext.ctypes.data, nf, fb.ctypes.data,
+                                        ids.ctypes.data, nw.ctypes.data, len(ids), ctypes.byref(nb),
+                                        out.ctypes.data, out.size, ctypes.byref(pb), packs.ctypes.data, packs.size,
+                                        ctypes.byref(np_))
+            if rc != MCDC_E_CAPACITY:
+                break
+            if nb.value > len(ids):
+                ids = np.zeros((nb.value, 32), np.uint8)
+                nw = np.zeros(nb.value, np.uint8)
+            if pb.value > out.size:
+                out = np.empty(pb.value, np.uint8)
+            if np_.value > packs.size:
+                packs = np.zeros(np_.value, PACK_DTYPE)
+        check(rc)
+        del keep, kbuf
+        per_file = [ids[int(fb[f]):int(fb[f + 1])].copy() for f in range(nf)]
+        return per_file, nw[:nb.value].astype(bool), out[:pb.value], packs[:np_.value]
 
     # ------------------------------------------------------- dedup index --
     @_locked

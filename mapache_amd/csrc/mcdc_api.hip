@@ -222,7 +222,8 @@ struct mcdc_ctx {
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
-      ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status;
+      ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
+      sv_in;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -878,7 +879,8 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->b3_goff, &ctx->b3_owner, &ctx->b3_nodes, &ctx->b3_ids, &ctx->b3_tmp, &ctx->b3_hist, &ctx->enc_in, &ctx->enc_out, &ctx->zf_sz,
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
-                    &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status};
+                    &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
+                    &ctx->sv_in};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1441,6 +1443,159 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   ctx->timing = tm;
   ctx->timing.total_ms = now_ms() - t0;
   if (bad) return fail(MCDC_E_AUTH, "%zu of %zu blobs failed to decode", bad, nblobs);
+  return MCDC_OK;
+}
+
+// ------------------------------------------------------------ save path --
+// The Archiver's save path for a run of files (processor.rs:138-205 +
+// Repository::save_blob, repository_v1.rs:155-195), composed from the stages
+// above: size gate, chunking (GPU), chunk IDs (GPU), dedup (GPU index),
+// SecureStorage::encode (zstd on host threads, sealing on the GPU), packer.
+int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, const mcdc_store *store,
+                    const void *data, size_t n, const mcdc_blob *files, size_t nfiles, uint64_t *file_blobs,
+                    uint8_t *ids, uint8_t *is_new, size_t blobs_cap, size_t *nblobs, void *packs_out,
+                    size_t packs_out_cap, size_t *packs_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!params || !ix || !store || (!data && n) || (nfiles && (!files || !file_blobs)) || !nblobs || !npacks)
+    return fail(MCDC_E_INVALID, "NULL argument");
+  if ((rc = mcdc_params_check(params, nullptr, nullptr))) return rc;
+  if (ix->device != ctx->device) return fail(MCDC_E_INVALID, "the index lives on device %d", ix->device);
+  if ((rc = check_extents(files, nfiles, n))) return rc;
+  if ((ids && is_device_ptr(ids)) || (is_new && is_device_ptr(is_new)) || (packs_out && is_device_ptr(packs_out)))
+    return fail(MCDC_E_INVALID, "ids / is_new / packs_out must be host memory");
+  *nblobs = 0;
+  *npacks = 0;
+  if (packs_bytes) *packs_bytes = 0;
+  const double t0 = now_ms();
+  const bool host_in = data && !is_device_ptr(data);
+  // the bytes in HBM (one copy of a host input)
+  const uint8_t *d = (const uint8_t *)data;
+  if (host_in && n) {
+    if ((rc = ensure(ctx, ctx->sv_in, n))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->sv_in.p, data, n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    d = (const uint8_t *)ctx->sv_in.p;
+  }
+  // processor::save_file: a file smaller than MIN_CHUNK_SIZE is one blob
+  // (:144-153); the others go through the chunker (:160-205)
+  std::vector<uint64_t> boff, blen;
+  std::vector<size_t> big;
+  size_t cap = 0;
+  for (size_t f = 0; f < nfiles; ++f)
+    if (files[f].length >= params->min_size) {
+      big.push_back(f);
+      boff.push_back(files[f].offset);
+      blen.push_back(files[f].length);
+      cap += files[f].length / (params->min_size - 1) + 2;
+    }
+  std::vector<mcdc_chunk> bch(std::max<size_t>(cap, 1));
+  std::vector<size_t> bcnt(std::max<size_t>(big.size(), 1));
+  if (!big.empty()) {
+    size_t got = 0;
+    if ((rc = mcdc_chunk_batch_device(ctx, params, d, boff.data(), blen.data(), big.size(), bch.data(), cap,
+                                      bcnt.data(), &got)))
+      return rc;
+  }
+  // every blob in processing order (file order, chunk order), offsets into d
+  std::vector<mcdc_chunk> list;
+  list.reserve(nfiles + cap);
+  size_t bi = 0, at = 0;
+  for (size_t f = 0; f < nfiles; ++f) {
+    file_blobs[f] = list.size();
+    if (bi < big.size() && big[bi] == f) {
+      for (size_t j = 0; j < bcnt[bi]; ++j, ++at)
+        list.push_back(mcdc_chunk{files[f].offset + bch[at].offset, bch[at].length, bch[at].hash});
+      ++bi;
+    } else {
+      list.push_back(mcdc_chunk{files[f].offset, files[f].length, 0});
+    }
+  }
+  if (nfiles) file_blobs[nfiles] = list.size();
+  const size_t nb = list.size();
+  *nblobs = nb;
+  if (nb > blobs_cap || (nb && !ids)) return fail(MCDC_E_CAPACITY, "%zu blobs, capacity %zu", nb, blobs_cap);
+  // ID::from_content of every blob (CalculateID of a small file is the same hash)
+  if (nb && (rc = mcdc_chunk_ids_device(ctx, d, n, list.data(), nb, ids))) return rc;
+  // save_blob's dedup check (:173-180) -- the index changes here; a later
+  // capacity failure puts it back (the previous buffer is intact until the
+  // next add)
+  std::vector<uint8_t> nw(std::max<size_t>(nb, 1));
+  size_t m = 0;
+  if (nb && (rc = mcdc_index_add(ctx, ix, ids, nb, nw.data(), nullptr, nullptr, &m))) return rc;
+  auto rollback = [&]() {
+    if (nb) {
+      ix->cur ^= 1;
+      ix->size -= m;
+    }
+  };
+  if (store->key && m > store->nnonces) {
+    rollback();
+    return fail(MCDC_E_INVALID, "%zu new blobs need %zu nonces (%zu given)", m, m, store->nnonces);
+  }
+  // the stored blobs' bytes in host memory for the zstd stage
+  std::vector<mcdc_blob> sext;
+  std::vector<uint8_t> sids, types;
+  sext.reserve(m);
+  sids.reserve(32 * m);
+  for (size_t i = 0; i < nb; ++i)
+    if (nw[i]) {
+      sext.push_back(mcdc_blob{list[i].offset, list[i].length});
+      sids.insert(sids.end(), ids + 32 * i, ids + 32 * i + 32);
+    }
+  types.assign(std::max<size_t>(m, 1), 0);  // BlobType::Data (processor.rs:191)
+  std::vector<uint8_t> staged;
+  const uint8_t *src = (const uint8_t *)data;
+  if (!host_in && m) {  // device input: bring the new blobs over (the zstd stage runs on the host)
+    size_t tot = 0;
+    for (auto &e : sext) tot += e.length;
+    staged.resize(std::max<size_t>(tot, 1));
+    size_t o = 0;
+    for (auto &e : sext) {
+      if (e.length) HIP_TRY(hipMemcpyAsync(staged.data() + o, d + e.offset, e.length, hipMemcpyDeviceToHost,
+                                           ctx->stream));
+      e.offset = o;
+      o += e.length;
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    src = staged.data();
+  }
+  const size_t src_n = host_in ? n : staged.size();
+  // SecureStorage::encode of every stored blob (:182)
+  std::vector<uint64_t> eo(m + 1, 0);
+  size_t ecap = 0;
+  for (auto &e : sext) ecap += e.length + e.length / 64 + 64;
+  std::vector<uint8_t> enc(std::max<size_t>(ecap, 1));
+  if (m) {
+    rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), ecap, eo.data());
+    if (rc == MCDC_E_CAPACITY) {
+      enc.resize(std::max<uint64_t>(eo[m], 1));
+      rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), enc.size(),
+                             eo.data());
+    }
+    if (rc) {
+      rollback();
+      return rc;
+    }
+  }
+  std::vector<mcdc_blob> eext(m);
+  for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
+  // Packer::add_blob + flush (:185-192) and the final flush
+  size_t pb = 0, np = 0;
+  rc = mcdc_pack_blobs(ctx, store->key, enc.data(), eo[m], eext.data(), sids.data(), types.data(), m,
+                       store->max_pack_size, store->header_nonces, store->nheader_nonces, store->padding,
+                       store->npadding, packs_out, packs_out_cap, &pb, packs, packs_cap, &np);
+  if (packs_bytes) *packs_bytes = pb;
+  *npacks = np;
+  if (rc) {
+    rollback();
+    return rc;
+  }
+  if (is_new) std::memcpy(is_new, nw.data(), nb);
+  ctx->timing = mcdc_timing{};
+  ctx->timing.bytes = n;
+  ctx->timing.chunks = nb;
+  ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
 }
 

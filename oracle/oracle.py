@@ -694,3 +694,51 @@ def parse_header(header_data: bytes, key=None):
         out.append((bytes(e[:32]), e[36], cur, ln))
         cur += ln
     return out
+
+
+def save_files(params: Params, files, index=None, key=None, nonces=None, header_nonces=None, padding=None,
+               max_pack_size: int = 16 << 20, threads: int = 8):
+    """The Archiver's save path for a run of files, in file order, restated
+    (test infrastructure; the product is mcdc_save_files):
+
+    * processor::save_file (processor.rs:138-157): a file smaller than
+      MIN_CHUNK_SIZE (params.min_size) is one blob, ID = ID::from_content of
+      the whole file (SaveID::CalculateID); otherwise chunk_and_save_blobs
+      (:160-205): StreamCDC chunks, ID::from_content per chunk, in order;
+    * Repository::save_blob (repository_v1.rs:155-195) per blob: skip it when
+      index.contains(id) || !add_pending_blob(id) (:173-180, DedupIndex), else
+      SecureStorage::encode (:182; storage_encode: nonces[k] for the k-th
+      stored blob) and Packer::add_blob, flushing once the packer holds more
+      than max_pack_size bytes (:185-192); one final flush at the end
+      (Repository::flush at the end of the snapshot);
+    * Packer::flush (pack_flush): header_nonces[j] for the j-th pack, padding
+      entries drawn in order from `padding` (36 bytes each).
+
+    Returns (ids_per_file: list of (k, 32) uint8 arrays, is_new: bool per blob
+    in processing order, packs: list of (data, descriptors))."""
+    index = DedupIndex() if index is None else index
+    per_file, blob_bytes = [], []
+    for f in files:
+        a = np.ascontiguousarray(np.frombuffer(f, np.uint8) if not isinstance(f, np.ndarray) else f, np.uint8)
+        if a.size < params.min_size:
+            ch = np.zeros(1, dtype=CHUNK_DTYPE)
+            ch["length"] = a.size
+        else:
+            ch = chunk(params, a)
+        ids = chunk_ids(a, ch, threads=threads)
+        per_file.append(ids)
+        blob_bytes += [a[int(o):int(o + n)].tobytes() for o, n in zip(ch["offset"], ch["length"])]
+    all_ids = np.concatenate(per_file) if per_file else np.zeros((0, 32), np.uint8)
+    is_new = index.add(all_ids) if len(all_ids) else np.zeros(0, bool)
+    stored = [(all_ids[i].tobytes(), blob_bytes[i]) for i in np.nonzero(is_new)[0]]
+    enc = [storage_encode(b, key, None if key is None else bytes(nonces[k])) for k, (_, b) in enumerate(stored)]
+    packs, pad_at = [], 0
+    for j, (f0, f1) in enumerate(pack_plan([len(e) for e in enc], max_pack_size)):
+        cnt = f1 - f0
+        npad = (HEADER_BLOB_MULTIPLE - cnt % HEADER_BLOB_MULTIPLE) % HEADER_BLOB_MULTIPLE
+        pad = [(bytes(padding[pad_at + t][:32]), 0, int.from_bytes(bytes(padding[pad_at + t][32:36]), "little"))
+               for t in range(npad)]
+        pad_at += npad
+        packs.append(pack_flush(enc[f0:f1], [stored[i][0] for i in range(f0, f1)], [0] * cnt, pad, key,
+                                None if key is None else bytes(header_nonces[j])))
+    return per_file, is_new, packs

@@ -113,7 +113,7 @@ def test_configs2_10000_files_full(ctx):
     p = _lib.params(*P16)
     offs = np.arange(nfiles, dtype=np.uint64) * np.uint64(size)
     lens = np.full(nfiles, size, dtype=np.uint64)
-    big = _lib.Context(0, 1 << 30)
+    big = _lib.Context(0, nfiles * size)
     try:
         arena = big.device_alloc(n)
         cap = nfiles * (size // (P16[0] - 1) + 2)
@@ -142,7 +142,7 @@ def test_configs4_rank_slice_8192_files(ctx):
     nfiles, size = 8192, 8 << 20
     p = _lib.params(*P16)
     sizes = [size] * nfiles
-    big = _lib.Context(0, 1 << 30)
+    big = _lib.Context(0, nfiles * size)
     try:
         arena = big.device_alloc(nfiles * size)
         cap = nfiles * (size // (P16[0] - 1) + 2)

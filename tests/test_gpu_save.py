@@ -1,0 +1,169 @@
+"""The composed save path (mcdc_save_files) against the composed restatement
+(oracle.save_files) of processor::save_file / chunk_and_save_blobs
+(/root/reference/src/archiver/processor.rs:138-205) and
+Repository::save_blob (repository_v1.rs:155-195): per-file ID lists in file
+order, which blobs were stored, and every pack byte for byte (blobs encoded by
+SecureStorage with and without a key, headers, trailers, pack IDs).
+
+Inputs: files of mixed sizes around the MIN_CHUNK_SIZE gate (empty, 1 byte,
+min - 1, min, min + 1, several MiB), a file repeated whole, two files sharing
+a long middle region (chunk-level duplicates after the chains resync), two
+equal small files; a second snapshot over the same index with one file
+changed; host and device input; capacity errors that leave the index as it
+was."""
+import numpy as np
+import pytest
+
+from mapache_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+P16 = (16384, 65536, 262144, 1)
+KEY = bytes(range(0xA0, 0xC0))
+
+
+def _files(seed=3):
+    r = lambda n, s: O.random_bytes(n, seed * 1000 + s)  # noqa: E731
+    shared = r(3 << 20, 1)
+    files = [np.zeros(0, np.uint8), r(1, 2), r(16383, 3), r(16384, 4), r(16385, 5), r(5 << 20, 6),
+             np.concatenate([r(700_001, 7), shared, r(90_000, 8)]), r(2 << 20, 9),
+             np.concatenate([r(123_457, 10), shared, r(400_000, 11)]), r(900, 12)]
+    files.insert(7, files[5].copy())  # a file repeated whole
+    files.append(files[10].copy())  # two equal small files
+    return files
+
+
+def _arena(files):
+    offs, at = [], 0
+    for f in files:
+        at += 3  # every file at another alignment
+        offs.append(at)
+        at += f.size
+    data = np.zeros(at + 5, np.uint8)
+    for o, f in zip(offs, files):
+        data[o:o + f.size] = f
+    return data, np.array(offs, np.uint64), np.array([f.size for f in files], np.uint64)
+
+
+def _rand(seed, n, width):
+    return np.random.default_rng(seed).integers(0, 256, (n, width), dtype=np.uint8)
+
+
+def _check(got, ref):
+    g_ids, g_new, g_out, g_packs = got
+    r_ids, r_new, r_packs = ref
+    assert len(g_ids) == len(r_ids)
+    for f, (a, b) in enumerate(zip(g_ids, r_ids)):
+        assert a.shape == b.shape and (a == b).all(), f
+    assert (g_new == r_new).all()
+    assert len(g_packs) == len(r_packs)
+    at = 0
+    for k, (rp, _) in enumerate(r_packs):
+        p = g_packs[k]
+        assert int(p["offset"]) == at and int(p["length"]) == len(rp), k
+        assert g_out[at:at + len(rp)].tobytes() == rp, k
+        assert bytes(p["id"]) == O.blake3(np.frombuffer(rp, np.uint8))
+        at += len(rp)
+    assert at == g_out.size
+
+
+@pytest.mark.parametrize("key", [None, KEY], ids=["no-key", "key"])
+def test_save_files_matches_restatement(ctx, key):
+    files = _files()
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    nonces, hn, pad = _rand(1, 4000, 12), _rand(2, 64, 12), _rand(3, 64 * 63, 36)
+    with ctx.index_create() as ix:
+        got = ctx.save_files(p, ix, data, offs, lens, key, nonces, hn, pad, max_pack_size=1 << 20)
+        assert len(ix) == int(got[1].sum())
+    ref = O.save_files(O.Params(*P16), files, None, key, nonces, hn, pad, max_pack_size=1 << 20)
+    _check(got, ref)
+    ids = got[0]
+    assert len(ids[0]) == 1 and ids[0][0].tobytes() == O.blake3(np.zeros(0, np.uint8))  # empty file: one blob
+    assert (ids[7] == ids[5]).all() and (ids[11] == ids[10]).all()
+    new = got[1]
+    assert new.sum() < len(new)  # duplicates stored once
+    # the shared region's interior chunks are stored once
+    assert len({x.tobytes() for x in ids[6]} & {x.tobytes() for x in ids[9]}) >= 30
+
+
+def test_second_snapshot_stores_only_changes(ctx):
+    files = _files(4)
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    nonces, hn, pad = _rand(4, 4000, 12), _rand(5, 64, 12), _rand(6, 64 * 63, 36)
+    ref_ix = O.DedupIndex()
+    with ctx.index_create() as ix:
+        ctx.save_files(p, ix, data, offs, lens, KEY, nonces, hn, pad)
+        O.save_files(O.Params(*P16), files, ref_ix, KEY, nonces, hn, pad)
+        files2 = [f.copy() for f in files]
+        files2[5][3_000_000] ^= 0xFF  # one byte changed in a 5 MiB file
+        files2.append(O.random_bytes(40_000, 99))  # one new file
+        data2, offs2, lens2 = _arena(files2)
+        got = ctx.save_files(p, ix, data2, offs2, lens2, KEY, nonces, hn, pad)
+        ref = O.save_files(O.Params(*P16), files2, ref_ix, KEY, nonces, hn, pad)
+        assert len(ix) == len(ref_ix)
+    _check(got, ref)
+    assert 1 <= int(got[1].sum()) <= 4  # the changed chunk(s) and the new file
+
+
+def test_device_input_equals_host_input(ctx):
+    files = _files(5)
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    nonces, hn, pad = _rand(7, 4000, 12), _rand(8, 64, 12), _rand(9, 64 * 63, 36)
+    dp = ctx.device_alloc(data.size)
+    try:
+        ctx.h2d(dp, data)
+        with ctx.index_create() as ix:
+            a = ctx.save_files(p, ix, dp, offs, lens, KEY, nonces, hn, pad, n=data.size)
+        with ctx.index_create() as ix:
+            b = ctx.save_files(p, ix, data, offs, lens, KEY, nonces, hn, pad)
+    finally:
+        ctx.device_free(dp)
+    assert all((x == y).all() for x, y in zip(a[0], b[0]))
+    assert (a[1] == b[1]).all() and a[2].tobytes() == b[2].tobytes()
+
+
+def test_mapache_defaults_and_empty_call(ctx):
+    """512K/1M/8M (mapache's own parameters): files below 512 KiB are single
+    blobs, larger ones chunked; an empty call stores nothing."""
+    rng = np.random.default_rng(11)
+    files = [O.random_bytes(int(n), 50 + i) for i, n in enumerate(rng.integers(0, 12 << 20, 7))]
+    files.append(O.random_bytes((512 << 10) - 1, 70))
+    data, offs, lens = _arena(files)
+    p = _lib.params(512 << 10, 1 << 20, 8 << 20, 1)
+    pad = _rand(10, 64 * 63, 36)
+    with ctx.index_create() as ix:
+        got = ctx.save_files(p, ix, data, offs, lens, None, None, None, pad)
+        empty = ctx.save_files(p, ix, np.zeros(0, np.uint8), [], [], None, None, None, pad)
+    ref = O.save_files(O.Params(512 << 10, 1 << 20, 8 << 20, 1), files, None, None, None, None, pad)
+    _check(got, ref)
+    assert len(got[0][-1]) == 1
+    assert empty[2].size == 0 and len(empty[3]) == 0
+
+
+def test_capacity_error_leaves_index_unchanged(ctx):
+    import ctypes
+    files = _files(6)
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    pad = _rand(12, 64 * 63, 36)
+    ext = np.stack([offs, lens], axis=1).astype(np.uint64)
+    st = _lib.McdcStore(None, 1 << 20, None, 0, None, 0, pad.ctypes.data, len(pad))
+    fb = np.zeros(len(files) + 1, np.uint64)
+    ids = np.zeros((4000, 32), np.uint8)
+    out = np.empty(100, np.uint8)
+    packs = np.zeros(64, _lib.PACK_DTYPE)
+    nb, pb, np_ = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    with ctx.index_create() as ix:
+        for cap_ids, cap_out in ((3, out.size), (len(ids), out.size)):
+            rc = _lib.load().mcdc_save_files(ctx._h, ctypes.byref(p), ctypes.c_void_p(ix._h), ctypes.byref(st),
+                                             data.ctypes.data, data.size, ext.ctypes.data, len(files),
+                                             fb.ctypes.data, ids.ctypes.data, None, cap_ids, ctypes.byref(nb),
+                                             out.ctypes.data, cap_out, ctypes.byref(pb), packs.ctypes.data,
+                                             packs.size, ctypes.byref(np_))
+            assert rc == _lib.MCDC_E_CAPACITY and len(ix) == 0
+        assert nb.value > 3 and pb.value > 100
+        got = ctx.save_files(p, ix, data, offs, lens, None, None, None, pad, max_pack_size=1 << 20)
+        assert len(ix) == int(got[1].sum()) and got[2].size == pb.value

@@ -11,7 +11,12 @@ instructions, register assignment and schedule stay byte-identical, only the
 allocation grows past the registers it uses, so it separates "the allocation
 ends at the last register used" from "this particular code".
 
-    python tools/dbg/kd_patch.py LIB.so CODE_OBJECT.out KERNEL_SUBSTR NEW_VGPRS OUT.so
+    python tools/dbg/kd_patch.py LIB.so CODE_OBJECT.out KERNEL_SUBSTR NEW_VGPRS OUT.so [NEW_ACCUM_OFFSET]
+
+NEW_ACCUM_OFFSET (optional) also moves COMPUTE_PGM_RSRC3.ACCUM_OFFSET (the
+first AGPR of the unified register file; the kernels here use no AGPRs) --
+only upwards and never past the new allocation, so the registers the code
+names stay architectural VGPRs.
 """
 import os
 import struct
@@ -21,7 +26,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from mapache_amd import devaudit as A  # noqa: E402
 
 
-def main(lib, co, ksub, new_vgprs, out):
+def main(lib, co, ksub, new_vgprs, out, new_acc=None):
     import re
     import subprocess
     syms = subprocess.run([f"{A.LLVM}/llvm-readelf", "-sW", co], capture_output=True, text=True, check=True).stdout
@@ -50,9 +55,18 @@ def main(lib, co, ksub, new_vgprs, out):
     if pos < 0 or data.find(kd, pos + 1) >= 0:
         raise SystemExit("descriptor not found exactly once in the library (compressed bundle or different build?)")
     struct.pack_into("<I", data, pos + 48, (rsrc1 & ~0x3F) | g_new)
+    msg = ""
+    if new_acc is not None:
+        rsrc3 = struct.unpack_from("<I", kd, 44)[0]
+        a_old = ((rsrc3 & 0x3F) + 1) * 4
+        if new_acc % 4 or new_acc < a_old or new_acc > new_vgprs:
+            raise SystemExit(f"refusing accum_offset {new_acc} (now {a_old}, allocation {new_vgprs})")
+        struct.pack_into("<I", data, pos + 44, (rsrc3 & ~0x3F) | (new_acc // 4 - 1))
+        msg = f", accum_offset {a_old} -> {new_acc}"
     open(out, "wb").write(bytes(data))
-    print(f"{name}: VGPR allocation {(g_old + 1) * 8} -> {new_vgprs} at file offset {pos:#x}; wrote {out}")
+    print(f"{name}: VGPR allocation {(g_old + 1) * 8} -> {new_vgprs}{msg} at file offset {pos:#x}; wrote {out}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5])
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5],
+         int(sys.argv[6]) if len(sys.argv) > 6 else None)
