@@ -251,6 +251,22 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
                             size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,
                             mcdc_blob *frames);
 
+/* SecureStorage::compress (storage.rs:74-84) of every chunk of a boundary
+ * list on the GPU: frame i is a zstd frame of chunk i in the crate's layout
+ * (magic, Frame_Header_Descriptor 0x00: no content size, no checksum; window
+ * 2^20 = storage.rs:31) of 16 KiB blocks, each compressed (raw literals,
+ * sequences with the predefined FSE tables) or raw when that is not smaller.
+ * mapache's decoder (zstd, window_log_max 20, :87-94) reads them; the bytes
+ * differ from libzstd's level 3 (parity = decode-equality, ratio reported by
+ * the bench).  Frames are written back to back from d_out (no alignment);
+ * frames[i] (host or device) receives (offset, length).  *out_bytes: the bytes
+ * written; on MCDC_E_CAPACITY the capacity that always suffices (the raw
+ * frames: sum of length + 6 + 3 per 16 KiB block).  chunks: host or device;
+ * a chunk outside [0, n) or of 2 GiB or more -> MCDC_E_INVALID. */
+int mcdc_zstd_compress_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
+                              size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,
+                              mcdc_blob *frames);
+
 /* Packer::add_blob + flush (/root/reference/src/repository/packer.rs:101-186;
  * flushed when the packer holds more than max_pack_size bytes,
  * repository_v1.rs:185-193, and once more at the end) over a run of encoded

@@ -38,6 +38,7 @@ EXPORTS = (
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
     "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device", "mcdc_save_files",
+    "mcdc_zstd_compress_device",
 )
 
 
@@ -142,8 +143,10 @@ def load():
     if hasattr(L, "mcdc_save_files"):
         L.mcdc_save_files.argtypes = [vp, P(McdcParams), vp, P(McdcStore), vp, sz, vp, sz, vp, vp, vp, sz, P(sz), vp,
                                       sz, P(sz), vp, sz, P(sz)]
+    if hasattr(L, "mcdc_zstd_compress_device"):
+        L.mcdc_zstd_compress_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, P(sz), vp]
     for name in EXPORTS:  # fail loudly if the build is stale (the in-tree build)
-        if not os.environ.get("MCDC_LIBRARY") or name != "mcdc_save_files":
+        if not os.environ.get("MCDC_LIBRARY") or name not in ("mcdc_save_files", "mcdc_zstd_compress_device"):
             getattr(L, name)
     _lib = L
     return L
@@ -389,6 +392,35 @@ class Context:
                                              ctypes.c_void_p(d_out), out_cap, ctypes.byref(span),
                                              ctypes.c_void_p(fptr)))
         return (None if fr is None else fr[:count]), span.value
+
+    @_locked
+    def zstd_compress(self, d_data: int, n: int, chunks, d_out: int, out_cap: int, frames_out=None):
+        """SecureStorage::compress of every chunk on the GPU
+        (mcdc_zstd_compress_device).  chunks: CHUNK_DTYPE array or (device
+        pointer, count).  Returns (frames as (count, 2) uint64 (offset, length)
+        or None with frames_out, bytes written).  out_cap too small raises
+        McdcError(MCDC_E_CAPACITY); zstd_compress_bound gives the capacity."""
+        if isinstance(chunks, tuple):
+            cptr, count = chunks
+        else:
+            arr = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+            cptr, count = arr.ctypes.data, arr.size
+            keep = arr  # noqa: F841
+        span = ctypes.c_size_t()
+        fr = None if frames_out is not None else np.zeros((max(count, 1), 2), dtype=np.uint64)
+        fptr = frames_out if frames_out is not None else fr.ctypes.data
+        check(load().mcdc_zstd_compress_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(cptr), count,
+                                               ctypes.c_void_p(d_out), out_cap, ctypes.byref(span),
+                                               ctypes.c_void_p(fptr)))
+        return (None if fr is None else fr[:count]), span.value
+
+    @staticmethod
+    def zstd_compress_bound(lengths) -> int:
+        """Output capacity that always suffices for zstd_compress: the raw frames
+        of 16 KiB blocks (length + 6 + 3 per block)."""
+        ln = np.asarray(lengths, dtype=np.uint64)
+        nb = np.maximum((ln + np.uint64(16383)) // np.uint64(16384), np.uint64(1))
+        return int((ln + np.uint64(6) + np.uint64(3) * nb).sum())
 
     @_locked
     def pack_blobs(self, key, data, offsets, lengths, ids, types, max_pack_size: int, header_nonces, padding):

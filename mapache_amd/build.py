@@ -22,8 +22,8 @@ ARCH = os.environ.get("MCDC_ARCH", "gfx950")
 CXXFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 LIB_SRCS = ["csrc/mcdc_kernels.hip", "csrc/mcdc_blake3.hip", "csrc/mcdc_aead.hip", "csrc/mcdc_index.hip",
-            "csrc/mcdc_zframe.hip", "csrc/mcdc_api.hip"]
-LIB_DEPS = LIB_SRCS + ["csrc/mcdc_internal.h", "csrc/mcdc_blake3.h", "csrc/mcdc_aead.h", "csrc/mcdc_index.h", "csrc/mcdc_zframe.h", "csrc/gear_table.h", "../include/mcdc.h",
+            "csrc/mcdc_zframe.hip", "csrc/mcdc_zcomp.hip", "csrc/mcdc_api.hip"]
+LIB_DEPS = LIB_SRCS + ["csrc/mcdc_internal.h", "csrc/mcdc_blake3.h", "csrc/mcdc_aead.h", "csrc/mcdc_index.h", "csrc/mcdc_zframe.h", "csrc/mcdc_zcomp.h", "csrc/mcdc_zstd.h", "csrc/gear_table.h", "../include/mcdc.h",
                        "host/batcher.hpp", "host/zstd_stage.hpp"]
 
 
@@ -192,6 +192,15 @@ def build_cpu_tests(force: bool = False) -> None:
               "-Lmapache_amd", "-lmcdc", "-Wl,-rpath,$ORIGIN/../../mapache_amd", "-lpthread", "-lm"], ROOT)
 
 
+def build_format_tests(force: bool = False) -> None:
+    """tests/cpp/test_zstd_format: the zstd format pieces of csrc/mcdc_zstd.h on
+    the host (hipcc for their __host__ __device__ functions), checked with libzstd."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_zstd_format.cpp")
+    out = os.path.join(ROOT, "tests", "cpp", "test_zstd_format")
+    if os.path.exists(src) and (force or _stale(out, [src, os.path.join(HERE, "csrc", "mcdc_zstd.h")])):
+        _run([HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-o", out, src, "-ldl"], ROOT)
+
+
 def build_tools(force: bool = False) -> None:
     for name in ("scanbench",):
         src = os.path.join(ROOT, "tools", f"{name}.hip")
@@ -219,6 +228,7 @@ def main(argv=None) -> int:
         build_oracle()
         build_host_tests(a.force)
         build_cpu_tests(a.force)
+        build_format_tests(a.force)
         build_tools(a.force)
     return 0
 

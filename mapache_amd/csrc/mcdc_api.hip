@@ -28,6 +28,7 @@
 #include "mcdc_blake3.h"
 #include "mcdc_index.h"
 #include "mcdc_zframe.h"
+#include "mcdc_zcomp.h"
 #include "mcdc_internal.h"
 #include "../host/zstd_stage.hpp"
 
@@ -223,7 +224,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in;
+      sv_in, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -880,7 +881,8 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in};
+                    &ctx->sv_in, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
+                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1595,6 +1597,82 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   ctx->timing = mcdc_timing{};
   ctx->timing.bytes = n;
   ctx->timing.chunks = nb;
+  ctx->timing.total_ms = now_ms() - t0;
+  return MCDC_OK;
+}
+
+// ---------------------------------------------------- zstd compression --
+// SecureStorage::compress (storage.rs:74-84) of every chunk on the GPU
+// (mcdc_zcomp.hip): one zstd frame per chunk, frames back to back.
+int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks, size_t nchunks,
+                              void *d_out, size_t out_cap, size_t *out_bytes, mcdc_blob *frames) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if ((!d_data && n) || (nchunks && (!chunks || !frames))) return fail(MCDC_E_INVALID, "NULL argument");
+  if ((d_data && !is_device_ptr(d_data)) || (d_out && !is_device_ptr(d_out)))
+    return fail(MCDC_E_INVALID, "d_data / d_out must be device pointers");
+  if (out_bytes) *out_bytes = 0;
+  if (nchunks == 0) return MCDC_OK;
+  if (nchunks >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many chunks (%zu)", nchunks);
+  static const zs::ZTables T = zs::build_tables();
+  const double t0 = now_ms();
+  hipStream_t st = ctx->stream;
+  const size_t tmpb = std::max(zc_tmp_bytes(nchunks), zc_tmp_bytes(kZcBatchBlocks));
+  if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, nchunks * sizeof(mcdc_chunk))) ||
+      (rc = ensure(ctx, ctx->zc_cnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->zc_first, (nchunks + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)))
+    return rc;
+  uint64_t *misc = (uint64_t *)ctx->zc_misc.p;  // [0] err, [1] raw bound, [2] output base
+  HIP_TRY(hipMemsetAsync(misc, 0, 32, st));
+  HIP_TRY(hipEventRecord(ctx->ev_start, st));
+  const DevChunk *dch = (const DevChunk *)ctx->b3_chunks.p;
+  uint64_t *first = (uint64_t *)ctx->zc_first.p;
+  launch_zc_nblocks(dch, nchunks, n, (uint64_t *)ctx->zc_cnt.p, first, (uint32_t *)misc, misc + 1, ctx->zc_tmp.p,
+                    tmpb, st);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint64_t> hfirst(nchunks + 1);
+  uint64_t hm[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(hm, misc, 16, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hfirst.data(), first, (nchunks + 1) * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hm[0]) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer or is 2 GiB or longer", n);
+  if (out_bytes) *out_bytes = hm[1];  // the capacity that always suffices (raw frames of 16 KiB blocks)
+  if (hm[1] > out_cap || !d_out)
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", out_cap, (unsigned long long)hm[1]);
+  uint64_t *ext = (uint64_t *)direct_out(ctx, frames);
+  if (!ext && is_device_ptr(frames)) return fail(MCDC_E_INVALID, "frames is a device pointer of another device");
+  if (!ext) {
+    if ((rc = ensure(ctx, ctx->zf_ext, nchunks * 16))) return rc;
+    ext = (uint64_t *)ctx->zf_ext.p;
+  }
+  const uint64_t total_blocks = hfirst[nchunks];
+  const uint64_t mb = std::min<uint64_t>(total_blocks, kZcBatchBlocks);
+  if ((rc = ensure(ctx, ctx->zc_blocks, mb * sizeof(ZcBlock))) || (rc = ensure(ctx, ctx->zc_stage, mb * kZcSlot)) ||
+      (rc = ensure(ctx, ctx->zc_seqs, mb * kZcSeqCap * 8)) || (rc = ensure(ctx, ctx->zc_piece, (mb + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)))
+    return rc;
+  for (uint64_t c0 = 0; c0 < nchunks;) {  // batches of whole chunks, <= kZcBatchBlocks blocks each
+    uint64_t c1 = c0 + 1;
+    while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb) ++c1;
+    launch_zc_batch((const uint8_t *)d_data, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
+                    (ZcBlock *)ctx->zc_blocks.p, (uint8_t *)ctx->zc_stage.p, (uint64_t *)ctx->zc_seqs.p, T,
+                    (uint64_t *)ctx->zc_piece.p, (uint64_t *)ctx->zc_poff.p, misc + 2, (uint8_t *)d_out, ext,
+                    ctx->zc_tmp.p, tmpb, st);
+    HIP_TRY(hipGetLastError());
+    c0 = c1;
+  }
+  HIP_TRY(hipEventRecord(ctx->ev_end, st));
+  uint64_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, misc + 2, 8, hipMemcpyDeviceToHost, st));
+  if (ext == ctx->zf_ext.p) HIP_TRY(hipMemcpyAsync(frames, ext, nchunks * 16, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (out_bytes) *out_bytes = total;
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_end));
+  ctx->timing = mcdc_timing{};
+  ctx->timing.device_ms = ms;
+  ctx->timing.bytes = n;
+  ctx->timing.chunks = nchunks;
   ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
 }

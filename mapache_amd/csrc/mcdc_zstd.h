@@ -1,0 +1,290 @@
+// mcdc_zstd.h — zstd (RFC 8878) compressed-block format pieces shared by the
+// GPU compressor (mcdc_zstd.hip) and its CPU format test
+// (tests/cpp/test_zstd_format.cpp, built with hipcc, run on the host).
+//
+// What mapache stores is SecureStorage::compress's output
+// (/root/reference/src/repository/storage.rs:74-84): one zstd frame per blob,
+// level 3, window log 20 (log2 AVG_CHUNK_SIZE, :31), no checksum, written by the
+// crate's streaming encoder (no content size).  The GPU writes the same frame
+// header (magic, descriptor 0x00, window descriptor 0x50) and blocks that are
+// either raw or compressed with
+//   * Raw_Literals_Block literals (3-byte header, Size_Format 11),
+//   * sequences coded with the predefined FSE distributions of RFC 8878
+//     §3.1.1.3.2.2 (Predefined_Mode for literal lengths, offsets and match
+//     lengths: no table descriptions),
+//   * offsets always as Offset_Value = offset + 3 (no repeat codes).
+// Any conforming decoder (mapache's: zstd with window_log_max 20,
+// storage.rs:87-94) reads them; the compressed bytes differ from libzstd's,
+// so parity is decode-equality.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace mcdc {
+namespace zs {
+
+constexpr uint32_t kMagic = 0xFD2FB528u;
+constexpr uint8_t kFhd = 0x00, kWd = 0x50;  // no content size / checksum; window 2^20
+constexpr uint32_t kWindow = 1u << 20;
+constexpr uint32_t kMinMatch = 4;           // the GPU parse's shortest match
+constexpr uint32_t kFrameHdr = 6, kBlockHdr = 3, kLitHdr = 3;
+
+// ---- sequence codes (RFC 8878 §3.1.1.3.2.1) -------------------------------
+__host__ __device__ inline uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+
+__host__ __device__ inline uint32_t ll_code(uint32_t ll) {
+  if (ll < 16) return ll;
+  if (ll < 64) {
+    // 16,18,20,22 (1 bit) 24,28 (2) 32,40 (3) 48 (4)
+    if (ll < 24) return 16 + ((ll - 16) >> 1);
+    if (ll < 32) return 20 + ((ll - 24) >> 2);
+    if (ll < 48) return 22 + ((ll - 32) >> 3);
+    return 24;
+  }
+  return highbit(ll) + 19;  // 64: code 25 (6 bits), 128: 26 (7 bits), ...
+}
+__host__ __device__ inline uint32_t ll_bits(uint32_t code) {
+  if (code < 16) return 0;
+  if (code < 20) return 1;
+  if (code < 22) return 2;
+  if (code < 24) return 3;
+  if (code == 24) return 4;
+  return code - 19;  // 25: 6 ... 35: 16
+}
+// mb = match length - 3
+__host__ __device__ inline uint32_t ml_code(uint32_t mb) {
+  if (mb < 32) return mb;
+  if (mb < 128) {
+    // 32,34,36,38 (1 bit) 40,44 (2) 48,56 (3) 64,80 (4) 96 (5)
+    if (mb < 40) return 32 + ((mb - 32) >> 1);
+    if (mb < 48) return 36 + ((mb - 40) >> 2);
+    if (mb < 64) return 38 + ((mb - 48) >> 3);
+    if (mb < 96) return 40 + ((mb - 64) >> 4);
+    return 42;
+  }
+  return highbit(mb) + 36;  // 128: code 43 (7 bits) ...
+}
+__host__ __device__ inline uint32_t ml_bits(uint32_t code) {
+  if (code < 32) return 0;
+  if (code < 36) return 1;
+  if (code < 38) return 2;
+  if (code < 40) return 3;
+  if (code < 42) return 4;
+  if (code == 42) return 5;
+  return code - 36;  // 43: 7 ... 52: 16
+}
+
+// ---- FSE compression tables for the predefined distributions --------------
+// Built exactly as the decoder's spread (RFC 8878 §4.1.1) defines the states,
+// in the encoder form of zstd's FSE_buildCTable: per symbol deltaNbBits /
+// deltaFindState, and the next-state table sorted by symbol.
+struct FseCT {
+  uint16_t state[64];
+  int32_t dfs[53];
+  uint32_t dnb[53];
+  uint32_t log;
+};
+struct ZTables {
+  FseCT ll, ml, of;
+};
+
+// Predefined normalized distributions (RFC 8878 §3.1.1.3.2.2).
+constexpr int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1,
+                                 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1,
+                                 -1, -1, -1, -1};
+constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1,
+                                 -1, -1, -1, -1, -1};
+constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCT &ct) {
+  const uint32_t size = 1u << tlog;
+  uint32_t high = size - 1;
+  uint8_t sym[64];
+  uint32_t cumul[54];
+  cumul[0] = 0;
+  for (int u = 1; u <= nsym; ++u) {
+    if (norm[u - 1] == -1) {
+      cumul[u] = cumul[u - 1] + 1;
+      sym[high--] = (uint8_t)(u - 1);
+    } else {
+      cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
+    }
+  }
+  const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+  uint32_t pos = 0;
+  for (int s = 0; s < nsym; ++s)
+    for (int i = 0; i < norm[s]; ++i) {
+      sym[pos] = (uint8_t)s;
+      pos = (pos + step) & mask;
+      while (pos > high) pos = (pos + step) & mask;
+    }
+  for (uint32_t u = 0; u < size; ++u) ct.state[cumul[sym[u]]++] = (uint16_t)(size + u);
+  int32_t total = 0;
+  for (int s = 0; s < nsym; ++s) {
+    const int n = norm[s];
+    if (n == 0) {
+      ct.dnb[s] = ((tlog + 1) << 16) - size;
+      ct.dfs[s] = 0;
+    } else if (n == -1 || n == 1) {
+      ct.dnb[s] = (tlog << 16) - size;
+      ct.dfs[s] = total - 1;
+      total += 1;
+    } else {
+      const uint32_t max_bits = tlog - (31u - (uint32_t)__builtin_clz((uint32_t)(n - 1)));
+      const uint32_t min_state_plus = (uint32_t)n << max_bits;
+      ct.dnb[s] = (max_bits << 16) - min_state_plus;
+      ct.dfs[s] = total - n;
+      total += n;
+    }
+  }
+  ct.log = tlog;
+}
+
+inline ZTables build_tables() {
+  ZTables t{};
+  fse_build(kLLNorm, 36, 6, t.ll);
+  fse_build(kMLNorm, 53, 6, t.ml);
+  fse_build(kOFNorm, 29, 5, t.of);
+  return t;
+}
+
+// ---- bit writer (forward, little-endian: the decoder reads it backwards) --
+struct BitW {
+  uint8_t *p;      // next byte to write
+  uint8_t *end;    // capacity limit (write fails past it)
+  uint64_t acc;    // pending bits
+  uint32_t n;      // pending bit count (< 64)
+  bool over;
+  __host__ __device__ void add(uint64_t v, uint32_t nb) {
+    acc |= (v & ((nb >= 64) ? ~0ull : ((1ull << nb) - 1))) << n;
+    n += nb;
+    if (n >= 32) flush();
+  }
+  __host__ __device__ void flush() {
+    while (n >= 8) {
+      if (p < end) *p = (uint8_t)acc; else over = true;
+      ++p;
+      acc >>= 8;
+      n -= 8;
+    }
+  }
+  // end mark (a 1 bit) + the last partial byte; returns false on overflow
+  __host__ __device__ bool close() {
+    add(1, 1);
+    flush();
+    if (n) {
+      if (p < end) *p = (uint8_t)acc; else over = true;
+      ++p;
+      n = 0;
+    }
+    return !over;
+  }
+};
+
+struct FseState {
+  uint32_t value;
+};
+__host__ __device__ inline void fse_init(FseState &st, const FseCT &ct, uint32_t s) {
+  const uint32_t nb = (ct.dnb[s] + (1u << 15)) >> 16;
+  uint32_t v = (nb << 16) - ct.dnb[s];
+  st.value = ct.state[(v >> nb) + ct.dfs[s]];
+}
+__host__ __device__ inline void fse_encode(BitW &bw, FseState &st, const FseCT &ct, uint32_t s) {
+  const uint32_t nb = (st.value + ct.dnb[s]) >> 16;
+  bw.add(st.value, nb);
+  st.value = ct.state[(st.value >> nb) + ct.dfs[s]];
+}
+__host__ __device__ inline void fse_flush(BitW &bw, const FseState &st, const FseCT &ct) { bw.add(st.value, ct.log); }
+
+// One sequence: literal length, match length (>= 3), offset (>= 1).
+// Packed in 64 bits: ll 21 | ml 21 | off 22 (block <= 128 KiB, window 2^20).
+__host__ __device__ inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t off) {
+  return (uint64_t)ll | (uint64_t)ml << 21 | (uint64_t)off << 42;
+}
+__host__ __device__ inline uint32_t seq_ll(uint64_t s) { return (uint32_t)(s & 0x1FFFFF); }
+__host__ __device__ inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >> 21) & 0x1FFFFF); }
+__host__ __device__ inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 42); }
+
+// Sequences_Section (RFC 8878 §3.1.1.3.2) of nseq sequences (seqs[i], in
+// order) with Predefined_Mode for all three symbol types, written at dst
+// (capacity cap).  Returns the section size, or 0 when it does not fit.
+template <class SeqAt>
+__host__ __device__ inline uint32_t encode_sequences(const ZTables &T, SeqAt seq_at, uint32_t nseq, uint8_t *dst,
+                                                     uint32_t cap) {
+  uint32_t h = 0;
+  if (cap < 4) return 0;
+  if (nseq < 128) {
+    dst[h++] = (uint8_t)nseq;
+  } else if (nseq < 0x7F00) {
+    dst[h++] = (uint8_t)((nseq >> 8) + 0x80);
+    dst[h++] = (uint8_t)nseq;
+  } else {
+    dst[h++] = 0xFF;
+    dst[h++] = (uint8_t)(nseq - 0x7F00);
+    dst[h++] = (uint8_t)((nseq - 0x7F00) >> 8);
+  }
+  if (nseq == 0) return h;
+  dst[h++] = 0x00;  // Symbol_Compression_Modes: Predefined_Mode x 3
+  BitW bw{dst + h, dst + cap, 0, 0, false};
+  // the last sequence first (the decoder reads the stream backwards)
+  uint64_t s = seq_at(nseq - 1);
+  uint32_t ll = seq_ll(s), mb = seq_ml(s) - 3, ob = seq_off(s) + 3;
+  uint32_t llc = ll_code(ll), mlc = ml_code(mb), ofc = highbit(ob);
+  FseState sml, sof, sll;
+  fse_init(sml, T.ml, mlc);
+  fse_init(sof, T.of, ofc);
+  fse_init(sll, T.ll, llc);
+  bw.add(ll, ll_bits(llc));
+  bw.add(mb, ml_bits(mlc));
+  bw.add(ob, ofc);
+  for (int32_t i = (int32_t)nseq - 2; i >= 0; --i) {
+    s = seq_at((uint32_t)i);
+    ll = seq_ll(s);
+    mb = seq_ml(s) - 3;
+    ob = seq_off(s) + 3;
+    llc = ll_code(ll);
+    mlc = ml_code(mb);
+    ofc = highbit(ob);
+    fse_encode(bw, sof, T.of, ofc);
+    fse_encode(bw, sml, T.ml, mlc);
+    fse_encode(bw, sll, T.ll, llc);
+    bw.add(ll, ll_bits(llc));
+    bw.add(mb, ml_bits(mlc));
+    bw.add(ob, ofc);
+    if (bw.over) return 0;
+  }
+  fse_flush(bw, sml, T.ml);
+  fse_flush(bw, sof, T.of);
+  fse_flush(bw, sll, T.ll);
+  if (!bw.close()) return 0;
+  return (uint32_t)(bw.p - dst);
+}
+
+// Headers.
+__host__ __device__ inline void put_block_header(uint8_t *d, bool last, uint32_t type, uint32_t size) {
+  const uint32_t h = (last ? 1u : 0u) | type << 1 | size << 3;
+  d[0] = (uint8_t)h;
+  d[1] = (uint8_t)(h >> 8);
+  d[2] = (uint8_t)(h >> 16);
+}
+// Raw_Literals_Block header, Size_Format 11 (3 bytes, 20-bit size)
+__host__ __device__ inline void put_raw_lit_header(uint8_t *d, uint32_t nlit) {
+  d[0] = (uint8_t)(0x0C | (nlit & 0xF) << 4);
+  d[1] = (uint8_t)(nlit >> 4);
+  d[2] = (uint8_t)(nlit >> 12);
+}
+__host__ __device__ inline void put_frame_header(uint8_t *d) {
+  d[0] = 0x28;
+  d[1] = 0xB5;
+  d[2] = 0x2F;
+  d[3] = 0xFD;
+  d[4] = kFhd;
+  d[5] = kWd;
+}
+
+}  // namespace zs
+}  // namespace mcdc

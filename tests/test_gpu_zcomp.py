@@ -1,0 +1,161 @@
+"""GPU zstd compression (mcdc_zstd_compress_device: SecureStorage::compress,
+/root/reference/src/repository/storage.rs:74-84, on the GPU).  The compressed
+bytes are the GPU's own (greedy LZ, raw literals, predefined-FSE sequences),
+so parity is decode-equality with mapache's decoder: every frame decodes with
+the system libzstd within a 2^20 window (storage.rs:87-94) to exactly its
+chunk; frames carry the crate's header (no content size, no checksum, window
+2^20); output is deterministic; compressible inputs compress; the frames seal
+and decode through mapache's whole decode (mcdc_decode_blobs: open + zstd)."""
+import numpy as np
+import pytest
+
+from mapache_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+P16 = (16384, 65536, 262144, 1)
+P512 = (524288, 1048576, 8388608, 1)
+
+
+def _text(n, seed=21):
+    rng = np.random.default_rng(seed)
+    vocab = [bytes(rng.integers(97, 123, int(k))) for k in rng.integers(2, 11, 2000)]
+    t = b" ".join(vocab[i] for i in rng.integers(0, 2000, n // 4 + 16))
+    return np.frombuffer(t[:n], np.uint8).copy()
+
+
+def _data(kind, n, seed):
+    if kind == "text":
+        return _text(n, seed)
+    if kind == "random":
+        return O.random_bytes(n, seed)
+    if kind == "zeros":
+        return np.zeros(n, np.uint8)
+    if kind == "periodic":
+        return np.tile(O.random_bytes(1000, seed), n // 1000 + 1)[:n]
+    # mixed: 5 KiB runs of text, random bytes and zeros
+    parts = [_text(5000, seed), O.random_bytes(5000, seed), np.zeros(5000, np.uint8)]
+    return np.concatenate([parts[(i // 5000) % 3][:5000] for i in range(0, n + 5000, 5000)])[:n]
+
+
+def _compress(ctx, data, chunks):
+    dp = ctx.device_alloc(max(data.size, 1))
+    cap = _lib.Context.zstd_compress_bound(chunks["length"]) + 64
+    d_out = ctx.device_alloc(cap)
+    try:
+        if data.size:
+            ctx.h2d(dp, data)
+        fr, nbytes = ctx.zstd_compress(dp, data.size, chunks, d_out, cap)
+        out = ctx.d2h_bytes(d_out, nbytes) if nbytes else np.zeros(0, np.uint8)
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(dp)
+    return fr, out, nbytes
+
+
+def _check_frames(data, chunks, fr, out, nbytes):
+    z = O.Zstd()
+    at = 0
+    for i in range(len(chunks)):
+        o, ln = int(fr[i, 0]), int(fr[i, 1])
+        assert o == at, i  # frames back to back, in chunk order
+        at += ln
+        frame = out[o:o + ln].tobytes()
+        assert frame[:6] == b"\x28\xb5\x2f\xfd\x00\x50", i
+        src = data[int(chunks["offset"][i]):int(chunks["offset"][i] + chunks["length"][i])].tobytes()
+        assert z.decompress(frame, len(src) + 64) == src, i
+    assert at == nbytes
+
+
+@pytest.mark.parametrize("kind", ["text", "random", "zeros", "periodic", "mixed"])
+@pytest.mark.parametrize("p", [P16, P512], ids=["P16", "P512"])
+def test_chunks_of_a_stream_decode(ctx, kind, p):
+    data = _data(kind, (24 << 20) + 7, 5)
+    ch = O.chunk(O.Params(*p), data)
+    fr, out, nbytes = _compress(ctx, data, ch)
+    _check_frames(data, ch, fr, out, nbytes)
+    ratio = data.size / nbytes
+    if kind in ("text", "zeros", "periodic", "mixed"):
+        assert ratio > {"text": 1.5, "zeros": 100, "periodic": 10, "mixed": 1.3}[kind], ratio
+    else:
+        assert nbytes <= data.size + 6 * len(ch) + 3 * (data.size // 16384 + len(ch))  # raw blocks, no growth
+
+
+def test_edge_lengths_offsets_overlaps(ctx):
+    data = _data("mixed", 3 << 20, 9)
+    lens = [0, 1, 3, 4, 5, 63, 64, 65, 16383, 16384, 16385, 32767, 32768, 32769, 100001, 1 << 20, (1 << 20) + 3]
+    recs = []
+    for i, ln in enumerate(lens):
+        o = (i * 7919) % (data.size - ln) if ln < data.size else 0
+        recs.append((o, ln))
+    recs += [(5, 200000), (5, 200000), (100, 150000)]  # repeated and overlapping extents
+    ch = np.zeros(len(recs), dtype=_lib.CHUNK_DTYPE)
+    ch["offset"] = [r[0] for r in recs]
+    ch["length"] = [r[1] for r in recs]
+    fr, out, nbytes = _compress(ctx, data, ch)
+    _check_frames(data, ch, fr, out, nbytes)
+
+
+def test_deterministic_and_device_lists(ctx):
+    data = _data("text", 8 << 20, 3)
+    ch = O.chunk(O.Params(*P16), data)
+    a = _compress(ctx, data, ch)
+    b = _compress(ctx, data, ch)
+    assert a[2] == b[2] and (a[0] == b[0]).all() and a[1].tobytes() == b[1].tobytes()
+    # chunk list and frame extents in HBM
+    dp = ctx.device_alloc(data.size)
+    cap = _lib.Context.zstd_compress_bound(ch["length"])
+    d_out, d_ch, d_fr = ctx.device_alloc(cap), ctx.device_alloc(24 * len(ch)), ctx.device_alloc(16 * len(ch))
+    try:
+        ctx.h2d(dp, data)
+        ctx.h2d(d_ch, ch.view(np.uint8))
+        _, nb = ctx.zstd_compress(dp, data.size, (d_ch, len(ch)), d_out, cap, frames_out=d_fr)
+        fr = ctx.d2h_bytes(d_fr, 16 * len(ch)).view(np.uint64).reshape(-1, 2)
+        out = ctx.d2h_bytes(d_out, nb)
+    finally:
+        for x in (d_fr, d_ch, d_out, dp):
+            ctx.device_free(x)
+    assert nb == a[2] and (fr == a[0]).all() and out.tobytes() == a[1].tobytes()
+
+
+def test_seal_and_decode_round_trip(ctx):
+    """compress -> seal (AES-256-GCM-SIV, mcdc_seal_device over the frames'
+    extents) -> mapache's decode (mcdc_decode_blobs: open, zstd decompress)."""
+    data = _data("mixed", 6 << 20, 4)
+    ch = O.chunk(O.Params(*P16), data)
+    fr, out, nbytes = _compress(ctx, data, ch)
+    key = bytes(range(32))
+    nz = np.zeros((len(ch), 12), np.uint8)
+    nz[:, :4] = np.arange(len(ch), dtype=np.uint32).view(np.uint8).reshape(-1, 4)
+    d_in = ctx.device_alloc(nbytes)
+    cap = nbytes + 28 * len(ch)
+    d_seal = ctx.device_alloc(cap)
+    try:
+        ctx.h2d(d_in, out)
+        oo = ctx.seal(key, d_in, nbytes, fr[:, 0], fr[:, 1], nz, d_seal, cap)
+        sealed = ctx.d2h_bytes(d_seal, int(oo[-1]))
+    finally:
+        ctx.device_free(d_seal)
+        ctx.device_free(d_in)
+    dec, do, st = ctx.decode_blobs(key, sealed, oo[:-1], np.diff(oo), data.size + 64)
+    assert (st == 0).all() and dec.tobytes() == data.tobytes()
+
+
+def test_errors(ctx):
+    data = O.random_bytes(1 << 20, 1)
+    ch = np.zeros(1, dtype=_lib.CHUNK_DTYPE)
+    ch["length"] = data.size
+    dp = ctx.device_alloc(data.size)
+    d_out = ctx.device_alloc(1024)
+    try:
+        ctx.h2d(dp, data)
+        with pytest.raises(_lib.McdcError) as ei:
+            ctx.zstd_compress(dp, data.size, ch, d_out, 1024)
+        assert ei.value.code == _lib.MCDC_E_CAPACITY
+        ch["offset"] = 1
+        with pytest.raises(_lib.McdcError) as ei:
+            ctx.zstd_compress(dp, data.size, ch, d_out, 1 << 30)
+        assert ei.value.code == _lib.MCDC_E_INVALID
+    finally:
+        ctx.device_free(d_out)
+        ctx.device_free(dp)
