@@ -497,7 +497,9 @@ def encode(ctx, gib: float, steps: int) -> dict:
     pick = rng.integers(0, len(ch), 8)  # sealed bytes open with the oracle
     ok_o = all(O.decrypt_with_key(bytes(range(32)), enc[int(oo[i]):int(oo[i + 1])].tobytes()) is not None
                for i in pick)
-    return {"bytes": n, "blobs": int(len(ch)), "sealed_bytes": int(oo[-1]), "ratio": round(n / int(oo[-1]), 3),
+    gpu = gpu_encode_text(ctx, data, ch, nz, steps, rng)
+    return {"gpu_compress": gpu,
+            "bytes": n, "blobs": int(len(ch)), "sealed_bytes": int(oo[-1]), "ratio": round(n / int(oo[-1]), 3),
             "encode_ms": round(dte * 1e3, 2), "encode_gib_s": round(n / dte / GIB, 3),
             "decode_ms": round(dtd * 1e3, 2), "decode_gib_s": round(n / dtd / GIB, 3),
             "round_trip_ok": ok, "oracle_open_ok": ok_o,
@@ -505,6 +507,52 @@ def encode(ctx, gib: float, steps: int) -> dict:
                     "sealing on the GPU, H2D and D2H included",
             "data": "synthetic text, 2 000-word vocabulary, 64 MiB pattern repeated (repeats lie beyond the "
                     "1 MiB window)"}
+
+
+def gpu_encode_text(ctx, data: np.ndarray, ch: np.ndarray, nz: np.ndarray, steps: int, rng) -> dict:
+    """SecureStorage::encode of the same text blobs with the compression on the
+    GPU too (mcdc_zstd_compress_device, then mcdc_seal_device over the frames),
+    device-resident in and out; the ratio beside the host level-3 one.  Parity:
+    sampled sealed blobs opened by the oracle and decoded by libzstd."""
+    from mapache_amd import _lib
+    from oracle import oracle as O
+    n = data.size
+    key = bytes(range(32))
+    cap = _lib.Context.zstd_compress_bound(ch["length"])
+    dp, d_z = ctx.device_alloc(n), ctx.device_alloc(cap)
+    d_ch, d_fr = ctx.device_alloc(24 * len(ch)), ctx.device_alloc(16 * len(ch))
+    d_nz, d_seal = ctx.device_alloc(12 * len(ch)), ctx.device_alloc(cap + 28 * len(ch))
+    d_off = ctx.device_alloc(8 * (len(ch) + 1))
+    try:
+        ctx.h2d(dp, data)
+        ctx.h2d(d_ch, ch.view(np.uint8))
+        ctx.h2d(d_nz, nz.reshape(-1))
+        dtc, (_, zb) = _timed(lambda: ctx.zstd_compress(dp, n, (d_ch, len(ch)), d_z, cap, frames_out=d_fr), steps, 1)
+        zdev = ctx.timing()["device_ms"]
+
+        def enc():
+            _, b = ctx.zstd_compress(dp, n, (d_ch, len(ch)), d_z, cap, frames_out=d_fr)
+            ctx.seal_device_ext(key, d_z, b, d_fr, len(ch), d_nz, d_seal, cap + 28 * len(ch), d_off)
+            return b
+        dte, _ = _timed(enc, steps, 1)
+        fr = ctx.d2h_bytes(d_fr, 16 * len(ch)).view(np.uint64).reshape(-1, 2)
+        oo = ctx.d2h_bytes(d_off, 8 * (len(ch) + 1)).view(np.uint64)
+        z = O.Zstd()
+        ok = True
+        for i in rng.integers(0, len(ch), 16):
+            blob = ctx.d2h_bytes(d_seal + int(oo[i]), int(oo[i + 1] - oo[i])).tobytes()
+            frame = O.decrypt_with_key(key, blob)
+            src = data[int(ch["offset"][i]):int(ch["offset"][i] + ch["length"][i])].tobytes()
+            ok &= frame is not None and z.decompress(frame, len(src) + 64) == src
+        return {"compress_ms": round(dtc * 1e3, 3), "compress_gib_s": round(n / dtc / GIB, 2),
+                "compress_device_ms": round(zdev, 3), "compressed_bytes": int(zb), "ratio": round(n / zb, 3),
+                "encode_ms": round(dte * 1e3, 3), "encode_gib_s": round(n / dte / GIB, 2),
+                "sealed_bytes": int(oo[-1]), "encode_ratio": round(n / int(oo[-1]), 3), "parity_probe_ok": bool(ok),
+                "note": "mcdc_zstd_compress_device (greedy LZ, raw literals, predefined-FSE sequences, 16 KiB blocks) "
+                        "+ mcdc_seal_device, all in HBM; ratio vs the host level-3 ratio of the same blobs above"}
+    finally:
+        for x in (d_off, d_seal, d_nz, d_fr, d_ch, d_z, dp):
+            ctx.device_free(x)
 
 
 def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> dict:
@@ -574,6 +622,26 @@ def seal(ctx, dp: int, n: int, chunks: np.ndarray, steps: int, no_cpu: bool) -> 
                          "frames_ms": round(t_fr, 3), "frame_bytes": int(span_s), "frames_probe_ok": probe_ok,
                          "note": "mcdc_chunk_device + mcdc_chunk_ids_device + mcdc_zstd_frames_device + "
                                  "mcdc_seal_device per step, all in HBM: zstd frames in raw-block mode"}
+
+                # the same with real compression on the GPU (mcdc_zstd_compress_device)
+                def comp_path():
+                    kk = ctx.chunk_device_to_device(p, dp, n, d_ch, cap_c)
+                    ctx.chunk_ids(dp, n, (d_ch, kk), ids=d_ids)
+                    _, zb = ctx.zstd_compress(dp, n, (d_ch, kk), d_open, n + (64 << 20), frames_out=d_fr)
+                    t_z = ctx.timing()["device_ms"]
+                    ctx.seal_device_ext(key, d_open, zb, d_fr, kk, d_nonce, d_seal, cap + (64 << 20), d_offs)
+                    return zb, t_z
+                dtz, (zb, t_z) = _timed(comp_path, steps, 1)
+                zf = ctx.d2h_bytes(d_fr, 16 * 4).view(np.uint64).reshape(4, 2)
+                zok = all(O.Zstd().decompress(ctx.d2h_bytes(d_open + int(zf[i, 0]), int(zf[i, 1])).tobytes(),
+                                              int(lens[i]) + 64)
+                          == O.random_bytes(int(lens[i]), SEED, pos=int(offs[i])).tobytes() for i in range(4))
+                store["compressed_encode_path"] = {
+                    "ms_per_step": round(dtz * 1e3, 3), "gib_s": round(n / dtz / GIB, 2),
+                    "compress_device_ms": round(t_z, 3), "compress_gib_s": round(n / (t_z * 1e-3) / GIB, 2),
+                    "compressed_bytes": int(zb), "ratio": round(n / zb, 4), "decode_probe_ok": bool(zok),
+                    "note": "chunk -> IDs -> mcdc_zstd_compress_device -> seal, all in HBM (random data: every "
+                            "block falls back to raw, as zstd stores incompressible data)"}
             finally:
                 ctx.device_free(d_fr)
         finally:

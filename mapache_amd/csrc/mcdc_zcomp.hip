@@ -124,6 +124,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
       }
     }
     const uint64_t m = __ballot(mlen >= kMinMatch);
+    if (cursor < s0) cursor = s0;  // positions before s0 that no match covered are literals
     while (true) {
       const uint32_t rel = cursor - s0;
       if (rel >= 64) break;
