@@ -1617,7 +1617,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   static const zs::ZTables T = zs::build_tables();
   const double t0 = now_ms();
   hipStream_t st = ctx->stream;
-  const size_t tmpb = std::max(zc_tmp_bytes(nchunks), zc_tmp_bytes(kZcBatchBlocks));
+  size_t tmpb = zc_tmp_bytes(nchunks);
   if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, nchunks * sizeof(mcdc_chunk))) ||
       (rc = ensure(ctx, ctx->zc_cnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->zc_first, (nchunks + 1) * 8)) ||
       (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)))
@@ -1646,7 +1646,11 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
     ext = (uint64_t *)ctx->zf_ext.p;
   }
   const uint64_t total_blocks = hfirst[nchunks];
-  const uint64_t mb = std::min<uint64_t>(total_blocks, kZcBatchBlocks);
+  uint64_t longest = 0;  // a batch holds whole chunks
+  for (size_t i = 0; i < nchunks; ++i) longest = std::max<uint64_t>(longest, hfirst[i + 1] - hfirst[i]);
+  const uint64_t mb = std::max(std::min<uint64_t>(total_blocks, kZcBatchBlocks), longest);
+  tmpb = std::max(tmpb, zc_tmp_bytes(mb));
+  if ((rc = ensure(ctx, ctx->zc_tmp, tmpb))) return rc;
   if ((rc = ensure(ctx, ctx->zc_blocks, mb * sizeof(ZcBlock))) || (rc = ensure(ctx, ctx->zc_stage, mb * kZcSlot)) ||
       (rc = ensure(ctx, ctx->zc_seqs, mb * kZcSeqCap * 8)) || (rc = ensure(ctx, ctx->zc_piece, (mb + 1) * 8)) ||
       (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)))

@@ -255,15 +255,20 @@ __global__ __launch_bounds__(256) void k_b3_owner(const DevChunk *chunks, const 
 // lane 16 q + k at the block's own byte address (gfx950 reads a misaligned
 // dwordx4 as the 16 bytes at that address: tools/dbg/unaligned_probe.hip), so
 // a wave-instruction touches 16 runs of 64 contiguous bytes instead of 64
-// scattered 16-byte pieces; the wave transposes through a private LDS pad
-// (row stride 80 B: conflict-free reads) and each lane reads its own block.
+// scattered 16-byte pieces; the wave transposes through a private 4 KiB LDS
+// pad and each lane reads its own block.  Pad layout: row r (a block) piece i
+// (16 B) at slot 4 r + (i ^ ((r >> 2) & 3)) -- conflict-free for both sides:
+// a ds_write_b128 8-lane group (two rows, bank (a/4) mod 32) covers the 8
+// distinct 16-byte slots of a 128-byte bank row, and each ds_read_b128
+// 16-lane group (bank (a/4) mod 64) reads 16 distinct slots of a 256-byte
+// row (the 80-byte row stride it replaces had 2-way write conflicts).
 // MCDC_B3_QUAD=0: each lane loads its own block (four 16-byte loads).  Block
 // j + 1 is requested before block j is compressed.
 #ifndef MCDC_B3_QUAD
 #define MCDC_B3_QUAD 1
 #endif
 #if MCDC_B3_QUAD
-constexpr int kB3Pad = 5;  // uint4 per pad row (80 B)
+constexpr int kB3Pad = 4;  // uint4 per pad row (64 B, swizzled)
 #endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 *gq;  // global (not flat) loads
@@ -330,8 +335,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     aq[q] = (((uint64_t)hi << 32) | lo) + 16 * qi;
   }
   uint4 *pad = pad_all[wv];
-  uint4 *wr = pad + kB3Pad * qk + qi;
+  uint4 *wr = pad + kB3Pad * qk + (qi ^ ((qk >> 2) & 3));
   const uint4 *rd = pad + kB3Pad * lane;
+  const uint32_t sw = (lane >> 2) & 3;  // the read side of the swizzle
   uint4 a0, a1, a2, a3;
   // block b of every source lane; past a lane's last full block (only in
   // waves of unequal lanes) the address is clamped to it, or to a readable
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     wr[16 * kB3Pad] = a1;
     wr[32 * kB3Pad] = a2;
     wr[48 * kB3Pad] = a3;
-    const uint4 c0 = rd[0], c1 = rd[1], c2 = rd[2], c3 = rd[3];
+    const uint4 c0 = rd[0 ^ sw], c1 = rd[1 ^ sw], c2 = rd[2 ^ sw], c3 = rd[3 ^ sw];
 #else
     const uint4 c0 = a0, c1 = a1, c2 = a2, c3 = a3;
 #endif

@@ -10,9 +10,9 @@
 namespace mcdc {
 
 constexpr uint64_t kZcBlock = 16384;               // zstd block: 16 KiB of one chunk
-constexpr uint32_t kZcSeqCap = 1024;               // sequences per block (then literals)
+constexpr uint32_t kZcSeqCap = 4096;               // sequences per block: a 16 KiB block of 4-byte matches
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
-constexpr uint64_t kZcBatchBlocks = 131072;        // blocks per batch (>= a 2 GiB chunk)
+constexpr uint64_t kZcBatchBlocks = 65536;         // blocks per batch (1 GiB; more for a longer chunk)
 
 struct ZcBlock {
   uint64_t src;                 // chunk bytes [src, src + len) of the input

@@ -14,11 +14,13 @@
 //                table in LDS (positions, ds_max_u32 so the result does not
 //                depend on lane timing) is primed with the previous 16 KiB of
 //                the same chunk (matches reach back up to 32 KiB); the wave
-//                hashes 64 positions at once, verifies and extends each lane's
+//                hashes 64 positions at once (every step-th position after
+//                match-free strides), verifies and extends each lane's
 //                candidate, then walks the lanes' matches greedily (ballot +
 //                readlane, wave-uniform); long matches are extended 64 bytes
 //                per step.  Literals go to the block's staging slot, sequences
-//                (<= 1024 per block, then the rest are literals) to scratch.
+//                (<= 1024 per block, then the rest are literals) straight to
+//                scratch (16 KiB of LDS per wave: 10 waves per CU).
 //   k_zc_encode  ONE LANE PER BLOCK: the serial FSE bitstream of the block's
 //                sequences (three interleaved state machines, tables in LDS);
 //                block kept compressed only if smaller than raw
@@ -88,10 +90,12 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
   for (uint32_t k = lane; k < n; k += 64) dst[k] = src[k];
 }
 
+// Lane i of a stride looks at position s0 + i * step.  step grows after
+// match-free strides (1, 2, 4, 8: zstd's fast strategies skip ahead the same
+// way on data that does not compress) and drops back to 1 at a match.
 __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
                                                  uint64_t *seqs) {
   __shared__ uint32_t ht[kHt];
-  __shared__ uint64_t sq[kZcSeqCap];
   const uint64_t bi = blockIdx.x;
   if (bi >= nblk) return;
   const uint32_t lane = lane_id();
@@ -104,20 +108,19 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
   for (uint32_t q = lane; q + 4 <= prime; q += 64) atomicMax(&ht[zhash(ld4(p0 + q))], q + 1);
   __syncthreads();
   uint8_t *lit = stage + bi * kZcSlot + kLitHdr;
-  uint32_t nlit = 0, nseq = 0, cursor = prime, lit0 = prime;
-  bool full = false;
-  for (uint32_t s0 = prime; s0 + 4 <= end && !full;) {
-    const uint32_t p = s0 + lane;
+  uint64_t *sq = seqs + bi * kZcSeqCap;
+  uint32_t nlit = 0, nseq = 0, cursor = prime, lit0 = prime, step = 1, miss = 0;
+  for (uint32_t s0 = prime; s0 + 4 <= end;) {
+    const uint32_t p = s0 + lane * step;
     const bool ok = p + 4 <= end;
     const uint32_t v = ok ? ld4(p0 + p) : 0u;
     const uint32_t h = zhash(v);
     const uint32_t cand = ok ? ht[h] : 0u;
-    __syncthreads();
-    if (ok) atomicMax(&ht[h], p + 1);
+    if (ok) atomicMax(&ht[h], p + 1);  // (issued after every lane's read: one wave, in order)
     uint32_t mlen = 0, c = 0;
     if (cand) {
       c = cand - 1;
-      if (p - c < kWindow && ld4(p0 + c) == v) {
+      if (c < p && p - c < kWindow && ld4(p0 + c) == v) {
         mlen = 4;
         while (mlen < kExt && p + mlen + 4 <= end && ld4(p0 + c + mlen) == ld4(p0 + p + mlen)) mlen += 4;
         while (mlen < kExt && p + mlen < end && p0[c + mlen] == p0[p + mlen]) ++mlen;
@@ -125,13 +128,16 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
     }
     const uint64_t m = __ballot(mlen >= kMinMatch);
     if (cursor < s0) cursor = s0;  // positions before s0 that no match covered are literals
+    const uint32_t span = 64 * step;
+    bool stop = false;
     while (true) {
-      const uint32_t rel = cursor - s0;
-      if (rel >= 64) break;
-      const uint64_t mm = m & (~0ull << rel);
+      if (cursor >= s0 + span) break;
+      const uint32_t first_lane = (cursor - s0 + step - 1) / step;  // lanes at or after the cursor
+      if (first_lane >= 64) break;
+      const uint64_t mm = m & (~0ull << first_lane);
       if (!mm) break;
       const uint32_t i = (uint32_t)__builtin_ctzll(mm);
-      const uint32_t pos = s0 + i;
+      const uint32_t pos = s0 + i * step;
       uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)mlen, (int)i);
       const uint32_t off = pos - (uint32_t)__builtin_amdgcn_readlane((int)c, (int)i);
       if (ml >= kExt) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
@@ -149,19 +155,24 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
       ++nseq;
       cursor = pos + ml;
       lit0 = cursor;
-      if (nseq == kZcSeqCap) {
-        full = true;
+      if (nseq == kZcSeqCap) {  // the rest of the block: literals
+        stop = true;
         break;
       }
     }
-    s0 = cursor > s0 + 64 ? cursor : s0 + 64;
+    if (stop) break;
+    if (m) {
+      miss = 0;
+      step = 1;
+    } else if (++miss >= 4 && step < 8) {
+      step *= 2;
+      miss = 0;
+    }
+    s0 = cursor > s0 + span ? cursor : s0 + span;
   }
-  __syncthreads();
   if (nseq) {  // (no sequence: the block is stored raw from the input, nothing to stage)
     wave_copy(lit + nlit, p0 + lit0, end - lit0, lane);
     nlit += end - lit0;
-    uint64_t *dst = seqs + bi * kZcSeqCap;
-    for (uint32_t k = lane; k < nseq; k += 64) dst[k] = sq[k];
   }
   if (lane == 0) {
     blocks[bi].nlit = nlit;

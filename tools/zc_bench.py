@@ -1,0 +1,52 @@
+"""GPU zstd compression throughput and ratio (mcdc_zstd_compress_device) on a
+random stream and on the bench's synthetic text, chunked at 16/64/256 KiB;
+device-resident in and out.  Usage: python tools/zc_bench.py [GiB] [steps]"""
+import json
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from mapache_amd import _lib  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+gib = float(sys.argv[1]) if len(sys.argv) > 1 else 4
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+n = int(gib * (1 << 30))
+p = _lib.params(16384, 65536, 262144, 1)
+ctx = _lib.Context(0, n + (1 << 20))
+res = {}
+for kind in ("random", "text"):
+    dp = ctx.device_alloc(n)
+    if kind == "random":
+        ctx.fill_random(dp, n, 0x6d61706163686521)
+    else:
+        rng = np.random.default_rng(21)
+        vocab = [bytes(rng.integers(97, 123, int(k))) for k in rng.integers(2, 11, 2000)]
+        base = b" ".join(vocab[i] for i in rng.integers(0, 2000, 12_000_000))[:64 << 20]
+        for o in range(0, n, len(base)):
+            ctx.h2d(dp + o, np.frombuffer(base[:min(len(base), n - o)], np.uint8))
+    cap_c = n // 16383 + 2
+    d_ch = ctx.device_alloc(24 * cap_c)
+    k = ctx.chunk_device_to_device(p, dp, n, d_ch, cap_c)
+    ch = ctx.d2h_chunks(d_ch, k)
+    cap = _lib.Context.zstd_compress_bound(ch["length"])
+    d_out, d_fr = ctx.device_alloc(cap), ctx.device_alloc(16 * k)
+    ctx.zstd_compress(dp, n, (d_ch, k), d_out, cap, frames_out=d_fr)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, nb = ctx.zstd_compress(dp, n, (d_ch, k), d_out, cap, frames_out=d_fr)
+    dt = (time.perf_counter() - t0) / steps
+    dev = ctx.timing()["device_ms"]
+    fr = ctx.d2h_bytes(d_fr, 16 * 8).view(np.uint64).reshape(8, 2)
+    z = O.Zstd()
+    ok = True
+    for i in range(8):
+        src = ctx.d2h_bytes(dp + int(ch["offset"][i]), int(ch["length"][i])).tobytes()
+        ok &= z.decompress(ctx.d2h_bytes(d_out + int(fr[i, 0]), int(fr[i, 1])).tobytes(), len(src) + 64) == src
+    res[kind] = {"gib_s": round(n / dt / (1 << 30), 2), "device_ms": round(dev, 3), "ratio": round(n / nb, 4),
+                 "chunks": int(k), "probe_ok": bool(ok)}
+    for x in (d_fr, d_out, d_ch, dp):
+        ctx.device_free(x)
+print(json.dumps(res))
