@@ -10,7 +10,7 @@
 // Per batch of blocks (a block = 16 KiB of one chunk; batches bound the
 // scratch):
 //   k_zc_blocks  block records of the batch's chunks (chunk, index, source)
-//   k_zc_match   ONE WAVE PER BLOCK: greedy LZ parse.  A 4096-entry hash
+//   k_zc_match   ONE WAVE PER BLOCK: greedy LZ parse.  A 2048-entry hash
 //                table in LDS (positions, ds_max_u32 so the result does not
 //                depend on lane timing) is primed with the previous 16 KiB of
 //                the same chunk (matches reach back up to 32 KiB); the wave
@@ -20,7 +20,7 @@
 //                readlane, wave-uniform); long matches are extended 64 bytes
 //                per step.  Literals go to the block's staging slot, sequences
 //                (<= 1024 per block, then the rest are literals) straight to
-//                scratch (16 KiB of LDS per wave: 10 waves per CU).
+//                scratch (8 KiB of LDS per wave: 20 waves per CU).
 //   k_zc_encode  ONE LANE PER BLOCK: the serial FSE bitstream of the block's
 //                sequences (three interleaved state machines, tables in LDS);
 //                block kept compressed only if smaller than raw
@@ -40,8 +40,9 @@ namespace {
 
 using namespace zs;
 
-constexpr uint32_t kHtLog = 12, kHt = 1u << kHtLog;
-constexpr uint32_t kExt = 36;  // per-lane match extension before the cooperative one
+// 2048 positions (8 KiB of LDS per wave: 20 waves per CU; the compiler then
+// allocates 88 VGPRs instead of the 136 it gives a 16 KiB table's 10 waves)
+constexpr uint32_t kHtLog = 11, kHt = 1u << kHtLog;
 
 __device__ __forceinline__ uint32_t ld4(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
 __device__ __forceinline__ uint32_t zhash(uint32_t v) { return (v * 2654435761u) >> (32 - kHtLog); }
@@ -90,9 +91,30 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
   for (uint32_t k = lane; k < n; k += 64) dst[k] = src[k];
 }
 
+// Match length at p against c, up to 32 bytes, from one 32-byte load on
+// each side (two misaligned 16-byte loads each; no dependent loop).
+__device__ __forceinline__ uint32_t match32(const uint8_t *p0, uint32_t p, uint32_t c, uint32_t end) {
+  if (p + 32 <= end) {
+    const uint4 x0 = *reinterpret_cast<const uint4 *>(p0 + p), x1 = *reinterpret_cast<const uint4 *>(p0 + p + 16);
+    const uint4 y0 = *reinterpret_cast<const uint4 *>(p0 + c), y1 = *reinterpret_cast<const uint4 *>(p0 + c + 16);
+    const uint32_t d[8] = {x0.x ^ y0.x, x0.y ^ y0.y, x0.z ^ y0.z, x0.w ^ y0.w,
+                           x1.x ^ y1.x, x1.y ^ y1.y, x1.z ^ y1.z, x1.w ^ y1.w};
+    uint32_t m = 32;
+#pragma unroll
+    for (int k = 7; k >= 0; --k)
+      if (d[k]) m = 4 * k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
+    return m;
+  }
+  uint32_t m = 0;  // the block's last 31 bytes
+  while (p + m < end && m < 32 && p0[c + m] == p0[p + m]) ++m;
+  return m;
+}
+
 // Lane i of a stride looks at position s0 + i * step.  step grows after
 // match-free strides (1, 2, 4, 8: zstd's fast strategies skip ahead the same
 // way on data that does not compress) and drops back to 1 at a match.
+// Literal runs are copied 64 at a time: lane (k mod 64) keeps run k's source,
+// length and destination, and the wave copies the 64 runs together.
 __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
                                                  uint64_t *seqs) {
   __shared__ uint32_t ht[kHt];
@@ -110,6 +132,15 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
   uint8_t *lit = stage + bi * kZcSlot + kLitHdr;
   uint64_t *sq = seqs + bi * kZcSeqCap;
   uint32_t nlit = 0, nseq = 0, cursor = prime, lit0 = prime, step = 1, miss = 0;
+  uint32_t run_src = 0, run_len = 0, run_dst = 0;  // this lane's pending literal run
+  auto flush_runs = [&]() {
+    uint32_t mx = run_len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+    for (uint32_t k = 0; k < mx; ++k)
+      if (k < run_len) lit[run_dst + k] = p0[run_src + k];
+    run_len = 0;
+  };
   for (uint32_t s0 = prime; s0 + 4 <= end;) {
     const uint32_t p = s0 + lane * step;
     const bool ok = p + 4 <= end;
@@ -120,11 +151,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
     uint32_t mlen = 0, c = 0;
     if (cand) {
       c = cand - 1;
-      if (c < p && p - c < kWindow && ld4(p0 + c) == v) {
-        mlen = 4;
-        while (mlen < kExt && p + mlen + 4 <= end && ld4(p0 + c + mlen) == ld4(p0 + p + mlen)) mlen += 4;
-        while (mlen < kExt && p + mlen < end && p0[c + mlen] == p0[p + mlen]) ++mlen;
-      }
+      if (c < p && p - c < kWindow && ld4(p0 + c) == v) mlen = match32(p0, p, c, end);
     }
     const uint64_t m = __ballot(mlen >= kMinMatch);
     if (cursor < s0) cursor = s0;  // positions before s0 that no match covered are literals
@@ -140,7 +167,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
       const uint32_t pos = s0 + i * step;
       uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)mlen, (int)i);
       const uint32_t off = pos - (uint32_t)__builtin_amdgcn_readlane((int)c, (int)i);
-      if (ml >= kExt) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
+      if (ml == 32) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
         for (;;) {
           const uint32_t q = pos + ml + lane;
           const bool same = q < end && p0[q] == p0[q - off];
@@ -149,10 +176,15 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
           if (diff) break;
         }
       }
-      wave_copy(lit + nlit, p0 + lit0, pos - lit0, lane);
+      if (lane == (nseq & 63)) {
+        run_src = lit0;
+        run_len = pos - lit0;
+        run_dst = nlit;
+        sq[nseq] = seq_pack(pos - lit0, ml, off);
+      }
       nlit += pos - lit0;
-      if (lane == 0) sq[nseq] = seq_pack(pos - lit0, ml, off);
       ++nseq;
+      if ((nseq & 63) == 0) flush_runs();
       cursor = pos + ml;
       lit0 = cursor;
       if (nseq == kZcSeqCap) {  // the rest of the block: literals
@@ -171,6 +203,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
     s0 = cursor > s0 + span ? cursor : s0 + span;
   }
   if (nseq) {  // (no sequence: the block is stored raw from the input, nothing to stage)
+    flush_runs();
     wave_copy(lit + nlit, p0 + lit0, end - lit0, lane);
     nlit += end - lit0;
   }

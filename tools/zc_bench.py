@@ -17,7 +17,7 @@ n = int(gib * (1 << 30))
 p = _lib.params(16384, 65536, 262144, 1)
 ctx = _lib.Context(0, n + (1 << 20))
 res = {}
-for kind in ("random", "text"):
+for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text")):
     dp = ctx.device_alloc(n)
     if kind == "random":
         ctx.fill_random(dp, n, 0x6d61706163686521)
