@@ -46,9 +46,11 @@ def _run(cmd, cwd):
 #   slots tile the whole 512-register file of a SIMD and a launch places one
 #   block per CU, which the failing kernels never did (§3a); every GPU round
 #   checks its output whole (64 GiB digests, repeated-call identity).
-# * rocPRIM/hipCUB library kernels that cannot be padded from here: listed by
-#   pattern in LIB_EXACT_FILL_OK with the reason (§3a: none of them is launched
-#   by the product paths, per the kernel trace of the GPU suite).
+# * rocPRIM/hipCUB library kernels (transform, onesweep histogram, block
+#   merge) whose source cannot carry MCDC_VGPR_PAD: build_lib raises their
+#   descriptors' allocation by one granule in the linked library instead
+#   (devaudit.pad_descriptors: code unchanged, the cure §3a measured) and
+#   re-reads the library's descriptors to confirm it.
 EXACT_FILL_OK = ("_ZN4mcdc8k_scan_qILi4096ELi2ELb1E",)
 LIB_EXACT_FILL_OK = ("_ZN7rocprim",)
 
@@ -106,6 +108,23 @@ def device_guard(asm_dir: str):
     return problems, rows
 
 
+def pad_library_fills(lib: str, asm_dir: str, rows) -> int:
+    """Library kernels (LIB_EXACT_FILL_OK) that fill their allocation exactly get
+    one more granule in `lib`'s descriptors; verified from the library bytes."""
+    from mapache_amd import devaudit
+    names = {r["name"] for r in rows if r["kernel"] and r["next_free_vgpr"] % 8 == 0
+             and r["name"].startswith(LIB_EXACT_FILL_OK)}
+    if not names:
+        return 0
+    done = devaudit.pad_descriptors(lib, asm_dir, names)
+    got = devaudit.library_allocations(lib, asm_dir, names)
+    nfv = {r["name"]: r["next_free_vgpr"] for r in rows if r["name"] in names}
+    bad = [k for k in names if got.get(k) != nfv[k] + 8]
+    if bad:
+        raise RuntimeError(f"descriptor padding not confirmed for {len(bad)} kernels, e.g. {bad[0]}")
+    return len(done)
+
+
 def build_lib(force: bool = False, ab: bool = False) -> str:
     out = os.path.join(HERE, "libmcdc_ab.so" if ab else "libmcdc.so")
     deps = [os.path.join(HERE, d) for d in LIB_DEPS]
@@ -125,6 +144,9 @@ def build_lib(force: bool = False, ab: bool = False) -> str:
                 raise RuntimeError("hipcc failed")
             _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], td)
             problems, rows = device_guard(td)
+            padded = pad_library_fills(tmp, td, rows)
+            if padded:
+                print(f"device-code guard: {padded} library kernel descriptors padded by one granule", flush=True)
         if problems and not ab:
             os.remove(tmp)
             raise RuntimeError("device-code guard (DESIGN.md §3a) failed:\n  " + "\n  ".join(problems))

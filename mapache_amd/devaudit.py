@@ -299,6 +299,11 @@ def top_reg_info(insns):
 
 def descriptors(code_object: str):
     """{kernel: (granulated vgpr field, vgprs allocated, accum_offset)} from the .kd symbols."""
+    return {k: v[:3] for k, v in descriptor_bytes(code_object).items()}
+
+
+def descriptor_bytes(code_object: str):
+    """{kernel: (granule field, vgprs allocated, accum_offset, 64 descriptor bytes)}."""
     syms = subprocess.run([f"{LLVM}/llvm-readelf", "-sW", code_object], capture_output=True, text=True,
                           check=True).stdout
     secs = subprocess.run([f"{LLVM}/llvm-readelf", "-SW", code_object], capture_output=True, text=True,
@@ -315,7 +320,66 @@ def descriptors(code_object: str):
         rsrc3, rsrc1 = struct.unpack_from("<II", kd, 44)
         g = rsrc1 & 0x3F
         acc = ((rsrc3 & 0x3F) + 1) * 4
-        out[name] = (g, (g + 1) * 8, acc)
+        out[name] = (g, (g + 1) * 8, acc, bytes(kd))
+    return out
+
+
+def pad_descriptors(lib: str, asm_dir: str, names) -> list:
+    """Raise the VGPR allocation of the named kernels by one 8-register granule
+    in the linked shared library `lib`, leaving their code untouched (the cure
+    DESIGN.md §3a established: the same instructions with one granule more
+    allocated never lost a value).  Each kernel's 64-byte descriptor is taken
+    from the code objects hipcc left in asm_dir (-save-temps) and must occur in
+    the library's uncompressed offload bundle; a byte pattern shared with a
+    kernel that is not to be padded is refused.  Returns [(kernel, old, new)]."""
+    names = set(names)
+    _, o_files = find_files(asm_dir)
+    want, other = {}, set()
+    for o in o_files:
+        for name, (g, alloc, _acc, kd) in descriptor_bytes(o).items():
+            if name in names:
+                want.setdefault(kd, set()).add(name)
+            else:
+                other.add(kd)
+    data = bytearray(open(lib, "rb").read())
+    done = []
+    for kd, ks in want.items():
+        if kd in other:
+            raise RuntimeError(f"descriptor of {sorted(ks)[0]} is shared with a kernel not to be padded")
+        rsrc1 = struct.unpack_from("<I", kd, 48)[0]
+        g = rsrc1 & 0x3F
+        if g + 1 > 63:
+            raise RuntimeError(f"{sorted(ks)[0]}: allocation cannot grow past 512 VGPRs")
+        new = kd[:48] + struct.pack("<I", (rsrc1 & ~0x3F) | (g + 1)) + kd[52:]
+        pos, hits = data.find(kd), 0
+        while pos >= 0:
+            data[pos:pos + 64] = new
+            hits += 1
+            pos = data.find(kd, pos + 64)
+        if hits == 0:
+            raise RuntimeError(f"descriptor of {sorted(ks)[0]} not found in {lib} (compressed bundle?)")
+        done += [(k, (g + 1) * 8, (g + 2) * 8) for k in sorted(ks)]
+    open(lib, "wb").write(bytes(data))
+    return done
+
+
+def library_allocations(lib: str, asm_dir: str, names):
+    """{kernel: VGPRs allocated} for the named kernels as the library's own
+    descriptors say (each located by its bytes outside the granule field)."""
+    names = set(names)
+    data = open(lib, "rb").read()
+    _, o_files = find_files(asm_dir)
+    out = {}
+    for o in o_files:
+        for name, (g, alloc, _acc, kd) in descriptor_bytes(o).items():
+            if name not in names:
+                continue
+            for cand in range(64):
+                rsrc1 = struct.unpack_from("<I", kd, 48)[0]
+                probe = kd[:48] + struct.pack("<I", (rsrc1 & ~0x3F) | cand) + kd[52:]
+                if data.find(probe) >= 0:
+                    out[name] = (cand + 1) * 8
+                    break
     return out
 
 

@@ -167,3 +167,28 @@ def test_shipped_library_was_guarded():
     src = open(os.path.join(B.HERE, "csrc", "mcdc_kernels.hip")).read()
     assert "MCDC_VGPR_PAD(MCDC_EMIT_VPAD)" in src and "#define MCDC_EMIT_VPAD 184" in src
     assert "_ZN4mcdc8k_scan_qILi4096ELi2ELb1E" in B.EXACT_FILL_OK
+
+
+def test_descriptor_padding_in_a_linked_library(tmp_path):
+    """pad_descriptors raises one kernel's allocation by a granule in a linked
+    shared library (the cure of §3a, applied to rocPRIM kernels by build_lib),
+    leaves the other kernel's descriptor alone, and library_allocations reads
+    the result back from the library bytes."""
+    src = tmp_path / "k.hip"
+    src.write_text(KSRC)
+    r = subprocess.run([B.HIPCC, "-O3", f"--offload-arch={B.ARCH}", "-save-temps", "-fPIC", "-c", "-o", "k.o",
+                        "k.hip"], cwd=tmp_path, capture_output=True, text=True)
+    if r.returncode:
+        pytest.skip("hipcc unavailable: " + r.stderr[-300:])
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", "k.so", "k.o"], cwd=tmp_path,
+                   check=True)
+    lib = str(tmp_path / "k.so")
+    names = {r["name"]: r for r in D.audit(str(tmp_path), quiet=True)[0] if r["kernel"]}
+    pad = [n for n in names if "k_padded" in n][0]
+    plain = [n for n in names if "k_plain" in n][0]
+    before = D.library_allocations(lib, str(tmp_path), names)
+    assert before[pad] == 16 and before[plain] == names[plain]["alloc"]
+    done = D.pad_descriptors(lib, str(tmp_path), [pad])
+    assert done == [(pad, 16, 24)]
+    after = D.library_allocations(lib, str(tmp_path), names)
+    assert after[pad] == 24 and after[plain] == before[plain]
