@@ -19,7 +19,7 @@
 //                candidate, then walks the lanes' matches greedily (ballot +
 //                readlane, wave-uniform); long matches are extended 64 bytes
 //                per step.  Literals go to the block's staging slot, sequences
-//                (<= 1024 per block, then the rest are literals) straight to
+//                (<= kZcSeqCap = 4096 per block, then the rest are literals) straight to
 //                scratch (8 KiB of LDS per wave: 20 waves per CU).
 //   k_zc_encode  ONE LANE PER BLOCK: the serial FSE bitstream of the block's
 //                sequences (three interleaved state machines, tables in LDS);
