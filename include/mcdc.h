@@ -91,6 +91,8 @@ typedef struct {
   uint64_t fallback_files; /* files resolved by the serial fallback     */
   double ids_ms;       /* chunk-ID (BLAKE3) kernels of mcdc_chunk_ids_device */
   double aead_ms;      /* sealing kernels of mcdc_seal_device / mcdc_open_device */
+  uint64_t lane_walk;  /* 1: the chains were walked one lane per chain */
+  uint64_t handed_back; /* lane walk: segments handed to the group walk (spec + link) */
 } mcdc_timing;
 
 /* ------------------------------------------------------------------ API -- */

@@ -69,7 +69,8 @@ class McdcTiming(ctypes.Structure):
                 ("d2h_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
                 ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64),
-                ("ids_ms", ctypes.c_double), ("aead_ms", ctypes.c_double)]
+                ("ids_ms", ctypes.c_double), ("aead_ms", ctypes.c_double),
+                ("lane_walk", ctypes.c_uint64), ("handed_back", ctypes.c_uint64)]
 
 
 class McdcBatcherStats(ctypes.Structure):

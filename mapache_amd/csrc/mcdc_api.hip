@@ -101,11 +101,21 @@ DevParams make_dev_params(const mcdc_params *p, uint64_t ms, uint64_t ml) {
   return d;
 }
 
-// Segment length: ~16 expected chunks per speculative chain (Knobs::seg_chunks,
-// an A/B-build knob), >= 2 * max so that a single chunk never skips a whole
-// segment.
+// The lane walk (one lane per chain, DESIGN.md §5 "Resolution, round 3") when
+// a chain step's window spans at most 64 runs (max <= 256 KiB): its steps
+// read run summaries 16 runs per batch, so larger windows favour the group
+// walk.  Single-part calls only (the staged pipeline keeps the group walk).
+bool use_lane_walk(const mcdc_params *p, const Knobs &kn) {
+  if (kn.parts != 1 || kn.lane_walk == 0) return false;
+  return kn.lane_walk == 2 || p->max_size <= 64u * kRun;
+}
+
+// Segment length: ~16 expected chunks per speculative chain on the group walk
+// (Knobs::seg_chunks, an A/B-build knob), ~4 on the lane walk (more, shorter
+// chains: one lane each), >= 2 * max so that a single chunk never skips a
+// whole segment.
 uint64_t segment_bytes(const mcdc_params *p, const Knobs &kn) {
-  const uint64_t k = (uint64_t)kn.seg_chunks;
+  const uint64_t k = (uint64_t)(use_lane_walk(p, kn) ? kn.lane_seg_chunks : kn.seg_chunks);
   uint64_t z = std::max<uint64_t>(2ull * p->max_size, k * ((uint64_t)p->min_size + p->avg_size));
   return (z + kRun - 1) / kRun * kRun;
 }
@@ -219,7 +229,7 @@ struct mcdc_ctx {
   Knobs knobs;                    // read once at creation (read_knobs)
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
-  DevBuf arena, run_cnt, run_sum, run_ent, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
+  DevBuf arena, run_cnt, run_sum, run_ent, punt, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
@@ -386,7 +396,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const uint64_t nruns = (n_al + kRun - 1) / kRun;
   const uint64_t ntiles_full = (n_al / kRun) / 64;
   if ((rc = ensure(ctx, ctx->run_cnt, nruns))) return rc;
-  if ((rc = ensure(ctx, ctx->run_sum, nruns * 4))) return rc;
+  // (+ one 16-run batch: the lane walk loads summaries a batch past its window)
+  if ((rc = ensure(ctx, ctx->run_sum, (nruns + 32) * 4))) return rc;
   if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
   if ((rc = ensure(ctx, ctx->tile_ctr, 64))) return rc;
   Work W{};
@@ -477,7 +488,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if ((rc = ensure(ctx, ctx->seg_count, (nsegs + 1) * 8))) return rc;
   if ((rc = ensure(ctx, ctx->seg_off, (nsegs + 1) * 8))) return rc;
   if (!out_dev && (rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
-  if ((rc = ensure(ctx, ctx->err, 16))) return rc;
+  if ((rc = ensure(ctx, ctx->err, 32))) return rc;
   const size_t tmpb = scan_tmp_bytes(nsegs);
   if ((rc = ensure(ctx, ctx->scan_tmp, tmpb))) return rc;
 
@@ -513,6 +524,13 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.irr_n = (uint32_t *)ctx->irr.p;
   W.irr_list = (uint32_t *)ctx->irr.p + 4;
   W.irr_flag = (uint8_t *)ctx->irr.p + 16 + (size_t)nsegs * 4;
+  const bool lane = use_lane_walk(params, kn);
+  if (lane) {
+    if ((rc = ensure(ctx, ctx->punt, (size_t)nsegs * 8 + 16))) return rc;
+    W.punt_spec = (uint32_t *)ctx->punt.p;
+    W.punt_link = (uint32_t *)ctx->punt.p + nsegs;
+  }
+  W.ncu = (uint32_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
 
   // ---- staged pipeline plan ----
   // parts: full tiles [tb[i], tb[i+1]); the last part also scans the partial tile
@@ -607,10 +625,16 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const bool want_counts = counts && nfiles;
   if (want_counts && (rc = ensure_fcnt(ctx, nfiles))) return rc;
   if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st2));
-  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 16, st2));
+  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st2));
   HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
   HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, st2));
-  for (int i = 0; i < K; ++i) {
+  const bool lane_all = lane && K == 1;
+  if (lane_all) {  // the lane walk over every segment
+    HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[0], 0));
+    launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
+    HIP_TRY(hipGetLastError());
+  }
+  for (int i = 0; i < (lane_all ? 0 : K); ++i) {
     HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[i], 0));
     const uint32_t a_s = i ? spec_hi[i - 1] : 0, a_l = i ? link_hi[i - 1] : 0;
     launch_spec(W, P, kn, a_s, spec_hi[i], st2);
@@ -667,6 +691,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->timing.chunks = total;
   ctx->timing.scan_launches = n_al > 0 ? (uint64_t)K : 0;
   ctx->timing.fallback_files = nfallback;
+  ctx->timing.lane_walk = lane_all ? 1 : 0;
+  ctx->timing.handed_back = lane_all ? ((volatile uint64_t *)ctx->h_res)[4] : 0;
   return MCDC_OK;
 }
 
@@ -871,7 +897,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
-  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->segs, &ctx->files, &ctx->nodes,
+  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,

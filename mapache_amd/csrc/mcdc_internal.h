@@ -6,12 +6,16 @@
 //               S/L flags for every position whose 48-byte window passes the
 //               prefilter -> per-run candidate lists and summaries (run = kRun
 //               bytes)
-//   k_spec6     one 16-lane group (a DPP row) per segment: speculative cut
-//               chain from the segment start (group_next = exact fastcdc
-//               cut_gear semantics)
-//   k_link      one 16-lane group per segment: continue past the segment end
-//               until the chain merges with a later segment's speculative
-//               chain (forced stretches taken whole: forced_run)
+//   k_spec_lane one lane per segment (default when max <= 64 runs):
+//               speculative cut chain from the segment start (lane_next =
+//               exact fastcdc cut_gear semantics); a segment it cannot walk
+//               goes to k_spec_list (the group walk below)
+//   k_spec6     one 16-lane group (a DPP row) per segment: the same chain
+//               (group_next), for large max and the staged pipeline
+//   k_link_lane / k_link
+//               per segment: continue past the segment end until the chain
+//               merges with a later segment's speculative chain (the group
+//               walk takes forced stretches whole: forced_run)
 //   clean path  k_incr_scan (or k_incr_count + scan + k_add_base) + k_emit
 //   general     k_fallback (one wave per file whose continuation never
 //               merged: serial walk), k_walk_fast / k_irr_flags / k_walk_jumps
@@ -128,6 +132,9 @@ struct Work {
   uint8_t *irr_flag;     // general path: segment's link is not to the next segment
   uint32_t *irr_list;    // sorted irregular segment indices, count in *irr_n
   uint32_t *irr_n;
+  uint32_t *punt_spec;   // lane walk: segments handed to the group walk (k_spec_list), count err[4]
+  uint32_t *punt_link;   // (k_link_list), count err[5]
+  uint32_t ncu;          // compute units (persistent grids)
 };
 
 // Tuning switches of a context, read from the environment once, when the
@@ -144,6 +151,8 @@ struct Knobs {
   int scan_pieces = 0;    // MCDC_SCAN_PIECES: lane pieces per run (0: by size, scan_pieces())
   int scan_cold = 1;      // MCDC_SCAN_COLD: cold-started lane pieces
   int pinned_direct = 1;  // MCDC_PINNED_DIRECT: k_emit writes pinned host output directly
+  int lane_walk = 1;      // MCDC_LANE_WALK: 0 group walk only, 1 lane walk when max <= 64 runs, 2 always
+  int lane_seg_chunks = 4;// MCDC_LANE_SEG_CHUNKS: expected chunks per segment on the lane walk
   // A/B builds only
   int group = 16;         // MCDC_GROUP: lanes per chain group (8, 16, 32)
   int spec_occ = 6;       // MCDC_SPEC_OCC: k_spec waves-per-SIMD build (5 or 6)
@@ -165,7 +174,11 @@ void launch_spec(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0,
 void launch_link(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0, uint32_t s1, uint64_t node_cap,
                  hipStream_t stream);
 void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
-                             void *scan_tmp, size_t scan_tmp_bytes, hipStream_t stream);
+                             void *scan_tmp, size_t scan_tmp_bytes, hipStream_t stream, int gs = 16);
+// whole-call resolution with the lane walk (single part): spec, link, counts,
+// offsets and boundaries of every segment, the group walk for handed-back ones
+void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void *scan_tmp, size_t scan_tmp_bytes,
+                         hipStream_t stream);
 void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
                             hipStream_t stream);
 size_t scan_tmp_bytes(uint32_t nsegs);

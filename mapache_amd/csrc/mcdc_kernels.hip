@@ -1024,15 +1024,10 @@ __device__ __forceinline__ void load_gear_lds(uint64_t *gt, const Work &W) {
 }
 
 
-// One group per segment.
+// One group per segment: the speculative chain of segment s.
 template <int GS>
-__device__ __forceinline__ void spec_body(Work &W, const DevParams &P, uint32_t s0, uint32_t s1) {
-  __builtin_amdgcn_s_setprio(3);
-  __shared__ uint64_t gt[256];
-  load_gear_lds(gt, W);
-  const Group<GS> G;
-  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
-  if (s >= s1) return;
+__device__ __forceinline__ void spec_chain(const Group<GS> &G, const Work &W, const DevParams &P, const uint64_t *gt,
+                                           uint32_t s) {
   const Seg S = W.segs[s];
   const uint64_t fend = W.files[S.file].end;
   uint64_t *out = W.nodes + W.node_off[s];
@@ -1053,6 +1048,17 @@ __device__ __forceinline__ void spec_body(Work &W, const DevParams &P, uint32_t 
 }
 
 template <int GS>
+__device__ __forceinline__ void spec_body(Work &W, const DevParams &P, uint32_t s0, uint32_t s1) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
+  const Group<GS> G;
+  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+  if (s >= s1) return;
+  spec_chain<GS>(G, W, P, gt, s);
+}
+
+template <int GS>
 __global__ __launch_bounds__(256) void k_spec(Work W, DevParams P, uint32_t s0, uint32_t s1) {
   spec_body<GS>(W, P, s0, s1);
 }
@@ -1065,6 +1071,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
                                                                                          uint32_t s0, uint32_t s1) {
   MCDC_VGPR_PAD(80);  // 80 used: not an exact fill (MCDC_VGPR_PAD)
   spec_body<GS>(W, P, s0, s1);
+}
+
+// The segments the lane walk handed back (list, *count of them): the group
+// walk, grid-stride over the list.
+template <int GS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_spec_list(
+    Work W, DevParams P, const uint32_t *list, const uint32_t *count) {
+  MCDC_VGPR_PAD(80);
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
+  const Group<GS> G;
+  const uint32_t n = *count, ng = gridDim.x * blockDim.x / GS;
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / GS; i < n; i += ng) spec_chain<GS>(G, W, P, gt, list[i]);
 }
 
 // index of c in nodes(j) (sorted), or -1; group-cooperative
@@ -1089,13 +1109,8 @@ __device__ int find_node(const Group<GS> &G, const Work &W, uint32_t j, uint64_t
 // cont_cnt = expanded node count, cont_ent = entries.  `node_cap` bounds the
 // expanded count (the staged pipeline's look-ahead assumes <= kContMax steps).
 template <int GS>
-__global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, uint32_t s1, uint64_t node_cap) {
-  __builtin_amdgcn_s_setprio(3);
-  __shared__ uint64_t gt[256];
-  load_gear_lds(gt, W);
-  const Group<GS> G;
-  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
-  if (s >= s1) return;
+__device__ __forceinline__ void link_chain(const Group<GS> &G, const Work &W, const DevParams &P, const uint64_t *gt,
+                                           uint32_t s, uint64_t node_cap) {
   const Seg S = W.segs[s];
   const File F = W.files[S.file];
   if (S.flags & kSegLast) {
@@ -1137,6 +1152,297 @@ __global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, 
       W.long_list[atomicAdd(W.long_n, 1u)] = s;
       atomicOr(W.err + 2, 1u);
     }
+  }
+}
+
+template <int GS>
+__global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, uint32_t s1, uint64_t node_cap) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
+  const Group<GS> G;
+  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+  if (s >= s1) return;
+  link_chain<GS>(G, W, P, gt, s, node_cap);
+}
+
+// The segments whose continuation the lane walk handed back (list, *count).
+template <int GS>
+__global__ __launch_bounds__(256) void k_link_list(Work W, DevParams P, const uint32_t *list, const uint32_t *count) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ uint64_t gt[256];
+  load_gear_lds(gt, W);
+  const Group<GS> G;
+  const uint32_t n = *count, ng = gridDim.x * blockDim.x / GS;
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / GS; i < n; i += ng)
+    link_chain<GS>(G, W, P, gt, list[i], ~0ull);
+}
+
+// ======================================================= lane walk =======
+// The chain walk with ONE LANE per chain: 64 chains per wave.  The group walk
+// above computes every chain-uniform quantity of a step in 16 lanes and the
+// four chains of a wave diverge in SALU/exec control: ~90 VALU + ~50 SALU per
+// chain step, issue-bound (PMC of k_spec6: 12 % of wave cycles waiting,
+// 251 us of a 64 GiB call).  Here a step is ~15 VALU per chain:
+//  * the (up to) 47 restart positions: the window's bytes are realigned in
+//    registers (v_cndmask + v_alignbyte) and hashed by one unrolled recurrence,
+//    GEAR from a 32x replicated LDS copy (one v_perm_b32 per address,
+//    conflict-free, as in the scan); the mask test is exact only for a lane
+//    whose accumulated test fired (rare) or whose window is irregular;
+//  * the windowed candidates from run summaries, 16 runs (4 x uint4) per
+//    batch per lane, the next batch loaded while one is evaluated; a run the
+//    window starts inside (the S window's first run, the L window's first
+//    run) is decided from its entry list when the summary cannot tell.
+// A step the lane walk does not take -- a run whose entry list overflowed, a
+// continuation of kContMax steps -- hands the whole segment to the group walk
+// (k_spec_list / k_link_list), which recomputes it from scratch.
+constexpr uint32_t kLaneBatch = 16;  // runs per summary batch past the first window
+constexpr uint32_t kLaneWin = 64;    // runs loaded at the start of a step (a 256 KiB max's whole window)
+
+__device__ __forceinline__ void load_gear_rep(uint64_t *tab, const Work &W) {
+  for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) tab[i] = W.gear[i >> 5];
+  __syncthreads();
+}
+
+// Per-lane select of a or b as one v_perm_b32 (sel from lane_sel): written as
+// a ?: on array elements the compiler turns the register realignments below
+// into dynamically indexed private arrays (scratch).
+__device__ __forceinline__ uint32_t lane_sel(bool take_b) { return take_b ? 0x07060504u : 0x03020100u; }
+__device__ __forceinline__ uint32_t sel32(uint32_t a, uint32_t b, uint32_t sel) { return __builtin_amdgcn_perm(b, a, sel); }
+
+// GEAR[byte k of w] from the replicated table (copy lo8 / 8)
+#define MCDC_GR(w, k, lo8) lds_gear(tab, __builtin_amdgcn_perm((w), (lo8), 0x0c0c0000u | ((4u + (k)) << 8)))
+
+// First candidate of run r in [lo_r, hi_r) (chunk-relative) from its entry
+// list, for a run a window edge splits; punt when the list overflowed.
+__device__ __forceinline__ int32_t lane_run_split(const Work &W, const DevParams &P, uint64_t r, int32_t rbase,
+                                                  int32_t lo_r, int32_t hi_r, int32_t cce_r, bool &punt) {
+  const uint32_t cnt = W.run_cnt[r];
+  if (cnt > P.cap) { punt = true; return INT32_MAX; }
+  if (P.cap == 8) {
+    const uint4 ea = *reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
+    return run_first_rel(cnt, ea, reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull) + 1, rbase, lo_r, hi_r,
+                         cce_r);
+  }
+  int32_t best = INT32_MAX;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t e = W.run_ent[r * (uint64_t)P.cap + i];
+    const int32_t p = rbase + (int32_t)(e & 0x00ffffffu);
+    const uint32_t kind = p < cce_r ? (e >> 31) : ((e >> 30) & 1u);
+    if (p >= lo_r && p < hi_r && kind) best = min(best, p);
+  }
+  return best;
+}
+
+// next(c) by one lane: group_next's semantics (the crate's cut_gear from c,
+// file end fend).  Sets punt (result void) for a step it does not take.
+__device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P, const uint64_t *tab, uint32_t lo8,
+                                              uint64_t c, uint64_t fend, bool &punt) {
+  const uint64_t rem = fend - c;
+  if (rem <= P.min) return fend;  // remaining <= min_size: whole tail
+  const uint32_t remaining = rem > P.max ? P.max : (uint32_t)rem;
+  const uint32_t center = (rem <= P.max && rem < P.avg) ? (uint32_t)rem : P.avg;
+  const uint32_t t0 = P.min / 2 * 2, ce = center / 2 * 2, re = remaining / 2 * 2;
+  if (re <= t0) return c + remaining;  // loop never runs: forced
+  const uint64_t t = c + t0;
+  const uint32_t wlen = min(re - t0, (uint32_t)(kWin - 1));
+  const int32_t lo_r = (int32_t)(t0 + kWin - 1), hi_r = (int32_t)re, cce_r = (int32_t)ce;
+  const bool cand = lo_r < hi_r;
+  const int32_t s_end = min(cce_r, hi_r), l_beg = max(lo_r, cce_r);
+  // ---- loads first: restart-window bytes, batch 0 of the run summaries, the
+  // summaries of the two runs a window edge can split
+  const uint64_t A = t & ~15ull;
+  uint32_t dw[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 v = A + 16 * k < W.n_al ? *reinterpret_cast<const uint4 *>(W.base + A + 16 * k) : make_uint4(0, 0, 0, 0);
+    dw[4 * k] = v.x; dw[4 * k + 1] = v.y; dw[4 * k + 2] = v.z; dw[4 * k + 3] = v.w;
+  }
+  const uint64_t r0 = cand ? (c + (uint64_t)lo_r) / kRun : 0, r1 = cand ? (c + (uint64_t)hi_r - 1) / kRun : 0;
+  const uint64_t rl = cand ? (c + (uint64_t)l_beg) / kRun : 0;
+  const uint64_t ra = r0 & ~3ull;  // batches start 16-byte aligned in run_sum
+  // the first kLaneWin runs (the whole window at max <= 256 KiB) in one go:
+  // one memory latency per step instead of one per batch
+  uint4 win[kLaneWin / 4];
+#pragma unroll
+  for (int k = 0; k < (int)kLaneWin / 4; ++k)
+    win[k] = (cand && ra + 4 * k <= r1) ? *reinterpret_cast<const uint4 *>(W.run_sum + ra + 4 * k)
+                                        : make_uint4(0, 0, 0, 0);
+  const uint32_t u_lo = cand ? W.run_sum[r0] : 0u, u_lb = (cand && l_beg < hi_r) ? W.run_sum[rl] : 0u;
+
+  // ---- (1) exact restarted hash of the first <= 47 tested positions
+  {
+    const uint32_t q = (uint32_t)(t - A);  // window start within the 64 loaded bytes (0..15)
+    uint32_t f[14], g[13], e[12];
+    const uint32_t s8 = lane_sel(q & 8), s4 = lane_sel(q & 4);
+#pragma unroll
+    for (int i = 0; i < 14; ++i) f[i] = sel32(dw[i], dw[i + 2], s8);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) g[i] = sel32(f[i], f[i + 1], s4);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = __builtin_amdgcn_alignbyte(g[j + 1], g[j], q & 3);
+    const uint32_t mlo = (uint32_t)P.ms, mhi = (uint32_t)(P.ms >> 32);
+    uint64_t h = 0;
+    uint32_t acc = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < kWin - 1; ++i) {
+      h = (h << 1) + MCDC_GR(e[i >> 2], i & 3, lo8);
+      acc = min(acc, ((uint32_t)h & mlo) | ((uint32_t)(h >> 32) & mhi));
+    }
+    // every position tests mask_s when the window is whole and before ce
+    const bool regular = wlen == (uint32_t)(kWin - 1) && ce >= t0 + (uint32_t)(kWin - 1);
+    if (__builtin_expect(!regular || acc == 0, 0)) {  // exact: per-position mask, first hit
+      uint32_t first = 0xffffffffu;
+      h = 0;
+#pragma unroll
+      for (int i = 0; i < kWin - 1; ++i) {
+        h = (h << 1) + MCDC_GR(e[i >> 2], i & 3, lo8);
+        const uint64_t m = (t0 + (uint32_t)i < ce) ? P.ms : P.ml;
+        if ((uint32_t)i < wlen && (h & m) == 0 && first == 0xffffffffu) first = (uint32_t)i;
+      }
+      if (first != 0xffffffffu) return t + first;
+    }
+  }
+  if (!cand) return c + remaining;
+
+  // ---- (2) windowed candidates for [t + 47, c + re)
+  int32_t best = INT32_MAX;
+  {  // a run a window edge splits: the summary's first S (L) lies before the edge and more follow
+    const uint32_t nc0 = u_lo >> 28, fs0 = u_lo & 0x3fffu;
+    const int32_t rb0 = (int32_t)((int64_t)(r0 * (uint64_t)kRun) - (int64_t)c);
+    if (fs0 && rb0 + (int32_t)fs0 - 1 < lo_r && nc0 >= 2 && lo_r < s_end)
+      best = min(best, lane_run_split(W, P, r0, rb0, lo_r, hi_r, cce_r, punt));
+    const uint32_t ncl = u_lb >> 28, fll = (u_lb >> 14) & 0x3fffu;
+    const int32_t rbl = (int32_t)((int64_t)(rl * (uint64_t)kRun) - (int64_t)c);
+    if (fll && rbl + (int32_t)fll - 1 < l_beg && ncl >= 2 && l_beg < hi_r)
+      best = min(best, lane_run_split(W, P, rl, rbl, lo_r, hi_r, cce_r, punt));
+  }
+  // Every other run is decided by its summary: its first S qualifies iff it
+  // lies in [lo, s_end), its first L iff in [l_beg, hi).  Runs before r0 or
+  // after r1 fail both tests by position, so batches need no masking.
+  const uint32_t lenS = s_end > lo_r ? (uint32_t)(s_end - lo_r) : 0u;
+  const uint32_t lenL = hi_r > l_beg ? (uint32_t)(hi_r - l_beg) : 0u;
+  const int32_t wstart = (int32_t)((int64_t)(ra * (uint64_t)kRun) - (int64_t)c);
+  auto eval_run = [&](uint32_t u, int32_t rbk) {
+    const uint32_t fs1 = u & 0x3fffu, fl1 = (u >> 14) & 0x3fffu;
+    const int32_t pS = rbk + (int32_t)fs1 - 1, pL = rbk + (int32_t)fl1 - 1;
+    const bool okS = fs1 != 0 && (uint32_t)(pS - lo_r) < lenS;
+    const bool okL = fl1 != 0 && (uint32_t)(pL - l_beg) < lenL;
+    best = min(best, min(okS ? pS : INT32_MAX, okL ? pL : INT32_MAX));
+  };
+  // the preloaded window, 16 runs at a time; stop once no lane of the wave
+  // can still find an earlier candidate
+#pragma unroll
+  for (int b = 0; b < (int)kLaneWin / 16; ++b) {
+    const int32_t bstart = wstart + b * 16 * kRun;
+    if (!__any(bstart < best && ra + 16 * b <= r1)) break;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = win[4 * b + k];
+      eval_run(v.x, bstart + (4 * k) * kRun);
+      eval_run(v.y, bstart + (4 * k + 1) * kRun);
+      eval_run(v.z, bstart + (4 * k + 2) * kRun);
+      eval_run(v.w, bstart + (4 * k + 3) * kRun);
+    }
+  }
+  // windows past kLaneWin runs (max > 256 KiB): batches of 16, loaded as needed
+  for (uint64_t rb = ra + kLaneWin; rb <= r1; rb += kLaneBatch) {
+    const int32_t bstart = wstart + (int32_t)((rb - ra) * kRun);
+    if (bstart >= best) break;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(W.run_sum + rb + 4 * k);
+      eval_run(v.x, bstart + (4 * k) * kRun);
+      eval_run(v.y, bstart + (4 * k + 1) * kRun);
+      eval_run(v.z, bstart + (4 * k + 2) * kRun);
+      eval_run(v.w, bstart + (4 * k + 3) * kRun);
+    }
+  }
+  return best != INT32_MAX ? c + (uint64_t)best : c + remaining;  // else forced cut
+}
+
+// One lane per segment, grid-stride: the speculative chain from the segment
+// start (spec_chain's outputs).
+__global__ __launch_bounds__(256) void k_spec_lane(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
+  __builtin_amdgcn_s_setprio(3);
+  load_gear_rep(tab, W);
+  const uint32_t lo8 = (threadIdx.x & 31) << 3;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x; s < s1; s += stride) {
+    const Seg S = W.segs[s];
+    const uint64_t fend = W.files[S.file].end;
+    uint64_t *out = W.nodes + W.node_off[s];
+    const uint64_t cap = W.node_off[s + 1] - W.node_off[s];
+    uint64_t c = S.start, k = 0, exitp = fend;
+    bool punt = false;
+    for (;;) {
+      if (k >= cap) { atomicOr(W.err, kErrNodeCap); break; }
+      out[k++] = c;
+      const uint64_t nc = lane_next(W, P, tab, lo8, c, fend, punt);
+      if (punt) break;
+      if (nc >= S.end) { exitp = nc; break; }
+      c = nc;
+    }
+    if (punt) {
+      W.punt_spec[atomicAdd(W.err + 4, 1u)] = s;
+    } else {
+      W.node_cnt[s] = (uint32_t)k;
+      W.seg_exit[s] = exitp;
+    }
+  }
+}
+
+// One lane per segment: the continuation past the segment end until it meets
+// a node of a later segment's speculative chain (link_chain's outputs).  A
+// forced cut is an ordinary step here (continuation entries of one node); a
+// continuation that reaches kContMax entries goes to the group walk, which
+// takes forced stretches whole.
+__global__ __launch_bounds__(256) void k_link_lane(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
+  __builtin_amdgcn_s_setprio(3);
+  load_gear_rep(tab, W);
+  const uint32_t lo8 = (threadIdx.x & 31) << 3;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x; s < s1; s += stride) {
+    const Seg S = W.segs[s];
+    const File F = W.files[S.file];
+    if (S.flags & kSegLast) {
+      W.link_seg[s] = kSegNone; W.link_idx[s] = 0; W.link_pos[s] = F.end; W.cont_cnt[s] = 0; W.cont_ent[s] = 0;
+      continue;
+    }
+    uint64_t c = W.seg_exit[s];
+    uint32_t ents = 0, ls = kSegNone, li = 0, j = 0xffffffffu, i = 0;
+    uint64_t lp = F.end;
+    bool punt = false;
+    for (;;) {
+      if (c >= F.end) { ls = kSegNone; lp = F.end; break; }
+      const uint32_t jj = F.first_seg + (uint32_t)((c - F.start) / W.zseg);
+      if (jj != j) { j = jj; i = 0; }
+      const uint64_t *nd = W.nodes + W.node_off[j];
+      const uint32_t n = W.node_cnt[j];
+      uint64_t v = ~0ull;
+      while (i < n) {  // nodes are sorted and c only grows: resume where the last step stopped
+        v = nd[i];
+        if (v >= c) break;
+        ++i;
+      }
+      if (i < n && v == c) { ls = j; li = i; lp = c; break; }
+      if (ents == (uint32_t)kContMax) { punt = true; break; }
+      const uint64_t nc = lane_next(W, P, tab, lo8, c, F.end, punt);
+      if (punt) break;
+      W.cont[(uint64_t)s * kContMax + ents] = c;
+      W.cont_rep[(uint64_t)s * kContMax + ents] = 1u;
+      ++ents;
+      c = nc;
+    }
+    if (punt) {
+      W.punt_link[atomicAdd(W.err + 5, 1u)] = s;
+      continue;
+    }
+    W.link_seg[s] = ls; W.link_idx[s] = li; W.link_pos[s] = lp;
+    W.cont_cnt[s] = ents; W.cont_ent[s] = ents;
+    if (ls != s + 1) atomicOr(&W.file_flags[S.file], kFileSkip);
   }
 }
 
@@ -1291,29 +1597,45 @@ __device__ __forceinline__ ChunkQ chunk_q(const DevParams &P, uint64_t c, uint64
   return r;
 }
 
-// ChunkData.hash of one chunk, computed by one lane: the <= 64 bytes [from, q]
+// ChunkData.hash of one chunk, computed by one lane: the 64 bytes ending at q
 // arrive as five aligned 16-byte loads (blocks past q are not read, so no
-// load leaves the arena), and the state is summed from independent table
-// lookups, 16 per block (no dependency chain through the hash).
-__device__ __forceinline__ uint64_t chunk_hash(const Work &W, const uint64_t *gt, const ChunkQ &cq) {
+// load leaves the arena), are realigned in registers so that byte i is
+// position q - 63 + i, and run through the 2-byte loop's recurrence
+// h = (h << 1) + GEAR[x] (the same sum: a term k bytes before q is shifted k
+// times).  Positions before `from` (a chunk that restarted < 63 bytes before
+// its cut) add nothing.  GEAR from the replicated LDS table (k_emit).
+// (Round 2 summed 80 independent lookups each with its own variable shift
+// and window select: ~10 VALU per byte; this is 2 VALU + 1 LDS per byte.)
+__device__ __forceinline__ uint64_t chunk_hash(const Work &W, const uint64_t *tab, uint32_t lo8, const ChunkQ &cq) {
   if (cq.q < cq.from) return 0;
-  const uint64_t A = cq.from & ~15ull;
-  const uint32_t lo = (uint32_t)(cq.from - A), hi = (uint32_t)(cq.q - A);  // window [lo, hi] in blk bytes
+  const uint64_t s0 = cq.q - 63;  // q >= t0 >= 64 (min_size >= 64)
+  const uint64_t B = s0 & ~15ull;
+  const uint32_t off = (uint32_t)(s0 - B);
+  uint32_t dw[20];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint4 b = B + 16 * k <= cq.q ? *reinterpret_cast<const uint4 *>(W.base + B + 16 * k) : make_uint4(0, 0, 0, 0);
+    dw[4 * k] = b.x; dw[4 * k + 1] = b.y; dw[4 * k + 2] = b.z; dw[4 * k + 3] = b.w;
+  }
+  uint32_t f[18], g[17], e[16];
+  const uint32_t s8 = lane_sel(off & 8), s4 = lane_sel(off & 4);
+#pragma unroll
+  for (int i = 0; i < 18; ++i) f[i] = sel32(dw[i], dw[i + 2], s8);
+#pragma unroll
+  for (int i = 0; i < 17; ++i) g[i] = sel32(f[i], f[i + 1], s4);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) e[j] = __builtin_amdgcn_alignbyte(g[j + 1], g[j], off & 3);
+  const uint32_t nex = (uint32_t)(cq.from - s0);  // leading positions outside the window
   uint64_t h = 0;
-  // (all 80 table reads in flight: rolling the block loop to cut registers,
-  // 129 -> 74 VGPRs with the global table, made k_emit 0.03 ms slower per
-  // 64 GiB call, tools/lib_ab.py)
+  if (__builtin_expect(__any(nex != 0), 0)) {
 #pragma unroll
-  for (uint32_t k = 0; k < 5; ++k) {
-    const uint4 b = A + 16 * k <= cq.q ? *reinterpret_cast<const uint4 *>(W.base + A + 16 * k) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-      const uint32_t i = 16 * k + j;
-      const uint32_t w = j < 4 ? b.x : j < 8 ? b.y : j < 12 ? b.z : b.w;
-      const uint32_t x = (w >> (8 * (j % 4))) & 0xffu;
-      const uint64_t g = gt[x] << ((hi - i) & 63u);
-      h += (i >= lo && i <= hi) ? g : 0;
+    for (int i = 0; i < 64; ++i) {
+      const uint64_t gv = MCDC_GR(e[i >> 2], i & 3, lo8);
+      h = (h << 1) + ((uint32_t)i < nex ? 0ull : gv);
     }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) h = (h << 1) + MCDC_GR(e[i >> 2], i & 3, lo8);
   }
   return cq.dbl ? h << 1 : h;
 }
@@ -1332,10 +1654,10 @@ __device__ __forceinline__ uint64_t cont_node(const uint64_t *ct, const uint32_t
 }
 
 // One output record: the chunk [pos, nxt) of file F at output index o.
-__device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, const uint64_t *gt, const File &F,
-                                         uint64_t o, uint64_t pos, uint64_t nxt) {
+__device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, const uint64_t *tab, uint32_t lo8,
+                                         const File &F, uint64_t o, uint64_t pos, uint64_t nxt) {
   const ChunkQ cq = chunk_q(P, pos, nxt - pos, F.end);
-  const uint64_t hash = chunk_hash(W, gt, cq);
+  const uint64_t hash = chunk_hash(W, tab, lo8, cq);
   if (o < W.out_cap) {
     DevChunk ch;
     ch.offset = pos - F.start;
@@ -1347,71 +1669,59 @@ __device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, cons
   }
 }
 
-// One group of GS lanes per segment, lane i owns chunk i (of each batch of
-// GS) and computes its hash itself.  Resolution kernels raise their wave priority:
-// they run beside the scan's later parts and are latency-bound.
+// One group of GS lanes per segment (grid-stride over segments: the 64 KiB
+// table is loaded once per 1024-thread block, 16 waves per CU share it: the
+// emit is latency-bound and needs the waves), lane i owns chunk i (of each batch of GS)
+// and computes its hash itself.  GS = 8 on the lane walk (segments of ~6
+// chunks), 16 on the group walk (~16).
 //
-// GEAR comes from an LDS copy.  Both emitters pad their VGPR allocation
-// (MCDC_VGPR_PAD): filling it exactly lost the memory returns
-// of whole waves -- k_emit_long at 88/88 with this LDS table (round 2), k_emit
-// at 184/184 with the global one and with this one -- and a wrong
-// ChunkData.hash is the one output no later stage re-checks.
-// tools/dbg/build_vpad.sh builds k_emit unpadded (MCDC_EMIT_VPAD=0).
-#ifndef MCDC_EMIT_VPAD
-#define MCDC_EMIT_VPAD 184
-#endif
-#ifndef MCDC_EMIT_LONG_VPAD
-#define MCDC_EMIT_LONG_VPAD 0  // (177 used, 184 allocated: not an exact fill)
-#endif
+// VGPR allocations are audited at build time: filling one
+// exactly lost the memory returns of whole waves (k_emit at 184/184 in round
+// 2), and a wrong ChunkData.hash is the one output no later stage re-checks.
 template <int GS>
-__global__ __launch_bounds__(256) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1) {
-#if MCDC_EMIT_VPAD
-  MCDC_VGPR_PAD(MCDC_EMIT_VPAD);
-#endif
+__global__ __launch_bounds__(1024) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+  __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
   __builtin_amdgcn_s_setprio(3);
-  __shared__ uint64_t gtl[256];
-  load_gear_lds(gtl, W);
-  const uint64_t *gt = gtl;
-  const uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS;
-  if (s >= s1) return;
-  const uint64_t n = W.seg_count[s];
-  if (n == 0) return;
+  load_gear_rep(tab, W);
+  const uint32_t lo8 = (threadIdx.x & 31) << 3;
   const uint32_t lane = lane_id() & (GS - 1);
-  const Seg S = W.segs[s];
-  const File F = W.files[S.file];
-  const uint32_t e = W.entry_idx[s];
-  const uint64_t nn = W.node_cnt[s] - e;
-  const uint64_t *nd = W.nodes + W.node_off[s] + e;
-  const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
-  const uint32_t *cr = W.cont_rep + (uint64_t)s * kContMax;
-  const uint64_t ncont = n - nn;                    // continuation nodes, expanded
-  const bool plain = ncont == W.cont_ent[s];        // every entry a single node
-  const uint64_t n_here = ncont > kEmitInline ? nn : n;  // a long stretch: k_emit_long
-  const uint64_t after = W.link_pos[s];
-  const uint64_t base_out = W.seg_off[s];
-  auto node = [&](uint64_t i) -> uint64_t {
-    if (i < nn) return nd[i];
-    return plain ? ct[i - nn] : cont_node(ct, cr, i - nn, P.max);
-  };
-  for (uint64_t i0 = 0; i0 < n_here; i0 += GS) {
-    const uint64_t i = i0 + lane;
-    if (i >= n_here) break;
-    const uint64_t pos = node(i);
-    const uint64_t nxt = i + 1 < n ? node(i + 1) : after;
-    emit_one(W, P, gt, F, base_out + i, pos, nxt);
+  const uint32_t ng = gridDim.x * blockDim.x / GS;
+  for (uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS; s < s1; s += ng) {
+    const uint64_t n = W.seg_count[s];
+    if (n == 0) continue;
+    const Seg S = W.segs[s];
+    const File F = W.files[S.file];
+    const uint32_t e = W.entry_idx[s];
+    const uint64_t nn = W.node_cnt[s] - e;
+    const uint64_t *nd = W.nodes + W.node_off[s] + e;
+    const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
+    const uint32_t *cr = W.cont_rep + (uint64_t)s * kContMax;
+    const uint64_t ncont = n - nn;                    // continuation nodes, expanded
+    const bool plain = ncont == W.cont_ent[s];        // every entry a single node
+    const uint64_t n_here = ncont > kEmitInline ? nn : n;  // a long stretch: k_emit_long
+    const uint64_t after = W.link_pos[s];
+    const uint64_t base_out = W.seg_off[s];
+    auto node = [&](uint64_t i) -> uint64_t {
+      if (i < nn) return nd[i];
+      return plain ? ct[i - nn] : cont_node(ct, cr, i - nn, P.max);
+    };
+    for (uint64_t i0 = 0; i0 < n_here; i0 += GS) {
+      const uint64_t i = i0 + lane;
+      if (i < n_here) {
+        const uint64_t pos = node(i);
+        const uint64_t nxt = i + 1 < n ? node(i + 1) : after;
+        emit_one(W, P, tab, lo8, F, base_out + i, pos, nxt);
+      }
+    }
   }
 }
 
 // Continuation stretches longer than kEmitInline nodes (k_link appended their
-// segments to long_list): the whole grid strides over each one's nodes.  GEAR
-// from LDS, VGPR allocation padded (see k_emit).
+// segments to long_list): the whole grid strides over each one's nodes.
 __global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
-#if MCDC_EMIT_LONG_VPAD
-  MCDC_VGPR_PAD(MCDC_EMIT_LONG_VPAD);
-#endif
-  __shared__ uint64_t gtl[256];
-  load_gear_lds(gtl, W);
-  const uint64_t *gt = gtl;
+  __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
+  load_gear_rep(tab, W);
+  const uint32_t lo8 = (threadIdx.x & 31) << 3;
   const uint32_t nl = *W.long_n;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint32_t li = 0; li < nl; ++li) {
@@ -1427,7 +1737,7 @@ __global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ncont; i += stride) {
       const uint64_t pos = cont_node(ct, cr, i, P.max);
       const uint64_t nxt = i + 1 < ncont ? cont_node(ct, cr, i + 1, P.max) : after;
-      emit_one(W, P, gt, F, base_out + i, pos, nxt);
+      emit_one(W, P, tab, lo8, F, base_out + i, pos, nxt);
     }
   }
 }
@@ -1440,6 +1750,7 @@ __global__ void k_finish(Work W, uint64_t *res) {
     res[1] = W.err[0];
     res[2] = W.err[1];
     res[3] = W.err[2];
+    res[4] = (uint64_t)W.err[4] + W.err[5];
   }
 }
 
@@ -1591,6 +1902,8 @@ Knobs read_knobs() {
   if (k.scan_pieces != 1 && k.scan_pieces != 2 && k.scan_pieces != 4) k.scan_pieces = 0;
   k.scan_cold = env("MCDC_SCAN_COLD", k.scan_cold) != 0;
   k.pinned_direct = env("MCDC_PINNED_DIRECT", k.pinned_direct) != 0;
+  k.lane_walk = std::min(std::max(env("MCDC_LANE_WALK", k.lane_walk), 0), 2);
+  k.lane_seg_chunks = std::max(env("MCDC_LANE_SEG_CHUNKS", k.lane_seg_chunks), 1);
 #ifdef MCDC_AB_KNOBS
   k.group = env("MCDC_GROUP", k.group);
   if (k.group != 8 && k.group != 16 && k.group != 32) k.group = kGroup;
@@ -1641,10 +1954,26 @@ void launch_link(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0,
   hipLaunchKernelGGL(k_link<16>, dim3(group_blocks(s1 - s0, 16)), dim3(256), 0, stream, w, p, s0, s1, node_cap);
 }
 
-// counts, offsets and boundaries of segments [s0, s1) assuming the clean case
-void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
-                             void *scan_tmp, size_t scan_tmp_bytes_, hipStream_t stream) {
+// Blocks of a grid-stride resolution kernel with a 64 KiB LDS table: two per
+// CU (the table is loaded once per block), fewer when the work is smaller.
+static unsigned lane_grid(const Work &w, uint64_t items_per_block_round, uint64_t items, uint64_t per_cu = 2) {
+  const uint64_t cap = per_cu * (w.ncu ? w.ncu : 256);
+  const uint64_t need = (items + items_per_block_round - 1) / items_per_block_round;
+  return (unsigned)std::max<uint64_t>(1, std::min(cap, need));
+}
+
+static void launch_emit(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, int gs, hipStream_t stream) {
   if (s1 <= s0) return;
+  if (gs == 8)
+    hipLaunchKernelGGL(k_emit<8>, dim3(lane_grid(w, 1024 / 8, s1 - s0, 1)), dim3(1024), 0, stream, w, p, s0, s1);
+  else
+    hipLaunchKernelGGL(k_emit<kGroup>, dim3(lane_grid(w, 1024 / kGroup, s1 - s0, 1)), dim3(1024), 0, stream, w, p, s0,
+                       s1);
+}
+
+// counts and offsets of segments [s0, s1) assuming the clean case
+static void launch_counts_incremental(const Work &w, uint32_t s0, uint32_t s1, uint64_t *incl, void *scan_tmp,
+                                      size_t scan_tmp_bytes_, hipStream_t stream) {
   const uint32_t n = s1 - s0;
   if (n <= 8192) {  // one block, one pass: a single launch for small batches
     hipLaunchKernelGGL(k_incr_scan, dim3(1), dim3(1024), 0, stream, w, s0, s1);
@@ -1655,7 +1984,33 @@ void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uin
     hipLaunchKernelGGL(k_add_base, dim3((n + 255) / 256), dim3(256), 0, stream, w, (const uint64_t *)incl, s0,
                        s1);
   }
-  hipLaunchKernelGGL(k_emit<kGroup>, dim3(group_blocks(n)), dim3(256), 0, stream, w, p, s0, s1);
+}
+
+// counts, offsets and boundaries of segments [s0, s1) assuming the clean case
+void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, uint64_t *incl,
+                             void *scan_tmp, size_t scan_tmp_bytes_, hipStream_t stream, int gs) {
+  if (s1 <= s0) return;
+  launch_counts_incremental(w, s0, s1, incl, scan_tmp, scan_tmp_bytes_, stream);
+  launch_emit(w, p, s0, s1, gs, stream);
+}
+
+// The whole call on the lane walk: spec of every segment (one lane each), the
+// group walk over the segments it handed back, the same for the links, then
+// the clean path's counts, offsets and boundaries (8-lane emit groups).  The
+// list kernels read their counts on the device (no host round trip): a fixed
+// grid that exits at once when nothing was handed back.
+void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void *scan_tmp, size_t scan_tmp_bytes_,
+                         hipStream_t stream) {
+  if (w.nsegs == 0) return;
+  const unsigned lg = lane_grid(w, 256, w.nsegs);
+  const unsigned listg = w.ncu ? w.ncu : 256;
+  hipLaunchKernelGGL(k_spec_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
+  hipLaunchKernelGGL(k_spec_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_spec,
+                     (const uint32_t *)(w.err + 4));
+  hipLaunchKernelGGL(k_link_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
+  hipLaunchKernelGGL(k_link_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_link,
+                     (const uint32_t *)(w.err + 5));
+  launch_emit_incremental(w, p, 0u, w.nsegs, incl, scan_tmp, scan_tmp_bytes_, stream, 8);
 }
 
 // General resolution after k_spec / k_link of every segment: serial fallback
@@ -1675,8 +2030,8 @@ void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, s
   bytes = scan_tmp_bytes_;
   // seg_count has nsegs + 1 entries (last = 0) so seg_off[nsegs] = total
   (void)hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, w.seg_count, w.seg_off, (int)w.nsegs + 1, stream);
-  hipLaunchKernelGGL(k_emit<kGroup>, dim3(group_blocks(w.nsegs)), dim3(256), 0, stream, w, p, 0u, w.nsegs);
-  hipLaunchKernelGGL(k_emit_long, dim3(1024), dim3(256), 0, stream, w, p);
+  launch_emit(w, p, 0u, w.nsegs, kGroup, stream);
+  hipLaunchKernelGGL(k_emit_long, dim3(2 * (w.ncu ? w.ncu : 256)), dim3(256), 0, stream, w, p);
 }
 
 }  // namespace mcdc

@@ -425,8 +425,10 @@ def test_scan_lane_pieces(knob_ctx, pieces, cold):
 
 
 def _segment_bytes(p):
-    """The library's segment size (mcdc_api.hip segment_bytes, default 16 chunks)."""
-    z = max(2 * p[2], 16 * (p[0] + p[1]))
+    """The library's segment size (mcdc_api.hip segment_bytes): ~4 expected
+    chunks on the lane walk (max <= 64 runs of 4 KiB), 16 on the group walk."""
+    k = 4 if p[2] <= 64 * 4096 else 16
+    z = max(2 * p[2], k * (p[0] + p[1]))
     return (z + 4095) // 4096 * 4096
 
 
@@ -448,6 +450,48 @@ def test_short_last_segment(ctx, p):
     r_, rc = O.chunk_files(O.Params(*p), files, threads=4)
     assert (gc == rc).all()
     _same(g, r_)
+
+
+@pytest.mark.parametrize("walk", [0, 2])
+def test_walk_variants(knob_ctx, walk):
+    """Both chain walks on the same inputs: the group walk (MCDC_LANE_WALK=0,
+    16 lanes per chain) where the library would take the lane walk, and the
+    lane walk forced (=2) where it would not (mapache's 512K/1M/8M): sizes,
+    adversarial patterns (overflowed runs hand segments back to the group
+    walk, forced stretches run into kContMax) and batches of ragged files."""
+    ctx = knob_ctx(MCDC_LANE_WALK=walk)
+    rng = np.random.default_rng(23)
+    for p in PARAMS:
+        for n in [0, 47, 4097, (1 << 20) + 3, 2 * p[2] + 1, 5 * p[2] + 77, (90 << 20) + 5]:
+            d = O.random_bytes(n, SEED + 3 * n + walk)
+            _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+            if n:
+                assert ctx.timing()["lane_walk"] == (1 if walk == 2 else 0)
+        pats = [np.zeros(6 << 20, np.uint8), np.tile(rng.integers(0, 256, 13, dtype=np.uint8), 300_000),
+                np.concatenate([O.random_bytes(3 << 20, 5), np.zeros(9 << 20, np.uint8), O.random_bytes(1 << 20, 6)])]
+        b = _find_dense_byte(p)
+        if b is not None:
+            pats.append(np.full(2 << 20, b, np.uint8))
+        for d in pats:
+            _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    files = [O.random_bytes(int(s), 900 + i) for i, s in enumerate(rng.integers(0, 3 << 20, 90))]
+    for p in PARAMS[:3]:
+        g, gc = ctx.chunk_batch(_lib.params(*p), files)
+        r, rc = O.chunk_files(O.Params(*p), files, threads=4)
+        assert (gc == rc).all()
+        _same(g, r)
+
+
+def test_lane_walk_is_the_default(ctx):
+    """At max <= 256 KiB a single-part call walks chains one lane per chain;
+    on random data no segment is handed back to the group walk."""
+    p = PARAMS[0]
+    d = O.random_bytes(64 << 20, SEED + 99)
+    _same(ctx.chunk_host(_lib.params(*p), d), O.chunk(O.Params(*p), d))
+    t = ctx.timing()
+    assert t["lane_walk"] == 1 and t["handed_back"] == 0, t
+    ctx.chunk_host(_lib.params(*PARAMS[1]), d)
+    assert ctx.timing()["lane_walk"] == 0
 
 
 def test_long_stretch_hashes_repeated(ctx):
