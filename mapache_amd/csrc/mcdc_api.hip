@@ -105,6 +105,9 @@ DevParams make_dev_params(const mcdc_params *p, uint64_t ms, uint64_t ml) {
 // a chain step's window spans at most 64 runs (max <= 256 KiB): its steps
 // read run summaries 16 runs per batch, so larger windows favour the group
 // walk.  Single-part calls only (the staged pipeline keeps the group walk).
+// Tiles of k_incr_lookback (4096 segments each), one status word per tile.
+size_t lb_tiles(uint32_t nsegs) { return (size_t)nsegs / 4096 + 1; }
+
 bool use_lane_walk(const mcdc_params *p, const Knobs &kn) {
   if (kn.parts != 1 || kn.lane_walk == 0) return false;
   return kn.lane_walk == 2 || p->max_size <= 64u * kRun;
@@ -225,11 +228,12 @@ struct mcdc_ctx {
              ev_h2d1 = nullptr;
   hipEvent_t ev_part[kMaxParts] = {};
   hipEvent_t ev_tab = nullptr;    // after the last async upload out of h_tab
+  hipEvent_t ev_prep = nullptr;   // after a call's table uploads and workspace resets on stream2
   bool tab_inflight = false;
   Knobs knobs;                    // read once at creation (read_knobs)
   uint64_t *d_gear = nullptr, *d_gear16 = nullptr;
   // workspace
-  DevBuf arena, run_cnt, run_sum, run_ent, punt, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
+  DevBuf arena, run_cnt, run_sum, run_ent, run_bits, punt, segs, files, nodes, node_off, node_cnt, seg_exit, cont, cont_cnt, cont_rep,
       cont_ent, long_list,
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
@@ -399,7 +403,11 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // (+ one 16-run batch: the lane walk loads summaries a batch past its window)
   if ((rc = ensure(ctx, ctx->run_sum, (nruns + 32) * 4))) return rc;
   if ((rc = ensure(ctx, ctx->run_ent, nruns * P.cap * sizeof(uint32_t)))) return rc;
-  if ((rc = ensure(ctx, ctx->tile_ctr, 64))) return rc;
+  // candidate-bitmap word pairs (+ read-ahead), then the scan's tile counter:
+  // the bitmap words of the partial last tile (set with atomics) and the
+  // counter are zeroed by one memset before the scan
+  const uint64_t nbitw = nruns / 64 + 4;
+  if ((rc = ensure(ctx, ctx->run_bits, nbitw * 16 + 64))) return rc;
   Work W{};
   W.base = base;
   W.n_al = n_al;
@@ -409,13 +417,18 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.run_cnt = (uint8_t *)ctx->run_cnt.p;
   W.run_sum = (uint32_t *)ctx->run_sum.p;
   W.run_ent = (uint32_t *)ctx->run_ent.p;
-  W.tile_ctr = kn.dyn_tiles ? (uint64_t *)ctx->tile_ctr.p : nullptr;
+  W.run_bits = (uint64_t *)ctx->run_bits.p;
+  W.tile_ctr = kn.dyn_tiles ? W.run_bits + 2 * nbitw : nullptr;
   W.first_static = kn.first_static ? 1u : 0u;
   hipStream_t st = ctx->stream;
   const bool early = kn.parts == 1;
+  // the bitmap words the partial last tile's runs share (set with atomics)
+  // through the tile counter
+  const uint64_t bw0 = nruns / 64 >= 2 ? nruns / 64 - 2 : 0;
+  const size_t zero_bytes = (nbitw - bw0) * 16 + 8;
   if (early) {
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
-    if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
+    HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
     const int pc = kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus);
     if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, (n_al / kRun) / (64 / pc), true, pc, kn.scan_cold);
     HIP_TRY(hipGetLastError());
@@ -526,9 +539,11 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.irr_flag = (uint8_t *)ctx->irr.p + 16 + (size_t)nsegs * 4;
   const bool lane = use_lane_walk(params, kn);
   if (lane) {
-    if ((rc = ensure(ctx, ctx->punt, (size_t)nsegs * 8 + 16))) return rc;
+    if ((rc = ensure(ctx, ctx->punt, (size_t)nsegs * 8 + 16 + lb_tiles(nsegs) * 8))) return rc;
     W.punt_spec = (uint32_t *)ctx->punt.p;
     W.punt_link = (uint32_t *)ctx->punt.p + nsegs;
+    // look-back status words after the lists (16-byte aligned: nsegs*8 + 16 bytes in)
+    W.lb_status = (uint64_t *)((char *)ctx->punt.p + (size_t)nsegs * 8 + 16);
   }
   W.ncu = (uint32_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
 
@@ -592,7 +607,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if (!early) {
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
     for (int i = 0; i < K; ++i) {
-      if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
+      if (i == 0) HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
+      else if (W.tile_ctr) HIP_TRY(hipMemsetAsync(W.tile_ctr, 0, 8, st));
       if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, tb[i], tb[i + 1], i == K - 1, 1, false);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
@@ -628,10 +644,24 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st2));
   HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
   HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, st2));
+  if (W.lb_status) HIP_TRY(hipMemsetAsync(W.lb_status, 0, lb_tiles(nsegs) * 8, st2));
   const bool lane_all = lane && K == 1;
-  if (lane_all) {  // the lane walk over every segment
-    HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[0], 0));
-    launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
+  // The lane walk runs on the scan's own stream: it follows the scan at a
+  // same-queue kernel boundary (~2 us) instead of a cross-queue event (~13 us
+  // measured); the resets and uploads on stream2 finished during the scan.
+  hipStream_t rs = lane_all ? st : st2;
+  static const int dbg = std::getenv("MCDC_DBG_LANE") ? std::atoi(std::getenv("MCDC_DBG_LANE")) : 0;  // TEMP
+  hipEvent_t dbg_ev[8] = {};
+  if (lane_all) {
+    if (dbg & 2) { for (auto &e : dbg_ev) (void)hipEventCreate(&e); (void)hipEventRecord(dbg_ev[7], st2); }
+    HIP_TRY(hipEventRecord(ctx->ev_prep, st2));
+    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prep, 0));
+    if (dbg & 1) HIP_TRY(hipStreamSynchronize(st));
+    if (dbg & 2) {
+      (void)hipEventRecord(dbg_ev[0], st);
+      W.dbg_ev = dbg_ev;
+    }
+    launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st);
     HIP_TRY(hipGetLastError());
   }
   for (int i = 0; i < (lane_all ? 0 : K); ++i) {
@@ -643,27 +673,27 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(ctx->ev_end, st2));
-  if (want_counts) launch_file_counts(W, ctx->d_fcnt, st2);
-  launch_finish(W, ctx->d_res, st2);
+  HIP_TRY(hipEventRecord(ctx->ev_end, rs));
+  if (want_counts) launch_file_counts(W, ctx->d_fcnt, rs);
+  launch_finish(W, ctx->d_res, rs);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(st2));
+  HIP_TRY(hipStreamSynchronize(rs));
   if (((volatile uint64_t *)ctx->h_res)[3]) {
     // some continuation did not merge into the next segment: resolve the whole
     // call with the general path (serial fallback / serial walk), which
     // rewrites every count, offset and boundary of the incremental pass
-    HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 4, st2));  // incremental capacity bits are void
-    launch_resolve_general(W, P, ctx->scan_tmp.p, tmpb, st2);
+    HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 4, rs));  // incremental capacity bits are void
+    launch_resolve_general(W, P, ctx->scan_tmp.p, tmpb, rs);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev_end, st2));
-    if (want_counts) launch_file_counts(W, ctx->d_fcnt, st2);
-    launch_finish(W, ctx->d_res, st2);
+    HIP_TRY(hipEventRecord(ctx->ev_end, rs));
+    if (want_counts) launch_file_counts(W, ctx->d_fcnt, rs);
+    launch_finish(W, ctx->d_res, rs);
     HIP_TRY(hipGetLastError());
   }
 
   // ---- results: one synchronisation in the common case ----
   const double t_d2h0 = now_ms();
-  HIP_TRY(hipStreamSynchronize(st2));
+  HIP_TRY(hipStreamSynchronize(rs));
   const uint64_t total = ((volatile uint64_t *)ctx->h_res)[0];
   const uint32_t err = (uint32_t)((volatile uint64_t *)ctx->h_res)[1];
   const uint64_t nfallback = ((volatile uint64_t *)ctx->h_res)[2];
@@ -673,10 +703,10 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if (err) return fail(MCDC_E_INTERNAL, "device consistency error 0x%x", err);
   bool copies = false;
   if (total && !out_dev) {
-    HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, st2));
+    HIP_TRY(hipMemcpyAsync(out, ctx->out.p, total * sizeof(mcdc_chunk), hipMemcpyDeviceToHost, rs));
     copies = true;
   }
-  if (copies) HIP_TRY(hipStreamSynchronize(st2));
+  if (copies) HIP_TRY(hipStreamSynchronize(rs));
   const double t_d2h1 = now_ms();
   static_assert(sizeof(size_t) == sizeof(uint64_t), "counts are 64-bit");
   if (want_counts) std::memcpy(counts, ctx->h_fcnt, nfiles * sizeof(uint64_t));
@@ -693,6 +723,29 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->timing.fallback_files = nfallback;
   ctx->timing.lane_walk = lane_all ? 1 : 0;
   ctx->timing.handed_back = lane_all ? ((volatile uint64_t *)ctx->h_res)[4] : 0;
+  if (dbg_ev[0]) {  // TEMP
+    float ms[6] = {};
+    for (int i = 0; i < 6; ++i) (void)hipEventElapsedTime(&ms[i], dbg_ev[i], dbg_ev[i + 1]);
+    float a = 0, b = 0, c2 = 0;
+    (void)hipEventElapsedTime(&a, ctx->ev_start, ctx->ev_scan);
+    (void)hipEventElapsedTime(&b, ctx->ev_start, dbg_ev[7]);
+    (void)hipEventElapsedTime(&c2, ctx->ev_start, dbg_ev[0]);
+    {
+      std::vector<uint32_t> ls(nsegs);
+      (void)hipMemcpy(ls.data(), ctx->link_seg.p, nsegs * 4, hipMemcpyDeviceToHost);
+      uint32_t irr = 0, none = 0, maxjump = 0;
+      for (uint32_t i = 0; i < nsegs; ++i) {
+        if (ctx->h_segs[i].flags & kSegLast) continue;
+        if (ls[i] == kSegNone) ++none;
+        else if (ls[i] != i + 1) { ++irr; maxjump = std::max(maxjump, ls[i] - i); }
+      }
+      fprintf(stderr, "DBG links: nsegs %u irregular %u none %u maxjump %u dirty %llu\n", nsegs, irr, none, maxjump,
+              (unsigned long long)((volatile uint64_t *)ctx->h_res)[3]);
+    }
+    fprintf(stderr, "DBG t: scan_end %.3f st2_resets_done %.3f lane_start %.3f\n", a, b, c2);
+    fprintf(stderr, "DBG lane: spec %.3f list %.3f link %.3f list %.3f counts %.3f emit %.3f\n", ms[0], ms[1], ms[2], ms[3], ms[4], ms[5]);
+    for (auto &e : dbg_ev) (void)hipEventDestroy(e);
+  }
   return MCDC_OK;
 }
 
@@ -872,6 +925,7 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
       return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&ctx->ev_tab, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_prep, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&ctx->ev_copy0) != hipSuccess)
     return bail(fail(MCDC_E_DEVICE, "hipEventCreate failed"));
   ctx->knobs = read_knobs();
@@ -897,7 +951,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
-  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
+  DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
                     &ctx->link_seg, &ctx->link_idx, &ctx->link_pos, &ctx->file_flags,
@@ -920,6 +974,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   for (hipEvent_t e : ctx->ev_part)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_tab) (void)hipEventDestroy(ctx->ev_tab);
+  if (ctx->ev_prep) (void)hipEventDestroy(ctx->ev_prep);
   if (ctx->ev_copy0) (void)hipEventDestroy(ctx->ev_copy0);
   ctx->pool.reset();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -100,6 +100,8 @@ struct Work {
   uint8_t *run_cnt;      // [nruns]
   uint32_t *run_sum;     // [nruns] run summary: first S / first L candidate (see run_summary)
   uint32_t *run_ent;     // [nruns * cap]: off | S<<31 | L<<30
+  uint64_t *run_bits;    // [2 * (nruns / 64 + 2)]: word pair w = runs [64w, 64w + 64): [2w] bit i = run
+                         // 64w + i has an S candidate, [2w + 1] an L candidate (the lane walk's index)
   uint64_t *tile_ctr;    // scan tile counter (dynamic tile order) or nullptr (static)
   uint32_t first_static; // dynamic order: each wave's first tile is its static one, the counter hands out the rest
 
@@ -135,6 +137,8 @@ struct Work {
   uint32_t *punt_spec;   // lane walk: segments handed to the group walk (k_spec_list), count err[4]
   uint32_t *punt_link;   // (k_link_list), count err[5]
   uint32_t ncu;          // compute units (persistent grids)
+  hipEvent_t *dbg_ev = nullptr;  // TEMP
+  uint64_t *lb_status;   // k_incr_lookback tile status words (lane walk: zeroed per call), ticket err[6]
 };
 
 // Tuning switches of a context, read from the environment once, when the

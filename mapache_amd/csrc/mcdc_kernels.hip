@@ -317,6 +317,11 @@ __device__ void scan_run_coop(const uint64_t *tab, uint32_t lo, const Work &W, c
   if (lane == 0) {
     W.run_cnt[run] = total > P.cap ? kRunOverflow : (uint8_t)total;
     W.run_sum[run] = run_summary(total, mfs, mfl);
+    // candidate bitmaps (their words were zeroed before the scan: tail runs
+    // share words with each other and with the last full tile)
+    uint32_t *b32 = reinterpret_cast<uint32_t *>(W.run_bits) + 4 * (run >> 6) + ((run >> 5) & 1);
+    if (mfs != 0xffffffffu) atomicOr(b32, 1u << (run & 31));
+    if (mfl != 0xffffffffu) atomicOr(b32 + 2, 1u << (run & 31));
   }
 }
 
@@ -477,6 +482,27 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
   }
 }
 
+// A tile's RPT (16, 32 or 64; run0 a multiple of it) runs into the candidate
+// bitmaps: bits [run0 % 64, + RPT) of word pair run0 / 64, by one vector store
+// per plane of the matching width.
+template <int RPT>
+__device__ __forceinline__ void store_run_bits(uint64_t *bits, uint64_t run0, uint64_t bs, uint64_t bl) {
+  const uint64_t w = run0 >> 6;
+  if constexpr (RPT == 64) {
+    bits[2 * w] = bs;
+    bits[2 * w + 1] = bl;
+  } else if constexpr (RPT == 32) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(bits) + 4 * w + ((run0 >> 5) & 1);
+    p[0] = (uint32_t)bs;
+    p[2] = (uint32_t)bl;
+  } else {
+    static_assert(RPT == 16, "16, 32 or 64 runs per tile");
+    uint16_t *p = reinterpret_cast<uint16_t *>(bits) + 8 * w + ((run0 >> 4) & 3);
+    p[0] = (uint16_t)bs;
+    p[4] = (uint16_t)bl;
+  }
+}
+
 // CW (cold warm-up): a piece starts from h = 0 instead of re-reading the 48
 // bytes before it; its first 48 bytes stay in registers and are re-walked at
 // the end of the tile from the previous lane's final hash (the state after
@@ -613,10 +639,15 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     q.lcnt[lane] = 0;
     q.lcnt[64 + lane] = 0xffffffffu;
     q.lcnt[128 + lane] = 0xffffffffu;
-    if (PC == 1 || lane < RPT) {
+    const bool mine = PC == 1 || lane < RPT;
+    if (mine) {
       const uint64_t run = run0 + lane;
       W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
       W.run_sum[run] = run_summary(cnt, fs, fl);
+    }
+    {  // the tile's runs in the candidate bitmaps: RPT bits per plane, one store each
+      const uint64_t bs = __ballot(mine && fs != 0xffffffffu), bl = __ballot(mine && fl != 0xffffffffu);
+      if (lane == 0) store_run_bits<RPT>(W.run_bits, run0, bs, bl);
     }
     t = t_next;
   }
@@ -1079,6 +1110,7 @@ template <int GS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_spec_list(
     Work W, DevParams P, const uint32_t *list, const uint32_t *count) {
   MCDC_VGPR_PAD(80);
+  if (*count == 0) return;  // (the common case: nothing handed back)
   __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
@@ -1169,6 +1201,7 @@ __global__ __launch_bounds__(256) void k_link(Work W, DevParams P, uint32_t s0, 
 // The segments whose continuation the lane walk handed back (list, *count).
 template <int GS>
 __global__ __launch_bounds__(256) void k_link_list(Work W, DevParams P, const uint32_t *list, const uint32_t *count) {
+  if (*count == 0) return;  // (the common case: nothing handed back)
   __builtin_amdgcn_s_setprio(3);
   __shared__ uint64_t gt[256];
   load_gear_lds(gt, W);
@@ -1196,8 +1229,6 @@ __global__ __launch_bounds__(256) void k_link_list(Work W, DevParams P, const ui
 // A step the lane walk does not take -- a run whose entry list overflowed, a
 // continuation of kContMax steps -- hands the whole segment to the group walk
 // (k_spec_list / k_link_list), which recomputes it from scratch.
-constexpr uint32_t kLaneBatch = 16;  // runs per summary batch past the first window
-constexpr uint32_t kLaneWin = 64;    // runs loaded at the start of a step (a 256 KiB max's whole window)
 
 __device__ __forceinline__ void load_gear_rep(uint64_t *tab, const Work &W) {
   for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) tab[i] = W.gear[i >> 5];
@@ -1213,11 +1244,30 @@ __device__ __forceinline__ uint32_t sel32(uint32_t a, uint32_t b, uint32_t sel) 
 // GEAR[byte k of w] from the replicated table (copy lo8 / 8)
 #define MCDC_GR(w, k, lo8) lds_gear(tab, __builtin_amdgcn_perm((w), (lo8), 0x0c0c0000u | ((4u + (k)) << 8)))
 
+// The recurrence h = (h << 1) + GEAR[byte i] over N realigned bytes (byte i =
+// byte i % 4 of e[i / 4]): step(i, GEAR[byte i]) in order, the LDS lookups
+// issued 8 positions ahead of the chain.  Left to itself the compiler issued
+// four lookups and waited for them before the next four: 12-16 exposed LDS
+// latencies per call; the scheduling barriers keep the issue order.
+template <int N, class Step>
+__device__ __forceinline__ void gear_chain(const uint64_t *tab, uint32_t lo8, const uint32_t *e, Step &&step) {
+  constexpr int D = 8;
+  uint64_t g[N];
+#pragma unroll
+  for (int i = 0; i < D && i < N; ++i) g[i] = MCDC_GR(e[i >> 2], i & 3, lo8);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i + D < N) g[i + D] = MCDC_GR(e[(i + D) >> 2], (i + D) & 3, lo8);
+    __builtin_amdgcn_sched_barrier(0);
+    step(i, g[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // First candidate of run r in [lo_r, hi_r) (chunk-relative) from its entry
 // list, for a run a window edge splits; punt when the list overflowed.
-__device__ __forceinline__ int32_t lane_run_split(const Work &W, const DevParams &P, uint64_t r, int32_t rbase,
-                                                  int32_t lo_r, int32_t hi_r, int32_t cce_r, bool &punt) {
-  const uint32_t cnt = W.run_cnt[r];
+__device__ __forceinline__ int32_t lane_run_split(const Work &W, const DevParams &P, uint64_t r, uint32_t cnt,
+                                                  int32_t rbase, int32_t lo_r, int32_t hi_r, int32_t cce_r, bool &punt) {
   if (cnt > P.cap) { punt = true; return INT32_MAX; }
   if (P.cap == 8) {
     const uint4 ea = *reinterpret_cast<const uint4 *>(W.run_ent + r * 8ull);
@@ -1234,8 +1284,40 @@ __device__ __forceinline__ int32_t lane_run_split(const Work &W, const DevParams
   return best;
 }
 
+__device__ __forceinline__ uint64_t bits_upto(uint32_t i) { return i == 63 ? ~0ull : ((2ull << i) - 1); }
+
+// First run in [a, b] whose bit is set in plane pl (0: S, 1: L) of the
+// candidate bitmaps, ~0 if none; v0 / v1 = the plane's words a/64 and a/64+1,
+// already loaded.  Windows of more than two words (max > 252 KiB) load the
+// rest here.
+__device__ __forceinline__ uint64_t first_bit_run(const uint64_t *bits, int pl, uint64_t a, uint64_t b, uint64_t v0,
+                                                  uint64_t v1) {
+  if (a > b) return ~0ull;
+  const uint64_t wa = a >> 6, wb = b >> 6;
+  uint64_t m = v0 & (~0ull << (a & 63));
+  if (wa == wb) m &= bits_upto((uint32_t)(b & 63));
+  if (m) return (wa << 6) + (uint64_t)__builtin_ctzll(m);
+  for (uint64_t w = wa + 1; w <= wb; ++w) {
+    uint64_t mm = w == wa + 1 ? v1 : bits[2 * w + pl];
+    if (w == wb) mm &= bits_upto((uint32_t)(b & 63));
+    if (mm) return (w << 6) + (uint64_t)__builtin_ctzll(mm);
+  }
+  return ~0ull;
+}
+
 // next(c) by one lane: group_next's semantics (the crate's cut_gear from c,
 // file end fend).  Sets punt (result void) for a step it does not take.
+// Two dependent memory levels per step:
+//  1. the restart window's 64 bytes; the summaries of the runs holding the S
+//     and the L window's first position (rS0, rL0); the S / L bitmap words
+//     after them;
+//  2. the summaries of the first run after rS0 with an S candidate and after
+//     rL0 with an L candidate (bitmap search), and, when a window edge splits
+//     rS0 or rL0 (first candidate before the edge, more in the run), its entry
+//     list.
+// The first qualifying S is the answer if there is one, else the first L:
+// every source below yields a qualifying candidate or nothing, and the first
+// qualifying one comes from one of them, so the minimum is exact.
 __device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P, const uint64_t *tab, uint32_t lo8,
                                               uint64_t c, uint64_t fend, bool &punt) {
   const uint64_t rem = fend - c;
@@ -1249,26 +1331,59 @@ __device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P,
   const int32_t lo_r = (int32_t)(t0 + kWin - 1), hi_r = (int32_t)re, cce_r = (int32_t)ce;
   const bool cand = lo_r < hi_r;
   const int32_t s_end = min(cce_r, hi_r), l_beg = max(lo_r, cce_r);
-  // ---- loads first: restart-window bytes, batch 0 of the run summaries, the
-  // summaries of the two runs a window edge can split
+  const bool hasS = cand && lo_r < s_end, hasL = cand && l_beg < hi_r;
+  // ---- level 1 (addresses clamped into the arrays: no branches around loads)
   const uint64_t A = t & ~15ull;
   uint32_t dw[16];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint4 v = A + 16 * k < W.n_al ? *reinterpret_cast<const uint4 *>(W.base + A + 16 * k) : make_uint4(0, 0, 0, 0);
+    const uint64_t ad = min(A + 16 * k, W.n_al - 16);  // (bytes past the arena are never used)
+    const uint4 v = *reinterpret_cast<const uint4 *>(W.base + ad);
     dw[4 * k] = v.x; dw[4 * k + 1] = v.y; dw[4 * k + 2] = v.z; dw[4 * k + 3] = v.w;
   }
-  const uint64_t r0 = cand ? (c + (uint64_t)lo_r) / kRun : 0, r1 = cand ? (c + (uint64_t)hi_r - 1) / kRun : 0;
-  const uint64_t rl = cand ? (c + (uint64_t)l_beg) / kRun : 0;
-  const uint64_t ra = r0 & ~3ull;  // batches start 16-byte aligned in run_sum
-  // the first kLaneWin runs (the whole window at max <= 256 KiB) in one go:
-  // one memory latency per step instead of one per batch
-  uint4 win[kLaneWin / 4];
-#pragma unroll
-  for (int k = 0; k < (int)kLaneWin / 4; ++k)
-    win[k] = (cand && ra + 4 * k <= r1) ? *reinterpret_cast<const uint4 *>(W.run_sum + ra + 4 * k)
-                                        : make_uint4(0, 0, 0, 0);
-  const uint32_t u_lo = cand ? W.run_sum[r0] : 0u, u_lb = (cand && l_beg < hi_r) ? W.run_sum[rl] : 0u;
+  const uint64_t rlast = W.nruns - 1;
+  const uint64_t rS0 = min((c + (uint64_t)lo_r) / kRun, rlast);
+  const uint64_t rL0 = min((c + (uint64_t)l_beg) / kRun, rlast);
+  const uint64_t rS1 = hasS ? (c + (uint64_t)s_end - 1) / kRun : 0, rL1 = hasL ? (c + (uint64_t)hi_r - 1) / kRun : 0;
+  const uint32_t uS0 = W.run_sum[rS0], uL0 = W.run_sum[rL0];
+  const uint32_t cS0 = W.run_cnt[rS0], cL0 = W.run_cnt[rL0];
+  const uint64_t wS = (rS0 + 1) >> 6, wL = (rL0 + 1) >> 6;  // (+ read-ahead words are allocated)
+  const uint4 bS0 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wS);
+  const uint4 bS1 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wS + 2);
+  const uint4 bL0 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wL);
+  const uint4 bL1 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wL + 2);
+
+  // ---- (2) windowed candidates: S in [lo, s_end), L in [l_beg, hi) (chunk-relative).
+  // Decided before the restart window's hash so that the level-2 loads are in
+  // flight while it runs; the restart window's hit, if any, takes precedence.
+  auto rel = [&](uint64_t r) { return (int32_t)((int64_t)(r * (uint64_t)kRun) - (int64_t)c); };
+  int32_t best = INT32_MAX;
+  // the runs holding each window's first position: their summaries decide,
+  // unless the first candidate of the kind lies before the edge and more follow
+  bool splitS = false, splitL = false;
+  if (hasS) {
+    const uint32_t fs1 = uS0 & 0x3fffu;
+    const int32_t p = rel(rS0) + (int32_t)fs1 - 1;
+    if (fs1 && p >= lo_r && p < s_end) best = p;
+    else splitS = fs1 && p < lo_r && (uS0 >> 28) >= 2;
+  }
+  if (hasL) {
+    const uint32_t fl1 = (uL0 >> 14) & 0x3fffu;
+    const int32_t p = rel(rL0) + (int32_t)fl1 - 1;
+    if (fl1 && p >= l_beg && p < hi_r) best = min(best, p);
+    else splitL = fl1 && p < l_beg && (uL0 >> 28) >= 2;
+  }
+  // the first later run with a candidate of the kind (bitmap search)
+  const uint64_t rS = hasS ? first_bit_run(W.run_bits, 0, rS0 + 1, rS1, ((uint64_t)bS0.y << 32) | bS0.x,
+                                           ((uint64_t)bS1.y << 32) | bS1.x)
+                           : ~0ull;
+  const uint64_t rL = hasL ? first_bit_run(W.run_bits, 1, rL0 + 1, rL1, ((uint64_t)bL0.w << 32) | bL0.z,
+                                           ((uint64_t)bL1.w << 32) | bL1.z)
+                           : ~0ull;
+  // ---- level 2
+  const uint32_t uS = W.run_sum[min(rS, rlast)], uL = W.run_sum[min(rL, rlast)];
+  if (__builtin_expect(splitS, 0)) best = min(best, lane_run_split(W, P, rS0, cS0, rel(rS0), lo_r, hi_r, cce_r, punt));
+  if (__builtin_expect(splitL, 0)) best = min(best, lane_run_split(W, P, rL0, cL0, rel(rL0), lo_r, hi_r, cce_r, punt));
 
   // ---- (1) exact restarted hash of the first <= 47 tested positions
   {
@@ -1284,79 +1399,31 @@ __device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P,
     const uint32_t mlo = (uint32_t)P.ms, mhi = (uint32_t)(P.ms >> 32);
     uint64_t h = 0;
     uint32_t acc = 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < kWin - 1; ++i) {
-      h = (h << 1) + MCDC_GR(e[i >> 2], i & 3, lo8);
+    gear_chain<kWin - 1>(tab, lo8, e, [&](int, uint64_t gv) {
+      h = (h << 1) + gv;
       acc = min(acc, ((uint32_t)h & mlo) | ((uint32_t)(h >> 32) & mhi));
-    }
+    });
     // every position tests mask_s when the window is whole and before ce
     const bool regular = wlen == (uint32_t)(kWin - 1) && ce >= t0 + (uint32_t)(kWin - 1);
     if (__builtin_expect(!regular || acc == 0, 0)) {  // exact: per-position mask, first hit
       uint32_t first = 0xffffffffu;
       h = 0;
-#pragma unroll
-      for (int i = 0; i < kWin - 1; ++i) {
-        h = (h << 1) + MCDC_GR(e[i >> 2], i & 3, lo8);
+      gear_chain<kWin - 1>(tab, lo8, e, [&](int i, uint64_t gv) {
+        h = (h << 1) + gv;
         const uint64_t m = (t0 + (uint32_t)i < ce) ? P.ms : P.ml;
         if ((uint32_t)i < wlen && (h & m) == 0 && first == 0xffffffffu) first = (uint32_t)i;
-      }
+      });
       if (first != 0xffffffffu) return t + first;
     }
   }
   if (!cand) return c + remaining;
-
-  // ---- (2) windowed candidates for [t + 47, c + re)
-  int32_t best = INT32_MAX;
-  {  // a run a window edge splits: the summary's first S (L) lies before the edge and more follow
-    const uint32_t nc0 = u_lo >> 28, fs0 = u_lo & 0x3fffu;
-    const int32_t rb0 = (int32_t)((int64_t)(r0 * (uint64_t)kRun) - (int64_t)c);
-    if (fs0 && rb0 + (int32_t)fs0 - 1 < lo_r && nc0 >= 2 && lo_r < s_end)
-      best = min(best, lane_run_split(W, P, r0, rb0, lo_r, hi_r, cce_r, punt));
-    const uint32_t ncl = u_lb >> 28, fll = (u_lb >> 14) & 0x3fffu;
-    const int32_t rbl = (int32_t)((int64_t)(rl * (uint64_t)kRun) - (int64_t)c);
-    if (fll && rbl + (int32_t)fll - 1 < l_beg && ncl >= 2 && l_beg < hi_r)
-      best = min(best, lane_run_split(W, P, rl, rbl, lo_r, hi_r, cce_r, punt));
+  if (rS != ~0ull) {  // its first S lies past lo (later run); it qualifies before s_end
+    const int32_t p = rel(rS) + (int32_t)(uS & 0x3fffu) - 1;
+    if (p < s_end) best = min(best, p);
   }
-  // Every other run is decided by its summary: its first S qualifies iff it
-  // lies in [lo, s_end), its first L iff in [l_beg, hi).  Runs before r0 or
-  // after r1 fail both tests by position, so batches need no masking.
-  const uint32_t lenS = s_end > lo_r ? (uint32_t)(s_end - lo_r) : 0u;
-  const uint32_t lenL = hi_r > l_beg ? (uint32_t)(hi_r - l_beg) : 0u;
-  const int32_t wstart = (int32_t)((int64_t)(ra * (uint64_t)kRun) - (int64_t)c);
-  auto eval_run = [&](uint32_t u, int32_t rbk) {
-    const uint32_t fs1 = u & 0x3fffu, fl1 = (u >> 14) & 0x3fffu;
-    const int32_t pS = rbk + (int32_t)fs1 - 1, pL = rbk + (int32_t)fl1 - 1;
-    const bool okS = fs1 != 0 && (uint32_t)(pS - lo_r) < lenS;
-    const bool okL = fl1 != 0 && (uint32_t)(pL - l_beg) < lenL;
-    best = min(best, min(okS ? pS : INT32_MAX, okL ? pL : INT32_MAX));
-  };
-  // the preloaded window, 16 runs at a time; stop once no lane of the wave
-  // can still find an earlier candidate
-#pragma unroll
-  for (int b = 0; b < (int)kLaneWin / 16; ++b) {
-    const int32_t bstart = wstart + b * 16 * kRun;
-    if (!__any(bstart < best && ra + 16 * b <= r1)) break;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 v = win[4 * b + k];
-      eval_run(v.x, bstart + (4 * k) * kRun);
-      eval_run(v.y, bstart + (4 * k + 1) * kRun);
-      eval_run(v.z, bstart + (4 * k + 2) * kRun);
-      eval_run(v.w, bstart + (4 * k + 3) * kRun);
-    }
-  }
-  // windows past kLaneWin runs (max > 256 KiB): batches of 16, loaded as needed
-  for (uint64_t rb = ra + kLaneWin; rb <= r1; rb += kLaneBatch) {
-    const int32_t bstart = wstart + (int32_t)((rb - ra) * kRun);
-    if (bstart >= best) break;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(W.run_sum + rb + 4 * k);
-      eval_run(v.x, bstart + (4 * k) * kRun);
-      eval_run(v.y, bstart + (4 * k + 1) * kRun);
-      eval_run(v.z, bstart + (4 * k + 2) * kRun);
-      eval_run(v.w, bstart + (4 * k + 3) * kRun);
-    }
+  if (rL != ~0ull) {
+    const int32_t p = rel(rL) + (int32_t)((uL >> 14) & 0x3fffu) - 1;
+    if (p < hi_r) best = min(best, p);
   }
   return best != INT32_MAX ? c + (uint64_t)best : c + remaining;  // else forced cut
 }
@@ -1627,16 +1694,10 @@ __device__ __forceinline__ uint64_t chunk_hash(const Work &W, const uint64_t *ta
   for (int j = 0; j < 16; ++j) e[j] = __builtin_amdgcn_alignbyte(g[j + 1], g[j], off & 3);
   const uint32_t nex = (uint32_t)(cq.from - s0);  // leading positions outside the window
   uint64_t h = 0;
-  if (__builtin_expect(__any(nex != 0), 0)) {
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      const uint64_t gv = MCDC_GR(e[i >> 2], i & 3, lo8);
-      h = (h << 1) + ((uint32_t)i < nex ? 0ull : gv);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 64; ++i) h = (h << 1) + MCDC_GR(e[i >> 2], i & 3, lo8);
-  }
+  if (__builtin_expect(__any(nex != 0), 0))
+    gear_chain<64>(tab, lo8, e, [&](int i, uint64_t gv) { h = (h << 1) + ((uint32_t)i < nex ? 0ull : gv); });
+  else
+    gear_chain<64>(tab, lo8, e, [&](int, uint64_t gv) { h = (h << 1) + gv; });
   return cq.dbl ? h << 1 : h;
 }
 
@@ -1782,51 +1843,88 @@ void launch_file_counts(const Work &w, uint64_t *dst, hipStream_t stream) {
 // and the per-segment counts / offsets / boundaries follow locally.  A segment
 // whose continuation did anything else sets err[2] ("dirty"); the host then
 // re-resolves the whole call with the general path (fallback, serial walk).
-// Clean-path link rule: segment s continues into s + 1, or its continuation
-// ran to the end of the file (kSegNone) and s + 1 is the file's last segment,
-// which is then off the true chain (count 0).  The second case is local
-// (nothing after s + 1 depends on it); a continuation to the file end that
-// skips more segments is left to the general path.
-__device__ __forceinline__ bool incr_link_ok(const Work &W, uint32_t s, uint32_t fl) {
-  if (fl & kSegLast) return true;
-  const uint32_t l = W.link_seg[s];
-  return l == s + 1 || (l == kSegNone && (W.segs[s + 1].flags & kSegLast));
+// Clean-path link rule: segment s continues into s + 1; or it skips exactly
+// one segment (link_seg[s] == s + 2: its continuation crossed s + 1 without
+// meeting s + 1's speculative chain, which is then off the true chain); or
+// its continuation ran to the end of the file (kSegNone) and s + 1 is the
+// file's last segment, which is then off the chain.  Anything else (a longer
+// skip, a continuation that gave up) is left to the general path.
+//
+// With one-segment skips a segment's state is local: s is off the chain iff
+// s - 1 is on it and skips s, so on(s) is the parity of the run of
+// consecutive skips that ends at s - 1 (a link never leaves its file, so the
+// run stops at the file's first segment).  The on-chain predecessor of an
+// on-chain s is s - 1, or s - 2 when s - 1 is off (s - 2 skipped it into s).
+// (Segments of ~4 expected chunks on the lane walk: ~165 of the 131 072
+// links of the 64 GiB stream skip one segment, and every call would go to
+// the general path.)
+__device__ __forceinline__ bool seg_skips(const Work &W, uint32_t k) { return W.link_seg[k] == k + 2; }
+
+// Clean-path state of segment s (incr_count_one computes it, incr_store
+// writes it): the loads of a thread's segments are all issued before any of
+// its stores (a store to a Work array may alias a later load for the
+// compiler, which then serialised eight segments' dependent loads: 48 us for
+// 8192 segments in one block).
+struct IncrSeg {
+  uint64_t count;
+  uint32_t entry;
+  bool on, bad;
+};
+
+__device__ __forceinline__ IncrSeg incr_count_one(const Work &W, uint32_t s) {
+  const uint32_t fl = W.segs[s].flags;
+  const bool first = fl & kSegFirst, last = fl & kSegLast;
+  // everything a segment normally needs, in one round of loads
+  const uint32_t nc = W.node_cnt[s], cc = W.cont_cnt[s];
+  const uint32_t lp = first ? 0u : W.link_seg[s - 1], lidx1 = first ? 0u : W.link_idx[s - 1];
+  const uint32_t l = last ? 0u : W.link_seg[s], nfl = last ? 0u : W.segs[s + 1].flags;
+  const uint32_t lpp = (first || s < 2) ? kSegNone : W.link_seg[s - 2];
+  bool on = true, bad = false;
+  uint32_t entry = 0;
+  if (!first) {
+    // on(s - 1): parity of the consecutive one-segment skips ending at s - 2
+    bool prev_on = true;
+    if (lpp == s) {  // s - 2 skips s - 1 (rare): walk the run back
+      prev_on = false;
+      for (uint32_t k = s - 2; k > 0 && seg_skips(W, k - 1); --k) prev_on = !prev_on;
+    }
+    if (prev_on) {
+      if (lp == s) entry = lidx1;
+      else if (lp == s + 1) on = false;                       // s - 1 skips s
+      else if (lp == kSegNone && last) on = false;            // continuation ran to the file end
+      else bad = true;
+    } else {  // s - 1 is off the chain: s - 2 skipped it into s
+      entry = W.link_idx[s - 2];
+    }
+  }
+  if (on && !last)  // s's own link must keep the next segments local
+    bad |= !(l == s + 1 || l == s + 2 || (l == kSegNone && (nfl & kSegLast)));
+  bad |= on && entry > nc;
+  IncrSeg r;
+  r.count = (bad || !on) ? 0 : (uint64_t)(nc - entry) + cc;
+  r.entry = entry;
+  r.on = on;
+  r.bad = bad;
+  return r;
 }
-__device__ __forceinline__ bool incr_off_chain(const Work &W, uint32_t s, uint32_t fl) {
-  return (fl & kSegLast) && !(fl & kSegFirst) && W.link_seg[s - 1] == kSegNone;
+
+__device__ __forceinline__ void incr_store(const Work &W, uint32_t s, const IncrSeg &r) {
+  W.seg_true[s] = r.on ? 1 : 0;
+  W.entry_idx[s] = r.entry;
+  W.seg_count[s] = r.count;
 }
 
 __global__ void k_incr_count(Work W, uint32_t s0, uint32_t s1) {
   const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= s1) return;
-  const uint32_t fl = W.segs[s].flags;
-  const uint32_t entry = (fl & kSegFirst) ? 0u : W.link_idx[s - 1];
-  const uint32_t nc = W.node_cnt[s];
-  const bool off = incr_off_chain(W, s, fl);
-  const bool bad = !incr_link_ok(W, s, fl) || (!off && entry > nc);
-  W.seg_true[s] = off ? 0 : 1;
-  W.entry_idx[s] = entry;
-  W.seg_count[s] = (bad || off) ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
-  if (bad) atomicOr(W.err + 2, 1u);
+  const IncrSeg r = incr_count_one(W, s);
+  incr_store(W, s, r);
+  if (r.bad) atomicOr(W.err + 2, 1u);
 }
 
-// Same, fused with the offsets for one block: counts of [s0, s1) and
+// Counts of [s0, s1) fused with the offsets for one block:
 // seg_off[s + 1] = seg_off[s0] + inclusive prefix, 1024 threads x 8 segments
 // per pass (one launch instead of count + device scan + add-base).
-__device__ __forceinline__ uint64_t incr_count_one(const Work &W, uint32_t s, uint32_t &dirty) {
-  const uint32_t fl = W.segs[s].flags;
-  const uint32_t entry = (fl & kSegFirst) ? 0u : W.link_idx[s - 1];
-  const uint32_t nc = W.node_cnt[s];
-  const bool off = incr_off_chain(W, s, fl);
-  const bool bad = !incr_link_ok(W, s, fl) || (!off && entry > nc);
-  const uint64_t c = (bad || off) ? 0 : (uint64_t)(nc - entry) + W.cont_cnt[s];
-  W.seg_true[s] = off ? 0 : 1;
-  W.entry_idx[s] = entry;
-  W.seg_count[s] = c;
-  dirty |= bad ? 1u : 0u;
-  return c;
-}
-
 __global__ __launch_bounds__(1024) void k_incr_scan(Work W, uint32_t s0, uint32_t s1) {
   __builtin_amdgcn_s_setprio(3);
   constexpr int IT = 8;
@@ -1836,10 +1934,19 @@ __global__ __launch_bounds__(1024) void k_incr_scan(Work W, uint32_t s0, uint32_
   uint32_t dirty = 0;
   for (uint64_t base = s0; base < s1; base += 1024 * IT) {
     uint64_t c[IT], tsum = 0;
+    IncrSeg r[IT];
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
       const uint64_t s = base + (uint64_t)tid * IT + k;
-      c[k] = s < s1 ? incr_count_one(W, (uint32_t)s, dirty) : 0;
+      if (s < s1) r[k] = incr_count_one(W, (uint32_t)s);
+      else r[k] = IncrSeg{0, 0, false, false};
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const uint64_t s = base + (uint64_t)tid * IT + k;
+      if (s < s1) incr_store(W, (uint32_t)s, r[k]);
+      c[k] = r[k].count;
+      dirty |= r[k].bad ? 1u : 0u;
       tsum += c[k];
     }
     uint64_t x = tsum;  // inclusive wave scan
@@ -1866,6 +1973,110 @@ __global__ __launch_bounds__(1024) void k_incr_scan(Work W, uint32_t s0, uint32_
     }
     carry += total;
     __syncthreads();
+  }
+  if (dirty) atomicOr(W.err + 2, 1u);
+}
+
+// Counts and offsets of segments [s0, s1) in ONE launch for any count
+// (k_incr_count + a rocPRIM scan + k_add_base were four launches, ~25 us per
+// 64 GiB call): tiles of 4096 segments are taken in order from a ticket
+// (err[6]); a tile publishes its aggregate, looks back over its predecessors
+// (decoupled look-back, one wave reading 64 predecessors' words at a time) and
+// then publishes its inclusive prefix.  A status word holds flag and value
+// together (flag in bits 62-63), written and read as one 8-byte agent-scope
+// atomic, so a reader sees both or neither on any XCD.  Predecessors were
+// ticketed earlier by resident blocks and publish their aggregates without
+// waiting, so the spin always ends.
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
+constexpr int kLbIt = 4;  // segments per thread: 4096 per tile
+
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(1024) void k_incr_lookback(Work W, uint32_t s0, uint32_t s1, uint64_t *status) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t sh_excl;
+  __shared__ uint32_t sh_tile;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) sh_tile = atomicAdd(W.err + 6, 1u);
+  __syncthreads();
+  const uint32_t tile = sh_tile;
+  const uint64_t base = s0 + (uint64_t)tile * (1024 * kLbIt);
+  uint32_t dirty = 0;
+  uint64_t c[kLbIt], tsum = 0;
+  IncrSeg r[kLbIt];
+#pragma unroll
+  for (int k = 0; k < kLbIt; ++k) {
+    const uint64_t s = base + (uint64_t)tid * kLbIt + k;
+    if (s < s1) r[k] = incr_count_one(W, (uint32_t)s);
+    else r[k] = IncrSeg{0, 0, false, false};
+  }
+#pragma unroll
+  for (int k = 0; k < kLbIt; ++k) {
+    const uint64_t s = base + (uint64_t)tid * kLbIt + k;
+    if (s < s1) incr_store(W, (uint32_t)s, r[k]);
+    c[k] = r[k].count;
+    dirty |= r[k].bad ? 1u : 0u;
+    tsum += c[k];
+  }
+  uint64_t x = tsum;  // inclusive wave scan
+#pragma unroll
+  for (unsigned d = 1; d < 64; d <<= 1) {
+    const uint64_t v = shfl_up64(x, d);
+    if (lane >= d) x += v;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint64_t wpre = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t v = wsum[k];
+    wpre += (uint32_t)k < wv ? v : 0;
+    total += v;
+  }
+  if (wv == 0) {
+    uint64_t excl = 0;
+    if (tile == 0) {
+      excl = W.seg_off[s0];
+    } else {
+      if (lane == 0) lb_store(status + tile, kLbAgg | total);
+      int64_t j = (int64_t)tile - 1;  // lane l looks at tile j - l
+      for (;;) {
+        const int64_t idx = j - (int64_t)lane;
+        const uint64_t v = idx >= 0 ? lb_load(status + idx) : kLbInc;  // (tile 0 is inclusive: never past it)
+        const uint64_t fl = v >> 62;
+        const uint64_t incm = __ballot(fl == 2), notready = __ballot(fl == 0);
+        const uint32_t f = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;  // nearest inclusive predecessor
+        const uint64_t need = f == 64 ? ~0ull : ((2ull << f) - 1);        // lanes 0..f
+        if (notready & need) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint64_t part = lane <= f ? (v & kLbVal) : 0;  // aggregates before f, f's inclusive value
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) part += shfl64(part, (int)(lane ^ d));
+        excl += part;
+        if (f != 64) break;
+        j -= 64;
+      }
+    }
+    if (lane == 0) {
+      lb_store(status + tile, kLbInc | (excl + total));
+      sh_excl = excl;
+    }
+  }
+  __syncthreads();
+  uint64_t run = sh_excl + wpre + x - tsum;  // exclusive prefix of this thread's first segment
+#pragma unroll
+  for (int k = 0; k < kLbIt; ++k) {
+    const uint64_t s = base + (uint64_t)tid * kLbIt + k;
+    run += c[k];
+    if (s < s1) W.seg_off[s + 1] = run;
   }
   if (dirty) atomicOr(W.err + 2, 1u);
 }
@@ -1977,6 +2188,9 @@ static void launch_counts_incremental(const Work &w, uint32_t s0, uint32_t s1, u
   const uint32_t n = s1 - s0;
   if (n <= 8192) {  // one block, one pass: a single launch for small batches
     hipLaunchKernelGGL(k_incr_scan, dim3(1), dim3(1024), 0, stream, w, s0, s1);
+  } else if (w.lb_status) {  // one launch, decoupled look-back (status words zeroed per call)
+    hipLaunchKernelGGL(k_incr_lookback, dim3((n + 1024 * kLbIt - 1) / (1024 * kLbIt)), dim3(1024), 0, stream, w, s0,
+                       s1, w.lb_status);
   } else {
     hipLaunchKernelGGL(k_incr_count, dim3((n + 255) / 256), dim3(256), 0, stream, w, s0, s1);
     size_t bytes = scan_tmp_bytes_;
@@ -2004,13 +2218,21 @@ void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void
   if (w.nsegs == 0) return;
   const unsigned lg = lane_grid(w, 256, w.nsegs);
   const unsigned listg = w.ncu ? w.ncu : 256;
+  auto rec = [&](int i) { if (w.dbg_ev) (void)hipEventRecord(w.dbg_ev[i], stream); };  // TEMP
   hipLaunchKernelGGL(k_spec_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
+  rec(1);
   hipLaunchKernelGGL(k_spec_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_spec,
                      (const uint32_t *)(w.err + 4));
+  rec(2);
   hipLaunchKernelGGL(k_link_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
+  rec(3);
   hipLaunchKernelGGL(k_link_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_link,
                      (const uint32_t *)(w.err + 5));
-  launch_emit_incremental(w, p, 0u, w.nsegs, incl, scan_tmp, scan_tmp_bytes_, stream, 8);
+  rec(4);
+  launch_counts_incremental(w, 0u, w.nsegs, incl, scan_tmp, scan_tmp_bytes_, stream);
+  rec(5);
+  launch_emit(w, p, 0u, w.nsegs, 8, stream);
+  rec(6);
 }
 
 // General resolution after k_spec / k_link of every segment: serial fallback
