@@ -105,9 +105,6 @@ DevParams make_dev_params(const mcdc_params *p, uint64_t ms, uint64_t ml) {
 // a chain step's window spans at most 64 runs (max <= 256 KiB): its steps
 // read run summaries 16 runs per batch, so larger windows favour the group
 // walk.  Single-part calls only (the staged pipeline keeps the group walk).
-// Tiles of k_incr_lookback (4096 segments each), one status word per tile.
-size_t lb_tiles(uint32_t nsegs) { return (size_t)nsegs / 4096 + 1; }
-
 bool use_lane_walk(const mcdc_params *p, const Knobs &kn) {
   if (kn.parts != 1 || kn.lane_walk == 0) return false;
   return kn.lane_walk == 2 || p->max_size <= 64u * kRun;
@@ -408,6 +405,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // counter are zeroed by one memset before the scan
   const uint64_t nbitw = nruns / 64 + 4;
   if ((rc = ensure(ctx, ctx->run_bits, nbitw * 16 + 64))) return rc;
+  if ((rc = ensure(ctx, ctx->err, 32))) return rc;  // (zeroed by the first scan launch)
   Work W{};
   W.base = base;
   W.n_al = n_al;
@@ -418,6 +416,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   W.run_sum = (uint32_t *)ctx->run_sum.p;
   W.run_ent = (uint32_t *)ctx->run_ent.p;
   W.run_bits = (uint64_t *)ctx->run_bits.p;
+  W.err = (uint32_t *)ctx->err.p;
   W.tile_ctr = kn.dyn_tiles ? W.run_bits + 2 * nbitw : nullptr;
   W.first_static = kn.first_static ? 1u : 0u;
   hipStream_t st = ctx->stream;
@@ -501,7 +500,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   if ((rc = ensure(ctx, ctx->seg_count, (nsegs + 1) * 8))) return rc;
   if ((rc = ensure(ctx, ctx->seg_off, (nsegs + 1) * 8))) return rc;
   if (!out_dev && (rc = ensure(ctx, ctx->out, out_bound * sizeof(DevChunk)))) return rc;
-  if ((rc = ensure(ctx, ctx->err, 32))) return rc;
   const size_t tmpb = scan_tmp_bytes(nsegs);
   if ((rc = ensure(ctx, ctx->scan_tmp, tmpb))) return rc;
 
@@ -615,7 +613,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     }
     HIP_TRY(hipEventRecord(ctx->ev_scan, st));
   }
+  bool uploaded = false;
   if (!ctx->plan_valid) {  // tables -> pinned stage -> one async copy each
+    uploaded = true;
     const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
                  b_noff = ctx->h_node_off.size() * 8;
     const size_t o_files = (b_segs + 255) / 256 * 256, o_noff = o_files + (b_files + 255) / 256 * 256;
@@ -640,26 +640,22 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   }
   const bool want_counts = counts && nfiles;
   if (want_counts && (rc = ensure_fcnt(ctx, nfiles))) return rc;
-  if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st2));
-  HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st2));
-  HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
-  HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, st2));
-  if (W.lb_status) HIP_TRY(hipMemsetAsync(W.lb_status, 0, lb_tiles(nsegs) * 8, st2));
   const bool lane_all = lane && K == 1;
+  if (lane_all && n_al == 0) HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st));  // (no scan launch to clear them)
+  if (!lane_all) {  // (the lane walk's first kernels reset these: k_scan_q, k_spec_lane)
+    if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st2));
+    HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st2));
+    HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
+    HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, st2));
+  }
   // The lane walk runs on the scan's own stream: it follows the scan at a
-  // same-queue kernel boundary (~2 us) instead of a cross-queue event (~13 us
-  // measured); the resets and uploads on stream2 finished during the scan.
+  // same-queue kernel boundary instead of a cross-queue event (~13 us
+  // measured), and waits for stream2 only for this call's table uploads.
   hipStream_t rs = lane_all ? st : st2;
-  static const int dbg = std::getenv("MCDC_DBG_LANE") ? std::atoi(std::getenv("MCDC_DBG_LANE")) : 0;  // TEMP
-  hipEvent_t dbg_ev[8] = {};
   if (lane_all) {
-    if (dbg & 2) { for (auto &e : dbg_ev) (void)hipEventCreate(&e); (void)hipEventRecord(dbg_ev[7], st2); }
-    HIP_TRY(hipEventRecord(ctx->ev_prep, st2));
-    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prep, 0));
-    if (dbg & 1) HIP_TRY(hipStreamSynchronize(st));
-    if (dbg & 2) {
-      (void)hipEventRecord(dbg_ev[0], st);
-      W.dbg_ev = dbg_ev;
+    if (uploaded) {
+      HIP_TRY(hipEventRecord(ctx->ev_prep, st2));
+      HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prep, 0));
     }
     launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st);
     HIP_TRY(hipGetLastError());
@@ -723,29 +719,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->timing.fallback_files = nfallback;
   ctx->timing.lane_walk = lane_all ? 1 : 0;
   ctx->timing.handed_back = lane_all ? ((volatile uint64_t *)ctx->h_res)[4] : 0;
-  if (dbg_ev[0]) {  // TEMP
-    float ms[6] = {};
-    for (int i = 0; i < 6; ++i) (void)hipEventElapsedTime(&ms[i], dbg_ev[i], dbg_ev[i + 1]);
-    float a = 0, b = 0, c2 = 0;
-    (void)hipEventElapsedTime(&a, ctx->ev_start, ctx->ev_scan);
-    (void)hipEventElapsedTime(&b, ctx->ev_start, dbg_ev[7]);
-    (void)hipEventElapsedTime(&c2, ctx->ev_start, dbg_ev[0]);
-    {
-      std::vector<uint32_t> ls(nsegs);
-      (void)hipMemcpy(ls.data(), ctx->link_seg.p, nsegs * 4, hipMemcpyDeviceToHost);
-      uint32_t irr = 0, none = 0, maxjump = 0;
-      for (uint32_t i = 0; i < nsegs; ++i) {
-        if (ctx->h_segs[i].flags & kSegLast) continue;
-        if (ls[i] == kSegNone) ++none;
-        else if (ls[i] != i + 1) { ++irr; maxjump = std::max(maxjump, ls[i] - i); }
-      }
-      fprintf(stderr, "DBG links: nsegs %u irregular %u none %u maxjump %u dirty %llu\n", nsegs, irr, none, maxjump,
-              (unsigned long long)((volatile uint64_t *)ctx->h_res)[3]);
-    }
-    fprintf(stderr, "DBG t: scan_end %.3f st2_resets_done %.3f lane_start %.3f\n", a, b, c2);
-    fprintf(stderr, "DBG lane: spec %.3f list %.3f link %.3f list %.3f counts %.3f emit %.3f\n", ms[0], ms[1], ms[2], ms[3], ms[4], ms[5]);
-    for (auto &e : dbg_ev) (void)hipEventDestroy(e);
-  }
   return MCDC_OK;
 }
 

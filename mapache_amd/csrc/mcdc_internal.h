@@ -69,6 +69,9 @@ __host__ __device__ inline uint32_t run_summary(uint32_t cnt, uint32_t first_s, 
          (first_s == 0xffffffffu ? 0u : first_s + 1u);
 }
 
+// Tiles of k_incr_lookback (1024 segments each), one status word per tile.
+__host__ __device__ inline uint64_t lb_tiles(uint32_t nsegs) { return (uint64_t)nsegs / 1024 + 1; }
+
 struct Seg {
   uint64_t start, end;  // arena positions [start, end)
   uint32_t file, flags;
@@ -137,7 +140,6 @@ struct Work {
   uint32_t *punt_spec;   // lane walk: segments handed to the group walk (k_spec_list), count err[4]
   uint32_t *punt_link;   // (k_link_list), count err[5]
   uint32_t ncu;          // compute units (persistent grids)
-  hipEvent_t *dbg_ev = nullptr;  // TEMP
   uint64_t *lb_status;   // k_incr_lookback tile status words (lane walk: zeroed per call), ticket err[6]
 };
 

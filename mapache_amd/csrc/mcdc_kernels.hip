@@ -531,6 +531,9 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   q.lcnt[lane] = 0;
   q.lcnt[64 + lane] = 0xffffffffu;
   q.lcnt[128 + lane] = 0xffffffffu;
+  // the call's error / dirty / hand-back words start at zero (the first part's
+  // launch clears them: no memset launch on the resolution's critical path)
+  if (tile0 == 0 && blockIdx.x == 0 && threadIdx.x < 8) W.err[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   // wave index, CU-major: the first gridDim.x tiles of a static round land on
@@ -1287,20 +1290,24 @@ __device__ __forceinline__ int32_t lane_run_split(const Work &W, const DevParams
 __device__ __forceinline__ uint64_t bits_upto(uint32_t i) { return i == 63 ? ~0ull : ((2ull << i) - 1); }
 
 // First run in [a, b] whose bit is set in plane pl (0: S, 1: L) of the
-// candidate bitmaps, ~0 if none; v0 / v1 = the plane's words a/64 and a/64+1,
-// already loaded.  Windows of more than two words (max > 252 KiB) load the
-// rest here.
-__device__ __forceinline__ uint64_t first_bit_run(const uint64_t *bits, int pl, uint64_t a, uint64_t b, uint64_t v0,
-                                                  uint64_t v1) {
+// candidate bitmaps, ~0 if none.  pw = the word pairs wB and wB + 1, already
+// loaded ({S, L} of wB in .x.y / .z.w of p0, of wB + 1 in p1); other words
+// (windows past them: max > 252 KiB) are loaded here.
+__device__ __forceinline__ uint64_t bit_word(const uint64_t *bits, int pl, uint64_t w, uint64_t wB, const uint4 &p0,
+                                             const uint4 &p1) {
+  if (w == wB) return pl ? ((uint64_t)p0.w << 32) | p0.z : ((uint64_t)p0.y << 32) | p0.x;
+  if (w == wB + 1) return pl ? ((uint64_t)p1.w << 32) | p1.z : ((uint64_t)p1.y << 32) | p1.x;
+  return bits[2 * w + pl];
+}
+__device__ __forceinline__ uint64_t first_bit_run(const uint64_t *bits, int pl, uint64_t a, uint64_t b, uint64_t wB,
+                                                  const uint4 &p0, const uint4 &p1) {
   if (a > b) return ~0ull;
   const uint64_t wa = a >> 6, wb = b >> 6;
-  uint64_t m = v0 & (~0ull << (a & 63));
-  if (wa == wb) m &= bits_upto((uint32_t)(b & 63));
-  if (m) return (wa << 6) + (uint64_t)__builtin_ctzll(m);
-  for (uint64_t w = wa + 1; w <= wb; ++w) {
-    uint64_t mm = w == wa + 1 ? v1 : bits[2 * w + pl];
-    if (w == wb) mm &= bits_upto((uint32_t)(b & 63));
-    if (mm) return (w << 6) + (uint64_t)__builtin_ctzll(mm);
+  for (uint64_t w = wa; w <= wb; ++w) {
+    uint64_t m = bit_word(bits, pl, w, wB, p0, p1);
+    if (w == wa) m &= ~0ull << (a & 63);
+    if (w == wb) m &= bits_upto((uint32_t)(b & 63));
+    if (m) return (w << 6) + (uint64_t)__builtin_ctzll(m);
   }
   return ~0ull;
 }
@@ -1346,12 +1353,11 @@ __device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P,
   const uint64_t rL0 = min((c + (uint64_t)l_beg) / kRun, rlast);
   const uint64_t rS1 = hasS ? (c + (uint64_t)s_end - 1) / kRun : 0, rL1 = hasL ? (c + (uint64_t)hi_r - 1) / kRun : 0;
   const uint32_t uS0 = W.run_sum[rS0], uL0 = W.run_sum[rL0];
-  const uint32_t cS0 = W.run_cnt[rS0], cL0 = W.run_cnt[rL0];
-  const uint64_t wS = (rS0 + 1) >> 6, wL = (rL0 + 1) >> 6;  // (+ read-ahead words are allocated)
-  const uint4 bS0 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wS);
-  const uint4 bS1 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wS + 2);
-  const uint4 bL0 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wL);
-  const uint4 bL1 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wL + 2);
+  // bitmap word pairs wB, wB + 1 (runs [64 wB, 64 wB + 128) hold both windows
+  // after rS0 at max <= 256 KiB; + read-ahead words are allocated)
+  const uint64_t wB = (rS0 + 1) >> 6;
+  const uint4 bp0 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wB);
+  const uint4 bp1 = *reinterpret_cast<const uint4 *>(W.run_bits + 2 * wB + 2);
 
   // ---- (2) windowed candidates: S in [lo, s_end), L in [l_beg, hi) (chunk-relative).
   // Decided before the restart window's hash so that the level-2 loads are in
@@ -1374,16 +1380,20 @@ __device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P,
     else splitL = fl1 && p < l_beg && (uL0 >> 28) >= 2;
   }
   // the first later run with a candidate of the kind (bitmap search)
-  const uint64_t rS = hasS ? first_bit_run(W.run_bits, 0, rS0 + 1, rS1, ((uint64_t)bS0.y << 32) | bS0.x,
-                                           ((uint64_t)bS1.y << 32) | bS1.x)
-                           : ~0ull;
-  const uint64_t rL = hasL ? first_bit_run(W.run_bits, 1, rL0 + 1, rL1, ((uint64_t)bL0.w << 32) | bL0.z,
-                                           ((uint64_t)bL1.w << 32) | bL1.z)
-                           : ~0ull;
+  const uint64_t rS = hasS ? first_bit_run(W.run_bits, 0, rS0 + 1, rS1, wB, bp0, bp1) : ~0ull;
+  const uint64_t rL = hasL ? first_bit_run(W.run_bits, 1, rL0 + 1, rL1, wB, bp0, bp1) : ~0ull;
   // ---- level 2
   const uint32_t uS = W.run_sum[min(rS, rlast)], uL = W.run_sum[min(rL, rlast)];
-  if (__builtin_expect(splitS, 0)) best = min(best, lane_run_split(W, P, rS0, cS0, rel(rS0), lo_r, hi_r, cce_r, punt));
-  if (__builtin_expect(splitL, 0)) best = min(best, lane_run_split(W, P, rL0, cL0, rel(rL0), lo_r, hi_r, cce_r, punt));
+  // (a run's count: the summary's 4-bit field is exact below 15, which decides
+  // "overflowed" for cap <= 14; larger caps read run_cnt)
+  if (__builtin_expect(splitS, 0)) {
+    const uint32_t cnt = P.cap <= 14 ? (uS0 >> 28) : W.run_cnt[rS0];
+    best = min(best, lane_run_split(W, P, rS0, cnt, rel(rS0), lo_r, hi_r, cce_r, punt));
+  }
+  if (__builtin_expect(splitL, 0)) {
+    const uint32_t cnt = P.cap <= 14 ? (uL0 >> 28) : W.run_cnt[rL0];
+    best = min(best, lane_run_split(W, P, rL0, cnt, rel(rL0), lo_r, hi_r, cce_r, punt));
+  }
 
   // ---- (1) exact restarted hash of the first <= 47 tested positions
   {
@@ -1433,6 +1443,16 @@ __device__ __forceinline__ uint64_t lane_next(const Work &W, const DevParams &P,
 __global__ __launch_bounds__(256) void k_spec_lane(Work W, DevParams P, uint32_t s0, uint32_t s1) {
   __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
   __builtin_amdgcn_s_setprio(3);
+  {  // per-call resets the later kernels rely on (link: file flags; counts: look-back words, offsets)
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+    for (uint32_t i = g; i < W.nfiles; i += gs) W.file_flags[i] = 0;
+    if (W.lb_status)
+      for (uint32_t i = g; i < lb_tiles(W.nsegs); i += gs) W.lb_status[i] = 0;
+    if (g == 0) {
+      W.seg_count[W.nsegs] = 0;
+      W.seg_off[0] = 0;
+    }
+  }
   load_gear_rep(tab, W);
   const uint32_t lo8 = (threadIdx.x & 31) << 3;
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -1680,8 +1700,8 @@ __device__ __forceinline__ uint64_t chunk_hash(const Work &W, const uint64_t *ta
   const uint32_t off = (uint32_t)(s0 - B);
   uint32_t dw[20];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const uint4 b = B + 16 * k <= cq.q ? *reinterpret_cast<const uint4 *>(W.base + B + 16 * k) : make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < 5; ++k) {  // (clamped, not skipped: bytes past q are never used; no branch per load)
+    const uint4 b = *reinterpret_cast<const uint4 *>(W.base + min(B + 16 * k, W.n_al - 16));
     dw[4 * k] = b.x; dw[4 * k + 1] = b.y; dw[4 * k + 2] = b.z; dw[4 * k + 3] = b.w;
   }
   uint32_t f[18], g[17], e[16];
@@ -1748,20 +1768,19 @@ __global__ __launch_bounds__(1024) void k_emit(Work W, DevParams P, uint32_t s0,
   const uint32_t lane = lane_id() & (GS - 1);
   const uint32_t ng = gridDim.x * blockDim.x / GS;
   for (uint32_t s = s0 + (blockIdx.x * blockDim.x + threadIdx.x) / GS; s < s1; s += ng) {
+    // the segment's metadata in one round of loads (nothing behind the n == 0 test)
     const uint64_t n = W.seg_count[s];
+    const uint32_t fi = W.segs[s].file, e = W.entry_idx[s], ncnt = W.node_cnt[s], cent = W.cont_ent[s];
+    const uint64_t noff = W.node_off[s], after = W.link_pos[s], base_out = W.seg_off[s];
+    const File F = W.files[fi];
     if (n == 0) continue;
-    const Seg S = W.segs[s];
-    const File F = W.files[S.file];
-    const uint32_t e = W.entry_idx[s];
-    const uint64_t nn = W.node_cnt[s] - e;
-    const uint64_t *nd = W.nodes + W.node_off[s] + e;
+    const uint64_t nn = ncnt - e;
+    const uint64_t *nd = W.nodes + noff + e;
     const uint64_t *ct = W.cont + (uint64_t)s * kContMax;
     const uint32_t *cr = W.cont_rep + (uint64_t)s * kContMax;
     const uint64_t ncont = n - nn;                    // continuation nodes, expanded
-    const bool plain = ncont == W.cont_ent[s];        // every entry a single node
+    const bool plain = ncont == cent;                 // every entry a single node
     const uint64_t n_here = ncont > kEmitInline ? nn : n;  // a long stretch: k_emit_long
-    const uint64_t after = W.link_pos[s];
-    const uint64_t base_out = W.seg_off[s];
     auto node = [&](uint64_t i) -> uint64_t {
       if (i < nn) return nd[i];
       return plain ? ct[i - nn] : cont_node(ct, cr, i - nn, P.max);
@@ -1872,13 +1891,16 @@ struct IncrSeg {
 };
 
 __device__ __forceinline__ IncrSeg incr_count_one(const Work &W, uint32_t s) {
-  const uint32_t fl = W.segs[s].flags;
-  const bool first = fl & kSegFirst, last = fl & kSegLast;
-  // everything a segment normally needs, in one round of loads
+  // everything a segment normally needs in one round of loads, at clamped
+  // indices (a load under `first ? 0 : ...` becomes a branch with its own wait)
+  const uint32_t sm1 = s > 0 ? s - 1 : 0, sm2 = s > 1 ? s - 2 : 0, sp1 = min(s + 1, W.nsegs - 1);
+  const uint32_t fl = W.segs[s].flags, nfl0 = W.segs[sp1].flags;
   const uint32_t nc = W.node_cnt[s], cc = W.cont_cnt[s];
-  const uint32_t lp = first ? 0u : W.link_seg[s - 1], lidx1 = first ? 0u : W.link_idx[s - 1];
-  const uint32_t l = last ? 0u : W.link_seg[s], nfl = last ? 0u : W.segs[s + 1].flags;
-  const uint32_t lpp = (first || s < 2) ? kSegNone : W.link_seg[s - 2];
+  const uint32_t lp0 = W.link_seg[sm1], lidx1 = W.link_idx[sm1], l0 = W.link_seg[s];
+  const uint32_t lpp0 = W.link_seg[sm2], lidx2 = W.link_idx[sm2];
+  const bool first = fl & kSegFirst, last = fl & kSegLast;
+  const uint32_t lp = first ? 0u : lp0, l = last ? 0u : l0, nfl = last ? 0u : nfl0;
+  const uint32_t lpp = (first || s < 2) ? kSegNone : lpp0;
   bool on = true, bad = false;
   uint32_t entry = 0;
   if (!first) {
@@ -1894,7 +1916,7 @@ __device__ __forceinline__ IncrSeg incr_count_one(const Work &W, uint32_t s) {
       else if (lp == kSegNone && last) on = false;            // continuation ran to the file end
       else bad = true;
     } else {  // s - 1 is off the chain: s - 2 skipped it into s
-      entry = W.link_idx[s - 2];
+      entry = lidx2;
     }
   }
   if (on && !last)  // s's own link must keep the next segments local
@@ -1915,6 +1937,7 @@ __device__ __forceinline__ void incr_store(const Work &W, uint32_t s, const Incr
 }
 
 __global__ void k_incr_count(Work W, uint32_t s0, uint32_t s1) {
+  MCDC_VGPR_PAD(16);  // 16 used: not an exact fill (MCDC_VGPR_PAD)
   const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= s1) return;
   const IncrSeg r = incr_count_one(W, s);
@@ -1979,7 +2002,7 @@ __global__ __launch_bounds__(1024) void k_incr_scan(Work W, uint32_t s0, uint32_
 
 // Counts and offsets of segments [s0, s1) in ONE launch for any count
 // (k_incr_count + a rocPRIM scan + k_add_base were four launches, ~25 us per
-// 64 GiB call): tiles of 4096 segments are taken in order from a ticket
+// 64 GiB call): tiles of 1024 segments are taken in order from a ticket
 // (err[6]); a tile publishes its aggregate, looks back over its predecessors
 // (decoupled look-back, one wave reading 64 predecessors' words at a time) and
 // then publishes its inclusive prefix.  A status word holds flag and value
@@ -1988,7 +2011,7 @@ __global__ __launch_bounds__(1024) void k_incr_scan(Work W, uint32_t s0, uint32_
 // ticketed earlier by resident blocks and publish their aggregates without
 // waiting, so the spin always ends.
 constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
-constexpr int kLbIt = 4;  // segments per thread: 4096 per tile
+constexpr int kLbIt = 1;  // segments per thread: 1024 per tile (consecutive lanes, consecutive segments)
 
 __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2173,24 +2196,28 @@ static unsigned lane_grid(const Work &w, uint64_t items_per_block_round, uint64_
   return (unsigned)std::max<uint64_t>(1, std::min(cap, need));
 }
 
+// One group of gs lanes per segment (8 on the lane walk's ~6-chunk segments,
+// 16 on the group walk's ~16): a lane per chunk.  (Measured at 64 GiB: a
+// quad of lanes per chunk sharing one 80-byte load was slower, 87-110 us vs
+// 62 us: the emit is bound by outstanding L1 misses, not by requests.)
 static void launch_emit(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, int gs, hipStream_t stream) {
   if (s1 <= s0) return;
+  const unsigned n = s1 - s0;
   if (gs == 8)
-    hipLaunchKernelGGL(k_emit<8>, dim3(lane_grid(w, 1024 / 8, s1 - s0, 1)), dim3(1024), 0, stream, w, p, s0, s1);
+    hipLaunchKernelGGL(k_emit<8>, dim3(lane_grid(w, 1024 / 8, n, 1)), dim3(1024), 0, stream, w, p, s0, s1);
   else
-    hipLaunchKernelGGL(k_emit<kGroup>, dim3(lane_grid(w, 1024 / kGroup, s1 - s0, 1)), dim3(1024), 0, stream, w, p, s0,
-                       s1);
+    hipLaunchKernelGGL(k_emit<kGroup>, dim3(lane_grid(w, 1024 / kGroup, n, 1)), dim3(1024), 0, stream, w, p, s0, s1);
 }
 
 // counts and offsets of segments [s0, s1) assuming the clean case
 static void launch_counts_incremental(const Work &w, uint32_t s0, uint32_t s1, uint64_t *incl, void *scan_tmp,
                                       size_t scan_tmp_bytes_, hipStream_t stream) {
   const uint32_t n = s1 - s0;
-  if (n <= 8192) {  // one block, one pass: a single launch for small batches
-    hipLaunchKernelGGL(k_incr_scan, dim3(1), dim3(1024), 0, stream, w, s0, s1);
-  } else if (w.lb_status) {  // one launch, decoupled look-back (status words zeroed per call)
+  if (w.lb_status) {  // one launch, decoupled look-back (status words zeroed per call)
     hipLaunchKernelGGL(k_incr_lookback, dim3((n + 1024 * kLbIt - 1) / (1024 * kLbIt)), dim3(1024), 0, stream, w, s0,
                        s1, w.lb_status);
+  } else if (n <= 8192) {  // one block, one pass: a single launch for small batches
+    hipLaunchKernelGGL(k_incr_scan, dim3(1), dim3(1024), 0, stream, w, s0, s1);
   } else {
     hipLaunchKernelGGL(k_incr_count, dim3((n + 255) / 256), dim3(256), 0, stream, w, s0, s1);
     size_t bytes = scan_tmp_bytes_;
@@ -2218,21 +2245,14 @@ void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void
   if (w.nsegs == 0) return;
   const unsigned lg = lane_grid(w, 256, w.nsegs);
   const unsigned listg = w.ncu ? w.ncu : 256;
-  auto rec = [&](int i) { if (w.dbg_ev) (void)hipEventRecord(w.dbg_ev[i], stream); };  // TEMP
   hipLaunchKernelGGL(k_spec_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
-  rec(1);
   hipLaunchKernelGGL(k_spec_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_spec,
                      (const uint32_t *)(w.err + 4));
-  rec(2);
   hipLaunchKernelGGL(k_link_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
-  rec(3);
   hipLaunchKernelGGL(k_link_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_link,
                      (const uint32_t *)(w.err + 5));
-  rec(4);
   launch_counts_incremental(w, 0u, w.nsegs, incl, scan_tmp, scan_tmp_bytes_, stream);
-  rec(5);
   launch_emit(w, p, 0u, w.nsegs, 8, stream);
-  rec(6);
 }
 
 // General resolution after k_spec / k_link of every segment: serial fallback

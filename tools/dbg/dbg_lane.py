@@ -1,5 +1,5 @@
 import os, sys, numpy as np
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from mapache_amd import _lib
 n = int(float(os.environ.get("GIB", "64")) * (1 << 30))
 p = _lib.params(16384, 65536, 262144, 1)
