@@ -482,7 +482,7 @@ def encode(ctx, gib: float, steps: int) -> dict:
     from mapache_amd import _lib
     from oracle import oracle as O
     rng = np.random.default_rng(21)
-    vocab = [bytes(rng.integers(97, 123, int(k))) for k in rng.integers(2, 11, 2000)]
+    vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
     base = b" ".join(vocab[i] for i in rng.integers(0, 2000, 12_000_000))[:64 << 20]
     n = int(gib * GIB) // len(base) * len(base)
     data = np.frombuffer(base * (n // len(base)), np.uint8)

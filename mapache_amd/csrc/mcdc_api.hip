@@ -1715,7 +1715,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
     launch_zc_batch((const uint8_t *)d_data, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
                     (ZcBlock *)ctx->zc_blocks.p, (uint8_t *)ctx->zc_stage.p, (uint64_t *)ctx->zc_seqs.p, T,
                     (uint64_t *)ctx->zc_piece.p, (uint64_t *)ctx->zc_poff.p, misc + 2, (uint8_t *)d_out, ext,
-                    ctx->zc_tmp.p, tmpb, st);
+                    ctx->zc_tmp.p, tmpb, st, ctx->knobs.zc_huf);
     HIP_TRY(hipGetLastError());
     c0 = c1;
   }

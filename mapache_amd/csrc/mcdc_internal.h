@@ -159,6 +159,7 @@ struct Knobs {
   int pinned_direct = 1;  // MCDC_PINNED_DIRECT: k_emit writes pinned host output directly
   int lane_walk = 1;      // MCDC_LANE_WALK: 0 group walk only, 1 lane walk when max <= 64 runs, 2 always
   int lane_seg_chunks = 4;// MCDC_LANE_SEG_CHUNKS: expected chunks per segment on the lane walk
+  bool zc_huf = true;      // MCDC_ZC_HUF: Huffman / RLE literals in the GPU zstd compressor
   // A/B builds only
   int group = 16;         // MCDC_GROUP: lanes per chain group (8, 16, 32)
   int spec_occ = 6;       // MCDC_SPEC_OCC: k_spec waves-per-SIMD build (5 or 6)

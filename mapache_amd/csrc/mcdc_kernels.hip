@@ -2138,6 +2138,7 @@ Knobs read_knobs() {
   k.pinned_direct = env("MCDC_PINNED_DIRECT", k.pinned_direct) != 0;
   k.lane_walk = std::min(std::max(env("MCDC_LANE_WALK", k.lane_walk), 0), 2);
   k.lane_seg_chunks = std::max(env("MCDC_LANE_SEG_CHUNKS", k.lane_seg_chunks), 1);
+  k.zc_huf = env("MCDC_ZC_HUF", k.zc_huf ? 1 : 0) != 0;
 #ifdef MCDC_AB_KNOBS
   k.group = env("MCDC_GROUP", k.group);
   if (k.group != 8 && k.group != 16 && k.group != 32) k.group = kGroup;
@@ -2246,6 +2247,8 @@ void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void
   const unsigned lg = lane_grid(w, 256, w.nsegs);
   const unsigned listg = w.ncu ? w.ncu : 256;
   hipLaunchKernelGGL(k_spec_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);
+  // (the two list kernels leave at once when nothing was handed back; skipping
+  // their launches measured no different, tools/walk_ab.py)
   hipLaunchKernelGGL(k_spec_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_spec,
                      (const uint32_t *)(w.err + 4));
   hipLaunchKernelGGL(k_link_lane, dim3(lg), dim3(256), 0, stream, w, p, 0u, w.nsegs);

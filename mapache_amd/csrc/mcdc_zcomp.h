@@ -18,7 +18,7 @@ struct ZcBlock {
   uint64_t src;                 // chunk bytes [src, src + len) of the input
   uint32_t len, chunk, b, nb;   // block b of nb of chunk
   uint32_t nlit, nseq, csize;   // parse result; csize 0 = stored raw
-  uint32_t pad;
+  uint32_t lsize;               // literals section already in the staging slot (Huffman / RLE), 0 = raw literals
 };
 
 size_t zc_tmp_bytes(uint64_t n);
@@ -31,6 +31,6 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 void launch_zc_batch(const uint8_t *base, const DevChunk *chunks, const uint64_t *first, uint64_t c0, uint64_t c1,
                      uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
-                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st);
+                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true);
 
 }  // namespace mcdc

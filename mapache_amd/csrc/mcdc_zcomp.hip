@@ -4,8 +4,8 @@
 // path chunk -> IDs -> compress -> seal never leaves HBM.  One zstd frame per
 // chunk (the blob mapache stores), in the crate's frame layout (magic, no
 // content size, window 2^20, no checksum); blocks of 16 KiB, each either
-// compressed (raw literals + predefined-FSE sequences, mcdc_zstd.h) or raw when
-// that is not smaller.  Decodes with mapache's decoder (storage.rs:87-94).
+// compressed (Huffman / RLE / raw literals + predefined-FSE sequences,
+// mcdc_zstd.h) or raw when that is not smaller.  Decodes with mapache's decoder (storage.rs:87-94).
 //
 // Per batch of blocks (a block = 16 KiB of one chunk; batches bound the
 // scratch):
@@ -21,6 +21,12 @@
 //                per step.  Literals go to the block's staging slot, sequences
 //                (<= kZcSeqCap = 4096 per block, then the rest are literals) straight to
 //                scratch (8 KiB of LDS per wave: 20 waves per CU).
+//   k_zc_huff    ONE WAVE PER BLOCK: the block's literals (all of a block
+//                without matches) as a Huffman-coded (or RLE) literals
+//                section when smaller than raw: histogram in LDS, symbols
+//                ranked by the wave, the length-limited canonical code by one
+//                lane, then the streams (four above 1023 literals) by the
+//                whole wave, bit positions from wave scans, assembled in LDS
 //   k_zc_encode  ONE LANE PER BLOCK: the serial FSE bitstream of the block's
 //                sequences (three interleaved state machines, tables in LDS);
 //                block kept compressed only if smaller than raw
@@ -81,7 +87,7 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
     z.chunk = (uint32_t)c;
     z.b = (uint32_t)b;
     z.nb = (uint32_t)nb;
-    z.nlit = z.nseq = z.csize = 0;
+    z.nlit = z.nseq = z.csize = z.lsize = 0;
     blocks[f + b - b0] = z;
   }
 }
@@ -213,6 +219,179 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
   }
 }
 
+// Inclusive sum over the wave's 64 lanes.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, d);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// The literals section of a compressed block: Huffman-coded or RLE when that
+// is smaller than the raw section (3-byte header + the literals), written
+// over the staging slot's raw literals; B.lsize its size, 0 = raw.  Literals
+// >= 128 keep the raw section (the direct weight representation covers
+// symbols 0..128; 128 itself is not worth the check).  The whole wave works
+// on every step but the tree (one lane, ~2n dependent steps on LDS):
+//   count    16 bytes per lane per step into 8 LDS histogram copies, leaving
+//            at the first KiB that holds a byte >= 128 (random data: 1 KiB)
+//   rank     symbols by count (ties by symbol), one rank per lane
+//   tree     huf_build on the ranked symbols (lane 0)
+//   sizes    bits per stream (wave sums); give up unless smaller than raw
+//   streams  64 literals per round, last first: code lengths -> wave scan ->
+//            bit positions -> codes OR-ed into the section assembled in LDS
+//            (literal loads 8 rounds ahead)
+//   store    header, tree, jump table; the section to the slot, 16-byte stores
+__global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage) {
+  // the section under assembly; its first 8 KiB hold the histogram copies and
+  // then the tree's scratch before it is cleared
+  __shared__ __attribute__((aligned(16))) uint32_t out[kZcSlot / 4];
+  __shared__ HufCT ct;
+  uint32_t(*hist)[256] = reinterpret_cast<uint32_t(*)[256]>(out);
+  HufWork &hw = *reinterpret_cast<HufWork *>(out + 8 * 256);
+  static_assert(8 * 256 * 4 + sizeof(HufWork) <= sizeof(out), "LDS");
+  const uint64_t bi = blockIdx.x;
+  if (bi >= nblk) return;
+  const uint32_t lane = lane_id();
+  const ZcBlock B = blocks[bi];
+  // a block without sequences: all of it literals, read from the input (k_zc_match staged nothing)
+  const uint32_t n = B.nseq ? B.nlit : B.len;
+  if (n < 32) return;  // (lsize stays 0: raw literals)
+  uint8_t *st = stage + bi * kZcSlot;
+  const uint8_t *src = B.nseq ? st + kLitHdr : base + B.src;
+  for (uint32_t k = lane; k < 8 * 256; k += 64) out[k] = 0;
+  __syncthreads();
+  // count (misaligned 16-byte loads: gfx950 reads the bytes at the address)
+  for (uint32_t k0 = 0; k0 < n; k0 += 1024) {
+    const uint32_t k = k0 + 16 * lane;
+    uint32_t w[4] = {0, 0, 0, 0}, m = 0;
+    if (k + 16 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(src + k);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      m = 16;
+    } else if (k < n) {
+      m = n - k;
+#pragma unroll
+      for (uint32_t j = 0; j < 16; ++j)
+        if (j < m) w[j >> 2] |= (uint32_t)src[k + j] << (8 * (j & 3));
+    }
+    if (__ballot(((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0)) return;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)
+      if (j < m) atomicAdd(&hist[lane & 7][(w[j >> 2] >> (8 * (j & 3))) & 0x7F], 1u);
+  }
+  __syncthreads();
+  uint32_t c[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t k = lane + 64 * h;
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += hist[j][k];
+    c[h] = v;
+  }
+  __syncthreads();
+  hist[0][lane] = c[0];
+  hist[0][lane + 64] = c[1];
+  if (lane == 0) hist[0][128] = 0;  // (huf_build reads 129 counts)
+  // rank: symbols by count ascending, ties by symbol (huf_build's stable order)
+  const uint64_t p0 = __ballot(c[0] != 0), p1 = __ballot(c[1] != 0);
+  const uint32_t distinct = (uint32_t)(__builtin_popcountll(p0) + __builtin_popcountll(p1));
+  if (distinct == 1) {  // RLE literals: 3-byte header + the byte
+    if (lane == 0) {
+      put_rle_lit_header(st, n);
+      st[3] = (uint8_t)(p0 ? __builtin_ctzll(p0) : 64 + __builtin_ctzll(p1));
+      blocks[bi].lsize = 4;
+    }
+    return;
+  }
+  __syncthreads();
+  uint32_t r[2] = {0, 0};
+  for (uint32_t t = 0; t < 128; t += 4) {
+    const uint4 q = *reinterpret_cast<const uint4 *>(&hist[0][t]);  // (broadcast)
+    const uint32_t qs[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        r[h] += (qs[j] && (qs[j] < c[h] || (qs[j] == c[h] && t + j < lane + 64 * h))) ? 1u : 0u;
+  }
+  if (c[0]) hw.sym[r[0]] = (uint16_t)lane;
+  if (c[1]) hw.sym[r[1]] = (uint16_t)(lane + 64);
+  __syncthreads();
+  if (lane == 0) huf_build(hist[0], ct, hw, true);
+  __syncthreads();
+  // bits per stream (stream k: literals [k seg, min((k + 1) seg, n)))
+  const bool one = n < 1024;
+  const uint32_t seg = one ? n : (n + 3) / 4, ns = one ? 1 : 4;
+  uint32_t sb[4] = {0, 0, 0, 0};
+  for (uint32_t k = 0; k < ns; ++k) {
+    const uint32_t a = k * seg, e = min(a + seg, n);
+    uint32_t b = 0;
+#pragma unroll 8
+    for (uint32_t i = a + lane; i < e; i += 64) b += ct.nb[src[i]];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) b += (uint32_t)__shfl_xor((int)b, d);
+    sb[k] = b;
+  }
+  uint32_t ssz[4];
+  const uint32_t total = huf_section_size(ct, n, sb, one, ssz);
+  if (total >= kLitHdr + n) return;  // not smaller than raw
+  const uint32_t tree = 1 + (ct.last + 1) / 2;
+  const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
+  if (one && csize >= 1024) return;  // (one stream: 10-bit sizes)
+  const uint32_t hdr = lit_hdr_size(n, csize, one);
+  const uint32_t nq = (total + 15) / 16;  // 16-byte units of the section
+  for (uint32_t k = lane; k < nq; k += 64) reinterpret_cast<uint4 *>(out)[k] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  // the streams
+  uint32_t o = hdr + tree + (one ? 0 : 6);  // byte offset of stream k in the section
+  for (uint32_t k = 0; k < ns; ++k) {
+    const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
+    uint32_t carry = 8 * o;  // bit position of the next round's first literal
+    for (uint32_t r0 = 0; r0 < len; r0 += 8 * 64) {
+      uint32_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t q = r0 + 64 * j + lane;
+        x[j] = q < len ? (uint32_t)src[e - 1 - q] : 0x100u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (r0 + 64 * j >= len) break;
+        const uint32_t nb = x[j] < 0x100u ? ct.nb[x[j]] : 0u;
+        const uint32_t incl = wave_incl_sum(nb, lane);
+        const uint32_t pos = carry + incl - nb;
+        if (nb) {
+          const uint32_t code = ct.code[x[j]], sft = pos & 31;
+          atomicOr(&out[pos >> 5], code << sft);
+          if (sft + nb > 32) atomicOr(&out[(pos >> 5) + 1], code >> (32 - sft));
+        }
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      }
+    }
+    if (lane == 0) atomicOr(&out[carry >> 5], 1u << (carry & 31));  // the end mark
+    o += ssz[k];
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint8_t *sec = reinterpret_cast<uint8_t *>(out);
+    put_huf_lit_header(sec, n, csize, one);
+    huf_tree_desc(ct, sec + hdr);
+    if (!one)
+      for (int k = 0; k < 3; ++k) {
+        sec[hdr + tree + 2 * k] = (uint8_t)ssz[k];
+        sec[hdr + tree + 2 * k + 1] = (uint8_t)(ssz[k] >> 8);
+      }
+    blocks[bi].lsize = total;
+  }
+  __syncthreads();
+  // (every read of the staged literals is done: the section replaces them)
+  for (uint32_t k = lane; k < nq; k += 64) reinterpret_cast<uint4 *>(st)[k] = reinterpret_cast<const uint4 *>(out)[k];
+}
+
 __global__ __launch_bounds__(256) void k_zc_encode(ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
                                                    const uint64_t *seqs, ZTables T, uint64_t *piece) {
   MCDC_VGPR_PAD(64);  // (not an exact fill)
@@ -227,10 +406,10 @@ __global__ __launch_bounds__(256) void k_zc_encode(ZcBlock *blocks, uint64_t nbl
   }
   ZcBlock B = blocks[bi];
   uint32_t csize = 0;
-  if (B.nseq) {
+  if (B.nseq || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
     uint8_t *st = stage + bi * kZcSlot;
-    put_raw_lit_header(st, B.nlit);
-    const uint32_t at = kLitHdr + B.nlit;
+    if (!B.lsize) put_raw_lit_header(st, B.nlit);
+    const uint32_t at = B.lsize ? B.lsize : kLitHdr + B.nlit;  // (Huffman / RLE section written by k_zc_huff)
     // kept only if smaller than the raw block
     const uint32_t cap = B.len > at + 1 ? B.len - at - 1 : 0;
     const uint64_t *sq = seqs + bi * kZcSeqCap;
@@ -305,11 +484,12 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 void launch_zc_batch(const uint8_t *base, const DevChunk *chunks, const uint64_t *first, uint64_t c0, uint64_t c1,
                      uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
-                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st) {
+                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf) {
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
   hipLaunchKernelGGL(k_zc_match, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, seqs);
+  if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)((nblk + 1 + 255) / 256)), dim3(256), 0, st, blocks, nblk, stage,
                      seqs, T, piece);
   size_t b = tmp_bytes;

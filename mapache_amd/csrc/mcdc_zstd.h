@@ -12,7 +12,11 @@
 //   * sequences coded with the predefined FSE distributions of RFC 8878
 //     §3.1.1.3.2.2 (Predefined_Mode for literal lengths, offsets and match
 //     lengths: no table descriptions),
-//   * offsets always as Offset_Value = offset + 3 (no repeat codes).
+//   * offsets always as Offset_Value = offset + 3 (no repeat codes);
+//   * literals raw, RLE (one distinct byte) or Huffman-coded (Compressed_
+//     Literals_Block: a length-limited canonical code, weights in the direct
+//     representation -- literals up to byte 128 -- one stream below 1024
+//     literals, four above), whichever section is smallest.
 // Any conforming decoder (mapache's: zstd with window_log_max 20,
 // storage.rs:87-94) reads them; the compressed bytes differ from libzstd's,
 // so parity is decode-equality.
@@ -264,6 +268,198 @@ __host__ __device__ inline uint32_t encode_sequences(const ZTables &T, SeqAt seq
   return (uint32_t)(bw.p - dst);
 }
 
+// ---- Huffman-coded literals (RFC 8878 §3.1.1.3.1, §4.2) ------------------
+constexpr uint32_t kHufMaxBits = 11;
+
+struct HufCT {
+  uint16_t code[129];  // canonical code (valid where nb > 0)
+  uint8_t nb[129];     // code length, 0 = absent
+  uint32_t last;       // highest present symbol (its weight is implied)
+  uint32_t maxb;       // longest code
+};
+
+// Scratch of huf_build (LDS on the GPU: dynamically indexed arrays in a
+// lane's registers would live in scratch memory).
+struct HufWork {
+  uint32_t f[258];      // node weights: leaves 0..n-1 (ascending), internal nodes after
+  uint16_t sym[129];    // symbols by count ascending (ties: by symbol)
+  uint16_t par[258];    // parent of each node
+  uint8_t dep[258];     // node depth
+  uint32_t bl[64];      // leaves per depth
+  uint32_t rank[kHufMaxBits + 2], val[kHufMaxBits + 2];
+};
+
+// Code lengths of a Huffman code over the symbols with cnt > 0 (all < 129,
+// at least two), limited to kHufMaxBits, then canonical codes as zstd's
+// decoder rebuilds them from the weights: by rank from the longest length
+// down (start 0; next rank's start = (start + count) >> 1), within a rank in
+// symbol order.  Serial (one lane per block on the GPU).  sorted: w.sym
+// already holds the present symbols by count ascending, ties by symbol (the
+// GPU ranks them with the whole wave).
+__host__ __device__ inline void huf_build(const uint32_t *cnt, HufCT &ct, HufWork &w, bool sorted = false) {
+  uint16_t *sym = w.sym;
+  uint32_t *f = w.f;
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < 129; ++s) {
+    ct.nb[s] = 0;
+    if (cnt[s]) {
+      if (!sorted) sym[n] = (uint16_t)s;
+      ++n;
+    }
+  }
+  // symbols by count ascending (insertion sort, stable: n <= 129)
+  for (uint32_t i = 1; !sorted && i < n; ++i) {
+    const uint16_t v = sym[i];
+    uint32_t j = i;
+    while (j > 0 && cnt[sym[j - 1]] > cnt[v]) {
+      sym[j] = sym[j - 1];
+      --j;
+    }
+    sym[j] = v;
+  }
+  // two-queue Huffman: leaves 0..n-1 (sorted), internal nodes n.. in creation order
+  for (uint32_t i = 0; i < n; ++i) f[i] = cnt[sym[i]];
+  uint32_t li = 0, ni = n, nn = n;
+  auto take = [&]() -> uint32_t {
+    if (li < n && (ni >= nn || f[li] <= f[ni])) return li++;
+    return ni++;
+  };
+  while (nn < 2 * n - 1) {
+    const uint32_t a = take(), b = take();
+    f[nn] = f[a] + f[b];
+    w.par[a] = w.par[b] = (uint16_t)nn;
+    ++nn;
+  }
+  // depths: the root (2n - 2) at 0, a node one deeper than its parent
+  uint32_t *bl = w.bl;
+  for (uint32_t d = 0; d < 64; ++d) bl[d] = 0;
+  w.dep[2 * n - 2] = 0;
+  for (int32_t i = (int32_t)(2 * n) - 3; i >= 0; --i) w.dep[i] = (uint8_t)(w.dep[w.par[i]] + 1);
+  uint32_t maxd = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t d = w.dep[i] < 63 ? w.dep[i] : 63;
+    ++bl[d];
+    if (d > maxd) maxd = d;
+  }
+  // limit to kHufMaxBits: leaves deeper than the limit move up to it, which
+  // over-subscribes the code by an integer number of 2^-kHufMaxBits units
+  // (the subtrees they came from were complete); each step below turns a
+  // shorter leaf into a node over itself and one leaf taken from the longest
+  // rank, -1 unit, until the Kraft sum is exactly 1 again (zlib's gen_bitlen)
+  if (maxd > kHufMaxBits) {
+    for (uint32_t d = kHufMaxBits + 1; d <= maxd; ++d) {
+      bl[kHufMaxBits] += bl[d];
+      bl[d] = 0;
+    }
+    uint64_t kraft = 0;  // in units of 2^-kHufMaxBits
+    for (uint32_t d = 1; d <= kHufMaxBits; ++d) kraft += (uint64_t)bl[d] << (kHufMaxBits - d);
+    while (kraft > (1ull << kHufMaxBits)) {  // (n <= 129 < 2^11 leaves: a shorter leaf always exists)
+      uint32_t d = kHufMaxBits - 1;
+      while (bl[d] == 0) --d;
+      --bl[d];
+      bl[d + 1] += 2;
+      --bl[kHufMaxBits];
+      --kraft;
+    }
+    maxd = kHufMaxBits;
+  }
+  // lengths: the most frequent symbols (sym[] ascending by count) get the shortest
+  uint32_t k = n;
+  for (uint32_t d = 1; d <= maxd; ++d)
+    for (uint32_t c = 0; c < bl[d]; ++c) ct.nb[sym[--k]] = (uint8_t)d;
+  ct.maxb = maxd;
+  ct.last = sym[0];
+  for (uint32_t i = 0; i < n; ++i)
+    if (sym[i] > ct.last) ct.last = sym[i];
+  // canonical codes
+  for (uint32_t d = 0; d < kHufMaxBits + 2; ++d) w.rank[d] = 0;
+  for (uint32_t d = 1; d <= maxd; ++d) w.rank[d] = bl[d];
+  uint32_t mn = 0;
+  for (uint32_t d = maxd; d > 0; --d) {
+    w.val[d] = mn;
+    mn = (mn + w.rank[d]) >> 1;
+  }
+  for (uint32_t s = 0; s <= ct.last; ++s)
+    if (ct.nb[s]) ct.code[s] = (uint16_t)w.val[ct.nb[s]]++;
+}
+
+// Huffman_Tree_Description in the direct representation: headerByte = 127 +
+// Number_of_Weights (the weights of symbols 0 .. last - 1, 4 bits each, first
+// in the high nibble; the last symbol's weight is implied).  Weight = maxb + 1
+// - length, 0 for an absent symbol.
+__host__ __device__ inline uint32_t huf_tree_desc(const HufCT &ct, uint8_t *dst) {
+  const uint32_t nw = ct.last;  // 1 .. 128
+  dst[0] = (uint8_t)(127 + nw);
+  for (uint32_t i = 0; i < nw; i += 2) {
+    const uint32_t w0 = ct.nb[i] ? ct.maxb + 1 - ct.nb[i] : 0;
+    const uint32_t w1 = (i + 1 < nw && ct.nb[i + 1]) ? ct.maxb + 1 - ct.nb[i + 1] : 0;
+    dst[1 + i / 2] = (uint8_t)(w0 << 4 | w1);
+  }
+  return 1 + (nw + 1) / 2;
+}
+
+// Bits of one Huffman stream of n literals (without the end mark).
+template <class LitAt>
+__host__ __device__ inline uint32_t huf_stream_bits(const HufCT &ct, LitAt lit_at, uint32_t a, uint32_t n) {
+  uint32_t b = 0;
+  for (uint32_t i = 0; i < n; ++i) b += ct.nb[lit_at(a + i)];
+  return b;
+}
+// One stream: literals [a, a + n) from the last to the first (the decoder
+// reads backwards and decodes them in order), closed by the end mark.
+template <class LitAt>
+__host__ __device__ inline uint32_t huf_stream(const HufCT &ct, LitAt lit_at, uint32_t a, uint32_t n, uint8_t *dst,
+                                               uint32_t cap) {
+  BitW bw{dst, dst + cap, 0, 0, false};
+  for (uint32_t i = n; i-- > 0;) {
+    const uint32_t x = lit_at(a + i);
+    bw.add(ct.code[x], ct.nb[x]);
+  }
+  if (!bw.close()) return 0;
+  return (uint32_t)(bw.p - dst);
+}
+
+// Literals_Section_Header of a Compressed_Literals_Block; returns its size.
+// Size_Format 00 (one stream, 10-bit sizes), 10 (four streams, 14-bit), 11
+// (four streams, 18-bit).
+__host__ __device__ inline uint32_t lit_hdr_size(uint32_t nlit, uint32_t csize, bool one) {
+  if (one) return 3;
+  return (nlit < (1u << 14) && csize < (1u << 14)) ? 4 : 5;
+}
+__host__ __device__ inline void put_huf_lit_header(uint8_t *d, uint32_t nlit, uint32_t csize, bool one) {
+  if (one) {  // 2 + 2 + 10 + 10 bits
+    const uint32_t v = 2u | 0u << 2 | nlit << 4 | csize << 14;
+    d[0] = (uint8_t)v; d[1] = (uint8_t)(v >> 8); d[2] = (uint8_t)(v >> 16);
+  } else if (lit_hdr_size(nlit, csize, false) == 4) {  // 2 + 2 + 14 + 14
+    const uint32_t v = 2u | 2u << 2 | nlit << 4 | csize << 18;
+    d[0] = (uint8_t)v; d[1] = (uint8_t)(v >> 8); d[2] = (uint8_t)(v >> 16); d[3] = (uint8_t)(v >> 24);
+  } else {  // 2 + 2 + 18 + 18
+    const uint64_t v = 2ull | 3ull << 2 | (uint64_t)nlit << 4 | (uint64_t)csize << 22;
+    for (int k = 0; k < 5; ++k) d[k] = (uint8_t)(v >> (8 * k));
+  }
+}
+// RLE_Literals_Block header, Size_Format 11 (3 bytes, 20-bit size), then the byte
+__host__ __device__ inline void put_rle_lit_header(uint8_t *d, uint32_t nlit) {
+  d[0] = (uint8_t)(0x0D | (nlit & 0xF) << 4);
+  d[1] = (uint8_t)(nlit >> 4);
+  d[2] = (uint8_t)(nlit >> 12);
+}
+
+// Sizes of a Huffman literals section for the literals whose Huffman table
+// is ct (stream bits sb[0..3], or sb[0] alone for one stream): section
+// size = header + tree + (jump table) + streams.
+__host__ __device__ inline uint32_t huf_section_size(const HufCT &ct, uint32_t nlit, const uint32_t *sb, bool one,
+                                                     uint32_t *ssz) {
+  const uint32_t tree = 1 + (ct.last + 1) / 2;
+  uint32_t streams = 0;
+  for (int k = 0; k < (one ? 1 : 4); ++k) {
+    ssz[k] = (sb[k] + 1 + 7) / 8;
+    streams += ssz[k];
+  }
+  const uint32_t csize = tree + (one ? 0 : 6) + streams;
+  return lit_hdr_size(nlit, csize, one) + csize;
+}
+
 // Headers.
 __host__ __device__ inline void put_block_header(uint8_t *d, bool last, uint32_t type, uint32_t size) {
   const uint32_t h = (last ? 1u : 0u) | type << 1 | size << 3;
@@ -284,6 +480,65 @@ __host__ __device__ inline void put_frame_header(uint8_t *d) {
   d[3] = 0xFD;
   d[4] = kFhd;
   d[5] = kWd;
+}
+
+// The literals section of a compressed block, serial (the CPU format test's
+// reference; k_zc_huff makes the same choice with the same pieces, in
+// parallel): Huffman when the literals are bytes < 128 and that section is
+// smaller than raw, RLE for one distinct byte, else raw.  dst holds at least
+// kLitHdr + n bytes.  Returns the section size.
+template <class LitAt>
+__host__ __device__ inline uint32_t encode_literals(LitAt lit_at, uint32_t n, uint8_t *dst) {
+  uint32_t hist[256] = {0};
+  for (uint32_t i = 0; i < n; ++i) ++hist[lit_at(i)];
+  uint32_t distinct = 0, high = 0;
+  for (uint32_t k = 0; k < 256; ++k)
+    if (hist[k]) {
+      ++distinct;
+      high = k;
+    }
+  auto raw = [&]() {
+    put_raw_lit_header(dst, n);
+    for (uint32_t i = 0; i < n; ++i) dst[kLitHdr + i] = (uint8_t)lit_at(i);
+    return kLitHdr + n;
+  };
+  if (n >= 32 && distinct == 1 && high < 128) {
+    put_rle_lit_header(dst, n);
+    dst[3] = (uint8_t)high;
+    return 4;
+  }
+  if (n < 32 || high >= 128) return raw();
+  HufCT ct;
+  HufWork hw;
+  huf_build(hist, ct, hw);
+  const bool one = n < 1024;
+  const uint32_t seg = one ? n : (n + 3) / 4;
+  uint32_t sb[4] = {0, 0, 0, 0}, ssz[4];
+  for (int k = 0; k < (one ? 1 : 4); ++k) {
+    const uint32_t a = k * seg, e = a + seg < n ? a + seg : n;
+    sb[k] = huf_stream_bits(ct, lit_at, a, e - a);
+  }
+  const uint32_t total = huf_section_size(ct, n, sb, one, ssz);
+  const uint32_t tree = 1 + (ct.last + 1) / 2;
+  const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
+  if (total >= kLitHdr + n || (one && csize >= 1024)) return raw();
+  const uint32_t hdr = lit_hdr_size(n, csize, one);
+  put_huf_lit_header(dst, n, csize, one);
+  huf_tree_desc(ct, dst + hdr);
+  uint32_t o = hdr + tree;
+  if (!one) {
+    for (int k = 0; k < 3; ++k) {
+      dst[o + 2 * k] = (uint8_t)ssz[k];
+      dst[o + 2 * k + 1] = (uint8_t)(ssz[k] >> 8);
+    }
+    o += 6;
+  }
+  for (int k = 0; k < (one ? 1 : 4); ++k) {
+    const uint32_t a = k * seg, e = a + seg < n ? a + seg : n;
+    huf_stream(ct, lit_at, a, e - a, dst + o, ssz[k]);
+    o += ssz[k];
+  }
+  return o;
 }
 
 }  // namespace zs

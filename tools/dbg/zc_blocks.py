@@ -24,7 +24,7 @@ for kind in ("zeros", "text"):
         data = np.zeros(256 << 10, np.uint8)
     else:
         rng = np.random.default_rng(1)
-        vocab = [bytes(rng.integers(97, 123, int(k))) for k in rng.integers(2, 11, 2000)]
+        vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
         data = np.frombuffer(b" ".join(vocab[i] for i in rng.integers(0, 2000, 80000))[:256 << 10], np.uint8).copy()
     ch = np.zeros(1, dtype=_lib.CHUNK_DTYPE)
     ch["length"] = data.size

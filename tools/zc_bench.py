@@ -7,7 +7,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from mapache_amd import _lib  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
@@ -23,7 +23,7 @@ for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text")
         ctx.fill_random(dp, n, 0x6d61706163686521)
     else:
         rng = np.random.default_rng(21)
-        vocab = [bytes(rng.integers(97, 123, int(k))) for k in rng.integers(2, 11, 2000)]
+        vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
         base = b" ".join(vocab[i] for i in rng.integers(0, 2000, 12_000_000))[:64 << 20]
         for o in range(0, n, len(base)):
             ctx.h2d(dp + o, np.frombuffer(base[:min(len(base), n - o)], np.uint8))
