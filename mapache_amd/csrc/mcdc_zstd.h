@@ -9,9 +9,11 @@
 // header (magic, descriptor 0x00, window descriptor 0x50) and blocks that are
 // either raw or compressed with
 //   * Raw_Literals_Block literals (3-byte header, Size_Format 11),
-//   * sequences coded with the predefined FSE distributions of RFC 8878
-//     §3.1.1.3.2.2 (Predefined_Mode for literal lengths, offsets and match
-//     lengths: no table descriptions),
+//   * sequences coded per symbol type (literal lengths, offsets, match
+//     lengths) with the predefined FSE distributions of RFC 8878
+//     §3.1.1.3.2.2 (Predefined_Mode) or with the block's own distribution
+//     (FSE_Compressed_Mode: normalized counts, table description), whichever
+//     is estimated smaller,
 //   * offsets always as Offset_Value = offset + 3 (no repeat codes);
 //   * literals raw, RLE (one distinct byte) or Huffman-coded (Compressed_
 //     Literals_Block: a length-limited canonical code, weights in the direct
@@ -21,6 +23,7 @@
 // storage.rs:87-94) reads them; the compressed bytes differ from libzstd's,
 // so parity is decode-equality.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>
@@ -83,12 +86,15 @@ __host__ __device__ inline uint32_t ml_bits(uint32_t code) {
 // Built exactly as the decoder's spread (RFC 8878 §4.1.1) defines the states,
 // in the encoder form of zstd's FSE_buildCTable: per symbol deltaNbBits /
 // deltaFindState, and the next-state table sorted by symbol.
-struct FseCT {
-  uint16_t state[64];
+template <uint32_t S>
+struct FseCTN {
+  uint16_t state[S];
   int32_t dfs[53];
   uint32_t dnb[53];
   uint32_t log;
 };
+using FseCT = FseCTN<64>;    // the predefined distributions (accuracy log <= 6)
+using FseCTL = FseCTN<512>;  // a block's own table (FSE_Compressed_Mode, log <= 9)
 struct ZTables {
   FseCT ll, ml, of;
 };
@@ -104,10 +110,11 @@ constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
 constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
                                  1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
-inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCT &ct) {
+template <uint32_t S>
+inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCTN<S> &ct) {
   const uint32_t size = 1u << tlog;
   uint32_t high = size - 1;
-  uint8_t sym[64];
+  uint8_t sym[S];
   uint32_t cumul[54];
   cumul[0] = 0;
   for (int u = 1; u <= nsym; ++u) {
@@ -163,6 +170,7 @@ struct BitW {
   uint64_t acc;    // pending bits
   uint32_t n;      // pending bit count (< 64)
   bool over;
+  bool wr = true;  // this lane stores (a wave running the writer in lockstep stores from one lane)
   __host__ __device__ void add(uint64_t v, uint32_t nb) {
     acc |= (v & ((nb >= 64) ? ~0ull : ((1ull << nb) - 1))) << n;
     n += nb;
@@ -170,7 +178,8 @@ struct BitW {
   }
   __host__ __device__ void flush() {
     while (n >= 8) {
-      if (p < end) *p = (uint8_t)acc; else over = true;
+      if (p >= end) over = true;
+      else if (wr) *p = (uint8_t)acc;
       ++p;
       acc >>= 8;
       n -= 8;
@@ -181,7 +190,8 @@ struct BitW {
     add(1, 1);
     flush();
     if (n) {
-      if (p < end) *p = (uint8_t)acc; else over = true;
+      if (p >= end) over = true;
+      else if (wr) *p = (uint8_t)acc;
       ++p;
       n = 0;
     }
@@ -192,17 +202,20 @@ struct BitW {
 struct FseState {
   uint32_t value;
 };
-__host__ __device__ inline void fse_init(FseState &st, const FseCT &ct, uint32_t s) {
+template <class CT>
+__host__ __device__ inline void fse_init(FseState &st, const CT &ct, uint32_t s) {
   const uint32_t nb = (ct.dnb[s] + (1u << 15)) >> 16;
   uint32_t v = (nb << 16) - ct.dnb[s];
   st.value = ct.state[(v >> nb) + ct.dfs[s]];
 }
-__host__ __device__ inline void fse_encode(BitW &bw, FseState &st, const FseCT &ct, uint32_t s) {
+template <class CT>
+__host__ __device__ inline void fse_encode(BitW &bw, FseState &st, const CT &ct, uint32_t s) {
   const uint32_t nb = (st.value + ct.dnb[s]) >> 16;
   bw.add(st.value, nb);
   st.value = ct.state[(st.value >> nb) + ct.dfs[s]];
 }
-__host__ __device__ inline void fse_flush(BitW &bw, const FseState &st, const FseCT &ct) { bw.add(st.value, ct.log); }
+template <class CT>
+__host__ __device__ inline void fse_flush(BitW &bw, const FseState &st, const CT &ct) { bw.add(st.value, ct.log); }
 
 // One sequence: literal length, match length (>= 3), offset (>= 1).
 // Packed in 64 bits: ll 21 | ml 21 | off 22 (block <= 128 KiB, window 2^20).
@@ -214,34 +227,49 @@ __host__ __device__ inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >>
 __host__ __device__ inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 42); }
 
 // Sequences_Section (RFC 8878 §3.1.1.3.2) of nseq sequences (seqs[i], in
-// order) with Predefined_Mode for all three symbol types, written at dst
-// (capacity cap).  Returns the section size, or 0 when it does not fit.
-template <class SeqAt>
-__host__ __device__ inline uint32_t encode_sequences(const ZTables &T, SeqAt seq_at, uint32_t nseq, uint8_t *dst,
-                                                     uint32_t cap) {
-  uint32_t h = 0;
-  if (cap < 4) return 0;
+// order) coded with the tables tll / tof / tml, written at dst (capacity
+// cap): the sequence count, the Symbol_Compression_Modes byte `modes`, the
+// table description desc[doff[k], + dlen[k]) of each type k (LL, OF, ML)
+// whose mode is FSE_Compressed, then the bitstream.  Returns the section
+// size, or 0 when it does not fit.  wr false: sizes only, nothing stored (a
+// wave running one writer in lockstep).
+template <class CLL, class COF, class CML, class SeqAt>
+__host__ __device__ inline uint32_t encode_sequences_with(const CLL &tll, const COF &tof, const CML &tml,
+                                                          uint32_t modes, const uint8_t *desc, const uint32_t *doff,
+                                                          const uint32_t *dlen, SeqAt seq_at, uint32_t nseq,
+                                                          uint8_t *dst, uint32_t cap, bool wr = true) {
+  uint32_t h = 0, ndesc = 0;
+  for (uint32_t k = 0; k < 3; ++k)
+    if (((modes >> (6 - 2 * k)) & 3) == 2) ndesc += dlen[k];
+  if (cap < 4 + ndesc) return 0;
+  auto put = [&](uint32_t v) {
+    if (wr) dst[h] = (uint8_t)v;
+    ++h;
+  };
   if (nseq < 128) {
-    dst[h++] = (uint8_t)nseq;
+    put(nseq);
   } else if (nseq < 0x7F00) {
-    dst[h++] = (uint8_t)((nseq >> 8) + 0x80);
-    dst[h++] = (uint8_t)nseq;
+    put((nseq >> 8) + 0x80);
+    put(nseq);
   } else {
-    dst[h++] = 0xFF;
-    dst[h++] = (uint8_t)(nseq - 0x7F00);
-    dst[h++] = (uint8_t)((nseq - 0x7F00) >> 8);
+    put(0xFF);
+    put(nseq - 0x7F00);
+    put((nseq - 0x7F00) >> 8);
   }
   if (nseq == 0) return h;
-  dst[h++] = 0x00;  // Symbol_Compression_Modes: Predefined_Mode x 3
-  BitW bw{dst + h, dst + cap, 0, 0, false};
+  put(modes);  // Symbol_Compression_Modes, then the descriptions of the FSE_Compressed types (LL, OF, ML)
+  for (uint32_t k = 0; k < 3; ++k)
+    if (((modes >> (6 - 2 * k)) & 3) == 2)
+      for (uint32_t j = 0; j < dlen[k]; ++j) put(desc[doff[k] + j]);
+  BitW bw{dst + h, dst + cap, 0, 0, false, wr};
   // the last sequence first (the decoder reads the stream backwards)
   uint64_t s = seq_at(nseq - 1);
   uint32_t ll = seq_ll(s), mb = seq_ml(s) - 3, ob = seq_off(s) + 3;
   uint32_t llc = ll_code(ll), mlc = ml_code(mb), ofc = highbit(ob);
   FseState sml, sof, sll;
-  fse_init(sml, T.ml, mlc);
-  fse_init(sof, T.of, ofc);
-  fse_init(sll, T.ll, llc);
+  fse_init(sml, tml, mlc);
+  fse_init(sof, tof, ofc);
+  fse_init(sll, tll, llc);
   bw.add(ll, ll_bits(llc));
   bw.add(mb, ml_bits(mlc));
   bw.add(ob, ofc);
@@ -253,19 +281,233 @@ __host__ __device__ inline uint32_t encode_sequences(const ZTables &T, SeqAt seq
     llc = ll_code(ll);
     mlc = ml_code(mb);
     ofc = highbit(ob);
-    fse_encode(bw, sof, T.of, ofc);
-    fse_encode(bw, sml, T.ml, mlc);
-    fse_encode(bw, sll, T.ll, llc);
+    fse_encode(bw, sof, tof, ofc);
+    fse_encode(bw, sml, tml, mlc);
+    fse_encode(bw, sll, tll, llc);
     bw.add(ll, ll_bits(llc));
     bw.add(mb, ml_bits(mlc));
     bw.add(ob, ofc);
     if (bw.over) return 0;
   }
-  fse_flush(bw, sml, T.ml);
-  fse_flush(bw, sof, T.of);
-  fse_flush(bw, sll, T.ll);
+  fse_flush(bw, sml, tml);
+  fse_flush(bw, sof, tof);
+  fse_flush(bw, sll, tll);
   if (!bw.close()) return 0;
   return (uint32_t)(bw.p - dst);
+}
+
+// The same with Predefined_Mode for all three symbol types.
+template <class SeqAt>
+__host__ __device__ inline uint32_t encode_sequences(const ZTables &T, SeqAt seq_at, uint32_t nseq, uint8_t *dst,
+                                                     uint32_t cap) {
+  const uint32_t none[3] = {0, 0, 0};
+  return encode_sequences_with(T.ll, T.of, T.ml, 0u, (const uint8_t *)nullptr, none, none, seq_at, nseq, dst, cap);
+}
+
+// ---- a block's own FSE tables (FSE_Compressed_Mode, RFC 8878 §4.1.1) -------
+// Per symbol type k (0 LL, 1 OF, 2 ML: the order of the modes byte and of the
+// descriptions): symbols, the largest accuracy log the format allows, and
+// the predefined distribution the choice is priced against.
+constexpr uint32_t kSeqNSym[3] = {36, 32, 53};
+constexpr uint32_t kSeqMaxLog[3] = {9, 8, 9};
+constexpr uint32_t kSeqDescMax = 80;  // bytes of one description (<= 53 symbols of <= 10 bits + 4)
+
+// Accuracy log for n symbols whose largest value is maxsym (zstd's
+// FSE_optimalTableLog: about log2(n) - 2, at least enough for the alphabet,
+// within [5, maxlog]).  n >= 2, maxsym >= 1.
+__host__ __device__ inline uint32_t fse_table_log(uint32_t n, uint32_t maxsym, uint32_t maxlog) {
+  const uint32_t hb = highbit(n - 1);
+  uint32_t tl = maxlog;
+  if (hb < 2 + tl) tl = hb >= 2 ? hb - 2 : 0;
+  uint32_t minb = highbit(maxsym) + 2;
+  if (hb + 1 < minb) minb = hb + 1;
+  if (minb > tl) tl = minb;
+  if (tl < 5) tl = 5;
+  if (tl > maxlog) tl = maxlog;
+  return tl;
+}
+
+// Normalized counts summing to 2^tl, every present symbol at least 1 (no
+// "less than 1" entries), the largest symbol absorbing the rounding.  false
+// when that leaves it below 1 (then the caller keeps the predefined table).
+__host__ __device__ inline bool fse_normalize(const uint32_t *cnt, uint32_t nsym, uint32_t total, uint32_t tl,
+                                              int16_t *norm) {
+  const uint32_t scale = 1u << tl;
+  int32_t sum = 0;
+  uint32_t big = 0, bigc = 0;
+  for (uint32_t s = 0; s < nsym; ++s) {
+    if (!cnt[s]) {
+      norm[s] = 0;
+      continue;
+    }
+    uint32_t v = (uint32_t)(((uint64_t)cnt[s] * scale + total / 2) / total);
+    if (v == 0) v = 1;
+    norm[s] = (int16_t)v;
+    sum += (int32_t)v;
+    if (cnt[s] > bigc) {
+      bigc = cnt[s];
+      big = s;
+    }
+  }
+  const int32_t fixed = norm[big] + ((int32_t)scale - sum);
+  if (fixed < 1) return false;
+  norm[big] = (int16_t)fixed;
+  return true;
+}
+
+// Bits to code cnt[] with the distribution norm[] (-1 = one state) at
+// accuracy log tl: sum of cnt * (tl - log2 states); huge when a present
+// symbol has no state.
+__host__ __device__ inline float fse_cost(const uint32_t *cnt, uint32_t ncnt, const int16_t *norm, uint32_t nnorm,
+                                          uint32_t tl) {
+  float b = 0;
+  for (uint32_t s = 0; s < ncnt; ++s) {
+    if (!cnt[s]) continue;
+    const int32_t n = s < nnorm ? (norm[s] == -1 ? 1 : norm[s]) : 0;
+    if (n <= 0) return 1e30f;
+    b += (float)cnt[s] * ((float)tl - log2f((float)n));
+  }
+  return b;
+}
+
+// FSE table description (zstd's FSE_writeNCount, read by RFC 8878 §4.1.1):
+// accuracy log - 5 in 4 bits, then per symbol its count + 1 in a variable
+// number of bits (one fewer for small values), zero runs as 2-bit repeat
+// flags, up to the last symbol with a nonzero count.  Returns its bytes.
+__host__ __device__ inline uint32_t fse_write_ncount(const int16_t *norm, uint32_t nsym, uint32_t tl, uint8_t *dst) {
+  uint32_t out = 0, nb = 4;
+  uint64_t bits = tl - 5;
+  auto drain = [&]() {
+    while (nb >= 8) {
+      dst[out++] = (uint8_t)bits;
+      bits >>= 8;
+      nb -= 8;
+    }
+  };
+  int32_t remaining = (1 << tl) + 1, threshold = 1 << tl;
+  uint32_t nbits = tl + 1, s = 0;
+  bool prev0 = false;
+  while (s < nsym && remaining > 1) {
+    if (prev0) {
+      uint32_t start = s;
+      while (s < nsym && !norm[s]) ++s;
+      while (s >= start + 24) {
+        start += 24;
+        bits |= 0xFFFFull << nb;
+        nb += 16;
+        drain();
+      }
+      while (s >= start + 3) {
+        start += 3;
+        bits |= 3ull << nb;
+        nb += 2;
+      }
+      bits |= (uint64_t)(s - start) << nb;
+      nb += 2;
+      drain();
+    }
+    int32_t count = norm[s++];
+    const int32_t mx = (2 * threshold - 1) - remaining;
+    remaining -= count < 0 ? -count : count;
+    ++count;
+    if (count >= threshold) count += mx;
+    bits |= (uint64_t)(uint32_t)count << nb;
+    nb += nbits;
+    nb -= (count < mx) ? 1u : 0u;
+    prev0 = count == 1;
+    while (remaining < threshold) {
+      --nbits;
+      threshold >>= 1;
+    }
+    drain();
+  }
+  if (nb) dst[out++] = (uint8_t)bits;
+  return out;
+}
+
+// The choice for one block's sequences, from the code histograms: per symbol
+// type the predefined table or the block's own (when its estimated bits plus
+// its description are fewer; only for 32 or more sequences with two or more
+// distinct codes).  The tables themselves are built by the caller from
+// norm / tl (fse_build on the host, k_zc_encode's wave on the GPU).
+//
+// The counts may cover several blocks (the GPU plans one table set for the 64
+// blocks of a wave, each of which then carries the descriptions): nblk blocks
+// pay the descriptions, and the accuracy log follows the mean block's count.
+struct SeqPlan {
+  int16_t norm[3][53];
+  uint32_t tl[3];
+  uint32_t own[3];               // 1: FSE_Compressed_Mode, 0: Predefined_Mode
+  uint32_t doff[3], dlen[3];     // description of type k: desc[doff[k], + dlen[k])
+  uint32_t modes, ndesc;
+  uint8_t desc[3 * kSeqDescMax];
+};
+__host__ __device__ inline void seq_plan(const uint32_t *cll, const uint32_t *cof, const uint32_t *cml, uint32_t nseq,
+                                         SeqPlan &P, uint32_t nblk = 1) {
+  const uint32_t *cnt[3] = {cll, cof, cml};
+  const int16_t *pre[3] = {kLLNorm, kOFNorm, kMLNorm};
+  const uint32_t npre[3] = {36, 29, 53}, tpre[3] = {6, 5, 6}, shift[3] = {6, 4, 2};
+  P.modes = 0;
+  P.ndesc = 0;
+  for (int k = 0; k < 3; ++k) {
+    P.own[k] = 0;
+    P.tl[k] = tpre[k];
+    P.doff[k] = P.ndesc;
+    P.dlen[k] = 0;
+    uint32_t distinct = 0, maxsym = 0;
+    for (uint32_t s = 0; s < kSeqNSym[k]; ++s)
+      if (cnt[k][s]) {
+        ++distinct;
+        maxsym = s;
+      }
+    const uint32_t mean = nseq / (nblk ? nblk : 1);
+    if (mean < 32 || distinct < 2) continue;
+    const uint32_t tl = fse_table_log(mean, maxsym, kSeqMaxLog[k]);
+    if (!fse_normalize(cnt[k], maxsym + 1, nseq, tl, P.norm[k])) continue;
+    uint8_t *d = P.desc + P.ndesc;
+    const uint32_t nd = fse_write_ncount(P.norm[k], maxsym + 1, tl, d);
+    const float own = fse_cost(cnt[k], maxsym + 1, P.norm[k], maxsym + 1, tl) + 8.0f * (float)nd * (float)nblk;
+    const float predef = fse_cost(cnt[k], maxsym + 1, pre[k], npre[k], tpre[k]);
+    if (own >= predef) continue;
+    for (uint32_t s = maxsym + 1; s < 53; ++s) P.norm[k][s] = 0;
+    P.own[k] = 1;
+    P.tl[k] = tl;
+    P.dlen[k] = nd;
+    P.ndesc += nd;
+    P.modes |= 2u << shift[k];
+  }
+}
+
+// Serial (host) form of the whole section with the planned tables: the CPU
+// format test's reference for k_zc_encode.
+template <class SeqAt>
+inline uint32_t encode_sequences_auto(const ZTables &T, SeqAt seq_at, uint32_t nseq, uint8_t *dst, uint32_t cap,
+                                      SeqPlan *plan_out = nullptr) {
+  uint32_t c[3][53] = {{0}};
+  for (uint32_t i = 0; i < nseq; ++i) {
+    const uint64_t s = seq_at(i);
+    ++c[0][ll_code(seq_ll(s))];
+    ++c[1][highbit(seq_off(s) + 3)];
+    ++c[2][ml_code(seq_ml(s) - 3)];
+  }
+  SeqPlan P;
+  seq_plan(c[0], c[1], c[2], nseq, P);
+  if (plan_out) *plan_out = P;
+  static FseCTL t[3];
+  const FseCT *pre[3] = {&T.ll, &T.of, &T.ml};
+  for (int k = 0; k < 3; ++k) {
+    if (P.own[k]) {
+      fse_build(P.norm[k], 53, P.tl[k], t[k]);
+    } else {
+      for (uint32_t u = 0; u < 64; ++u) t[k].state[u] = pre[k]->state[u];
+      for (uint32_t u = 0; u < 53; ++u) {
+        t[k].dfs[u] = pre[k]->dfs[u];
+        t[k].dnb[u] = pre[k]->dnb[u];
+      }
+      t[k].log = pre[k]->log;
+    }
+  }
+  return encode_sequences_with(t[0], t[1], t[2], P.modes, P.desc, P.doff, P.dlen, seq_at, nseq, dst, cap);
 }
 
 // ---- Huffman-coded literals (RFC 8878 §3.1.1.3.1, §4.2) ------------------

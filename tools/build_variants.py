@@ -1,5 +1,6 @@
 """Build library variants for on-box A/B runs: one .so per -D set, into ablib/
-(not the product library; MCDC_LIBRARY selects one).
+(not the product library; MCDC_LIBRARY selects one; MCDC_AB_DIR=abship puts
+them where gpurun sends them).
 usage: python tools/build_variants.py name:DEF=1,DEF2=0 ..."""
 import os
 import subprocess
@@ -12,15 +13,17 @@ from mapache_amd import build as B  # noqa: E402
 
 def one(spec):
     name, _, defs = spec.partition(":")
-    out = os.path.join(B.ROOT, "ablib", name + ".so")
+    out = os.path.join(B.ROOT, OUTDIR, name + ".so")
     cmd = [B.HIPCC, *B.CXXFLAGS, *[f"-D{d}" for d in defs.split(",") if d], "-fPIC", "-shared",
            f"-I{os.path.join(B.ROOT, 'include')}", "-o", out, *[os.path.join(B.HERE, x) for x in B.LIB_SRCS]]
     subprocess.run(cmd, check=True, cwd=B.ROOT)
     return out
 
 
+OUTDIR = os.environ.get("MCDC_AB_DIR", "ablib")  # (abship/: variants sent to the GPU box)
+
 if __name__ == "__main__":
-    os.makedirs(os.path.join(B.ROOT, "ablib"), exist_ok=True)
+    os.makedirs(os.path.join(B.ROOT, OUTDIR), exist_ok=True)
     with ThreadPoolExecutor(4) as ex:
         for o in ex.map(one, sys.argv[1:]):
             print(o)
