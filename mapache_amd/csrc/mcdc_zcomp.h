@@ -13,7 +13,7 @@ constexpr uint64_t kZcBlock = 16384;               // zstd block: 16 KiB of one 
 constexpr uint32_t kZcSeqCap = 4096;               // sequences per block: a 16 KiB block of 4-byte matches
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
 #ifndef MCDC_ZC_RUN
-#define MCDC_ZC_RUN 4  // (compile-time A/B knob)
+#define MCDC_ZC_RUN 2  // (compile-time A/B knob; tools/build_variants.py)
 #endif
 constexpr uint32_t kZcRun = MCDC_ZC_RUN;           // blocks parsed in a row by one wave (table kept)
 constexpr uint64_t kZcBatchBlocks = 65536;         // blocks per batch (1 GiB; more for a longer chunk)
