@@ -256,8 +256,9 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
 /* SecureStorage::compress (storage.rs:74-84) of every chunk of a boundary
  * list on the GPU: frame i is a zstd frame of chunk i in the crate's layout
  * (magic, Frame_Header_Descriptor 0x00: no content size, no checksum; window
- * 2^20 = storage.rs:31) of 16 KiB blocks, each compressed (raw literals,
- * sequences with the predefined FSE tables) or raw when that is not smaller.
+ * 2^20 = storage.rs:31) of 16 KiB blocks, each compressed (Huffman / RLE /
+ * raw literals; sequences with per-block or predefined FSE tables) or raw
+ * when that is not smaller.
  * mapache's decoder (zstd, window_log_max 20, :87-94) reads them; the bytes
  * differ from libzstd's level 3 (parity = decode-equality, ratio reported by
  * the bench).  Frames are written back to back from d_out (no alignment);

@@ -63,7 +63,12 @@ constexpr uint32_t kHtLog = MCDC_ZC_HLOG, kHt = 1u << kHtLog;
 static_assert(2 * kZcBlock <= 0xFFFF + 1, "16-bit positions");
 
 __device__ __forceinline__ uint32_t ld4(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
-__device__ __forceinline__ uint32_t zhash(uint32_t v) { return (v * 2654435761u) >> (32 - kHtLog); }
+// Hash of the 5 bytes at a position (4 in v, the fifth in b4): a 5-byte key
+// keeps 4-byte coincidences out of the table (tools/zc_model.cpp: text
+// 2.21 -> 2.25, CSV-like records 2.92 -> 3.05).
+__device__ __forceinline__ uint32_t zhash(uint32_t v, uint32_t b4) {
+  return (v * 2654435761u + (b4 & 0xFFu) * 0x85EBCA77u) >> (32 - kHtLog);
+}
 // Positions go into the table with plain 16-bit LDS stores (there is no
 // 16-bit max atomic), so when lanes of one store collide on a slot the
 // hardware keeps one of them; the slot must end at the largest (the latest
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
       for (int j = 0; j < 8; ++j) {
         const uint32_t q = q0 + 64 * j + lane;
         ok[j] = q + 4 <= prime;  // (the block's own bytes are not read here)
-        h[j] = ok[j] ? zhash(ld4(p0 + q)) : 0u;
+        h[j] = ok[j] ? zhash(ld4(p0 + q), p0[q + 4]) : 0u;  // (q + 4 <= prime: byte q + 4 is the block's own at worst)
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
       x1 = *reinterpret_cast<const uint4 *>(p0 + p + 16);
     }
     const uint32_t v = full ? x0.x : ok ? ld4(p0 + p) : 0u;
-    const uint32_t h = zhash(v);
+    const uint32_t h = zhash(v, full ? x0.y : p + 5 <= end ? p0[p + 4] : 0u);
     const uint32_t cand = ok ? ht[h] : 0u;
     {  // (issued after every lane's read: one wave, in order)
       volatile uint16_t *vt = ht;

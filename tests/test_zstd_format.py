@@ -1,5 +1,5 @@
 """The zstd format pieces of the GPU compressor (mapache_amd/csrc/mcdc_zstd.h:
-predefined FSE tables, sequence bitstream, literal / sequence / block / frame
+predefined and per-block FSE tables (table descriptions), sequence bitstream, literal / sequence / block / frame
 headers) on the CPU: tests/cpp/test_zstd_format builds frames from synthetic
 sequences (every literal-length, match-length and offset code, the 3-byte
 sequence-count header) and from a greedy LZ parse of text, random, zero,

@@ -2,12 +2,14 @@
 random stream and on the bench's synthetic text, chunked at 16/64/256 KiB;
 device-resident in and out.  Usage: python tools/zc_bench.py [GiB] [steps]"""
 import json
+import os
 import sys
 import time
 
 import numpy as np
 
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from mapache_amd import _lib  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
@@ -17,10 +19,16 @@ n = int(gib * (1 << 30))
 p = _lib.params(16384, 65536, 262144, 1)
 ctx = _lib.Context(0, n + (1 << 20))
 res = {}
-for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text")):
+for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records")):
     dp = ctx.device_alloc(n)
     if kind == "random":
         ctx.fill_random(dp, n, 0x6d61706163686521)
+    elif kind == "records":  # CSV-like rows (tests/test_gpu_zcomp.py _records), 64 MiB repeated
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_gpu_zcomp import _records
+        base = _records(64 << 20).tobytes()
+        for o in range(0, n, len(base)):
+            ctx.h2d(dp + o, np.frombuffer(base[:min(len(base), n - o)], np.uint8))
     else:
         rng = np.random.default_rng(21)
         vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
