@@ -313,7 +313,9 @@ int mcdc_pack_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_b
  *   - a stored blob is SecureStorage::encode'd (:182; store->key NULL =
  *     SecureStorage::build()) and added to the packer, which is flushed once
  *     it holds more than store->max_pack_size bytes (:185-192) and once at the
- *     end of the call (the end of the snapshot: Repository::flush).
+ *     end of the call (the end of the snapshot: Repository::flush);
+ *     with store->gpu_compress the compression runs on the GPU (packs whose
+ *     blobs decode to the same bytes; IDs, dedup and pack layout unchanged).
  * data: host memory or a device pointer (n bytes); files: extents in it (the
  * chunked ones must not overlap).  Randomness is the caller's (OsRng in the
  * crate): store->nonces, 12 bytes per stored blob in storing order (unused
@@ -337,6 +339,10 @@ typedef struct {
   size_t nheader_nonces;
   const uint8_t *padding;       /* 36 B per padding header entry */
   size_t npadding;
+  uint32_t gpu_compress;        /* 0: zstd level 3 on host threads (the crate's bytes);
+                                   1: mcdc_zstd_compress_device in HBM (frames mapache's
+                                   decoder reads, not byte-equal to level 3), then the
+                                   seal in HBM: the whole save path on the GPU */
 } mcdc_store;
 struct mcdc_index;
 int mcdc_save_files(struct mcdc_ctx *ctx, const mcdc_params *params, struct mcdc_index *ix,

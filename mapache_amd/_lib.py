@@ -47,7 +47,7 @@ class McdcStore(ctypes.Structure):
     repository's max pack size and the caller's randomness."""
     _fields_ = [("key", ctypes.c_void_p), ("max_pack_size", ctypes.c_uint64), ("nonces", ctypes.c_void_p),
                 ("nnonces", ctypes.c_size_t), ("header_nonces", ctypes.c_void_p), ("nheader_nonces", ctypes.c_size_t),
-                ("padding", ctypes.c_void_p), ("npadding", ctypes.c_size_t)]
+                ("padding", ctypes.c_void_p), ("npadding", ctypes.c_size_t), ("gpu_compress", ctypes.c_uint32)]
 
 
 PACK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("nblobs", "<u8"), ("meta_size", "<u8"),
@@ -453,10 +453,13 @@ class Context:
     # --------------------------------------------------------- save path --
     @_locked
     def save_files(self, p: "McdcParams", index: "Index", data, offsets, lengths, key=None, nonces=None,
-                   header_nonces=None, padding=None, max_pack_size: int = 16 << 20, n: int | None = None):
+                   header_nonces=None, padding=None, max_pack_size: int = 16 << 20, n: int | None = None,
+                   gpu_compress: bool = False):
         """The Archiver's save path for a run of files (mcdc_save_files): data is
         a host array (or a device pointer with n bytes); file f = data[offsets[f],
-        + lengths[f]).  Returns (ids_per_file: list of (k, 32) uint8 arrays,
+        + lengths[f]); gpu_compress: compress with the GPU zstd kernels in HBM
+        (decode-equal blobs) instead of level 3 on host threads.  Returns
+        (ids_per_file: list of (k, 32) uint8 arrays,
         is_new per blob, packed bytes, PACK_DTYPE records)."""
         if isinstance(data, int):
             dptr, nbytes, keep = data, int(n), None
@@ -471,7 +474,7 @@ class Context:
         kbuf = ctypes.create_string_buffer(k, len(k)) if k else None
         st = McdcStore(ctypes.addressof(kbuf) if k else None, max_pack_size,
                        arrs[0].ctypes.data, arrs[0].size // NONCE_BYTES, arrs[1].ctypes.data,
-                       arrs[1].size // NONCE_BYTES, arrs[2].ctypes.data, arrs[2].size // 36)
+                       arrs[1].size // NONCE_BYTES, arrs[2].ctypes.data, arrs[2].size // 36, int(bool(gpu_compress)))
         fb = np.zeros(nf + 1, np.uint64)
         bcap = int(sum(int(x) // max(p.min_size - 1, 1) + 2 for x in ext[:, 1])) if nf else 1
         ids = np.zeros((max(bcap, 1), 32), np.uint8)

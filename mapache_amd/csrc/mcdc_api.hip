@@ -1600,9 +1600,44 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
       sids.insert(sids.end(), ids + 32 * i, ids + 32 * i + 32);
     }
   types.assign(std::max<size_t>(m, 1), 0);  // BlobType::Data (processor.rs:191)
+  std::vector<uint64_t> eo(m + 1, 0);
+  std::vector<uint8_t> enc;
+  std::vector<mcdc_blob> eext(m);
+  if (store->gpu_compress && m) {
+    // SecureStorage::encode in HBM: the GPU compressor over the stored blobs
+    // of the device copy, then the seal; only the encoded blobs come back
+    std::vector<mcdc_chunk> sch(m);
+    for (size_t k = 0; k < m; ++k) sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
+    std::vector<mcdc_blob> fr(m);
+    size_t bound = 0, cbytes = 0;
+    rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, nullptr, 0, &bound, fr.data());
+    if (rc == MCDC_E_CAPACITY) {
+      if ((rc = ensure(ctx, ctx->enc_in, std::max<size_t>(bound, 1))) == MCDC_OK)
+        rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->enc_in.p, bound, &cbytes, fr.data());
+    }
+    if (!rc && store->key) {
+      const size_t scap = cbytes + (size_t)kAeadOverhead * m;
+      if ((rc = ensure(ctx, ctx->enc_out, scap)) == MCDC_OK)
+        rc = aead_run(ctx, 0, store->key, ctx->enc_in.p, cbytes, fr.data(), m, store->nonces, ctx->enc_out.p, scap,
+                      eo.data(), nullptr);
+    } else if (!rc) {
+      for (size_t k = 0; k < m; ++k) eo[k] = fr[k].offset;
+      eo[m] = cbytes;
+    }
+    if (rc) {
+      rollback();
+      return rc;
+    }
+    enc.resize(std::max<uint64_t>(eo[m], 1));
+    if (eo[m])
+      HIP_TRY(hipMemcpyAsync(enc.data(), store->key ? ctx->enc_out.p : ctx->enc_in.p, eo[m], hipMemcpyDeviceToHost,
+                             ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (size_t k = 0; k < m; ++k) eext[k] = store->key ? mcdc_blob{eo[k], eo[k + 1] - eo[k]} : fr[k];
+  }
   std::vector<uint8_t> staged;
   const uint8_t *src = (const uint8_t *)data;
-  if (!host_in && m) {  // device input: bring the new blobs over (the zstd stage runs on the host)
+  if (!host_in && m && !store->gpu_compress) {  // device input: bring the new blobs over (the zstd stage runs on the host)
     size_t tot = 0;
     for (auto &e : sext) tot += e.length;
     staged.resize(std::max<size_t>(tot, 1));
@@ -1618,11 +1653,10 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   }
   const size_t src_n = host_in ? n : staged.size();
   // SecureStorage::encode of every stored blob (:182)
-  std::vector<uint64_t> eo(m + 1, 0);
   size_t ecap = 0;
   for (auto &e : sext) ecap += e.length + e.length / 64 + 64;
-  std::vector<uint8_t> enc(std::max<size_t>(ecap, 1));
-  if (m) {
+  if (!store->gpu_compress) enc.resize(std::max<size_t>(ecap, 1));
+  if (m && !store->gpu_compress) {
     rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), ecap, eo.data());
     if (rc == MCDC_E_CAPACITY) {
       enc.resize(std::max<uint64_t>(eo[m], 1));
@@ -1634,8 +1668,8 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
       return rc;
     }
   }
-  std::vector<mcdc_blob> eext(m);
-  for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
+  if (!store->gpu_compress)
+    for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
   // Packer::add_blob + flush (:185-192) and the final flush
   size_t pb = 0, np = 0;
   rc = mcdc_pack_blobs(ctx, store->key, enc.data(), eo[m], eext.data(), sids.data(), types.data(), m,

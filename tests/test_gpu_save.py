@@ -167,3 +167,59 @@ def test_capacity_error_leaves_index_unchanged(ctx):
         assert nb.value > 3 and pb.value > 100
         got = ctx.save_files(p, ix, data, offs, lens, None, None, None, pad, max_pack_size=1 << 20)
         assert len(ix) == int(got[1].sum()) and got[2].size == pb.value
+
+
+def _text(n, seed):
+    rng = np.random.default_rng(seed)
+    vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
+    return np.frombuffer(b" ".join(vocab[i] for i in rng.integers(0, 2000, n // 4 + 16))[:n], np.uint8).copy()
+
+
+@pytest.mark.parametrize("key", [None, KEY], ids=["no-key", "key"])
+@pytest.mark.parametrize("device_in", [False, True], ids=["host-in", "device-in"])
+def test_gpu_compressed_save_path(ctx, key, device_in):
+    """store.gpu_compress: the blobs are compressed by the GPU zstd kernels in
+    HBM and sealed there.  IDs, the dedup decisions and the order of the stored
+    blobs are the host path's (oracle.save_files); the encoded bytes are the
+    GPU compressor's, so parity is decode-equality: every pack parses
+    (Packer::parse_header), each blob decodes (SecureStorage::decode: open,
+    then zstd within 2^20) to bytes whose BLAKE3 is its ID, in storing order,
+    and the text files' blobs come out compressed."""
+    files = _files() + [_text(3 << 20, 4), _text(100_000, 5)]
+    files.append(files[-2].copy())  # a repeated text file: stored once
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    nonces, hn, pad = _rand(1, 4000, 12), _rand(2, 64, 12), _rand(3, 64 * 63, 36)
+    with ctx.index_create() as ix:
+        if device_in:
+            dp = ctx.device_alloc(data.size)
+            ctx.h2d(dp, data)
+            got = ctx.save_files(p, ix, dp, offs, lens, key, nonces, hn, pad, max_pack_size=1 << 20, n=data.size,
+                                 gpu_compress=True)
+        else:
+            got = ctx.save_files(p, ix, data, offs, lens, key, nonces, hn, pad, max_pack_size=1 << 20,
+                                 gpu_compress=True)
+    ids, new, out, packs = got
+    r_ids, r_new, _ = O.save_files(O.Params(*P16), files, None, key, nonces, hn, pad, max_pack_size=1 << 20)
+    assert len(ids) == len(r_ids)
+    for f, (a, b) in enumerate(zip(ids, r_ids)):
+        assert a.shape == b.shape and (a == b).all(), f
+    assert (new == r_new).all()
+    stored = [x.tobytes() for x in np.concatenate(ids)[new]]
+    seen, at, enc_text, raw_text = [], 0, 0, 0
+    text_ids = {x.tobytes() for f in (12, 13) for x in ids[f]}
+    for k, pk in enumerate(packs):
+        assert int(pk["offset"]) == at
+        body = out[at:at + int(pk["length"])].tobytes()
+        assert bytes(pk["id"]) == O.blake3(np.frombuffer(body, np.uint8))
+        for bid, typ, off, ln in O.parse_header(body, key):
+            dec = O.storage_decode(body[off:off + ln], key, size_hint=1 << 20)
+            assert O.blake3(np.frombuffer(dec, np.uint8)) == bid and typ == 0
+            seen.append(bid)
+            if bid in text_ids:
+                enc_text += ln
+                raw_text += len(dec)
+        at += int(pk["length"])
+    assert at == out.size
+    assert seen == stored
+    assert raw_text > 0 and enc_text < raw_text / 1.8, (enc_text, raw_text)
