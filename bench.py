@@ -498,7 +498,8 @@ def encode(ctx, gib: float, steps: int) -> dict:
     ok_o = all(O.decrypt_with_key(bytes(range(32)), enc[int(oo[i]):int(oo[i + 1])].tobytes()) is not None
                for i in pick)
     gpu = gpu_encode_text(ctx, data, ch, nz, steps, rng)
-    return {"gpu_compress": gpu,
+    save = save_path_text(ctx, base, n, steps)
+    return {"gpu_compress": gpu, "save_path": save,
             "bytes": n, "blobs": int(len(ch)), "sealed_bytes": int(oo[-1]), "ratio": round(n / int(oo[-1]), 3),
             "encode_ms": round(dte * 1e3, 2), "encode_gib_s": round(n / dte / GIB, 3),
             "decode_ms": round(dtd * 1e3, 2), "decode_gib_s": round(n / dtd / GIB, 3),
@@ -507,6 +508,45 @@ def encode(ctx, gib: float, steps: int) -> dict:
                     "sealing on the GPU, H2D and D2H included",
             "data": "synthetic text, 2 000-word vocabulary, 64 MiB pattern repeated (repeats lie beyond the "
                     "1 MiB window)"}
+
+
+def save_path_text(ctx, base: bytes, n: int, steps: int) -> dict:
+    """mcdc_save_files (the composed save path: size gate, chunk, IDs, dedup,
+    encode, packs) over n bytes of text in 4 MiB files from device memory,
+    with a key and a fresh index per call (every blob new), encode by host
+    zstd level 3 vs the GPU compressor (store.gpu_compress).  Each 64 MiB
+    copy of the text pattern is XOR-ed with its index so no copy dedups
+    against another.  Wall clock of the call: packs come back to host memory."""
+    from mapache_amd import _lib
+    b = np.frombuffer(base, np.uint8)
+    data = np.concatenate([b ^ np.uint8(k % 31 + 1) for k in range(n // b.size)])
+    fsz = 4 << 20
+    offs = np.arange(0, n, fsz, dtype=np.uint64)
+    lens = np.minimum(fsz, n - offs).astype(np.uint64)
+    p = _lib.params(*PARAMS)
+    key = bytes(range(32))
+    rng = np.random.default_rng(5)
+    nonces = rng.integers(0, 256, (n // (PARAMS[0] - 1) + len(offs) + 2, 12), dtype=np.uint8)
+    hn, pad = rng.integers(0, 256, (4096, 12), dtype=np.uint8), rng.integers(0, 256, (4096 * 63, 36), dtype=np.uint8)
+    dp = ctx.device_alloc(n)
+    out = {}
+    try:
+        ctx.h2d(dp, data)
+        for mode in ("host_zstd", "gpu_compress"):
+            def call():
+                with ctx.index_create() as ix:
+                    return ctx.save_files(p, ix, dp, offs, lens, key, nonces, hn, pad, n=n,
+                                          gpu_compress=mode == "gpu_compress")
+            dt, (ids, new, packed, packs) = _timed(call, steps, 1)
+            out[mode] = {"ms": round(dt * 1e3, 1), "gib_s": round(n / dt / GIB, 2), "blobs": int(new.size),
+                         "stored": int(new.sum()), "packs": int(len(packs)), "packed_bytes": int(packed.size),
+                         "ratio": round(n / packed.size, 3)}
+    finally:
+        ctx.device_free(dp)
+    out["note"] = ("mcdc_save_files from device memory, 4 MiB files of synthetic text, with a key; wall clock "
+                   "incl. the packs' D2H and host packing; gpu_compress: compress + seal in HBM "
+                   "(decode-equal frames, tests/test_gpu_save.py)")
+    return out
 
 
 def gpu_encode_text(ctx, data: np.ndarray, ch: np.ndarray, nz: np.ndarray, steps: int, rng) -> dict:
