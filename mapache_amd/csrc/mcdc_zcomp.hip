@@ -79,12 +79,19 @@ __device__ __forceinline__ uint32_t zhash(uint32_t v, uint32_t b4) {
 // top of the next stride), so its latency is off the critical path.  Later
 // stores of larger positions only raise a slot, so a lane seeing a value >= its
 // own is done.  Called by the whole wave (ballot).
+// (relaxed workgroup-scope atomics: LDS loads and stores the compiler may not
+// merge or forward -- a volatile generic pointer compiled to flat accesses)
+__device__ __forceinline__ void ht_st(uint16_t *ht, uint32_t h, uint32_t v) {
+  __hip_atomic_store(ht + h, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t ht_ld(uint16_t *ht, uint32_t h) {
+  return __hip_atomic_load(ht + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void ht_fix(uint16_t *ht, uint32_t h, uint32_t v, bool ok, uint32_t rb) {
-  volatile uint16_t *t = ht;
   bool again = ok && rb < v;
   while (__ballot(again)) {
-    if (again) t[h] = (uint16_t)v;
-    again = again && t[h] < v;
+    if (again) ht_st(ht, h, v);
+    again = again && ht_ld(ht, h) < v;
   }
 }
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -218,7 +225,6 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
   const uint8_t *p0 = base + B.src - prime;   // positions are relative to p0
   const uint32_t end = prime + B.len;
   if (r == 0) {  // a run's first block: the table primed with the previous 16 KiB
-    volatile uint16_t *vt = ht;
     for (uint32_t q0 = 0; q0 < prime; q0 += 8 * 64) {  // (prime: 0 or 16 KiB, a multiple of 512)
       uint32_t h[8], rb[8];
       bool ok[8];
@@ -230,9 +236,9 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (ok[j]) vt[h[j]] = (uint16_t)(q0 + 64 * j + lane + 1);
+        if (ok[j]) ht_st(ht, h[j], q0 + 64 * j + lane + 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rb[j] = vt[h[j]];
+      for (int j = 0; j < 8; ++j) rb[j] = ht_ld(ht, h[j]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) ht_fix(ht, h[j], q0 + 64 * j + lane + 1, ok[j], rb[j]);
     }
@@ -297,9 +303,8 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
     const uint32_t h = zhash(v, full ? x0.y : p + 5 <= end ? p0[p + 4] : 0u);
     const uint32_t cand = ok ? ht[h] : 0u;
     {  // (issued after every lane's read: one wave, in order)
-      volatile uint16_t *vt = ht;
-      if (ok) vt[h] = (uint16_t)(p + 1);
-      frb = ok ? vt[h] : 0u;
+      if (ok) ht_st(ht, h, p + 1);
+      frb = ok ? ht_ld(ht, h) : 0u;
       fh = h;
       fv = p + 1;
       fok = ok;
