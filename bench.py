@@ -530,24 +530,22 @@ def save_path_text(ctx, base: bytes, n: int, steps: int) -> dict:
     hn, pad = rng.integers(0, 256, (4096, 12), dtype=np.uint8), rng.integers(0, 256, (4096 * 63, 36), dtype=np.uint8)
     dp = ctx.device_alloc(n)
     out = {}
-    obuf = np.ones(int(n * 1.01) + 4096 * len(offs) + (1 << 16), np.uint8)  # (reused: pages faulted in once)
     try:
         ctx.h2d(dp, data)
         for mode in ("host_zstd", "gpu_compress"):
             def call():
                 with ctx.index_create() as ix:
                     return ctx.save_files(p, ix, dp, offs, lens, key, nonces, hn, pad, n=n,
-                                          gpu_compress=mode == "gpu_compress", out_buf=obuf)
+                                          gpu_compress=mode == "gpu_compress")
             dt, (ids, new, packed, packs) = _timed(call, steps, 1)
             out[mode] = {"ms": round(dt * 1e3, 1), "gib_s": round(n / dt / GIB, 2), "blobs": int(new.size),
                          "stored": int(new.sum()), "packs": int(len(packs)), "packed_bytes": int(packed.size),
                          "ratio": round(n / packed.size, 3)}
     finally:
         ctx.device_free(dp)
-    out["note"] = ("mcdc_save_files from device memory, 4 MiB files of synthetic text, with a key, fresh index per "
-                   "call, output buffer reused; wall clock incl. the packs' D2H (pageable); host_zstd: level 3 on "
-                   "16 host threads, packs assembled on the host; gpu_compress: compress + seal + pack assembly + "
-                   "pack IDs in HBM, one D2H (decode-equal frames, tests/test_gpu_save.py)")
+    out["note"] = ("mcdc_save_files from device memory, 4 MiB files of synthetic text, with a key; wall clock "
+                   "incl. the packs' D2H and host packing; gpu_compress: compress + seal in HBM "
+                   "(decode-equal frames, tests/test_gpu_save.py)")
     return out
 
 

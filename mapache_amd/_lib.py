@@ -454,12 +454,11 @@ class Context:
     @_locked
     def save_files(self, p: "McdcParams", index: "Index", data, offsets, lengths, key=None, nonces=None,
                    header_nonces=None, padding=None, max_pack_size: int = 16 << 20, n: int | None = None,
-                   gpu_compress: bool = False, out_buf: np.ndarray | None = None):
+                   gpu_compress: bool = False):
         """The Archiver's save path for a run of files (mcdc_save_files): data is
         a host array (or a device pointer with n bytes); file f = data[offsets[f],
         + lengths[f]); gpu_compress: compress with the GPU zstd kernels in HBM
-        (decode-equal blobs) instead of level 3 on host threads; out_buf: an
-        output buffer to reuse (the packed bytes returned are a view of it).  Returns
+        (decode-equal blobs) instead of level 3 on host threads.  Returns
         (ids_per_file: list of (k, 32) uint8 arrays,
         is_new per blob, packed bytes, PACK_DTYPE records)."""
         if isinstance(data, int):
@@ -481,8 +480,7 @@ class Context:
         ids = np.zeros((max(bcap, 1), 32), np.uint8)
         nw = np.zeros(max(bcap, 1), np.uint8)
         ocap = int(ext[:, 1].sum() * 1.01) + 4096 * nf + (1 << 16) if nf else 1
-        # (out_buf: a caller's buffer kept across calls, so its pages are not faulted in again)
-        out = out_buf if out_buf is not None and out_buf.size >= ocap else np.empty(max(ocap, 1), np.uint8)
+        out = np.empty(max(ocap, 1), np.uint8)
         packs = np.zeros(max(1, ocap // max(max_pack_size, 1) + 2), PACK_DTYPE)
         nb, pb, np_ = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         for _ in range(3):

@@ -235,7 +235,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_enc, sv_pack, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
+      sv_in, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -934,7 +934,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in, &ctx->sv_enc, &ctx->sv_pack, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
+                    &ctx->sv_in, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
@@ -1507,12 +1507,6 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
 // Repository::save_blob, repository_v1.rs:155-195), composed from the stages
 // above: size gate, chunking (GPU), chunk IDs (GPU), dedup (GPU index),
 // SecureStorage::encode (zstd on host threads, sealing on the GPU), packer.
-static int pack_blobs_impl(mcdc_ctx *ctx, const uint8_t key[32], const uint8_t *h_blobs, const uint8_t *d_blobs,
-                           size_t n_in, const mcdc_blob *blobs, const uint8_t *ids, const uint8_t *types,
-                           size_t nblobs, uint64_t max_pack_size, const uint8_t *header_nonces, size_t nnonces,
-                           const uint8_t *padding, size_t npadding, void *h_out, size_t out_cap, size_t *out_bytes,
-                           mcdc_pack *packs, size_t packs_cap, size_t *npacks);
-
 int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, const mcdc_store *store,
                     const void *data, size_t n, const mcdc_blob *files, size_t nfiles, uint64_t *file_blobs,
                     uint8_t *ids, uint8_t *is_new, size_t blobs_cap, size_t *nblobs, void *packs_out,
@@ -1623,8 +1617,8 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
     }
     if (!rc && store->key) {
       const size_t scap = cbytes + (size_t)kAeadOverhead * m;
-      if ((rc = ensure(ctx, ctx->sv_enc, scap)) == MCDC_OK)
-        rc = aead_run(ctx, 0, store->key, ctx->enc_in.p, cbytes, fr.data(), m, store->nonces, ctx->sv_enc.p, scap,
+      if ((rc = ensure(ctx, ctx->enc_out, scap)) == MCDC_OK)
+        rc = aead_run(ctx, 0, store->key, ctx->enc_in.p, cbytes, fr.data(), m, store->nonces, ctx->enc_out.p, scap,
                       eo.data(), nullptr);
     } else if (!rc) {
       for (size_t k = 0; k < m; ++k) eo[k] = fr[k].offset;
@@ -1634,8 +1628,11 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
       rollback();
       return rc;
     }
-    // (the encoded blobs stay in HBM: sv_enc sealed, enc_in compressed without a key; the packer
-    // assembles the packs there -- the headers' own encode uses enc_in / enc_out only with a key)
+    enc.resize(std::max<uint64_t>(eo[m], 1));
+    if (eo[m])
+      HIP_TRY(hipMemcpyAsync(enc.data(), store->key ? ctx->enc_out.p : ctx->enc_in.p, eo[m], hipMemcpyDeviceToHost,
+                             ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     for (size_t k = 0; k < m; ++k) eext[k] = store->key ? mcdc_blob{eo[k], eo[k + 1] - eo[k]} : fr[k];
   }
   std::vector<uint8_t> staged;
@@ -1675,11 +1672,9 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
     for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
   // Packer::add_blob + flush (:185-192) and the final flush
   size_t pb = 0, np = 0;
-  const bool dev_enc = store->gpu_compress && m;
-  const uint8_t *d_enc = dev_enc ? (const uint8_t *)(store->key ? ctx->sv_enc.p : ctx->enc_in.p) : nullptr;
-  rc = pack_blobs_impl(ctx, store->key, dev_enc ? nullptr : enc.data(), d_enc, eo[m], eext.data(), sids.data(),
-                       types.data(), m, store->max_pack_size, store->header_nonces, store->nheader_nonces,
-                       store->padding, store->npadding, packs_out, packs_out_cap, &pb, packs, packs_cap, &np);
+  rc = mcdc_pack_blobs(ctx, store->key, enc.data(), eo[m], eext.data(), sids.data(), types.data(), m,
+                       store->max_pack_size, store->header_nonces, store->nheader_nonces, store->padding,
+                       store->npadding, packs_out, packs_out_cap, &pb, packs, packs_cap, &np);
   if (packs_bytes) *packs_bytes = pb;
   *npacks = np;
   if (rc) {
@@ -1837,17 +1832,18 @@ int mcdc_zstd_frames_device(mcdc_ctx *ctx, const void *d_data, size_t n, const m
 // mcdc_encode_blobs, pack IDs (BLAKE3 of each pack) by mcdc_chunk_ids_device.
 static constexpr size_t kHeaderEntry = 37, kHeaderMultiple = 64;  // packer.rs:30, defaults.rs:32
 
-// The packer over blobs in host memory (h_blobs) or, for the composed save
-// path's GPU encode, in device memory (d_blobs): then the packs are assembled
-// in HBM (bodies copied device to device, the small encoded headers from the
-// host), hashed there, and cross PCIe once into h_out.
-static int pack_blobs_impl(mcdc_ctx *ctx, const uint8_t key[32], const uint8_t *h_blobs, const uint8_t *d_blobs,
-                           size_t n_in, const mcdc_blob *blobs, const uint8_t *ids, const uint8_t *types,
-                           size_t nblobs, uint64_t max_pack_size, const uint8_t *header_nonces, size_t nnonces,
-                           const uint8_t *padding, size_t npadding, void *h_out, size_t out_cap, size_t *out_bytes,
-                           mcdc_pack *packs, size_t packs_cap, size_t *npacks) {
-  int rc = check_extents(blobs, nblobs, n_in);
+int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, size_t n_in, const mcdc_blob *blobs,
+                    const uint8_t *ids, const uint8_t *types, size_t nblobs, uint64_t max_pack_size,
+                    const uint8_t *header_nonces, size_t nnonces, const uint8_t *padding, size_t npadding,
+                    void *h_out, size_t out_cap, size_t *out_bytes, mcdc_pack *packs, size_t packs_cap,
+                    size_t *npacks) {
+  int rc = check_ctx(ctx);
   if (rc) return rc;
+  if ((!h_blobs && n_in) || (nblobs && (!blobs || !ids || !types)) || !npacks)
+    return fail(MCDC_E_INVALID, "NULL argument");
+  if ((h_blobs && is_device_ptr(h_blobs)) || (h_out && is_device_ptr(h_out)))
+    return fail(MCDC_E_INVALID, "h_blobs / h_out must be host memory");
+  if ((rc = check_extents(blobs, nblobs, n_in))) return rc;
   for (size_t i = 0; i < nblobs; ++i)
     if (blobs[i].length > 0xffffffffull) return fail(MCDC_E_INVALID, "blob %zu exceeds the header's u32 length", i);
   *npacks = 0;
@@ -1919,42 +1915,8 @@ static int pack_blobs_impl(mcdc_ctx *ctx, const uint8_t key[32], const uint8_t *
   if (np > packs_cap || (packs_cap && !packs)) return fail(MCDC_E_CAPACITY, "%zu packs, capacity %zu", np, packs_cap);
   if (total > out_cap || (total && !h_out))
     return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
-  std::vector<uint8_t> pid(32 * std::max<size_t>(np, 1));
-  if (d_blobs && np) {
-    if ((rc = ensure(ctx, ctx->sv_pack, total))) return rc;
-    uint8_t *P = (uint8_t *)ctx->sv_pack.p;
-    std::vector<uint8_t> meta;  // every pack's encoded header || le32(len), back to back
-    meta.reserve(eo[np] + 4 * np);
-    for (size_t k = 0; k < np; ++k) {
-      // the body: runs of blobs contiguous in d_blobs as one copy each
-      uint8_t *d = P + pk[k].offset;
-      for (size_t i = first[k]; i < first[k + 1];) {
-        size_t j = i + 1;
-        uint64_t len = blobs[i].length;
-        while (j < first[k + 1] && blobs[j].offset == blobs[j - 1].offset + blobs[j - 1].length)
-          len += blobs[j++].length;
-        if (len) HIP_TRY(hipMemcpyAsync(d, d_blobs + blobs[i].offset, len, hipMemcpyDeviceToDevice, ctx->stream));
-        d += len;
-        i = j;
-      }
-      const uint32_t hl = (uint32_t)(eo[k + 1] - eo[k]);
-      meta.insert(meta.end(), enc.begin() + eo[k], enc.begin() + eo[k + 1]);
-      for (int b = 0; b < 4; ++b) meta.push_back((uint8_t)(hl >> (8 * b)));
-    }
-    size_t at = 0;
-    for (size_t k = 0; k < np; ++k) {
-      const size_t ml = (eo[k + 1] - eo[k]) + 4;
-      HIP_TRY(hipMemcpyAsync(P + pk[k].offset + pk[k].length - ml, meta.data() + at, ml, hipMemcpyHostToDevice,
-                             ctx->stream));
-      at += ml;
-    }
-    HIP_TRY(hipStreamSynchronize(ctx->stream));  // (meta is pageable and local)
-    if ((rc = mcdc_chunk_ids_device(ctx, P, total, pk.data(), np, pid.data()))) return rc;
-    HIP_TRY(hipMemcpyAsync(h_out, P, total, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-  }
   uint8_t *o = (uint8_t *)h_out;
-  if (!d_blobs) mcdc::host::parallel_items(np, zstd_threads(), [&](size_t k, int) {
+  mcdc::host::parallel_items(np, zstd_threads(), [&](size_t k, int) {
     uint8_t *d = o + pk[k].offset;
     for (size_t i = first[k]; i < first[k + 1]; ++i) {
       std::memcpy(d, (const uint8_t *)h_blobs + blobs[i].offset, blobs[i].length);
@@ -1965,7 +1927,8 @@ static int pack_blobs_impl(mcdc_ctx *ctx, const uint8_t key[32], const uint8_t *
     for (int b = 0; b < 4; ++b) d[hl + b] = (uint8_t)(hl >> (8 * b));
   });
   // pack IDs: BLAKE3 of each pack (flush: utils::calculate_hash(&data)), on the GPU
-  if (np && !d_blobs) {
+  std::vector<uint8_t> pid(32 * std::max<size_t>(np, 1));
+  if (np) {
     if ((rc = ensure(ctx, ctx->enc_in, total))) return rc;
     HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_out, total, hipMemcpyHostToDevice, ctx->stream));
     if ((rc = mcdc_chunk_ids_device(ctx, ctx->enc_in.p, total, pk.data(), np, pid.data()))) return rc;
@@ -1979,22 +1942,6 @@ static int pack_blobs_impl(mcdc_ctx *ctx, const uint8_t key[32], const uint8_t *
   }
   ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
-}
-
-int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, size_t n_in, const mcdc_blob *blobs,
-                    const uint8_t *ids, const uint8_t *types, size_t nblobs, uint64_t max_pack_size,
-                    const uint8_t *header_nonces, size_t nnonces, const uint8_t *padding, size_t npadding,
-                    void *h_out, size_t out_cap, size_t *out_bytes, mcdc_pack *packs, size_t packs_cap,
-                    size_t *npacks) {
-  int rc = check_ctx(ctx);
-  if (rc) return rc;
-  if ((!h_blobs && n_in) || (nblobs && (!blobs || !ids || !types)) || !npacks)
-    return fail(MCDC_E_INVALID, "NULL argument");
-  if ((h_blobs && is_device_ptr(h_blobs)) || (h_out && is_device_ptr(h_out)))
-    return fail(MCDC_E_INVALID, "h_blobs / h_out must be host memory");
-  return pack_blobs_impl(ctx, key, (const uint8_t *)h_blobs, nullptr, n_in, blobs, ids, types, nblobs, max_pack_size,
-                         header_nonces, nnonces, padding, npadding, h_out, out_cap, out_bytes, packs, packs_cap,
-                         npacks);
 }
 
 // ------------------------------------------------------------ batcher --
