@@ -11,7 +11,7 @@ device-resident array (the next pipeline stage consumes it in HBM).
 N GPUs (one process per GPU, torchrun): ONE stream of N x 64 GiB split across
 the GPUs (weak scaling: 64 GiB per GPU) — mapache_amd.shard.split_stream: each
 rank chunks its slice plus a max-byte right halo, the ranks exchange their exit
-positions (one int64 each, RCCL all_gather) and each continues the previous
+positions (one int64 each, gloo all_gather) and each continues the previous
 rank's exit until it meets its own chain.  At N = 1 that is exactly configs[1].
 
 Prints ONE JSON line (rank 0).  Extra objects:
@@ -68,13 +68,22 @@ def _dist():
 
 def _pmc_traffic():
     """Calibrated PMC read traffic of the scan (profiles/rNN/pmc_traffic.json, written from
-    separate rocprofv3 --pmc FETCH_SIZE passes by tools/profile_round.sh): HBM bytes per input byte."""
-    for rnd in ("r02", "r02/part2", "r02/part1", "r01"):  # the latest measurement
-        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+    separate rocprofv3 --pmc FETCH_SIZE passes by tools/profile_round.sh): HBM bytes per input byte.
+    The newest round's file wins (a round's top level before its part directories)."""
+    import glob
+    import re
+    cands = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "pmc_traffic.json")) + \
+            glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "*", "pmc_traffic.json")):
+        rel = os.path.relpath(path, ROOT)
+        m = re.match(r"profiles/r(\d+)/", rel)
+        if m:
+            cands.append((int(m.group(1)), rel.count("/") == 2, rel))
+    for _, _, rel in sorted(cands, reverse=True):
         try:
-            with open(path) as f:
+            with open(os.path.join(ROOT, rel)) as f:
                 d = json.load(f)
-            return float(d["traffic_per_input_byte"]), os.path.relpath(path, ROOT)
+            return float(d["traffic_per_input_byte"]), rel
         except (OSError, KeyError, ValueError):
             continue
     return None, None
@@ -529,6 +538,7 @@ def save_path_text(ctx, base: bytes, n: int, steps: int) -> dict:
     nonces = rng.integers(0, 256, (n // (PARAMS[0] - 1) + len(offs) + 2, 12), dtype=np.uint8)
     hn, pad = rng.integers(0, 256, (4096, 12), dtype=np.uint8), rng.integers(0, 256, (4096 * 63, 36), dtype=np.uint8)
     dp = ctx.device_alloc(n)
+    ob = ctx.pinned_bytes(int(n * 1.01) + 4096 * len(offs) + (1 << 16))  # the packs' host buffer, reused
     out = {}
     try:
         ctx.h2d(dp, data)
@@ -536,7 +546,7 @@ def save_path_text(ctx, base: bytes, n: int, steps: int) -> dict:
             def call():
                 with ctx.index_create() as ix:
                     return ctx.save_files(p, ix, dp, offs, lens, key, nonces, hn, pad, n=n,
-                                          gpu_compress=mode == "gpu_compress")
+                                          gpu_compress=mode == "gpu_compress", out_buf=ob)
             dt, (ids, new, packed, packs) = _timed(call, steps, 1)
             out[mode] = {"ms": round(dt * 1e3, 1), "gib_s": round(n / dt / GIB, 2), "blobs": int(new.size),
                          "stored": int(new.sum()), "packs": int(len(packs)), "packed_bytes": int(packed.size),
@@ -544,7 +554,8 @@ def save_path_text(ctx, base: bytes, n: int, steps: int) -> dict:
     finally:
         ctx.device_free(dp)
     out["note"] = ("mcdc_save_files from device memory, 4 MiB files of synthetic text, with a key; wall clock "
-                   "incl. the packs' D2H and host packing; gpu_compress: compress + seal in HBM "
+                   "incl. the packs' D2H into a reused pinned buffer; host_zstd: level 3 on host threads, packs "
+                   "on the host; gpu_compress: compress, seal, pack assembly and pack IDs in HBM, one D2H "
                    "(decode-equal frames, tests/test_gpu_save.py)")
     return out
 
@@ -818,19 +829,21 @@ def main() -> int:
     world, rank, local = _dist()
     if world != a.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
-    # Rehearsal only (a 1-GPU box standing in for a node): every rank on
-    # device 0, the exchange and barriers over gloo.
+    # One backend for every N: gloo carries the exit exchange (one int64 per
+    # rank), the barriers and the gathers (no data-path
+    # collective).  The process never touches torch.cuda: torch ships its own
+    # HIP runtime, and libmcdc's is the only one initialised here.  The timed
+    # region's device-side bracket is mcdc_ctx_synchronize.
+    # Rehearsal (a 1-GPU box standing in for a node): every rank on device 0;
+    # the code path is otherwise the one an 8-GPU node runs.
     rehearse = os.environ.get("MCDC_BENCH_ONE_DEVICE") == "1"
     if rehearse:
         local = 0
     numa_node = _bind_near_gpu(local)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        if not rehearse:
-            torch.cuda.set_device(local)
-        dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
+        dist.init_process_group("gloo", init_method="env://")
 
     from mapache_amd import _lib, shard
     p = _lib.params(*PARAMS)
@@ -839,20 +852,17 @@ def main() -> int:
     corpus_bytes = a.corpus_files_per_gpu * (8 << 20)
     max_bytes = max(n + PARAMS[2], corpus_bytes, a.batch_files * (8 << 20) if extras else 0)
     ctx = _lib.Context(local, max_bytes)
-    dev = None if (dist is None or rehearse) else f"cuda:{local}"
 
     def barrier():
+        ctx.synchronize()
         if dist is not None:
-            import torch
-            if dev is not None:
-                torch.cuda.synchronize()
             dist.barrier()
 
     def allreduce_max(x: float) -> float:
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device=dev or "cpu")
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -876,7 +886,7 @@ def main() -> int:
     ctx.fill_random(dp, hi - s, SEED, pos=s)  # the one stream (rank 0 at N = 1: configs[1])
     cap = (hi - s) // (p.min_size - 1) + 2
     d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
-    allgather = shard.torch_allgather(device=dev) if dist is not None else None
+    allgather = shard.torch_allgather() if dist is not None else None
     split_stats = {}
 
     def step():
@@ -929,8 +939,8 @@ def main() -> int:
                    "params": "FastCDC v2020 16/64/256 KiB Level1",
                    "bytes_per_gpu": n, "chunks_per_step": int(sum(counts)) if counts else int(count),
                    "parallelism": ("1 GPU" if world == 1 else
-                                   f"{n_gpus} slices of one stream; exits exchanged (RCCL all_gather, int64 per "
-                                   f"rank), seam continuations on the receiving GPU"),
+                                   f"{n_gpus} slices of one stream; exits exchanged (gloo all_gather, int64 per "
+                                   f"rank, no data-path collective), seam continuations on the receiving GPU"),
                    "host_numa_node": numa_node},
         "roofline": {"bound": "hbm", "kernel": "k_scan_q", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MCDC_ABI_VERSION 3
+#define MCDC_ABI_VERSION 4
 
 /* status codes */
 #define MCDC_OK 0
@@ -304,8 +304,9 @@ int mcdc_pack_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_b
  * processor::save_file / chunk_and_save_blobs do per file
  * (/root/reference/src/archiver/processor.rs:138-205) and
  * Repository::save_blob per blob (repository_v1.rs:155-195), in file order:
- *   - a file smaller than params->min_size (MIN_CHUNK_SIZE, :144) is one blob
- *     whose ID is ID::from_content of the whole file (SaveID::CalculateID);
+ *   - a file smaller than store->gate_bytes (default MIN_CHUNK_SIZE = 512 KiB,
+ *     :144, independent of the chunker's params) is one blob whose ID is
+ *     ID::from_content of the whole file (SaveID::CalculateID);
  *     any other file is chunked (StreamCDC, :173-179) and each chunk is a
  *     blob with ID::from_content (:184);
  *   - each blob is stored unless its ID is in the index or already pending
@@ -314,8 +315,11 @@ int mcdc_pack_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_b
  *     SecureStorage::build()) and added to the packer, which is flushed once
  *     it holds more than store->max_pack_size bytes (:185-192) and once at the
  *     end of the call (the end of the snapshot: Repository::flush);
- *     with store->gpu_compress the compression runs on the GPU (packs whose
- *     blobs decode to the same bytes; IDs, dedup and pack layout unchanged).
+ *     with store->gpu_compress the compression runs on the GPU: the packs'
+ *     blobs decode to the same bytes, IDs, dedup decisions and the storing
+ *     order are unchanged, but the encoded sizes are the GPU compressor's, so
+ *     pack boundaries (the flush rule runs on encoded sizes), the pack count
+ *     and the header padding follow those sizes.
  * data: host memory or a device pointer (n bytes); files: extents in it (the
  * chunked ones must not overlap).  Randomness is the caller's (OsRng in the
  * crate): store->nonces, 12 bytes per stored blob in storing order (unused
@@ -328,8 +332,9 @@ int mcdc_pack_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_b
  * back to back in packs_out and their records (as mcdc_pack_blobs).  Too
  * small a blobs_cap / packs_out_cap / packs_cap -> MCDC_E_CAPACITY with
  * *nblobs / *packs_bytes / *npacks set and the index unchanged: call again
- * with larger outputs.  Input larger than the context's max_bytes ->
- * MCDC_E_TOOBIG. */
+ * with larger outputs.  Any failure after the dedup step (capacity, nonces,
+ * a device error) leaves the index exactly as before the call.  Input larger
+ * than the context's max_bytes -> MCDC_E_TOOBIG. */
 typedef struct {
   const uint8_t *key;           /* 32-byte key, or NULL (SecureStorage::build()) */
   uint64_t max_pack_size;       /* the repository's max_packer_size (16 MiB) */
@@ -342,7 +347,12 @@ typedef struct {
   uint32_t gpu_compress;        /* 0: zstd level 3 on host threads (the crate's bytes);
                                    1: mcdc_zstd_compress_device in HBM (frames mapache's
                                    decoder reads, not byte-equal to level 3), then the
-                                   seal in HBM: the whole save path on the GPU */
+                                   seal, pack assembly and pack IDs in HBM; one D2H of
+                                   the packs: the whole save path on the GPU */
+  uint64_t gate_bytes;          /* processor::save_file's size gate (:144): a file shorter
+                                   than this is one blob, never chunked; 0 = the
+                                   reference's MIN_CHUNK_SIZE (512 KiB, defaults.rs:35),
+                                   whatever params->min_size is */
 } mcdc_store;
 struct mcdc_index;
 int mcdc_save_files(struct mcdc_ctx *ctx, const mcdc_params *params, struct mcdc_index *ix,
@@ -417,6 +427,10 @@ const char *mcdc_last_error(void);
 /* Device / pinned-host allocation on the context's device. */
 int mcdc_device_alloc(struct mcdc_ctx *ctx, size_t bytes, void **d_ptr);
 int mcdc_device_free(struct mcdc_ctx *ctx, void *d_ptr);
+/* Wait until all work on the context's device has finished (the timed
+ * region's device-side bracket in bench.py: the bench never initialises a
+ * second HIP runtime, e.g. torch's, in the libmcdc process). */
+int mcdc_ctx_synchronize(struct mcdc_ctx *ctx);
 int mcdc_host_alloc(struct mcdc_ctx *ctx, size_t bytes, void **h_ptr);
 int mcdc_host_free(struct mcdc_ctx *ctx, void *h_ptr);
 int mcdc_memcpy_h2d(struct mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);

@@ -38,7 +38,7 @@ EXPORTS = (
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
     "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device", "mcdc_save_files",
-    "mcdc_zstd_compress_device",
+    "mcdc_zstd_compress_device", "mcdc_ctx_synchronize",
 )
 
 
@@ -47,7 +47,8 @@ class McdcStore(ctypes.Structure):
     repository's max pack size and the caller's randomness."""
     _fields_ = [("key", ctypes.c_void_p), ("max_pack_size", ctypes.c_uint64), ("nonces", ctypes.c_void_p),
                 ("nnonces", ctypes.c_size_t), ("header_nonces", ctypes.c_void_p), ("nheader_nonces", ctypes.c_size_t),
-                ("padding", ctypes.c_void_p), ("npadding", ctypes.c_size_t), ("gpu_compress", ctypes.c_uint32)]
+                ("padding", ctypes.c_void_p), ("npadding", ctypes.c_size_t), ("gpu_compress", ctypes.c_uint32),
+                ("gate_bytes", ctypes.c_uint64)]
 
 
 PACK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("nblobs", "<u8"), ("meta_size", "<u8"),
@@ -112,6 +113,7 @@ def load():
     L.mcdc_last_error.restype = ctypes.c_char_p
     L.mcdc_device_alloc.argtypes = [vp, sz, P(vp)]
     L.mcdc_device_free.argtypes = [vp, vp]
+    L.mcdc_ctx_synchronize.argtypes = [vp]
     L.mcdc_host_alloc.argtypes = [vp, sz, P(vp)]
     L.mcdc_host_free.argtypes = [vp, vp]
     L.mcdc_memcpy_h2d.argtypes = [vp, vp, vp, sz]
@@ -193,6 +195,7 @@ class Context:
         self.max_bytes = max_bytes
         self._out = None      # reusable pinned output buffer (np view) and its pointer
         self._out_ptr = None
+        self._pinned = []     # pinned_bytes allocations, freed at close()
 
     def close(self):
         lock = getattr(self, "_lock", None)
@@ -203,8 +206,18 @@ class Context:
                 if self._out_ptr:
                     load().mcdc_host_free(self._h, ctypes.c_void_p(self._out_ptr))
                     self._out, self._out_ptr = None, None
+                for ptr in self._pinned:
+                    load().mcdc_host_free(self._h, ctypes.c_void_p(ptr))
+                self._pinned = []
                 load().mcdc_ctx_destroy(self._h)
                 self._h = None
+
+    @_locked
+    def pinned_bytes(self, n: int) -> np.ndarray:
+        """A pinned-host uint8 array of n bytes, valid until close()."""
+        ptr = self.host_alloc(max(int(n), 1))
+        self._pinned.append(ptr)
+        return np.frombuffer((ctypes.c_uint8 * max(int(n), 1)).from_address(ptr), dtype=np.uint8)[:int(n)]
 
     @_locked
     def pinned_out(self, cap: int) -> np.ndarray:
@@ -454,11 +467,14 @@ class Context:
     @_locked
     def save_files(self, p: "McdcParams", index: "Index", data, offsets, lengths, key=None, nonces=None,
                    header_nonces=None, padding=None, max_pack_size: int = 16 << 20, n: int | None = None,
-                   gpu_compress: bool = False):
+                   gpu_compress: bool = False, gate_bytes: int = 0, out_buf: np.ndarray | None = None):
         """The Archiver's save path for a run of files (mcdc_save_files): data is
         a host array (or a device pointer with n bytes); file f = data[offsets[f],
         + lengths[f]); gpu_compress: compress with the GPU zstd kernels in HBM
-        (decode-equal blobs) instead of level 3 on host threads.  Returns
+        (decode-equal blobs) instead of level 3 on host threads; gate_bytes:
+        save_file's size gate (0 = MIN_CHUNK_SIZE, 512 KiB); out_buf: a uint8
+        host array (e.g. pinned_bytes) the packs are written into when it is
+        large enough (the returned packed bytes are then a view of it).  Returns
         (ids_per_file: list of (k, 32) uint8 arrays,
         is_new per blob, packed bytes, PACK_DTYPE records)."""
         if isinstance(data, int):
@@ -474,13 +490,14 @@ class Context:
         kbuf = ctypes.create_string_buffer(k, len(k)) if k else None
         st = McdcStore(ctypes.addressof(kbuf) if k else None, max_pack_size,
                        arrs[0].ctypes.data, arrs[0].size // NONCE_BYTES, arrs[1].ctypes.data,
-                       arrs[1].size // NONCE_BYTES, arrs[2].ctypes.data, arrs[2].size // 36, int(bool(gpu_compress)))
+                       arrs[1].size // NONCE_BYTES, arrs[2].ctypes.data, arrs[2].size // 36, int(bool(gpu_compress)),
+                       int(gate_bytes))
         fb = np.zeros(nf + 1, np.uint64)
         bcap = int(sum(int(x) // max(p.min_size - 1, 1) + 2 for x in ext[:, 1])) if nf else 1
         ids = np.zeros((max(bcap, 1), 32), np.uint8)
         nw = np.zeros(max(bcap, 1), np.uint8)
         ocap = int(ext[:, 1].sum() * 1.01) + 4096 * nf + (1 << 16) if nf else 1
-        out = np.empty(max(ocap, 1), np.uint8)
+        out = out_buf if out_buf is not None else np.empty(max(ocap, 1), np.uint8)
         packs = np.zeros(max(1, ocap // max(max_pack_size, 1) + 2), PACK_DTYPE)
         nb, pb, np_ = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         for _ in range(3):
@@ -600,6 +617,11 @@ class Context:
             check(load().mcdc_memcpy_d2h(self._h, out.ctypes.data, ctypes.c_void_p(d_out),
                                          count * CHUNK_DTYPE.itemsize))
         return out[:count]
+
+    @_locked
+    def synchronize(self) -> None:
+        """Wait for all work on the context's device (mcdc_ctx_synchronize)."""
+        check(load().mcdc_ctx_synchronize(self._h))
 
     @_locked
     def timing(self) -> dict:

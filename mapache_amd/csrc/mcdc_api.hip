@@ -235,7 +235,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
+      sv_in, sv_pack, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -1148,6 +1148,13 @@ int mcdc_device_free(mcdc_ctx *ctx, void *d_ptr) {
   return MCDC_OK;
 }
 
+int mcdc_ctx_synchronize(mcdc_ctx *ctx) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  return MCDC_OK;
+}
+
 int mcdc_host_alloc(mcdc_ctx *ctx, size_t bytes, void **h_ptr) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
@@ -1502,11 +1509,224 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   return MCDC_OK;
 }
 
+// ------------------------------------------------------------ pack plan --
+// Packer::add_blob / flush over a run of encoded blob lengths
+// (packer.rs:101-186, flush rule repository_v1.rs:185-193): which blobs go in
+// which pack, each pack's header (generate_header: 37-byte entries, padded to
+// a multiple of 64 with the caller's random entries) SecureStorage-encoded
+// (mcdc_encode_blobs), and the pack extents: blobs || encode(header) ||
+// le32(len).  Shared by the host packer (mcdc_pack_blobs) and the GPU save
+// path, which assembles the same layout in HBM.
+static constexpr size_t kHeaderEntry = 37, kHeaderMultiple = 64;  // packer.rs:30, defaults.rs:32
+
+struct PackPlan {
+  std::vector<size_t> first;    // first blob of each pack, + nblobs
+  std::vector<uint8_t> meta;    // per pack: encode(header) || le32(len), back to back
+  std::vector<uint64_t> moff;   // pack k's meta = meta[moff[k], moff[k + 1])
+  std::vector<uint64_t> body;   // body bytes per pack
+  std::vector<mcdc_chunk> pk;   // pack extents in the output (offset, length)
+  size_t total = 0;
+  size_t np() const { return first.empty() ? 0 : first.size() - 1; }
+};
+
+static int plan_packs(mcdc_ctx *ctx, const uint8_t key[32], const uint64_t *lens, const uint8_t *ids,
+                      const uint8_t *types, size_t nblobs, uint64_t max_pack_size, const uint8_t *header_nonces,
+                      size_t nnonces, const uint8_t *padding, size_t npadding, PackPlan &P) {
+  for (size_t i = 0; i < nblobs; ++i)
+    if (lens[i] > 0xffffffffull) return fail(MCDC_E_INVALID, "blob %zu exceeds the header's u32 length", i);
+  // add, then flush once the packer holds more than max_pack_size bytes; the
+  // rest is flushed last
+  P.first.clear();
+  uint64_t size = 0;
+  bool open = false;
+  for (size_t i = 0; i < nblobs; ++i) {
+    if (!open) P.first.push_back(i), open = true;
+    size += lens[i];
+    if (size > max_pack_size) size = 0, open = false;
+  }
+  const size_t np = P.first.size();
+  P.first.push_back(nblobs);
+  if (key && np > nnonces)  // (without a key the headers are only compressed: no nonces)
+    return fail(MCDC_E_INVALID, "%zu packs need %zu header nonces (%zu given)", np, np, nnonces);
+  std::vector<uint8_t> hdr;
+  std::vector<mcdc_blob> hext(np);
+  size_t pad_used = 0;
+  for (size_t k = 0; k < np; ++k) {
+    const size_t cnt = P.first[k + 1] - P.first[k];
+    const size_t pad = cnt % kHeaderMultiple ? kHeaderMultiple - cnt % kHeaderMultiple : 0;
+    if (pad_used + pad > npadding)
+      return fail(MCDC_E_INVALID, "the padding pool holds %zu entries, the headers need more", npadding);
+    hext[k] = mcdc_blob{hdr.size(), (cnt + pad) * kHeaderEntry};
+    for (size_t i = P.first[k]; i < P.first[k + 1]; ++i) {
+      const uint32_t len = (uint32_t)lens[i];
+      hdr.insert(hdr.end(), ids + 32 * i, ids + 32 * i + 32);
+      for (int b = 0; b < 4; ++b) hdr.push_back((uint8_t)(len >> (8 * b)));
+      hdr.push_back(types[i]);
+    }
+    for (size_t j = 0; j < pad; ++j, ++pad_used) {
+      hdr.insert(hdr.end(), padding + 36 * pad_used, padding + 36 * pad_used + 36);
+      hdr.push_back(0xff);
+    }
+  }
+  // SecureStorage::encode of every header (zstd on host threads, sealing on the GPU)
+  size_t enc_cap = hdr.size() + hdr.size() / 64 + 1024 * np + 64;
+  std::vector<uint8_t> enc(enc_cap);
+  std::vector<uint64_t> eo(np + 1, 0);
+  if (np) {
+    int rc = mcdc_encode_blobs(ctx, key, hdr.data(), hdr.size(), hext.data(), np, header_nonces, enc.data(), enc_cap,
+                               eo.data());
+    if (rc == MCDC_E_CAPACITY) {
+      enc.resize(eo[np]);
+      enc_cap = enc.size();
+      rc = mcdc_encode_blobs(ctx, key, hdr.data(), hdr.size(), hext.data(), np, header_nonces, enc.data(), enc_cap,
+                             eo.data());
+    }
+    if (rc) return rc;
+  }
+  P.meta.clear();
+  P.moff.assign(np + 1, 0);
+  P.body.assign(np, 0);
+  P.pk.assign(np, mcdc_chunk{});
+  P.total = 0;
+  for (size_t k = 0; k < np; ++k) {
+    const uint32_t hl = (uint32_t)(eo[k + 1] - eo[k]);
+    P.meta.insert(P.meta.end(), enc.data() + eo[k], enc.data() + eo[k + 1]);
+    for (int b = 0; b < 4; ++b) P.meta.push_back((uint8_t)(hl >> (8 * b)));
+    P.moff[k + 1] = P.meta.size();
+    for (size_t i = P.first[k]; i < P.first[k + 1]; ++i) P.body[k] += lens[i];
+    P.pk[k] = mcdc_chunk{P.total, P.body[k] + hl + 4, 0};
+    P.total += P.body[k] + hl + 4;
+  }
+  return MCDC_OK;
+}
+
+static void fill_pack_records(const PackPlan &P, const uint8_t *pid, mcdc_pack *packs) {
+  for (size_t k = 0; k < P.np(); ++k) {
+    packs[k].offset = P.pk[k].offset;
+    packs[k].length = P.pk[k].length;
+    packs[k].nblobs = P.first[k + 1] - P.first[k];
+    packs[k].meta_size = P.moff[k + 1] - P.moff[k];
+    std::memcpy(packs[k].id, pid + 32 * k, 32);
+  }
+}
+
 // ------------------------------------------------------------ save path --
 // The Archiver's save path for a run of files (processor.rs:138-205 +
 // Repository::save_blob, repository_v1.rs:155-195), composed from the stages
 // above: size gate, chunking (GPU), chunk IDs (GPU), dedup (GPU index),
-// SecureStorage::encode (zstd on host threads, sealing on the GPU), packer.
+// SecureStorage::encode (zstd on host threads or on the GPU, sealing on the
+// GPU), packer.
+static constexpr uint64_t kMinChunkSize = 512 * 1024;  // global::defaults::MIN_CHUNK_SIZE (defaults.rs:35)
+
+// GPU encode (store->gpu_compress): the stored blobs of the device copy d are
+// compressed and sealed in HBM, the packs assembled there (each pack's body is
+// one contiguous run of encoded blobs: one device-to-device copy; its encoded
+// header and trailer come from the host), hashed there, and copied out once.
+static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t *d, size_t n,
+                           const std::vector<mcdc_blob> &sext, const std::vector<uint8_t> &sids,
+                           const std::vector<uint8_t> &types, void *packs_out, size_t packs_out_cap,
+                           size_t *packs_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks) {
+  const size_t m = sext.size();
+  std::vector<mcdc_chunk> sch(m);
+  for (size_t k = 0; k < m; ++k) sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
+  std::vector<mcdc_blob> fr(m);
+  size_t bound = 0, cbytes = 0;
+  int rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, nullptr, 0, &bound, fr.data());
+  if (rc != MCDC_E_CAPACITY) return rc ? rc : fail(MCDC_E_INTERNAL, "compress bound query did not report a bound");
+  if ((rc = ensure(ctx, ctx->enc_in, std::max<size_t>(bound, 1))) ||
+      (rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->enc_in.p, bound, &cbytes, fr.data())))
+    return rc;
+  std::vector<uint64_t> eo(m + 1, 0);
+  const uint8_t *E = (const uint8_t *)ctx->enc_in.p;  // encoded blob k = E[eo[k], eo[k + 1])
+  if (store->key) {
+    const size_t scap = cbytes + (size_t)kAeadOverhead * m;
+    if ((rc = ensure(ctx, ctx->enc_out, scap)) ||
+        (rc = aead_run(ctx, 0, store->key, ctx->enc_in.p, cbytes, fr.data(), m, store->nonces, ctx->enc_out.p, scap,
+                       eo.data(), nullptr)))
+      return rc;
+    E = (const uint8_t *)ctx->enc_out.p;
+  } else {  // frames are back to back from enc_in
+    for (size_t k = 0; k < m; ++k) eo[k] = fr[k].offset;
+    eo[m] = cbytes;
+  }
+  std::vector<uint64_t> lens(m);
+  for (size_t k = 0; k < m; ++k) lens[k] = eo[k + 1] - eo[k];
+  PackPlan P;
+  if ((rc = plan_packs(ctx, store->key, lens.data(), sids.data(), types.data(), m, store->max_pack_size,
+                       store->header_nonces, store->nheader_nonces, store->padding, store->npadding, P)))
+    return rc;
+  const size_t np = P.np();
+  *npacks = np;
+  if (packs_bytes) *packs_bytes = P.total;
+  if (np > packs_cap || (np && !packs)) return fail(MCDC_E_CAPACITY, "%zu packs, capacity %zu", np, packs_cap);
+  if (P.total > packs_out_cap || (P.total && !packs_out))
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", packs_out_cap, P.total);
+  if (!np) return MCDC_OK;
+  if ((rc = ensure(ctx, ctx->sv_pack, P.total))) return rc;
+  uint8_t *D = (uint8_t *)ctx->sv_pack.p;
+  for (size_t k = 0; k < np; ++k) {  // body: blobs first[k] .. first[k+1]-1 are contiguous in E
+    const uint64_t b0 = eo[P.first[k]];
+    if (P.body[k])
+      HIP_TRY(hipMemcpyAsync(D + P.pk[k].offset, E + b0, P.body[k], hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(D + P.pk[k].offset + P.body[k], P.meta.data() + P.moff[k], P.moff[k + 1] - P.moff[k],
+                           hipMemcpyHostToDevice, ctx->stream));
+  }
+  std::vector<uint8_t> pid(32 * np);
+  if ((rc = mcdc_chunk_ids_device(ctx, D, P.total, P.pk.data(), np, pid.data()))) return rc;
+  HIP_TRY(hipMemcpyAsync(packs_out, D, P.total, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  fill_pack_records(P, pid.data(), packs);
+  return MCDC_OK;
+}
+
+// Host encode (the crate's exact bytes): zstd level 3 / window 20 on host
+// threads, the seal on the GPU (mcdc_encode_blobs), packs on the host.
+static int save_encode_host(mcdc_ctx *ctx, const mcdc_store *store, const void *data, const uint8_t *d, size_t n,
+                            bool host_in, std::vector<mcdc_blob> sext, const std::vector<uint8_t> &sids,
+                            const std::vector<uint8_t> &types, void *packs_out, size_t packs_out_cap,
+                            size_t *packs_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks) {
+  const size_t m = sext.size();
+  std::vector<uint8_t> staged;
+  const uint8_t *src = (const uint8_t *)data;
+  if (!host_in && m) {  // device input: bring the new blobs over (the zstd stage runs on the host)
+    size_t tot = 0;
+    for (auto &e : sext) tot += e.length;
+    staged.resize(std::max<size_t>(tot, 1));
+    size_t o = 0;
+    for (auto &e : sext) {
+      if (e.length)
+        HIP_TRY(hipMemcpyAsync(staged.data() + o, d + e.offset, e.length, hipMemcpyDeviceToHost, ctx->stream));
+      e.offset = o;
+      o += e.length;
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    src = staged.data();
+  }
+  const size_t src_n = host_in ? n : staged.size();
+  size_t ecap = 0;
+  for (auto &e : sext) ecap += e.length + e.length / 64 + 64;
+  std::vector<uint8_t> enc(std::max<size_t>(ecap, 1));
+  std::vector<uint64_t> eo(m + 1, 0);
+  int rc = MCDC_OK;
+  if (m) {
+    rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), ecap, eo.data());
+    if (rc == MCDC_E_CAPACITY) {
+      enc.resize(std::max<uint64_t>(eo[m], 1));
+      rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), enc.size(),
+                             eo.data());
+    }
+    if (rc) return rc;
+  }
+  std::vector<mcdc_blob> eext(m);
+  for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
+  size_t pb = 0;
+  rc = mcdc_pack_blobs(ctx, store->key, enc.data(), eo[m], eext.data(), sids.data(), types.data(), m,
+                       store->max_pack_size, store->header_nonces, store->nheader_nonces, store->padding,
+                       store->npadding, packs_out, packs_out_cap, &pb, packs, packs_cap, npacks);
+  if (packs_bytes) *packs_bytes = pb;
+  return rc;
+}
+
 int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, const mcdc_store *store,
                     const void *data, size_t n, const mcdc_blob *files, size_t nfiles, uint64_t *file_blobs,
                     uint8_t *ids, uint8_t *is_new, size_t blobs_cap, size_t *nblobs, void *packs_out,
@@ -1534,12 +1754,14 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
     d = (const uint8_t *)ctx->sv_in.p;
   }
   // processor::save_file: a file smaller than MIN_CHUNK_SIZE is one blob
-  // (:144-153); the others go through the chunker (:160-205)
+  // (:144-153; the constant, whatever the chunker's own min); the others go
+  // through the chunker (:160-205)
+  const uint64_t gate = store->gate_bytes ? store->gate_bytes : kMinChunkSize;
   std::vector<uint64_t> boff, blen;
   std::vector<size_t> big;
   size_t cap = 0;
   for (size_t f = 0; f < nfiles; ++f)
-    if (files[f].length >= params->min_size) {
+    if (files[f].length >= gate) {
       big.push_back(f);
       boff.push_back(files[f].offset);
       blen.push_back(files[f].length);
@@ -1573,112 +1795,40 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   if (nb > blobs_cap || (nb && !ids)) return fail(MCDC_E_CAPACITY, "%zu blobs, capacity %zu", nb, blobs_cap);
   // ID::from_content of every blob (CalculateID of a small file is the same hash)
   if (nb && (rc = mcdc_chunk_ids_device(ctx, d, n, list.data(), nb, ids))) return rc;
-  // save_blob's dedup check (:173-180) -- the index changes here; a later
-  // capacity failure puts it back (the previous buffer is intact until the
-  // next add)
+  // save_blob's dedup check (:173-180) -- the index changes here.  From here
+  // on every failure, whatever returns it (capacity, nonces, a HIP call),
+  // leaves through the one rollback below: the previous index buffer is
+  // intact until the next add, so the index is exactly as before the call.
   std::vector<uint8_t> nw(std::max<size_t>(nb, 1));
   size_t m = 0;
   if (nb && (rc = mcdc_index_add(ctx, ix, ids, nb, nw.data(), nullptr, nullptr, &m))) return rc;
-  auto rollback = [&]() {
-    if (nb) {
+  auto rest = [&]() -> int {
+    if (store->key && m > store->nnonces)
+      return fail(MCDC_E_INVALID, "%zu new blobs need %zu nonces (%zu given)", m, m, store->nnonces);
+    std::vector<mcdc_blob> sext;
+    std::vector<uint8_t> sids;
+    sext.reserve(m);
+    sids.reserve(32 * m);
+    for (size_t i = 0; i < nb; ++i)
+      if (nw[i]) {
+        sext.push_back(mcdc_blob{list[i].offset, list[i].length});
+        sids.insert(sids.end(), ids + 32 * i, ids + 32 * i + 32);
+      }
+    const std::vector<uint8_t> types(std::max<size_t>(m, 1), 0);  // BlobType::Data (processor.rs:191)
+    if (store->gpu_compress && m)
+      return save_encode_gpu(ctx, store, d, n, sext, sids, types, packs_out, packs_out_cap, packs_bytes, packs,
+                             packs_cap, npacks);
+    return save_encode_host(ctx, store, data, d, n, host_in, std::move(sext), sids, types, packs_out, packs_out_cap,
+                            packs_bytes, packs, packs_cap, npacks);
+  };
+  rc = rest();
+  if (rc == MCDC_OK && ctx->knobs.test_fail_after_index)  // test hook (tests/test_gpu_save.py)
+    rc = fail(MCDC_E_DEVICE, "injected failure after the index add (MCDC_TEST_FAIL_AFTER_INDEX)");
+  if (rc) {
+    if (nb) {  // rollback: the index as before the call
       ix->cur ^= 1;
       ix->size -= m;
     }
-  };
-  if (store->key && m > store->nnonces) {
-    rollback();
-    return fail(MCDC_E_INVALID, "%zu new blobs need %zu nonces (%zu given)", m, m, store->nnonces);
-  }
-  // the stored blobs' bytes in host memory for the zstd stage
-  std::vector<mcdc_blob> sext;
-  std::vector<uint8_t> sids, types;
-  sext.reserve(m);
-  sids.reserve(32 * m);
-  for (size_t i = 0; i < nb; ++i)
-    if (nw[i]) {
-      sext.push_back(mcdc_blob{list[i].offset, list[i].length});
-      sids.insert(sids.end(), ids + 32 * i, ids + 32 * i + 32);
-    }
-  types.assign(std::max<size_t>(m, 1), 0);  // BlobType::Data (processor.rs:191)
-  std::vector<uint64_t> eo(m + 1, 0);
-  std::vector<uint8_t> enc;
-  std::vector<mcdc_blob> eext(m);
-  if (store->gpu_compress && m) {
-    // SecureStorage::encode in HBM: the GPU compressor over the stored blobs
-    // of the device copy, then the seal; only the encoded blobs come back
-    std::vector<mcdc_chunk> sch(m);
-    for (size_t k = 0; k < m; ++k) sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
-    std::vector<mcdc_blob> fr(m);
-    size_t bound = 0, cbytes = 0;
-    rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, nullptr, 0, &bound, fr.data());
-    if (rc == MCDC_E_CAPACITY) {
-      if ((rc = ensure(ctx, ctx->enc_in, std::max<size_t>(bound, 1))) == MCDC_OK)
-        rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->enc_in.p, bound, &cbytes, fr.data());
-    }
-    if (!rc && store->key) {
-      const size_t scap = cbytes + (size_t)kAeadOverhead * m;
-      if ((rc = ensure(ctx, ctx->enc_out, scap)) == MCDC_OK)
-        rc = aead_run(ctx, 0, store->key, ctx->enc_in.p, cbytes, fr.data(), m, store->nonces, ctx->enc_out.p, scap,
-                      eo.data(), nullptr);
-    } else if (!rc) {
-      for (size_t k = 0; k < m; ++k) eo[k] = fr[k].offset;
-      eo[m] = cbytes;
-    }
-    if (rc) {
-      rollback();
-      return rc;
-    }
-    enc.resize(std::max<uint64_t>(eo[m], 1));
-    if (eo[m])
-      HIP_TRY(hipMemcpyAsync(enc.data(), store->key ? ctx->enc_out.p : ctx->enc_in.p, eo[m], hipMemcpyDeviceToHost,
-                             ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    for (size_t k = 0; k < m; ++k) eext[k] = store->key ? mcdc_blob{eo[k], eo[k + 1] - eo[k]} : fr[k];
-  }
-  std::vector<uint8_t> staged;
-  const uint8_t *src = (const uint8_t *)data;
-  if (!host_in && m && !store->gpu_compress) {  // device input: bring the new blobs over (the zstd stage runs on the host)
-    size_t tot = 0;
-    for (auto &e : sext) tot += e.length;
-    staged.resize(std::max<size_t>(tot, 1));
-    size_t o = 0;
-    for (auto &e : sext) {
-      if (e.length) HIP_TRY(hipMemcpyAsync(staged.data() + o, d + e.offset, e.length, hipMemcpyDeviceToHost,
-                                           ctx->stream));
-      e.offset = o;
-      o += e.length;
-    }
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    src = staged.data();
-  }
-  const size_t src_n = host_in ? n : staged.size();
-  // SecureStorage::encode of every stored blob (:182)
-  size_t ecap = 0;
-  for (auto &e : sext) ecap += e.length + e.length / 64 + 64;
-  if (!store->gpu_compress) enc.resize(std::max<size_t>(ecap, 1));
-  if (m && !store->gpu_compress) {
-    rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), ecap, eo.data());
-    if (rc == MCDC_E_CAPACITY) {
-      enc.resize(std::max<uint64_t>(eo[m], 1));
-      rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), enc.size(),
-                             eo.data());
-    }
-    if (rc) {
-      rollback();
-      return rc;
-    }
-  }
-  if (!store->gpu_compress)
-    for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
-  // Packer::add_blob + flush (:185-192) and the final flush
-  size_t pb = 0, np = 0;
-  rc = mcdc_pack_blobs(ctx, store->key, enc.data(), eo[m], eext.data(), sids.data(), types.data(), m,
-                       store->max_pack_size, store->header_nonces, store->nheader_nonces, store->padding,
-                       store->npadding, packs_out, packs_out_cap, &pb, packs, packs_cap, &np);
-  if (packs_bytes) *packs_bytes = pb;
-  *npacks = np;
-  if (rc) {
-    rollback();
     return rc;
   }
   if (is_new) std::memcpy(is_new, nw.data(), nb);
@@ -1827,11 +1977,9 @@ int mcdc_zstd_frames_device(mcdc_ctx *ctx, const void *d_data, size_t n, const m
 }
 
 // --------------------------------------------------------------- packer --
-// Packer::add_blob / flush for a run of encoded blobs (packer.rs:101-186,
-// repository_v1.rs:182-193): packs on the host, their headers encoded by
-// mcdc_encode_blobs, pack IDs (BLAKE3 of each pack) by mcdc_chunk_ids_device.
-static constexpr size_t kHeaderEntry = 37, kHeaderMultiple = 64;  // packer.rs:30, defaults.rs:32
-
+// Packer::add_blob / flush for a run of encoded blobs in host memory
+// (plan_packs), packs assembled on the host, pack IDs (BLAKE3 of each pack)
+// by mcdc_chunk_ids_device.
 int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, size_t n_in, const mcdc_blob *blobs,
                     const uint8_t *ids, const uint8_t *types, size_t nblobs, uint64_t max_pack_size,
                     const uint8_t *header_nonces, size_t nnonces, const uint8_t *padding, size_t npadding,
@@ -1844,102 +1992,38 @@ int mcdc_pack_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_blobs, s
   if ((h_blobs && is_device_ptr(h_blobs)) || (h_out && is_device_ptr(h_out)))
     return fail(MCDC_E_INVALID, "h_blobs / h_out must be host memory");
   if ((rc = check_extents(blobs, nblobs, n_in))) return rc;
-  for (size_t i = 0; i < nblobs; ++i)
-    if (blobs[i].length > 0xffffffffull) return fail(MCDC_E_INVALID, "blob %zu exceeds the header's u32 length", i);
   *npacks = 0;
   if (out_bytes) *out_bytes = 0;
   const double t0 = now_ms();
-  // plan: add, then flush once the packer holds more than max_pack_size bytes;
-  // the rest is flushed last
-  std::vector<size_t> first;  // first blob of each pack (+ nblobs at the end)
-  uint64_t size = 0;
-  bool open = false;
-  for (size_t i = 0; i < nblobs; ++i) {
-    if (!open) first.push_back(i), open = true;
-    size += blobs[i].length;
-    if (size > max_pack_size) size = 0, open = false;
-  }
-  const size_t np = first.size();
-  first.push_back(nblobs);
-  if (key && np > nnonces)  // (without a key the headers are only compressed: no nonces)
-    return fail(MCDC_E_INVALID, "%zu packs need %zu header nonces (%zu given)", np, np, nnonces);
-  // headers: 37-byte entries (ID, le32 length, type), padded with random entries
-  // (36 random bytes + BlobType::Padding) to a multiple of 64 (generate_header)
-  std::vector<uint8_t> hdr;
-  std::vector<mcdc_blob> hext(np);
-  size_t pad_used = 0;
-  for (size_t k = 0; k < np; ++k) {
-    const size_t cnt = first[k + 1] - first[k];
-    const size_t pad = cnt % kHeaderMultiple ? kHeaderMultiple - cnt % kHeaderMultiple : 0;
-    if (pad_used + pad > npadding)
-      return fail(MCDC_E_INVALID, "the padding pool holds %zu entries, the headers need more", npadding);
-    hext[k] = mcdc_blob{hdr.size(), (cnt + pad) * kHeaderEntry};
-    for (size_t i = first[k]; i < first[k + 1]; ++i) {
-      const uint32_t len = (uint32_t)blobs[i].length;
-      hdr.insert(hdr.end(), ids + 32 * i, ids + 32 * i + 32);
-      for (int b = 0; b < 4; ++b) hdr.push_back((uint8_t)(len >> (8 * b)));
-      hdr.push_back(types[i]);
-    }
-    for (size_t j = 0; j < pad; ++j, ++pad_used) {
-      hdr.insert(hdr.end(), padding + 36 * pad_used, padding + 36 * pad_used + 36);
-      hdr.push_back(0xff);
-    }
-  }
-  // SecureStorage::encode of every header (zstd on host threads, sealing on the GPU)
-  size_t enc_cap = hdr.size() + hdr.size() / 64 + 1024 * np + 64;
-  std::vector<uint8_t> enc(enc_cap);
-  std::vector<uint64_t> eo(np + 1);
-  if (np) {
-    rc = mcdc_encode_blobs(ctx, key, hdr.data(), hdr.size(), hext.data(), np, header_nonces, enc.data(), enc_cap,
-                           eo.data());
-    if (rc == MCDC_E_CAPACITY) {
-      enc.resize(eo[np]);
-      enc_cap = enc.size();
-      rc = mcdc_encode_blobs(ctx, key, hdr.data(), hdr.size(), hext.data(), np, header_nonces, enc.data(), enc_cap,
-                             eo.data());
-    }
-    if (rc) return rc;
-  }
-  // layout: blobs || encoded header || le32(len)
-  std::vector<mcdc_chunk> pk(np);
-  size_t total = 0;
-  for (size_t k = 0; k < np; ++k) {
-    uint64_t body = 0;
-    for (size_t i = first[k]; i < first[k + 1]; ++i) body += blobs[i].length;
-    const uint64_t meta = (eo[k + 1] - eo[k]) + 4;
-    pk[k] = mcdc_chunk{total, body + meta, 0};
-    total += body + meta;
-  }
+  std::vector<uint64_t> lens(nblobs);
+  for (size_t i = 0; i < nblobs; ++i) lens[i] = blobs[i].length;
+  PackPlan P;
+  if ((rc = plan_packs(ctx, key, lens.data(), ids, types, nblobs, max_pack_size, header_nonces, nnonces, padding,
+                       npadding, P)))
+    return rc;
+  const size_t np = P.np();
   *npacks = np;
-  if (out_bytes) *out_bytes = total;
+  if (out_bytes) *out_bytes = P.total;
   if (np > packs_cap || (packs_cap && !packs)) return fail(MCDC_E_CAPACITY, "%zu packs, capacity %zu", np, packs_cap);
-  if (total > out_cap || (total && !h_out))
-    return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
+  if (P.total > out_cap || (P.total && !h_out))
+    return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, P.total);
   uint8_t *o = (uint8_t *)h_out;
   mcdc::host::parallel_items(np, zstd_threads(), [&](size_t k, int) {
-    uint8_t *d = o + pk[k].offset;
-    for (size_t i = first[k]; i < first[k + 1]; ++i) {
+    uint8_t *d = o + P.pk[k].offset;
+    for (size_t i = P.first[k]; i < P.first[k + 1]; ++i) {
       std::memcpy(d, (const uint8_t *)h_blobs + blobs[i].offset, blobs[i].length);
       d += blobs[i].length;
     }
-    const uint32_t hl = (uint32_t)(eo[k + 1] - eo[k]);
-    std::memcpy(d, enc.data() + eo[k], hl);
-    for (int b = 0; b < 4; ++b) d[hl + b] = (uint8_t)(hl >> (8 * b));
+    std::memcpy(d, P.meta.data() + P.moff[k], P.moff[k + 1] - P.moff[k]);
   });
   // pack IDs: BLAKE3 of each pack (flush: utils::calculate_hash(&data)), on the GPU
   std::vector<uint8_t> pid(32 * std::max<size_t>(np, 1));
   if (np) {
-    if ((rc = ensure(ctx, ctx->enc_in, total))) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_out, total, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = mcdc_chunk_ids_device(ctx, ctx->enc_in.p, total, pk.data(), np, pid.data()))) return rc;
+    if ((rc = ensure(ctx, ctx->enc_in, P.total))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, h_out, P.total, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = mcdc_chunk_ids_device(ctx, ctx->enc_in.p, P.total, P.pk.data(), np, pid.data()))) return rc;
   }
-  for (size_t k = 0; k < np; ++k) {
-    packs[k].offset = pk[k].offset;
-    packs[k].length = pk[k].length;
-    packs[k].nblobs = first[k + 1] - first[k];
-    packs[k].meta_size = (eo[k + 1] - eo[k]) + 4;
-    std::memcpy(packs[k].id, pid.data() + 32 * k, 32);
-  }
+  fill_pack_records(P, pid.data(), packs);
   ctx->timing.total_ms = now_ms() - t0;
   return MCDC_OK;
 }

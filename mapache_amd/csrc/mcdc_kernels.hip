@@ -511,7 +511,9 @@ __device__ __forceinline__ void store_run_bits(uint64_t *bits, uint64_t run0, ui
 template <int RUN, int PC, bool CW>
 __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_t tile0, uint64_t tile1,
                                                    int do_tail) {
-  __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8];
+  // + one 8-byte slot per wave: lane 0's warm-up hash waits there for the
+  // tile-end re-walk (CW) instead of holding two VGPRs across the tile
+  __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8 + 16];
   if constexpr (PC == 2 && !CW) MCDC_VGPR_PAD(112);  // 112 used: not an exact fill (MCDC_VGPR_PAD)
   for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) smem[i] = W.gear16[i >> 5];
   const uint32_t lane = threadIdx.x & 63;
@@ -587,6 +589,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
       hash16(q.tab, q.lo, w2, hw);
     }
     if (!CW) h = hw;
+    else if (lane == 0) smem[(kSTab + 16 * kQWaveBytes) / 8 + wv] = hw;
     uint4 f0, f1, f2;  // CW: the piece's first 48 bytes
     uint32_t qn = 0;  // wave-uniform queue length
     const uint8_t *tb = W.base + run0 * (uint64_t)RUN;  // wave-uniform tile base (SGPR)
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
 #undef MCDC_LDQ
     if (CW) {  // re-walk the first 48 positions from the state after the previous piece
       const uint32_t plo = __shfl_up((uint32_t)h, 1u), phi = __shfl_up((uint32_t)(h >> 32), 1u);
-      uint64_t hp = lane == 0 ? hw : (((uint64_t)phi << 32) | plo);
+      uint64_t hp = lane == 0 ? smem[(kSTab + 16 * kQWaveBytes) / 8 + wv] : (((uint64_t)phi << 32) | plo);
       const uint32_t w[12] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, f2.x, f2.y, f2.z, f2.w};
       scan64q<RUN, PC, 12>(q, w, hp, 0u, qn, run0);
     }
@@ -2139,6 +2142,7 @@ Knobs read_knobs() {
   k.lane_walk = std::min(std::max(env("MCDC_LANE_WALK", k.lane_walk), 0), 2);
   k.lane_seg_chunks = std::max(env("MCDC_LANE_SEG_CHUNKS", k.lane_seg_chunks), 1);
   k.zc_huf = env("MCDC_ZC_HUF", k.zc_huf ? 1 : 0) != 0;
+  k.test_fail_after_index = env("MCDC_TEST_FAIL_AFTER_INDEX", 0) != 0;
 #ifdef MCDC_AB_KNOBS
   k.group = env("MCDC_GROUP", k.group);
   if (k.group != 8 && k.group != 16 && k.group != 32) k.group = kGroup;

@@ -77,6 +77,20 @@ def kernel_fields(asm: str):
     return out
 
 
+def max_workgroup_sizes(asm: str):
+    """{kernel: .max_flat_workgroup_size} from the code object metadata."""
+    return {m.group(2): int(m.group(1))
+            for m in re.finditer(r"\.max_flat_workgroup_size:\s+(\d+)\s*\n\s*\.name:\s+(\S+)", asm)}
+
+
+def vgpr_ceiling(wg_size: int) -> int:
+    """Most VGPRs per lane a kernel of this workgroup size may allocate and
+    still launch: the block's waves spread over the CU's 4 SIMDs, each SIMD
+    holding 512 VGPRs per lane, in 8-register granules."""
+    waves_per_simd = -(-(-(-wg_size // 64)) // 4)
+    return 512 // max(waves_per_simd, 1) // 8 * 8
+
+
 class Insn:
     __slots__ = ("idx", "op", "args", "text", "label")
 
@@ -399,6 +413,7 @@ def audit(d, kernel_filter=None, show_hazards=False, quiet=False):
     for sf in s_files:
         asm = open(sf).read()
         fields = kernel_fields(asm)
+        wgs = max_workgroup_sizes(asm)
         for name, lines in split_units(asm).items():
             if kernel_filter and kernel_filter not in name:
                 continue
@@ -411,7 +426,7 @@ def audit(d, kernel_filter=None, show_hazards=False, quiet=False):
             first = insns[0].text if insns else ""
             rows.append(dict(name=name, kernel=name in fields, next_free_vgpr=f.get("next_free_vgpr"),
                              accum_offset=f.get("accum_offset"), top=top, top_is_load_dst=top in ldst,
-                             alloc=dd[1] if dd else None, kd_accum=dd[2] if dd else None, hazards=len(raw),
+                             alloc=dd[1] if dd else None, wg_size=wgs.get(name), kd_accum=dd[2] if dd else None, hazards=len(raw),
                              waw=len(hz) - len(raw),
                              entry_wait=name in fields or first.startswith("s_waitcnt vmcnt(0) expcnt(0) lgkmcnt(0)")))
             all_h += hz

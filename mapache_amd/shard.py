@@ -307,18 +307,20 @@ def split_stream(chunk, allgather, s: int, e: int, n: int, max_size: int, rank: 
     return (mine.materialize() if materialize else mine), stats
 
 
-def torch_allgather(group=None, device=None):
-    """allgather(v) over torch.distributed: one int64 per rank (gloo on CPU, or
-    RCCL with a device tensor when `device` is given)."""
+def torch_allgather(group=None):
+    """allgather(v) over torch.distributed's gloo backend: one int64 per rank,
+    host tensors only.  The exchange is 8 bytes per rank (no
+    data-path collective), so it never needs RCCL, and the libmcdc process
+    never initialises torch's own HIP runtime beside libmcdc's."""
     import torch
     import torch.distributed as dist
 
     def ag(v):
         world = dist.get_world_size(group)
-        t = torch.tensor([int(v)], dtype=torch.int64, device=device)
-        out = torch.zeros(world, dtype=torch.int64, device=device)
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        out = torch.zeros(world, dtype=torch.int64)
         dist.all_gather_into_tensor(out, t, group=group)
-        return out.cpu().tolist()
+        return out.tolist()
     return ag
 
 

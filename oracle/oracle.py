@@ -696,13 +696,17 @@ def parse_header(header_data: bytes, key=None):
     return out
 
 
+MIN_CHUNK_SIZE = 512 << 10  # global::defaults::MIN_CHUNK_SIZE (/root/reference/src/global/defaults.rs:35)
+
+
 def save_files(params: Params, files, index=None, key=None, nonces=None, header_nonces=None, padding=None,
-               max_pack_size: int = 16 << 20, threads: int = 8):
+               max_pack_size: int = 16 << 20, threads: int = 8, gate_bytes: int = MIN_CHUNK_SIZE):
     """The Archiver's save path for a run of files, in file order, restated
     (test infrastructure; the product is mcdc_save_files):
 
     * processor::save_file (processor.rs:138-157): a file smaller than
-      MIN_CHUNK_SIZE (params.min_size) is one blob, ID = ID::from_content of
+      MIN_CHUNK_SIZE (the constant, :144-145, whatever the chunker's min;
+      gate_bytes, default 512 KiB) is one blob, ID = ID::from_content of
       the whole file (SaveID::CalculateID); otherwise chunk_and_save_blobs
       (:160-205): StreamCDC chunks, ID::from_content per chunk, in order;
     * Repository::save_blob (repository_v1.rs:155-195) per blob: skip it when
@@ -720,7 +724,7 @@ def save_files(params: Params, files, index=None, key=None, nonces=None, header_
     per_file, blob_bytes = [], []
     for f in files:
         a = np.ascontiguousarray(np.frombuffer(f, np.uint8) if not isinstance(f, np.ndarray) else f, np.uint8)
-        if a.size < params.min_size:
+        if a.size < gate_bytes:
             ch = np.zeros(1, dtype=CHUNK_DTYPE)
             ch["length"] = a.size
         else:

@@ -102,3 +102,45 @@ def test_batcher_many_submitters(threads):
     assert not bad, bad
     assert st["files"] == nfiles and st["bytes"] == int(sizes.sum())
     assert st["batches"] < nfiles and st["max_batch_files"] > 1, st
+
+
+def test_two_contexts_24gib_streams_concurrently():
+    """Two worker threads, each with its own context (INTEGRATION.md §2's
+    per-worker context), chunk a distinct 24 GiB device-resident stream at the
+    same time, three calls each, so the two LDS-filling scans share the CUs
+    with each other's resolution waves (k_spec_lane / k_emit) -- the
+    co-residence the round-3 exact-fill exemption of k_scan_q assumed never
+    happened.  Every call's whole boundary list and every
+    ChunkData.hash against the oracle's streamed digest of its stream."""
+    n = 24 << 30
+    seeds = [0x6d61706163686521 ^ 0x24A, 0x6d61706163686521 ^ 0x24B]
+    ref = [None, None]
+
+    def oracle_digest(i):
+        ref[i] = O.random_stream_digest(O.Params(*P16), seeds[i], n, hashes=True)
+    oth = [threading.Thread(target=oracle_digest, args=(i,)) for i in range(2)]
+    for t in oth:  # the oracle digests run on the host while the GPU works
+        t.start()
+    got = [[], []]
+    cap = n // (P16[0] - 1) + 2
+
+    def worker(i):
+        with _lib.Context(0, n) as c:
+            dp = c.device_alloc(n)
+            d_out = c.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+            try:
+                c.fill_random(dp, n, seeds[i])
+                for _ in range(3):
+                    k = c.chunk_device_to_device(_lib.params(*P16), dp, n, d_out, cap)
+                    g = c.d2h_chunks(d_out, k)
+                    got[i].append((k, _lib.digest(g), int(g["length"].sum()), O.hash_digest(g)))
+            finally:
+                c.device_free(d_out)
+                c.device_free(dp)
+    _threads(2, worker)
+    for t in oth:
+        t.join()
+    for i in range(2):
+        assert len(got[i]) == 3
+        for j, r in enumerate(got[i]):
+            assert r == ref[i], (i, j, r, ref[i])

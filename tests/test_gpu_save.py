@@ -5,8 +5,9 @@ Repository::save_blob (repository_v1.rs:155-195): per-file ID lists in file
 order, which blobs were stored, and every pack byte for byte (blobs encoded by
 SecureStorage with and without a key, headers, trailers, pack IDs).
 
-Inputs: files of mixed sizes around the MIN_CHUNK_SIZE gate (empty, 1 byte,
-min - 1, min, min + 1, several MiB), a file repeated whole, two files sharing
+Inputs: files of mixed sizes around the size gate (empty, 1 byte, min - 1,
+min, min + 1, several MiB; the gate at the reference's MIN_CHUNK_SIZE = 512
+KiB, processor.rs:144-145, and at the chunker's own min), a file repeated whole, two files sharing
 a long middle region (chunk-level duplicates after the chains resync), two
 equal small files; a second snapshot over the same index with one file
 changed; host and device input; capacity errors that leave the index as it
@@ -67,17 +68,21 @@ def _check(got, ref):
     assert at == g_out.size
 
 
+@pytest.mark.parametrize("gate", [0, P16[0]], ids=["gate-512k", "gate-min"])
 @pytest.mark.parametrize("key", [None, KEY], ids=["no-key", "key"])
-def test_save_files_matches_restatement(ctx, key):
+def test_save_files_matches_restatement(ctx, key, gate):
     files = _files()
     data, offs, lens = _arena(files)
     p = _lib.params(*P16)
     nonces, hn, pad = _rand(1, 4000, 12), _rand(2, 64, 12), _rand(3, 64 * 63, 36)
     with ctx.index_create() as ix:
-        got = ctx.save_files(p, ix, data, offs, lens, key, nonces, hn, pad, max_pack_size=1 << 20)
+        got = ctx.save_files(p, ix, data, offs, lens, key, nonces, hn, pad, max_pack_size=1 << 20, gate_bytes=gate)
         assert len(ix) == int(got[1].sum())
-    ref = O.save_files(O.Params(*P16), files, None, key, nonces, hn, pad, max_pack_size=1 << 20)
+    ref = O.save_files(O.Params(*P16), files, None, key, nonces, hn, pad, max_pack_size=1 << 20,
+                       gate_bytes=gate or O.MIN_CHUNK_SIZE)
     _check(got, ref)
+    if gate:  # the files of min .. 512 KiB are chunked at the chunker's own min
+        assert len(got[0][4]) == 1 and len(got[0][5]) > 1
     ids = got[0]
     assert len(ids[0]) == 1 and ids[0][0].tobytes() == O.blake3(np.zeros(0, np.uint8))  # empty file: one blob
     assert (ids[7] == ids[5]).all() and (ids[11] == ids[10]).all()
@@ -85,6 +90,59 @@ def test_save_files_matches_restatement(ctx, key):
     assert new.sum() < len(new)  # duplicates stored once
     # the shared region's interior chunks are stored once
     assert len({x.tobytes() for x in ids[6]} & {x.tobytes() for x in ids[9]}) >= 30
+
+
+def test_gate_is_min_chunk_size_not_the_chunkers_min(ctx):
+    """processor::save_file gates on the constant MIN_CHUNK_SIZE (512 KiB,
+    processor.rs:144-145, defaults.rs:35), not on the chunker's min: at P16,
+    files of 16-512 KiB are stored whole (one blob, ID of the whole file);
+    files of 512 KiB and more are chunked at 16/64/256 KiB."""
+    sizes = [16384, 16385, 100_000, 300_001, (512 << 10) - 1, 512 << 10, (512 << 10) + 1, 3 << 20]
+    files = [O.random_bytes(n, 900 + i) for i, n in enumerate(sizes)]
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    pad = _rand(13, 64 * 63, 36)
+    with ctx.index_create() as ix:
+        got = ctx.save_files(p, ix, data, offs, lens, None, None, None, pad, max_pack_size=1 << 20)
+    ref = O.save_files(O.Params(*P16), files, None, None, None, None, pad, max_pack_size=1 << 20)
+    _check(got, ref)
+    for f, n in enumerate(sizes):
+        if n < (512 << 10):
+            assert len(got[0][f]) == 1 and got[0][f][0].tobytes() == O.blake3(files[f]), f
+        else:
+            assert len(got[0][f]) == len(O.chunk(O.Params(*P16), files[f])) > 1, f
+
+
+def test_failure_after_index_add_rolls_back(monkeypatch):
+    """Every failure after the dedup step leaves the index as it was (ADVICE
+    r03): a context built with the test hook MCDC_TEST_FAIL_AFTER_INDEX fails
+    each call after its encode and pack steps have run; the index keeps its
+    size and a later call on a normal context stores the same blobs."""
+    files = _files(8)
+    data, offs, lens = _arena(files)
+    p = _lib.params(*P16)
+    nonces, hn, pad = _rand(14, 4000, 12), _rand(15, 64, 12), _rand(16, 64 * 63, 36)
+    monkeypatch.setenv("MCDC_TEST_FAIL_AFTER_INDEX", "1")
+    bad = _lib.Context(0, 64 << 20)
+    monkeypatch.delenv("MCDC_TEST_FAIL_AFTER_INDEX")
+    good = _lib.Context(0, 64 << 20)
+    try:
+        with bad.index_create() as ix:
+            for gpu in (False, True):
+                with pytest.raises(_lib.McdcError) as ei:
+                    bad.save_files(p, ix, data, offs, lens, KEY, nonces, hn, pad, gpu_compress=gpu)
+                assert ei.value.code == _lib.MCDC_E_DEVICE and len(ix) == 0
+            # too few nonces (an error of the encode step itself)
+            with pytest.raises(_lib.McdcError):
+                good.save_files(p, ix, data, offs, lens, KEY, nonces[:2], hn, pad)
+            assert len(ix) == 0
+            got = good.save_files(p, ix, data, offs, lens, KEY, nonces, hn, pad)
+            assert len(ix) == int(got[1].sum()) > 0
+        ref = O.save_files(O.Params(*P16), files, None, KEY, nonces, hn, pad)
+        _check(got, ref)
+    finally:
+        bad.close()
+        good.close()
 
 
 def test_second_snapshot_stores_only_changes(ctx):
@@ -207,12 +265,17 @@ def test_gpu_compressed_save_path(ctx, key, device_in):
     assert (new == r_new).all()
     stored = [x.tobytes() for x in np.concatenate(ids)[new]]
     seen, at, enc_text, raw_text = [], 0, 0, 0
+    enc_lens, per_pack = [], []
     text_ids = {x.tobytes() for f in (12, 13) for x in ids[f]}
     for k, pk in enumerate(packs):
         assert int(pk["offset"]) == at
         body = out[at:at + int(pk["length"])].tobytes()
         assert bytes(pk["id"]) == O.blake3(np.frombuffer(body, np.uint8))
-        for bid, typ, off, ln in O.parse_header(body, key):
+        hdr = O.parse_header(body, key)
+        per_pack.append(len(hdr))
+        assert int(pk["nblobs"]) == len(hdr)
+        for bid, typ, off, ln in hdr:
+            enc_lens.append(ln)
             dec = O.storage_decode(body[off:off + ln], key, size_hint=1 << 20)
             assert O.blake3(np.frombuffer(dec, np.uint8)) == bid and typ == 0
             seen.append(bid)
@@ -222,4 +285,7 @@ def test_gpu_compressed_save_path(ctx, key, device_in):
         at += int(pk["length"])
     assert at == out.size
     assert seen == stored
+    # pack layout: the flush rule (repository_v1.rs:185-192) over the GPU
+    # encoded sizes, which differ from level 3's
+    assert per_pack == [f1 - f0 for f0, f1 in O.pack_plan(enc_lens, 1 << 20)]
     assert raw_text > 0 and enc_text < raw_text / 1.8, (enc_text, raw_text)
