@@ -821,6 +821,9 @@ def main() -> int:
     ap.add_argument("--no-ids", action="store_true", help="skip the chunk-ID (BLAKE3) stage")
     ap.add_argument("--no-seal", action="store_true", help="skip the SecureStorage sealing stage")
     ap.add_argument("--encode-gib", type=float, default=1.0, help="host encode/decode sample (GiB, 0: skip)")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the timed headline steps (warmup + steps calls of the 64 GiB stream): the command "
+                         "whose rocprofv3 kernel trace is the roofline's evidence (profiles/rNN/headline_*)")
     ap.add_argument("--parity", action="store_true",
                     help="after timing, gather every rank's exact chunks of the split stream and compare the "
                          "whole list with the oracle's (small --gib; tests/test_gpu_multirank.py)")
@@ -848,7 +851,9 @@ def main() -> int:
     from mapache_amd import _lib, shard
     p = _lib.params(*PARAMS)
     n = int(a.gib * GIB)
-    extras = rank == 0 and world == 1
+    extras = rank == 0 and world == 1 and not a.headline_only
+    if a.headline_only:
+        a.corpus_files_per_gpu = 0
     corpus_bytes = a.corpus_files_per_gpu * (8 << 20)
     max_bytes = max(n + PARAMS[2], corpus_bytes, a.batch_files * (8 << 20) if extras else 0)
     ctx = _lib.Context(local, max_bytes)
