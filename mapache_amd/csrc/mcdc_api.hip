@@ -235,7 +235,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
+      sv_in, sv_pack, sv_comp, sv_seal, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -934,7 +934,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
+                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
@@ -1633,19 +1633,20 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   size_t bound = 0, cbytes = 0;
   int rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, nullptr, 0, &bound, fr.data());
   if (rc != MCDC_E_CAPACITY) return rc ? rc : fail(MCDC_E_INTERNAL, "compress bound query did not report a bound");
-  if ((rc = ensure(ctx, ctx->enc_in, std::max<size_t>(bound, 1))) ||
-      (rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->enc_in.p, bound, &cbytes, fr.data())))
+  // (buffers of their own: plan_packs' header encode reuses enc_in / enc_out)
+  if ((rc = ensure(ctx, ctx->sv_comp, std::max<size_t>(bound, 1))) ||
+      (rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->sv_comp.p, bound, &cbytes, fr.data())))
     return rc;
   std::vector<uint64_t> eo(m + 1, 0);
-  const uint8_t *E = (const uint8_t *)ctx->enc_in.p;  // encoded blob k = E[eo[k], eo[k + 1])
+  const uint8_t *E = (const uint8_t *)ctx->sv_comp.p;  // encoded blob k = E[eo[k], eo[k + 1])
   if (store->key) {
     const size_t scap = cbytes + (size_t)kAeadOverhead * m;
-    if ((rc = ensure(ctx, ctx->enc_out, scap)) ||
-        (rc = aead_run(ctx, 0, store->key, ctx->enc_in.p, cbytes, fr.data(), m, store->nonces, ctx->enc_out.p, scap,
+    if ((rc = ensure(ctx, ctx->sv_seal, scap)) ||
+        (rc = aead_run(ctx, 0, store->key, ctx->sv_comp.p, cbytes, fr.data(), m, store->nonces, ctx->sv_seal.p, scap,
                        eo.data(), nullptr)))
       return rc;
-    E = (const uint8_t *)ctx->enc_out.p;
-  } else {  // frames are back to back from enc_in
+    E = (const uint8_t *)ctx->sv_seal.p;
+  } else {  // frames are back to back from sv_comp
     for (size_t k = 0; k < m; ++k) eo[k] = fr[k].offset;
     eo[m] = cbytes;
   }

@@ -1,0 +1,97 @@
+"""Synthetic compression corpora shared by the GPU zstd tests, bench.py and
+tools/ (test and benchmark data, not product code).  All deterministic.
+
+* text     a 2 000-word vocabulary of random lowercase words, words drawn
+           uniformly, space separated (the bench's encode corpus)
+* records  CSV-like rows: ids, two names from 300, amounts, dates
+* binary   a mix of the byte shapes a backup holds besides text: fixed-width
+           little-endian structs (incrementing ids, small counters, float32
+           measurements with shared exponents, zero-padded name fields, flag
+           bytes), runs of code-like bytes (opcode templates with random
+           immediates and displacements) and short incompressible stretches
+           (compressed or encrypted payloads), interleaved in 1-16 KiB pieces;
+           bytes >= 128 throughout (it is the corpus that exercises
+           Huffman literals with FSE-compressed weights)
+"""
+import numpy as np
+
+
+def text(n: int, seed: int = 21) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
+    t = b" ".join(vocab[i] for i in rng.integers(0, 2000, n // 4 + 16))
+    return np.frombuffer(t[:n], np.uint8).copy()
+
+
+def records(n: int, seed: int = 3) -> np.ndarray:
+    """CSV-like rows (ids, names, amounts, dates): long repeats at varied
+    offsets and skewed codes."""
+    rng = np.random.default_rng(seed)
+    names = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(4, 12, 300)]
+    m = n // 24 + 16  # rows (>= 25 bytes each)
+    a, b = rng.integers(0, 300, m), rng.integers(0, 300, m)
+    x, y, d = rng.integers(0, 1000, m), rng.integers(0, 100, m), rng.integers(1, 29, m)
+    t = b"".join(b"%d,%s,%s,%d.%02d,2026-10-%02d\n" % (100000 + i, names[a[i]], names[b[i]], x[i], y[i], d[i])
+                 for i in range(m))
+    return np.frombuffer(t[:n], np.uint8).copy()
+
+
+def _structs(rng, nbytes: int, id0: int) -> bytes:
+    m = nbytes // 48 + 1
+    rec = np.zeros(m, dtype=[("id", "<u4"), ("count", "<u2"), ("kind", "u1"), ("flags", "u1"),
+                             ("value", "<f4"), ("scale", "<f4"), ("stamp", "<u8"), ("name", "S16"),
+                             ("pad", "<u4"), ("crc", "<u4")])
+    rec["id"] = np.arange(id0, id0 + m, dtype=np.uint32)
+    rec["count"] = rng.integers(0, 40, m)
+    rec["kind"] = rng.choice(np.array([1, 2, 3, 7, 0x81, 0xC0], np.uint8), m)
+    rec["flags"] = rng.choice(np.array([0, 0, 0x80, 0x01, 0xFF], np.uint8), m)
+    rec["value"] = (rng.normal(100.0, 3.0, m)).astype(np.float32)
+    rec["scale"] = rng.choice(np.array([0.5, 1.0, 2.0, 1000.0], np.float32), m)
+    rec["stamp"] = 1_790_000_000_000 + np.cumsum(rng.integers(1, 5000, m)).astype(np.uint64)
+    names = [b"alpha", b"beta", b"gamma_ray", b"delta.cfg", b"\xc3\xa9t\xc3\xa9", b"omega-7", b"", b"sigma.log"]
+    rec["name"] = [names[i] for i in rng.integers(0, len(names), m)]
+    rec["crc"] = rng.integers(0, 1 << 32, m, dtype=np.uint64).astype(np.uint32)
+    return rec.tobytes()[:nbytes]
+
+
+_OPS = [b"\x48\x89\xe5", b"\x48\x83\xec", b"\x48\x8b\x45", b"\x48\x8d\x05", b"\xe8", b"\xe9", b"\x0f\x84",
+        b"\x0f\x85", b"\x41\x57", b"\x41\x56", b"\x55", b"\x5d", b"\xc3", b"\x31\xc0", b"\x48\x85\xc0",
+        b"\x74", b"\x75", b"\x89\x45", b"\x8b\x45", b"\xff\x15", b"\x66\x0f\x1f\x44\x00\x00", b"\x90"]
+_IMM = [0, 0, 1, 2, 4, 8, 1, 2, 4, 4]  # immediate bytes after each template (cycled)
+
+
+def _code(rng, nbytes: int) -> bytes:
+    out = bytearray()
+    ops = rng.integers(0, len(_OPS), nbytes // 3 + 8)
+    for k, o in enumerate(ops):
+        out += _OPS[o]
+        w = _IMM[(o + k) % len(_IMM)] if o in (1, 2, 3, 4, 5, 6, 7, 15, 16, 17, 18, 19) else 0
+        if w:
+            v = int(rng.integers(-200, 200)) if w <= 2 else int(rng.integers(-(1 << 20), 1 << 20))
+            out += (v & ((1 << (8 * w)) - 1)).to_bytes(w, "little")
+        if len(out) >= nbytes:
+            break
+    return bytes(out[:nbytes])
+
+
+def binary(n: int, seed: int = 5) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    parts, at, id0 = [], 0, 1000
+    while at < n:
+        k = int(rng.integers(1 << 10, 16 << 10))
+        r = rng.random()
+        if r < 0.5:
+            b = _structs(rng, k, id0)
+            id0 += k // 48 + 1
+        elif r < 0.85:
+            b = _code(rng, k)
+        else:
+            b = rng.integers(0, 256, min(k, 4096), dtype=np.uint8).tobytes()
+        parts.append(b)
+        at += len(b)
+    return np.frombuffer(b"".join(parts)[:n], np.uint8).copy()
+
+
+def by_name(kind: str, n: int, seed: int | None = None) -> np.ndarray:
+    f = {"text": text, "records": records, "binary": binary}[kind]
+    return f(n) if seed is None else f(n, seed)
