@@ -707,6 +707,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   static_assert(sizeof(size_t) == sizeof(uint64_t), "counts are 64-bit");
   if (want_counts) std::memcpy(counts, ctx->h_fcnt, nfiles * sizeof(uint64_t));
   float scan_ms = 0, dev_ms = 0;
+  // (the resolution stream waited for the scan's last part event, not for
+  // ev_scan recorded after it on the scan's stream: it may still be pending)
+  if (rs != st) HIP_TRY(hipEventSynchronize(ctx->ev_scan));
   HIP_TRY(hipEventElapsedTime(&scan_ms, ctx->ev_start, ctx->ev_scan));
   HIP_TRY(hipEventElapsedTime(&dev_ms, ctx->ev_start, ctx->ev_end));
   ctx->timing.scan_ms = scan_ms;
