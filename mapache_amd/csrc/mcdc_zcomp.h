@@ -9,14 +9,11 @@
 
 namespace mcdc {
 
-constexpr uint64_t kZcBlock = 16384;               // zstd block: 16 KiB of one chunk
-constexpr uint32_t kZcSeqCap = 4096;               // sequences per block: a 16 KiB block of 4-byte matches
+constexpr uint64_t kZcBlock = 32768;               // zstd block: 32 KiB of one chunk
+constexpr uint32_t kZcSeqCap = kZcBlock / 4;       // sequences per block: every match is >= 4 bytes
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
-#ifndef MCDC_ZC_RUN
-#define MCDC_ZC_RUN 2  // (compile-time A/B knob; tools/build_variants.py)
-#endif
-constexpr uint32_t kZcRun = MCDC_ZC_RUN;           // blocks parsed in a row by one wave (table kept)
-constexpr uint64_t kZcBatchBlocks = 65536;         // blocks per batch (1 GiB; more for a longer chunk)
+constexpr uint32_t kZcSegBlocks = 8;               // blocks of a chunk one match-finder workgroup covers
+constexpr uint64_t kZcBatchBlocks = 8192;          // blocks per batch (256 MiB; more for a longer chunk)
 
 struct ZcBlock {
   uint64_t src;                 // chunk bytes [src, src + len) of the input
@@ -31,9 +28,15 @@ size_t zc_tmp_bytes(uint64_t n);
 // frame sizes (the output capacity that always suffices).
 void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint64_t *first,
                        uint32_t *err, uint64_t *bound, void *tmp, size_t tmp_bytes, hipStream_t st);
+// Scratch per batch of nblk blocks (bytes), all device memory of the context:
+//   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot, seqs nblk x kZcSeqCap
+//   x 8, match words nblk x kZcBlock x 4 (6.1 x the batch's input in all),
+//   piece / poff (nblk + 1) x 8.  A batch holds whole chunks, at most
+//   kZcBatchBlocks blocks unless one chunk is longer (1 GiB: 7 x 2^18 words).
 // one batch: the chunks [c0, c1), blocks [b0, b0 + nblk)
-void launch_zc_batch(const uint8_t *base, const DevChunk *chunks, const uint64_t *first, uint64_t c0, uint64_t c1,
-                     uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
+void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
+                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
+                     uint32_t *words,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true);
 

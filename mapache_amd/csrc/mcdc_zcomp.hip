@@ -7,28 +7,37 @@
 // compressed (Huffman / RLE / raw literals + FSE sequences, predefined or per-block tables,
 // mcdc_zstd.h) or raw when that is not smaller.  Decodes with mapache's decoder (storage.rs:87-94).
 //
-// Per batch of blocks (a block = 16 KiB of one chunk; batches bound the
+// Per batch of blocks (a block = 32 KiB of one chunk; batches bound the
 // scratch):
 //   k_zc_blocks  block records of the batch's chunks (chunk, index, source)
-//   k_zc_match   ONE WAVE PER BLOCK: greedy LZ parse.  An 8192-entry hash
-//                table in LDS (16-bit positions, colliding lanes resolved to
-//                the largest, ht_put) is primed with the previous 16 KiB of
-//                the same chunk (matches reach back up to 32 KiB); the wave
-//                hashes 64 positions at once (every step-th position after
-//                match-free strides), verifies and extends each lane's
-//                candidate, then walks the lanes' matches greedily (ballot +
-//                readlane, wave-uniform); long matches are extended 64 bytes
-//                per step.  Literals go to the block's staging slot, sequences
-//                (<= kZcSeqCap = 4096 per block, then the rest are literals) straight to
-//                scratch (16 KiB of LDS per wave: 10 waves per CU).
+//   k_zc_find    ONE WORKGROUP (4 waves) PER SEGMENT of up to 8 blocks of a
+//                chunk: candidate matches for every position.  Two tables of
+//                2^15 16-bit positions in LDS (128 KiB: a 5-byte key and an
+//                8-byte key, as zstd's double-fast pair), filled 256
+//                positions at a time: a tile reads its candidates from the
+//                tables as the earlier tiles left them, then inserts its own
+//                positions (the latest position per slot kept, whichever
+//                lane's store lands: a read-back loop, so the result never
+//                depends on the hardware's choice).  A segment after a
+//                chunk's first re-inserts the 64 KiB before it (the reach).
+//                Each candidate is verified on 16 bytes; per position one
+//                word (match length <= 16 | offset << 16, 0 = none) to scratch
+//   k_zc_parse   ONE WAVE PER BLOCK: greedy parse over the words, 256
+//                positions per window (4 ballots of "has a match"), the next
+//                match found with scalar bit scans; a match of 16 bytes is
+//                extended 64 bytes per step; literals to the block's staging
+//                slot (64 runs copied at a time), sequences to scratch
 //   k_zc_huff    ONE WAVE PER BLOCK: the block's literals (all of a block
 //                without matches) as a Huffman-coded (or RLE) literals
-//                section when smaller than raw: histogram in LDS, symbols
-//                ranked by the wave, the length-limited canonical code by one
-//                lane, then the streams (four above 1023 literals) by the
-//                whole wave, bit positions from wave scans, assembled in LDS
+//                section when smaller than raw: histogram of the 256 byte
+//                values in LDS, symbols ranked by the wave, the
+//                length-limited canonical code and its description (direct
+//                or FSE-compressed weights) by one lane, then the streams
+//                (four above 1023 literals) by the whole wave, bit positions
+//                from wave scans, assembled in LDS
 //   k_zc_encode  ONE LANE PER BLOCK, 64 blocks per wave sharing one table
-//                set: code histograms of the wave's blocks, per symbol type a
+//                set: repeat codes where an offset repeats one the block set,
+//                code histograms of the wave's blocks, per symbol type a
 //                shared table or the predefined one (seq_plan), the shared
 //                tables built by the wave in LDS; each block takes the shared
 //                table of a type only when its own sequences cost less with
@@ -51,48 +60,33 @@ namespace {
 
 using namespace zs;
 
-// 8192 positions of 16 bits (16 KiB of LDS per wave: 10 waves per CU).
-// Positions are relative to the block's priming window (< 32 KiB, + 1 so 0
-// means empty), so 16 bits hold them; 4x the slots of the 32-bit 2048-entry
-// table in the same LDS per CU keeps ~30 % more of the text's matches
-// (tools/zc_model.cpp: literals 68 -> 35 % of the input).
-#ifndef MCDC_ZC_HLOG
-#define MCDC_ZC_HLOG 13  // (compile-time A/B knob)
-#endif
-constexpr uint32_t kHtLog = MCDC_ZC_HLOG, kHt = 1u << kHtLog;
-static_assert(2 * kZcBlock <= 0xFFFF + 1, "16-bit positions");
+// Match finder tables: 2^15 16-bit positions each (position + 1 modulo
+// 2^16, 0 = empty), so a candidate lies at most 65535 bytes back (the
+// distance is taken modulo 2^16; a stale entry aliases to a nearer position
+// and is rejected by the byte check, or is a valid match there).
+// tools/zc_model2.cpp priced the choices on the bench's corpora (16/64/256
+// KiB chunks): one 2^14 5-byte-key table 2.44 / 3.20 / 1.74 (text / records
+// / binary) -> 2^15 + 2^15 (8-byte key) 2.63 / 3.31 / 1.79, zstd level 3
+// 2.68 / 3.23 / 1.78; 256-position tiles cost < 0.1 % against exact
+// most-recent insertion (1024: 2 % on records).
+constexpr uint32_t kHsLog = 15, kHlLog = 15;
+constexpr uint32_t kFindTile = 256;   // positions per step = threads per workgroup
+constexpr uint32_t kMlCap = 16;       // match bytes verified per candidate (longer: k_zc_parse extends)
+constexpr uint32_t kPrime = 65536;    // bytes before a segment re-inserted (the reach)
 
-__device__ __forceinline__ uint32_t ld4(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
-// Hash of the 5 bytes at a position (4 in v, the fifth in b4): a 5-byte key
-// keeps 4-byte coincidences out of the table (tools/zc_model.cpp: text
-// 2.21 -> 2.25, CSV-like records 2.92 -> 3.05).
-__device__ __forceinline__ uint32_t zhash(uint32_t v, uint32_t b4) {
-  return (v * 2654435761u + (b4 & 0xFFu) * 0x85EBCA77u) >> (32 - kHtLog);
+__device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
+  return (lo * 2654435761u + (hi & 0xFFu) * 0x85EBCA77u) >> (32 - kHsLog);
 }
-// Positions go into the table with plain 16-bit LDS stores (there is no
-// 16-bit max atomic), so when lanes of one store collide on a slot the
-// hardware keeps one of them; the slot must end at the largest (the latest
-// position, as a max would keep it) so the parse does not depend on which.
-// A store is read back after it has landed; lanes that see a smaller value
-// store again (ht_fix), until none does.  The read-back is issued with the
-// store and consumed later (priming: 8 strides at a time; the parse: at the
-// top of the next stride), so its latency is off the critical path.  Later
-// stores of larger positions only raise a slot, so a lane seeing a value >= its
-// own is done.  Called by the whole wave (ballot).
+__device__ __forceinline__ uint32_t hash8(uint32_t lo, uint32_t hi) {
+  return ((lo * 0x9E3779B1u) ^ (hi * 0x85EBCA77u) ^ ((lo ^ hi) >> 15)) * 0xC2B2AE3Du >> (32 - kHlLog);
+}
 // (relaxed workgroup-scope atomics: LDS loads and stores the compiler may not
-// merge or forward -- a volatile generic pointer compiled to flat accesses)
+// merge, forward or move across the barriers of the insert loop)
 __device__ __forceinline__ void ht_st(uint16_t *ht, uint32_t h, uint32_t v) {
   __hip_atomic_store(ht + h, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t ht_ld(uint16_t *ht, uint32_t h) {
   return __hip_atomic_load(ht + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void ht_fix(uint16_t *ht, uint32_t h, uint32_t v, bool ok, uint32_t rb) {
-  bool again = ok && rb < v;
-  while (__ballot(again)) {
-    if (again) ht_st(ht, h, v);
-    again = again && ht_ld(ht, h) < v;
-  }
 }
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
@@ -134,6 +128,104 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
   }
 }
 
+// 16 bytes at p of a buffer of nbytes (zero past its end).
+__device__ __forceinline__ uint4 ld16(const uint8_t *base, uint64_t p, uint64_t nbytes) {
+  if (p + 16 <= nbytes) return *reinterpret_cast<const uint4 *>(base + p);  // (misaligned: gfx950 reads the bytes)
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t i = 0; i < 16 && p + i < nbytes; ++i) w[i >> 2] |= (uint32_t)base[p + i] << (8 * (i & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Common prefix of two 16-byte strings.
+__device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
+  const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
+  uint32_t m = 16;
+#pragma unroll
+  for (int k = 3; k >= 0; --k)
+    if (d[k]) m = 4 * k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
+  return m;
+}
+
+// Slot value v (16-bit, position + 1) against the tile [t0, t0 + kFindTile):
+// true when v is a position of the tile at or after position p (the slot
+// already holds a position as new as p's own).
+__device__ __forceinline__ bool ht_newer(uint32_t v, uint32_t t0, uint32_t p) {
+  const uint32_t r = (v - (t0 + 1)) & 0xFFFFu;  // (its offset in the tile, if it is one of the tile's)
+  return v != 0 && r < kFindTile && t0 + r >= p;
+}
+
+// The match finder: one workgroup of kFindTile threads per segment (up to
+// kZcSegBlocks blocks of one chunk, the first record of the segment's blocks:
+// other workgroups return).  Writes words[(block - batch start) * kZcBlock +
+// position in block] for every position of the segment.
+__global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint64_t nbytes, const ZcBlock *blocks,
+                                                       uint64_t nblk, uint32_t *words) {
+  __shared__ __attribute__((aligned(16))) uint16_t hts[1u << kHsLog], htl[1u << kHlLog];
+  const uint64_t bi0 = blockIdx.x;
+  if (bi0 >= nblk) return;
+  const ZcBlock B0 = blocks[bi0];
+  if (B0.b % kZcSegBlocks) return;
+  const uint32_t tid = threadIdx.x;
+  // chunk geometry (a batch holds whole chunks: the chunk's last block is a record of this batch)
+  const uint64_t csrc = B0.src - (uint64_t)B0.b * kZcBlock;
+  const uint32_t clen = (B0.nb - 1) * (uint32_t)kZcBlock + blocks[bi0 + (B0.nb - 1 - B0.b)].len;
+  const uint32_t seg0 = B0.b * (uint32_t)kZcBlock;
+  const uint32_t seg1 = min(clen, seg0 + kZcSegBlocks * (uint32_t)kZcBlock);
+  const uint32_t prime0 = seg0 > kPrime ? seg0 - kPrime : 0u;
+  for (uint32_t k = tid; k < (1u << kHsLog) / 8; k += kFindTile) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = tid; k < (1u << kHlLog) / 8; k += kFindTile) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
+  const uint8_t *cb = base + csrc;
+  const uint64_t cbytes = nbytes - csrc;  // (bytes readable from the chunk start)
+  uint4 nx = ld16(cb, prime0 + tid, cbytes);  // the next tile's bytes, loaded a tile ahead
+  __syncthreads();
+  for (uint32_t t0 = prime0; t0 < seg1; t0 += kFindTile) {
+    const uint32_t p = t0 + tid;
+    const uint4 x = nx;
+    if (t0 + kFindTile < seg1) nx = ld16(cb, p + kFindTile, cbytes);
+    const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert)
+    const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
+    const uint32_t v = (p + 1) & 0xFFFFu;
+    const uint32_t hs = hash5(x.x, x.y), hl = hash8(x.x, x.y);
+    uint32_t cs = 0, cl = 0;
+    if (find && vs) cs = ht_ld(hts, hs);
+    if (find && vl) cl = ht_ld(htl, hl);
+    // candidates (distance modulo 2^16, within the chunk) and their bytes
+    const uint32_t ds = (p + 1 - cs) & 0xFFFFu, dl = (p + 1 - cl) & 0xFFFFu;
+    const bool oks = cs != 0 && ds != 0 && ds <= p, okl = cl != 0 && dl != 0 && dl <= p && dl != ds;
+    uint4 ys = make_uint4(0, 0, 0, 0), yl = ys;
+    if (oks) ys = ld16(cb, p - ds, cbytes);
+    if (okl) yl = ld16(cb, p - dl, cbytes);
+    __syncthreads();  // every lookup of the tile before any insert
+    const bool ws = vs && v != 0, wl = vl && v != 0;
+    if (ws) ht_st(hts, hs, v);
+    if (wl) ht_st(htl, hl, v);
+    // the latest position per slot: lanes whose store lost to an older
+    // position of the tile (or that an older tile's value still holds) store
+    // again until none does
+    bool ps = ws, pl = wl;
+    while (__syncthreads_or(ps || pl)) {
+      if (ps) {
+        ps = !ht_newer(ht_ld(hts, hs), t0, p);
+        if (ps) ht_st(hts, hs, v);
+      }
+      if (pl) {
+        pl = !ht_newer(ht_ld(htl, hl), t0, p);
+        if (pl) ht_st(htl, hl, v);
+      }
+    }
+    if (find) {
+      const uint32_t bend = min(clen, (p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
+      const uint32_t lim = min(kMlCap, bend - p);
+      uint32_t ms = oks ? min(prefix16(x, ys), lim) : 0u, ml = okl ? min(prefix16(x, yl), lim) : 0u;
+      uint32_t m = 0, d = 0;
+      if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
+      else if (ml >= zs::kMinMatch) m = ml, d = dl;
+      const uint64_t wi = (bi0 + (p / (uint32_t)kZcBlock - B0.b)) * kZcBlock + p % (uint32_t)kZcBlock;
+      words[wi] = m ? (m << 16 | d) : 0u;
+    }
+  }
+}
+
 // Copy bytes [a, a + n) of src to dst, the whole wave (64 lanes) together,
 // four bytes per lane per round loaded before any is stored.
 __device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint32_t n,
@@ -153,121 +245,51 @@ __device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8
   }
 }
 
-// Length of the common prefix of two 32-byte strings (x at p, y at c).
-__device__ __forceinline__ uint32_t match32_xor(uint4 x0, uint4 x1, uint4 y0, uint4 y1) {
-  const uint32_t d[8] = {x0.x ^ y0.x, x0.y ^ y0.y, x0.z ^ y0.z, x0.w ^ y0.w,
-                         x1.x ^ y1.x, x1.y ^ y1.y, x1.z ^ y1.z, x1.w ^ y1.w};
-  uint32_t m = 32;
-#pragma unroll
-  for (int k = 7; k >= 0; --k)
-    if (d[k]) m = 4 * k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
-  return m;
+__device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return j == 0 ? a : j == 1 ? b : j == 2 ? c : d;
+}
+__device__ __forceinline__ uint64_t sel4(uint32_t j, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+  return j == 0 ? a : j == 1 ? b : j == 2 ? c : d;
 }
 
-// Match length at p against c, up to 32 bytes, from one 32-byte load on
-// each side (two misaligned 16-byte loads each; no dependent loop).
-__device__ __forceinline__ uint32_t match32(const uint8_t *p0, uint32_t p, uint32_t c, uint32_t end) {
-  if (p + 32 <= end) {
-    const uint4 x0 = *reinterpret_cast<const uint4 *>(p0 + p), x1 = *reinterpret_cast<const uint4 *>(p0 + p + 16);
-    const uint4 y0 = *reinterpret_cast<const uint4 *>(p0 + c), y1 = *reinterpret_cast<const uint4 *>(p0 + c + 16);
-    const uint32_t d[8] = {x0.x ^ y0.x, x0.y ^ y0.y, x0.z ^ y0.z, x0.w ^ y0.w,
-                           x1.x ^ y1.x, x1.y ^ y1.y, x1.z ^ y1.z, x1.w ^ y1.w};
-    uint32_t m = 32;
-#pragma unroll
-    for (int k = 7; k >= 0; --k)
-      if (d[k]) m = 4 * k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
-    return m;
-  }
-  uint32_t m = 0;  // the block's last 31 bytes
-  while (p + m < end && m < 32 && p0[c + m] == p0[p + m]) ++m;
-  return m;
-}
-
-// One wave parses a run of up to kZcRun consecutive blocks of a chunk,
-// keeping the table from block to block (the run's first block primes it
-// with the previous 16 KiB, as every block did before runs: that re-hash was
-// a large share of the parse).
-// Lane i of a stride looks at position s0 + i * step.  step grows after
-// match-free strides (1, 2, 4, 8: zstd's fast strategies skip ahead the same
-// way on data that does not compress) and drops back to 1 at a match.
-// Literal runs are copied 64 at a time: lane (k mod 64) keeps run k's source,
-// length and destination, and the wave copies the 64 runs together.
-__global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                 uint64_t *seqs) {
-  __shared__ __attribute__((aligned(16))) uint16_t ht[kHt];
-  const uint64_t bi0 = blockIdx.x;
-  if (bi0 >= nblk) return;
+// The greedy parse of one block over k_zc_find's words: a window of 256
+// positions' words (4 per lane) and their "has a match" ballots; the next
+// match at or after the cursor by scalar bit scans; the match's word by
+// readlane.  Literal runs are copied 64 at a time: lane (k mod 64) keeps run
+// k's source, length and destination, and the wave copies the 64 runs
+// together.
+__global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *blocks, uint64_t nblk,
+                                                 const uint32_t *words, uint8_t *stage, uint64_t *seqs) {
+  const uint64_t bi = blockIdx.x;
+  if (bi >= nblk) return;
   const uint32_t lane = lane_id();
-  ZcBlock B = blocks[bi0];
-  if (B.b % kZcRun) return;  // (parsed by its run's first wave)
-  // a run's blocks are consecutive records of the batch (a batch holds whole chunks)
-  const uint32_t nrun = B.nb - B.b < kZcRun ? B.nb - B.b : kZcRun;
-  for (uint32_t k = lane; k < kHt / 8; k += 64) reinterpret_cast<uint4 *>(ht)[k] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  for (uint32_t r = 0; r < nrun; ++r) {
-  const uint64_t bi = bi0 + r;
-  if (r) {
-    // the table as the previous block's parse left it, its positions moved to
-    // this block's frame (p0 advances by the previous block's prime: 0 after
-    // a chunk's first block, else 16 KiB; positions before the new p0 drop)
-    const uint32_t shift = B.b ? (uint32_t)kZcBlock : 0u;
-    B = blocks[bi];
-    if (shift) {
-      for (uint32_t k = lane; k < kHt / 2; k += 64) {
-        const uint32_t w = reinterpret_cast<uint32_t *>(ht)[k];
-        const uint32_t lo = w & 0xFFFFu, hi = w >> 16;
-        reinterpret_cast<uint32_t *>(ht)[k] = (lo > shift ? lo - shift : 0u) | (hi > shift ? hi - shift : 0u) << 16;
-      }
-    }
-    __syncthreads();
-  }
-  const uint32_t prime = B.b ? kZcBlock : 0;  // the previous 16 KiB of the chunk
-  const uint8_t *p0 = base + B.src - prime;   // positions are relative to p0
-  const uint32_t end = prime + B.len;
-  if (r == 0) {  // a run's first block: the table primed with the previous 16 KiB
-    for (uint32_t q0 = 0; q0 < prime; q0 += 8 * 64) {  // (prime: 0 or 16 KiB, a multiple of 512)
-      uint32_t h[8], rb[8];
-      bool ok[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t q = q0 + 64 * j + lane;
-        ok[j] = q + 4 <= prime;  // (the block's own bytes are not read here)
-        h[j] = ok[j] ? zhash(ld4(p0 + q), p0[q + 4]) : 0u;  // (q + 4 <= prime: byte q + 4 is the block's own at worst)
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (ok[j]) ht_st(ht, h[j], q0 + 64 * j + lane + 1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) rb[j] = ht_ld(ht, h[j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ht_fix(ht, h[j], q0 + 64 * j + lane + 1, ok[j], rb[j]);
-    }
-  }
-  __syncthreads();
-  uint8_t *lit = stage + bi * kZcSlot + kLitHdr;
+  const ZcBlock B = blocks[bi];
+  const uint32_t end = B.len;
+  const uint8_t *p0 = base + B.src;
+  const uint32_t *w = words + bi * kZcBlock;
+  uint8_t *lit = stage + bi * kZcSlot + zs::kLitHdr;
   uint64_t *sq = seqs + bi * kZcSeqCap;
-  uint32_t nlit = 0, nseq = 0, cursor = prime, lit0 = prime, step = 1, miss = 0;
+  uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0;
   uint32_t run_src = 0, run_len = 0, run_dst = 0;  // this lane's pending literal run
   // 64 bytes of each lane's run per step: four 16-byte loads in flight, then
-  // byte stores (a byte-at-a-time copy paid one memory round trip per byte:
-  // the loads could not pass the stores to the possibly aliasing staging slot)
+  // byte stores
   auto flush_runs = [&]() {
     uint32_t mx = run_len;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
     for (uint32_t k0 = 0; k0 < mx; k0 += 64) {
-      uint4 w[4];
+      uint4 q[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t k = k0 + 16 * j;
-        w[j] = make_uint4(0, 0, 0, 0);
+        q[j] = make_uint4(0, 0, 0, 0);
         if (k < run_len) {
           if (run_src + k + 16 <= end) {
-            w[j] = *reinterpret_cast<const uint4 *>(p0 + run_src + k);
+            q[j] = *reinterpret_cast<const uint4 *>(p0 + run_src + k);
           } else {  // (the block's last bytes: no read past them)
             uint32_t b[4] = {0, 0, 0, 0};
             for (uint32_t i = 0; i < 16 && run_src + k + i < end; ++i) b[i >> 2] |= (uint32_t)p0[run_src + k + i] << (8 * (i & 3));
-            w[j] = make_uint4(b[0], b[1], b[2], b[3]);
+            q[j] = make_uint4(b[0], b[1], b[2], b[3]);
           }
         }
       }
@@ -276,7 +298,7 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
         const uint32_t k = k0 + 16 * j;
         if (k < run_len) {
           const uint32_t n = run_len - k < 16 ? run_len - k : 16;
-          const uint32_t b[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+          const uint32_t b[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
           uint8_t *d = lit + run_dst + k;
 #pragma unroll
           for (uint32_t i = 0; i < 16; ++i)
@@ -286,59 +308,38 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
     }
     run_len = 0;
   };
-  uint32_t fh = 0, fv = 0, frb = 0;  // the previous stride's store, checked at the top of this one
-  bool fok = false;
-  for (uint32_t s0 = prime; s0 + 4 <= end;) {
-    ht_fix(ht, fh, fv, fok, frb);
-    const uint32_t p = s0 + lane * step;
-    const bool ok = p + 4 <= end, full = p + 32 <= end;
-    // this position's 32 bytes up front (they hold v), so a candidate costs one
-    // more round trip (its 32 bytes), not two (4 bytes to verify, then 32)
-    uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;
-    if (full) {
-      x0 = *reinterpret_cast<const uint4 *>(p0 + p);
-      x1 = *reinterpret_cast<const uint4 *>(p0 + p + 16);
+  auto load_win = [&](uint32_t wb, uint32_t *v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t q = wb + 64 * j + lane;
+      v[j] = q < end ? w[q] : 0u;
     }
-    const uint32_t v = full ? x0.x : ok ? ld4(p0 + p) : 0u;
-    const uint32_t h = zhash(v, full ? x0.y : p + 5 <= end ? p0[p + 4] : 0u);
-    const uint32_t cand = ok ? ht[h] : 0u;
-    {  // (issued after every lane's read: one wave, in order)
-      if (ok) ht_st(ht, h, p + 1);
-      frb = ok ? ht_ld(ht, h) : 0u;
-      fh = h;
-      fv = p + 1;
-      fok = ok;
-    }
-    uint32_t mlen = 0, c = 0;
-    if (cand) {
-      c = cand - 1;
-      if (c < p && p - c < kWindow) {
-        if (full) {
-          const uint4 y0 = *reinterpret_cast<const uint4 *>(p0 + c), y1 = *reinterpret_cast<const uint4 *>(p0 + c + 16);
-          mlen = match32_xor(x0, x1, y0, y1);
-        } else if (ld4(p0 + c) == v) {
-          mlen = match32(p0, p, c, end);
-        }
+  };
+  uint32_t wb = 0, v[4], nv[4];
+  load_win(0, v);
+  load_win(256, nv);
+  while (wb < end) {
+    const uint64_t m0 = __ballot(v[0] != 0), m1 = __ballot(v[1] != 0), m2 = __ballot(v[2] != 0),
+                   m3 = __ballot(v[3] != 0);
+    while (cur < wb + 256) {  // the matches of this window, in order
+      const uint32_t rel = cur - wb;
+      uint32_t j = rel >> 6;
+      uint64_t mm = sel4(j, m0, m1, m2, m3) & (~0ull << (rel & 63));
+      while (!mm && ++j < 4) mm = sel4(j, m0, m1, m2, m3);
+      if (!mm) {
+        cur = wb + 256;
+        break;
       }
-    }
-    const uint64_t m = __ballot(mlen >= kMinMatch);
-    if (cursor < s0) cursor = s0;  // positions before s0 that no match covered are literals
-    const uint32_t span = 64 * step;
-    bool stop = false;
-    while (true) {
-      if (cursor >= s0 + span) break;
-      const uint32_t first_lane = (cursor - s0 + step - 1) / step;  // lanes at or after the cursor
-      if (first_lane >= 64) break;
-      const uint64_t mm = m & (~0ull << first_lane);
-      if (!mm) break;
       const uint32_t i = (uint32_t)__builtin_ctzll(mm);
-      const uint32_t pos = s0 + i * step;
-      uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)mlen, (int)i);
-      const uint32_t off = pos - (uint32_t)__builtin_amdgcn_readlane((int)c, (int)i);
-      if (ml == 32) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
+      const uint32_t pos = wb + 64 * j + i;
+      const uint32_t wd = (uint32_t)__builtin_amdgcn_readlane((int)sel4(j, v[0], v[1], v[2], v[3]), (int)i);
+      uint32_t ml = wd >> 16;
+      const uint32_t off = wd & 0xFFFFu;
+      if (ml == kMlCap) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
         for (;;) {
           const uint32_t q = pos + ml + lane;
-          const bool same = q < end && p0[q] == p0[q - off];
+          // (the source may lie in an earlier block of the chunk: p0 - off + q, signed)
+          const bool same = q < end && p0[q] == p0[(int64_t)q - (int64_t)off];
           const uint64_t diff = __ballot(!same);
           ml += diff ? (uint32_t)__builtin_ctzll(diff) : 64u;
           if (diff) break;
@@ -348,29 +349,25 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
         run_src = lit0;
         run_len = pos - lit0;
         run_dst = nlit;
-        sq[nseq] = seq_pack(pos - lit0, ml, off);
+        sq[nseq] = zs::seq_pack(pos - lit0, ml, off);
       }
       nlit += pos - lit0;
       ++nseq;
       if ((nseq & 63) == 0) flush_runs();
-      cursor = pos + ml;
-      lit0 = cursor;
-      if (nseq == kZcSeqCap) {  // the rest of the block: literals
-        stop = true;
-        break;
-      }
+      cur = pos + ml;
+      lit0 = cur;
     }
-    if (stop) break;
-    if (m) {
-      miss = 0;
-      step = 1;
-    } else if (++miss >= 4 && step < 8) {
-      step *= 2;
-      miss = 0;
+    // the next window: the prefetched one, or (after a long match) the cursor's
+    const uint32_t nb = cur & ~63u;
+    if (nb == wb + 256) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = nv[j];
+    } else {
+      load_win(nb, v);
     }
-    s0 = cursor > s0 + span ? cursor : s0 + span;
+    wb = nb;
+    load_win(wb + 256, nv);
   }
-  ht_fix(ht, fh, fv, fok, frb);  // (the last stride's store: the next block reads the table)
   if (nseq) {  // (no sequence: the block is stored raw from the input, nothing to stage)
     flush_runs();
     wave_copy(lit + nlit, p0 + lit0, end - lit0, lane);
@@ -379,8 +376,6 @@ __global__ __launch_bounds__(64) void k_zc_match(const uint8_t *base, ZcBlock *b
   if (lane == 0) {
     blocks[bi].nlit = nlit;
     blocks[bi].nseq = nseq;
-  }
-  __syncthreads();
   }
 }
 
@@ -396,24 +391,23 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
 
 // The literals section of a compressed block: Huffman-coded or RLE when that
 // is smaller than the raw section (3-byte header + the literals), written
-// over the staging slot's raw literals; B.lsize its size, 0 = raw.  Literals
-// >= 128 keep the raw section (the direct weight representation covers
-// symbols 0..128; 128 itself is not worth the check).  The whole wave works
-// on every step but the tree (one lane, ~2n dependent steps on LDS):
-//   count    16 bytes per lane per step into 8 LDS histogram copies, leaving
-//            at the first KiB that holds a byte >= 128 (random data: 1 KiB)
-//   rank     symbols by count (ties by symbol), one rank per lane
-//   tree     huf_build on the ranked symbols (lane 0)
+// over the staging slot's raw literals; B.lsize its size, 0 = raw.  The whole
+// wave works on every step but the tree and its description (one lane):
+//   count    16 bytes per lane per step into 8 LDS histogram copies
+//   rank     the 256 symbols by count (ties by symbol), four per lane
+//   tree     huf_build on the ranked symbols, the weights' description
+//            (direct or FSE-compressed, the shorter; lane 0)
 //   sizes    bits per stream (wave sums); give up unless smaller than raw
 //   streams  64 literals per round, last first: code lengths -> wave scan ->
 //            bit positions -> codes OR-ed into the section assembled in LDS
-//            (literal loads 8 rounds ahead)
 //   store    header, tree, jump table; the section to the slot, 16-byte stores
 __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage) {
   // the section under assembly; its first 8 KiB hold the histogram copies and
   // then the tree's scratch before it is cleared
   __shared__ __attribute__((aligned(16))) uint32_t out[kZcSlot / 4];
   __shared__ HufCT ct;
+  __shared__ uint8_t tdesc[132];
+  __shared__ uint32_t tree_sz;
   uint32_t(*hist)[256] = reinterpret_cast<uint32_t(*)[256]>(out);
   HufWork &hw = *reinterpret_cast<HufWork *>(out + 8 * 256);
   static_assert(8 * 256 * 4 + sizeof(HufWork) <= sizeof(out), "LDS");
@@ -421,7 +415,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
   if (bi >= nblk) return;
   const uint32_t lane = lane_id();
   const ZcBlock B = blocks[bi];
-  // a block without sequences: all of it literals, read from the input (k_zc_match staged nothing)
+  // a block without sequences: all of it literals, read from the input (k_zc_parse staged nothing)
   const uint32_t n = B.nseq ? B.nlit : B.len;
   if (n < 32) return;  // (lsize stays 0: raw literals)
   uint8_t *st = stage + bi * kZcSlot;
@@ -442,15 +436,14 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
       for (uint32_t j = 0; j < 16; ++j)
         if (j < m) w[j >> 2] |= (uint32_t)src[k + j] << (8 * (j & 3));
     }
-    if (__ballot(((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0)) return;
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j)
-      if (j < m) atomicAdd(&hist[lane & 7][(w[j >> 2] >> (8 * (j & 3))) & 0x7F], 1u);
+      if (j < m) atomicAdd(&hist[lane & 7][(w[j >> 2] >> (8 * (j & 3))) & 0xFF], 1u);
   }
   __syncthreads();
-  uint32_t c[2];
+  uint32_t c[4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < 4; ++h) {
     const uint32_t k = lane + 64 * h;
     uint32_t v = 0;
 #pragma unroll
@@ -458,36 +451,49 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
     c[h] = v;
   }
   __syncthreads();
-  hist[0][lane] = c[0];
-  hist[0][lane + 64] = c[1];
-  if (lane == 0) hist[0][128] = 0;  // (huf_build reads 129 counts)
+#pragma unroll
+  for (int h = 0; h < 4; ++h) hist[0][lane + 64 * h] = c[h];
   // rank: symbols by count ascending, ties by symbol (huf_build's stable order)
-  const uint64_t p0 = __ballot(c[0] != 0), p1 = __ballot(c[1] != 0);
-  const uint32_t distinct = (uint32_t)(__builtin_popcountll(p0) + __builtin_popcountll(p1));
+  uint64_t pm[4];
+  uint32_t distinct = 0;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    pm[h] = __ballot(c[h] != 0);
+    distinct += (uint32_t)__builtin_popcountll(pm[h]);
+  }
   if (distinct == 1) {  // RLE literals: 3-byte header + the byte
     if (lane == 0) {
+      uint32_t sym = 0;
+      for (int h = 0; h < 4; ++h)
+        if (pm[h]) sym = 64 * h + (uint32_t)__builtin_ctzll(pm[h]);
       put_rle_lit_header(st, n);
-      st[3] = (uint8_t)(p0 ? __builtin_ctzll(p0) : 64 + __builtin_ctzll(p1));
+      st[3] = (uint8_t)sym;
       blocks[bi].lsize = 4;
     }
     return;
   }
   __syncthreads();
-  uint32_t r[2] = {0, 0};
-  for (uint32_t t = 0; t < 128; t += 4) {
+  uint32_t r[4] = {0, 0, 0, 0};
+  for (uint32_t t = 0; t < 256; t += 4) {
     const uint4 q = *reinterpret_cast<const uint4 *>(&hist[0][t]);  // (broadcast)
     const uint32_t qs[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 4; ++h)
         r[h] += (qs[j] && (qs[j] < c[h] || (qs[j] == c[h] && t + j < lane + 64 * h))) ? 1u : 0u;
   }
-  if (c[0]) hw.sym[r[0]] = (uint16_t)lane;
-  if (c[1]) hw.sym[r[1]] = (uint16_t)(lane + 64);
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+    if (c[h]) hw.sym[r[h]] = (uint16_t)(lane + 64 * h);
   __syncthreads();
-  if (lane == 0) huf_build(hist[0], ct, hw, true);
+  if (lane == 0) {
+    huf_build(hist[0], ct, hw, true);
+    tree_sz = huf_tree_desc(ct, tdesc);
+  }
   __syncthreads();
+  const uint32_t tree = tree_sz;
+  if (!tree) return;  // (no description applies: raw literals)
   // bits per stream (stream k: literals [k seg, min((k + 1) seg, n)))
   const bool one = n < 1024;
   const uint32_t seg = one ? n : (n + 3) / 4, ns = one ? 1 : 4;
@@ -502,9 +508,8 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
     sb[k] = b;
   }
   uint32_t ssz[4];
-  const uint32_t total = huf_section_size(ct, n, sb, one, ssz);
+  const uint32_t total = huf_section_size(tree, n, sb, one, ssz);
   if (total >= kLitHdr + n) return;  // not smaller than raw
-  const uint32_t tree = 1 + (ct.last + 1) / 2;
   const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
   if (one && csize >= 1024) return;  // (one stream: 10-bit sizes)
   const uint32_t hdr = lit_hdr_size(n, csize, one);
@@ -544,7 +549,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
   if (lane == 0) {
     uint8_t *sec = reinterpret_cast<uint8_t *>(out);
     put_huf_lit_header(sec, n, csize, one);
-    huf_tree_desc(ct, sec + hdr);
+    for (uint32_t i = 0; i < tree; ++i) sec[hdr + i] = tdesc[i];
     if (!one)
       for (int k = 0; k < 3; ++k) {
         sec[hdr + tree + 2 * k] = (uint8_t)ssz[k];
@@ -639,7 +644,7 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
 constexpr uint32_t kEncOwnMin = 64;  // sequences for a block to consider the shared tables
 
 __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                  const uint64_t *seqs, ZTables T, uint64_t *piece) {
+                                                  uint64_t *seqs, ZTables T, uint64_t *piece) {
   MCDC_VGPR_PAD(40);  // (not an exact fill)
   __shared__ FseCTL t[3], pt[3];  // shared (own) and predefined tables
   __shared__ SeqPlan P;
@@ -666,13 +671,19 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   }
   __syncthreads();
   const bool cand = ns >= kEncOwnMin;
-  if (cand)
+  {  // repeat codes (the block's own history, rep_code), in place; the histograms
+    RepHist R{{0, 0, 0}, 0};
+    uint64_t *sw = seqs + bi * kZcSeqCap;
     for (uint32_t i = 0; i < ns; ++i) {
-      const uint64_t q = sq[i];
-      atomicAdd(&hist[0][ll_code(seq_ll(q))], 1u);
-      atomicAdd(&hist[1][highbit(seq_off(q) + 3)], 1u);
-      atomicAdd(&hist[2][ml_code(seq_ml(q) - 3)], 1u);
+      const uint64_t q = rep_code(R, sq[i]);
+      sw[i] = q;
+      if (cand) {
+        atomicAdd(&hist[0][ll_code(seq_ll(q))], 1u);
+        atomicAdd(&hist[1][highbit(seq_ov(q))], 1u);
+        atomicAdd(&hist[2][ml_code(seq_ml(q) - 3)], 1u);
+      }
     }
+  }
   const uint32_t ncand = (uint32_t)__builtin_popcountll(__ballot(cand));
   uint32_t total = cand ? ns : 0;
 #pragma unroll
@@ -698,7 +709,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
     float c0[3] = {0, 0, 0}, c1[3] = {0, 0, 0};
     for (uint32_t i = 0; i < ns; ++i) {
       const uint64_t q = sq[i];
-      const uint32_t code[3] = {ll_code(seq_ll(q)), highbit(seq_off(q) + 3), ml_code(seq_ml(q) - 3)};
+      const uint32_t code[3] = {ll_code(seq_ll(q)), highbit(seq_ov(q)), ml_code(seq_ml(q) - 3)};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         c0[k] += bits[0][k][code[k]];
@@ -790,14 +801,15 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, cnt, first, (int)n + 1, st);
 }
 
-void launch_zc_batch(const uint8_t *base, const DevChunk *chunks, const uint64_t *first, uint64_t c0, uint64_t c1,
-                     uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
-                     const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
-                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf) {
+void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
+                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
+                     uint32_t *words, const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase,
+                     uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf) {
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
-  hipLaunchKernelGGL(k_zc_match, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, seqs);
+  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindTile), 0, st, base, nbytes, blocks, nblk, words);
+  hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, words, stage, seqs);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)((nblk + 1 + 63) / 64)), dim3(64), 0, st, blocks, nblk, stage, seqs,
                      T, piece);

@@ -14,11 +14,13 @@
 //     §3.1.1.3.2.2 (Predefined_Mode) or with the block's own distribution
 //     (FSE_Compressed_Mode: normalized counts, table description), whichever
 //     is estimated smaller,
-//   * offsets always as Offset_Value = offset + 3 (no repeat codes);
+//   * offsets as Offset_Value = offset + 3, or a repeat code (1-3) where the
+//     offset equals a repeat offset the block itself set (rep_code_block);
 //   * literals raw, RLE (one distinct byte) or Huffman-coded (Compressed_
-//     Literals_Block: a length-limited canonical code, weights in the direct
-//     representation -- literals up to byte 128 -- one stream below 1024
-//     literals, four above), whichever section is smallest.
+//     Literals_Block: a length-limited canonical code over all 256 byte
+//     values, weights in the direct representation or FSE-compressed,
+//     whichever is shorter; one stream below 1024 literals, four above),
+//     whichever section is smallest.
 // Any conforming decoder (mapache's: zstd with window_log_max 20,
 // storage.rs:87-94) reads them; the compressed bytes differ from libzstd's,
 // so parity is decode-equality.
@@ -111,7 +113,7 @@ constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
                                  1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
 template <uint32_t S>
-inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCTN<S> &ct) {
+__host__ __device__ inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCTN<S> &ct) {
   const uint32_t size = 1u << tlog;
   uint32_t high = size - 1;
   uint8_t sym[S];
@@ -217,14 +219,68 @@ __host__ __device__ inline void fse_encode(BitW &bw, FseState &st, const CT &ct,
 template <class CT>
 __host__ __device__ inline void fse_flush(BitW &bw, const FseState &st, const CT &ct) { bw.add(st.value, ct.log); }
 
-// One sequence: literal length, match length (>= 3), offset (>= 1).
-// Packed in 64 bits: ll 21 | ml 21 | off 22 (block <= 128 KiB, window 2^20).
+// One sequence: literal length, match length (>= 3) and the Offset_Value
+// (RFC 8878 §3.1.1.5: offset + 3 for an explicit offset, 1-3 a repeat code).
+// Packed in 64 bits: ll 21 | ml 21 | offset value 22 (block <= 128 KiB,
+// window 2^20).
+__host__ __device__ inline uint64_t seq_pack_ov(uint32_t ll, uint32_t ml, uint32_t ov) {
+  return (uint64_t)ll | (uint64_t)ml << 21 | (uint64_t)ov << 42;
+}
+// an explicit offset (>= 1)
 __host__ __device__ inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t off) {
-  return (uint64_t)ll | (uint64_t)ml << 21 | (uint64_t)off << 42;
+  return seq_pack_ov(ll, ml, off + 3);
 }
 __host__ __device__ inline uint32_t seq_ll(uint64_t s) { return (uint32_t)(s & 0x1FFFFF); }
 __host__ __device__ inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >> 21) & 0x1FFFFF); }
-__host__ __device__ inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 42); }
+__host__ __device__ inline uint32_t seq_ov(uint64_t s) { return (uint32_t)(s >> 42); }
+__host__ __device__ inline uint32_t seq_off(uint64_t s) { return seq_ov(s) - 3; }  // (explicit offsets)
+
+// Repeat offsets (RFC 8878 §3.1.1.5) over one block's sequences, in order,
+// in place: an explicit offset equal to a repeat offset becomes its repeat
+// code.  Only repeat offsets this block itself set are used (bit k of
+// `known`: rep[k] came from this block's sequences): the history a block
+// starts with depends on whether the blocks before it ended up compressed,
+// which is decided after every block is encoded in parallel.  rep / known
+// start as {0, 0, 0} / 0 for a block.
+struct RepHist {
+  uint32_t rep[3];
+  uint32_t known;
+};
+__host__ __device__ inline uint64_t rep_code(RepHist &R, uint64_t s) {
+  const uint32_t ll = seq_ll(s), off = seq_off(s);
+  const uint32_t r0 = R.rep[0], r1 = R.rep[1], r2 = R.rep[2], k = R.known;
+  uint32_t code = 0;
+  if (ll) {
+    if ((k & 1) && off == r0) code = 1;
+    else if ((k & 2) && off == r1) code = 2;
+    else if ((k & 4) && off == r2) code = 3;
+  } else {  // ll == 0: 1 = rep[1], 2 = rep[2], 3 = rep[0] - 1
+    if ((k & 2) && off == r1) code = 2;       // (as the value 1)
+    else if ((k & 4) && off == r2) code = 3;  // (as the value 2)
+    else if ((k & 1) && r0 > 1 && off == r0 - 1) code = 4;  // (as the value 3)
+  }
+  auto kb = [&](uint32_t i) { return (k >> i) & 1u; };
+  switch (code) {
+    case 0:  // a new offset: [off, r0, r1]
+      R.rep[0] = off; R.rep[1] = r0; R.rep[2] = r1;
+      R.known = 1u | kb(0) << 1 | kb(1) << 2;
+      return s;
+    case 1:  // rep[0]: unchanged
+      return seq_pack_ov(ll, seq_ml(s), 1);
+    case 2:  // rep[1]: [r1, r0, r2]
+      R.rep[0] = r1; R.rep[1] = r0;
+      R.known = kb(1) | kb(0) << 1 | kb(2) << 2;
+      return seq_pack_ov(ll, seq_ml(s), ll ? 2 : 1);
+    case 3:  // rep[2]: [r2, r0, r1]
+      R.rep[0] = r2; R.rep[1] = r0; R.rep[2] = r1;
+      R.known = kb(2) | kb(0) << 1 | kb(1) << 2;
+      return seq_pack_ov(ll, seq_ml(s), ll ? 3 : 2);
+    default:  // rep[0] - 1 (ll == 0): a new offset [r0 - 1, r0, r1]
+      R.rep[0] = r0 - 1; R.rep[1] = r0; R.rep[2] = r1;
+      R.known = 1u | kb(0) << 1 | kb(1) << 2;
+      return seq_pack_ov(ll, seq_ml(s), 3);
+  }
+}
 
 // Sequences_Section (RFC 8878 §3.1.1.3.2) of nseq sequences (seqs[i], in
 // order) coded with the tables tll / tof / tml, written at dst (capacity
@@ -264,7 +320,7 @@ __host__ __device__ inline uint32_t encode_sequences_with(const CLL &tll, const 
   BitW bw{dst + h, dst + cap, 0, 0, false, wr};
   // the last sequence first (the decoder reads the stream backwards)
   uint64_t s = seq_at(nseq - 1);
-  uint32_t ll = seq_ll(s), mb = seq_ml(s) - 3, ob = seq_off(s) + 3;
+  uint32_t ll = seq_ll(s), mb = seq_ml(s) - 3, ob = seq_ov(s);
   uint32_t llc = ll_code(ll), mlc = ml_code(mb), ofc = highbit(ob);
   FseState sml, sof, sll;
   fse_init(sml, tml, mlc);
@@ -277,7 +333,7 @@ __host__ __device__ inline uint32_t encode_sequences_with(const CLL &tll, const 
     s = seq_at((uint32_t)i);
     ll = seq_ll(s);
     mb = seq_ml(s) - 3;
-    ob = seq_off(s) + 3;
+    ob = seq_ov(s);
     llc = ll_code(ll);
     mlc = ml_code(mb);
     ofc = highbit(ob);
@@ -487,7 +543,7 @@ inline uint32_t encode_sequences_auto(const ZTables &T, SeqAt seq_at, uint32_t n
   for (uint32_t i = 0; i < nseq; ++i) {
     const uint64_t s = seq_at(i);
     ++c[0][ll_code(seq_ll(s))];
-    ++c[1][highbit(seq_off(s) + 3)];
+    ++c[1][highbit(seq_ov(s))];
     ++c[2][ml_code(seq_ml(s) - 3)];
   }
   SeqPlan P;
@@ -514,8 +570,8 @@ inline uint32_t encode_sequences_auto(const ZTables &T, SeqAt seq_at, uint32_t n
 constexpr uint32_t kHufMaxBits = 11;
 
 struct HufCT {
-  uint16_t code[129];  // canonical code (valid where nb > 0)
-  uint8_t nb[129];     // code length, 0 = absent
+  uint16_t code[256];  // canonical code (valid where nb > 0)
+  uint8_t nb[256];     // code length, 0 = absent
   uint32_t last;       // highest present symbol (its weight is implied)
   uint32_t maxb;       // longest code
 };
@@ -523,33 +579,33 @@ struct HufCT {
 // Scratch of huf_build (LDS on the GPU: dynamically indexed arrays in a
 // lane's registers would live in scratch memory).
 struct HufWork {
-  uint32_t f[258];      // node weights: leaves 0..n-1 (ascending), internal nodes after
-  uint16_t sym[129];    // symbols by count ascending (ties: by symbol)
-  uint16_t par[258];    // parent of each node
-  uint8_t dep[258];     // node depth
+  uint32_t f[512];      // node weights: leaves 0..n-1 (ascending), internal nodes after
+  uint16_t sym[256];    // symbols by count ascending (ties: by symbol)
+  uint16_t par[512];    // parent of each node
+  uint8_t dep[512];     // node depth
   uint32_t bl[64];      // leaves per depth
   uint32_t rank[kHufMaxBits + 2], val[kHufMaxBits + 2];
 };
 
-// Code lengths of a Huffman code over the symbols with cnt > 0 (all < 129,
-// at least two), limited to kHufMaxBits, then canonical codes as zstd's
-// decoder rebuilds them from the weights: by rank from the longest length
-// down (start 0; next rank's start = (start + count) >> 1), within a rank in
-// symbol order.  Serial (one lane per block on the GPU).  sorted: w.sym
-// already holds the present symbols by count ascending, ties by symbol (the
-// GPU ranks them with the whole wave).
+// Code lengths of a Huffman code over the symbols with cnt > 0 (cnt: 256
+// counts, at least two present), limited to kHufMaxBits, then canonical codes
+// as zstd's decoder rebuilds them from the weights: by rank from the longest
+// length down (start 0; next rank's start = (start + count) >> 1), within a
+// rank in symbol order.  Serial (one lane per block on the GPU).  sorted:
+// w.sym already holds the present symbols by count ascending, ties by symbol
+// (the GPU ranks them with the whole wave).
 __host__ __device__ inline void huf_build(const uint32_t *cnt, HufCT &ct, HufWork &w, bool sorted = false) {
   uint16_t *sym = w.sym;
   uint32_t *f = w.f;
   uint32_t n = 0;
-  for (uint32_t s = 0; s < 129; ++s) {
+  for (uint32_t s = 0; s < 256; ++s) {
     ct.nb[s] = 0;
     if (cnt[s]) {
       if (!sorted) sym[n] = (uint16_t)s;
       ++n;
     }
   }
-  // symbols by count ascending (insertion sort, stable: n <= 129)
+  // symbols by count ascending (insertion sort, stable: n <= 256)
   for (uint32_t i = 1; !sorted && i < n; ++i) {
     const uint16_t v = sym[i];
     uint32_t j = i;
@@ -595,7 +651,7 @@ __host__ __device__ inline void huf_build(const uint32_t *cnt, HufCT &ct, HufWor
     }
     uint64_t kraft = 0;  // in units of 2^-kHufMaxBits
     for (uint32_t d = 1; d <= kHufMaxBits; ++d) kraft += (uint64_t)bl[d] << (kHufMaxBits - d);
-    while (kraft > (1ull << kHufMaxBits)) {  // (n <= 129 < 2^11 leaves: a shorter leaf always exists)
+    while (kraft > (1ull << kHufMaxBits)) {  // (n <= 256 < 2^11 leaves: a shorter leaf always exists)
       uint32_t d = kHufMaxBits - 1;
       while (bl[d] == 0) --d;
       --bl[d];
@@ -625,19 +681,88 @@ __host__ __device__ inline void huf_build(const uint32_t *cnt, HufCT &ct, HufWor
     if (ct.nb[s]) ct.code[s] = (uint16_t)w.val[ct.nb[s]]++;
 }
 
+// Weight of symbol s: maxb + 1 - length, 0 for an absent symbol.
+__host__ __device__ inline uint32_t huf_weight(const HufCT &ct, uint32_t s) {
+  return ct.nb[s] ? ct.maxb + 1 - ct.nb[s] : 0u;
+}
+
 // Huffman_Tree_Description in the direct representation: headerByte = 127 +
 // Number_of_Weights (the weights of symbols 0 .. last - 1, 4 bits each, first
-// in the high nibble; the last symbol's weight is implied).  Weight = maxb + 1
-// - length, 0 for an absent symbol.
-__host__ __device__ inline uint32_t huf_tree_desc(const HufCT &ct, uint8_t *dst) {
+// in the high nibble; the last symbol's weight is implied).  Only for last <=
+// 128.  Returns its size.
+__host__ __device__ inline uint32_t huf_tree_direct(const HufCT &ct, uint8_t *dst) {
   const uint32_t nw = ct.last;  // 1 .. 128
   dst[0] = (uint8_t)(127 + nw);
   for (uint32_t i = 0; i < nw; i += 2) {
-    const uint32_t w0 = ct.nb[i] ? ct.maxb + 1 - ct.nb[i] : 0;
-    const uint32_t w1 = (i + 1 < nw && ct.nb[i + 1]) ? ct.maxb + 1 - ct.nb[i + 1] : 0;
+    const uint32_t w0 = huf_weight(ct, i), w1 = i + 1 < nw ? huf_weight(ct, i + 1) : 0u;
     dst[1 + i / 2] = (uint8_t)(w0 << 4 | w1);
   }
   return 1 + (nw + 1) / 2;
+}
+
+// The weights FSE-compressed (RFC 8878 §4.2.1.2, as zstd's HUF_compressWeights
+// writes them): an FSE table description of the weight histogram (accuracy
+// log <= 6), then one bitstream with two interleaved states -- weights at even
+// indices decoded from state 1, odd from state 2 -- written from the last
+// weight back (FSE_compress_usingCTable's order), the first two encoded
+// weights as the initial states.  headerByte = the compressed size (< 128).
+// Returns the description's size (1 + compressed size), or 0 when the weights
+// do not FSE-compress (a single distinct weight, or 128 bytes or more).
+__host__ __device__ inline uint32_t huf_tree_fse(const HufCT &ct, uint8_t *dst) {
+  const uint32_t nw = ct.last;  // 1 .. 255
+  if (nw < 2) return 0;
+  uint32_t cnt[13] = {0};
+  uint32_t maxw = 0;
+  for (uint32_t i = 0; i < nw; ++i) {
+    const uint32_t w = huf_weight(ct, i);
+    ++cnt[w];
+    if (w > maxw) maxw = w;
+  }
+  for (uint32_t w = 0; w <= maxw; ++w)
+    if (cnt[w] == nw) return 0;  // (one distinct weight: zstd's "rle", not FSE-coded)
+  const uint32_t tl = fse_table_log(nw, maxw, 6);
+  int16_t norm[53];
+  if (!fse_normalize(cnt, maxw + 1, nw, tl, norm)) return 0;
+  for (uint32_t w = maxw + 1; w < 53; ++w) norm[w] = 0;
+  uint8_t *o = dst + 1;
+  const uint32_t nd = fse_write_ncount(norm, maxw + 1, tl, o);
+  FseCTN<64> t;
+  fse_build(norm, (int)(maxw + 1), tl, t);
+  BitW bw{o + nd, dst + 128, 0, 0, false};
+  FseState s1, s2;
+  uint32_t i = nw;
+  if (nw & 1) {
+    fse_init(s1, t, huf_weight(ct, --i));
+    fse_init(s2, t, huf_weight(ct, --i));
+    fse_encode(bw, s1, t, huf_weight(ct, --i));
+  } else {
+    fse_init(s2, t, huf_weight(ct, --i));
+    fse_init(s1, t, huf_weight(ct, --i));
+  }
+  while (i > 0) {
+    fse_encode(bw, s2, t, huf_weight(ct, --i));
+    fse_encode(bw, s1, t, huf_weight(ct, --i));
+  }
+  fse_flush(bw, s2, t);
+  fse_flush(bw, s1, t);
+  if (!bw.close()) return 0;
+  const uint32_t csize = (uint32_t)(bw.p - o);
+  if (csize >= 128) return 0;
+  dst[0] = (uint8_t)csize;
+  return 1 + csize;
+}
+
+// The shorter of the two descriptions (direct only for last <= 128); 0 when
+// neither applies (the literals then stay raw).  dst holds 130 bytes.
+__host__ __device__ inline uint32_t huf_tree_desc(const HufCT &ct, uint8_t *dst) {
+  uint8_t tmp[130];
+  const uint32_t f = huf_tree_fse(ct, tmp);
+  const uint32_t d = ct.last <= 128 ? 1 + (ct.last + 1) / 2 : 0xFFFFFFFFu;
+  if (f && f < d) {
+    for (uint32_t i = 0; i < f; ++i) dst[i] = tmp[i];
+    return f;
+  }
+  return d != 0xFFFFFFFFu ? huf_tree_direct(ct, dst) : 0u;
 }
 
 // Bits of one Huffman stream of n literals (without the end mark).
@@ -688,11 +813,11 @@ __host__ __device__ inline void put_rle_lit_header(uint8_t *d, uint32_t nlit) {
 }
 
 // Sizes of a Huffman literals section for the literals whose Huffman table
-// is ct (stream bits sb[0..3], or sb[0] alone for one stream): section
-// size = header + tree + (jump table) + streams.
-__host__ __device__ inline uint32_t huf_section_size(const HufCT &ct, uint32_t nlit, const uint32_t *sb, bool one,
+// is ct, with a tree description of `tree` bytes (stream bits sb[0..3], or
+// sb[0] alone for one stream): section size = header + tree + (jump table) +
+// streams.
+__host__ __device__ inline uint32_t huf_section_size(uint32_t tree, uint32_t nlit, const uint32_t *sb, bool one,
                                                      uint32_t *ssz) {
-  const uint32_t tree = 1 + (ct.last + 1) / 2;
   uint32_t streams = 0;
   for (int k = 0; k < (one ? 1 : 4); ++k) {
     ssz[k] = (sb[k] + 1 + 7) / 8;
@@ -725,10 +850,10 @@ __host__ __device__ inline void put_frame_header(uint8_t *d) {
 }
 
 // The literals section of a compressed block, serial (the CPU format test's
-// reference; k_zc_huff makes the same choice with the same pieces, in
-// parallel): Huffman when the literals are bytes < 128 and that section is
-// smaller than raw, RLE for one distinct byte, else raw.  dst holds at least
-// kLitHdr + n bytes.  Returns the section size.
+// reference; the GPU makes the same choice with the same pieces, in
+// parallel): RLE for one distinct byte, Huffman when that section is smaller
+// than raw, else raw.  dst holds at least kLitHdr + n bytes.  Returns the
+// section size.
 template <class LitAt>
 __host__ __device__ inline uint32_t encode_literals(LitAt lit_at, uint32_t n, uint8_t *dst) {
   uint32_t hist[256] = {0};
@@ -744,15 +869,18 @@ __host__ __device__ inline uint32_t encode_literals(LitAt lit_at, uint32_t n, ui
     for (uint32_t i = 0; i < n; ++i) dst[kLitHdr + i] = (uint8_t)lit_at(i);
     return kLitHdr + n;
   };
-  if (n >= 32 && distinct == 1 && high < 128) {
+  if (n >= 32 && distinct == 1) {
     put_rle_lit_header(dst, n);
     dst[3] = (uint8_t)high;
     return 4;
   }
-  if (n < 32 || high >= 128) return raw();
+  if (n < 32) return raw();
   HufCT ct;
   HufWork hw;
   huf_build(hist, ct, hw);
+  uint8_t tdesc[130];
+  const uint32_t tree = huf_tree_desc(ct, tdesc);
+  if (!tree) return raw();
   const bool one = n < 1024;
   const uint32_t seg = one ? n : (n + 3) / 4;
   uint32_t sb[4] = {0, 0, 0, 0}, ssz[4];
@@ -760,13 +888,12 @@ __host__ __device__ inline uint32_t encode_literals(LitAt lit_at, uint32_t n, ui
     const uint32_t a = k * seg, e = a + seg < n ? a + seg : n;
     sb[k] = huf_stream_bits(ct, lit_at, a, e - a);
   }
-  const uint32_t total = huf_section_size(ct, n, sb, one, ssz);
-  const uint32_t tree = 1 + (ct.last + 1) / 2;
+  const uint32_t total = huf_section_size(tree, n, sb, one, ssz);
   const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
   if (total >= kLitHdr + n || (one && csize >= 1024)) return raw();
   const uint32_t hdr = lit_hdr_size(n, csize, one);
   put_huf_lit_header(dst, n, csize, one);
-  huf_tree_desc(ct, dst + hdr);
+  for (uint32_t i = 0; i < tree; ++i) dst[hdr + i] = tdesc[i];
   uint32_t o = hdr + tree;
   if (!one) {
     for (int k = 0; k < 3; ++k) {

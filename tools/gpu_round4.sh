@@ -43,6 +43,36 @@ for stage in "$@"; do
     done
     cd $R
     echo prof done ;;
+  zc)  # the GPU compressor: its tests, the save path's, then tools/zc_bench.py (2 GiB per corpus)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_zcomp.py tests/test_gpu_save.py -m gpu -x -v --timeout 300 \
+      --timeout-method thread > $OUT/zc_tests.log 2>&1 || { echo "zc tests rc=$?"; tail -30 $OUT/zc_tests.log; exit 1; }
+    tail -2 $OUT/zc_tests.log
+    timeout -k 10 300 python -u tools/zc_bench.py 2 3 > $OUT/zc_bench.json 2> $OUT/zc_bench.err \
+      || { echo "zc bench rc=$?"; tail -20 $OUT/zc_bench.err; exit 1; }
+    cat $OUT/zc_bench.json ;;
+  zcprof)  # kernel trace + stats of the compressor (1 GiB text), then PMC passes
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/zc_stats -o zc --output-format csv -- \
+      python3 $R/tools/zc_bench.py 1 2 text,binary > $OUT/zc_under_rocprof.json 2> $OUT/zc_stats.err \
+      || { echo "zc stats rc=$?"; tail -5 $OUT/zc_stats.err; exit 1; }
+    i=0
+    for ctrs in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES GRBM_GUI_ACTIVE" \
+                "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
+                "FETCH_SIZE WRITE_SIZE"; do
+      i=$((i+1))
+      timeout -s KILL 150 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/zc_pmc/p$i -o run -- \
+        python3 $R/tools/zc_bench.py 1 1 text > $OUT/zc_pmc_p$i.log 2>&1 || { echo "zc pmc pass $i rc=$?"; exit 1; }
+    done
+    cd $R
+    echo zcprof done ;;
+  calib)  # FETCH_SIZE of the scan (tools/scanbench prod) against the bare load pattern (quadread)
+    cd /tmp && export TMPDIR=/tmp
+    for mode in quadread prod; do
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib/$mode -o run -- \
+        $R/tools/scanbench 8 $mode > $OUT/calib_$mode.log 2>&1 || { echo "calib $mode rc=$?"; exit 1; }
+    done
+    cd $R
+    echo calib done ;;
   *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

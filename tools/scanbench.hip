@@ -207,6 +207,16 @@ int main(int argc, char **argv) {
   Work W{};
   W.base = d; W.n_al = n; W.gear16 = dg16; W.run_cnt = cnt; W.run_ent = ent; W.run_sum = sum;
   W.nruns = (n + kRun - 1) / kRun;
+  // everything the product scan writes besides the run data (round 3: the
+  // candidate bitmaps, the call's error words; the dynamic tile counter)
+  const size_t bits_bytes = 16 * (W.nruns / 64 + 2);
+  CK(hipMalloc(&W.run_bits, bits_bytes));
+  CK(hipMalloc(&W.err, 64));
+  CK(hipMalloc(&W.tile_ctr, 64));
+  CK(hipMemset(W.run_bits, 0, bits_bytes));
+  CK(hipMemset(W.err, 0, 64));
+  W.long_n = W.err + 3;
+  W.first_static = 1;
   CK(hipStreamSynchronize(st));
   auto report = [&](const char *name, float med, float best) {
     printf("%-44s median %8.3f ms  %7.3f TB/s   best %7.3f TB/s\n", name, med, n / (med * 1e9), n / (best * 1e9));
@@ -221,7 +231,11 @@ int main(int argc, char **argv) {
   };
   float best, med;
   const int it = 7;
-  auto prod = [&] { launch_scan(W, P, cus, st, 0, ~0ull, true, scan_pieces(W.n_al / kRun, cus), true); };
+  auto prod = [&] {  // (as run_pipeline: bitmaps and the tile counter cleared before the launch)
+    (void)hipMemsetAsync(W.run_bits, 0, bits_bytes, st);
+    (void)hipMemsetAsync(W.tile_ctr, 0, 8, st);
+    launch_scan(W, P, cus, st, 0, ~0ull, true, scan_pieces(W.n_al / kRun, cus), true);
+  };
   if (mode == "quadread") {
     med = time_it(st, 3, [&] {
       hipLaunchKernelGGL(k_read_quad<kRun>, dim3(cus), dim3(1024), 0, st, (const uint8_t *)d, n, sink);
@@ -273,7 +287,12 @@ int main(int argc, char **argv) {
     for (uint64_t sz = 32ull << 20; sz <= n; sz *= 2) {
       Work Ws = W; Ws.n_al = sz; Ws.nruns = (sz + kRun - 1) / kRun;
       const int reps = (int)std::max<uint64_t>(1, (4ull << 30) / sz);
-      med = time_it(st, 5, [&] { for (int r = 0; r < reps; ++r) launch_scan(Ws, P, cus, st, 0, ~0ull, true, scan_pieces(Ws.n_al / kRun, cus), true); }, &best);
+      med = time_it(st, 5, [&] {
+        for (int r = 0; r < reps; ++r) {
+          (void)hipMemsetAsync(Ws.tile_ctr, 0, 8, st);
+          launch_scan(Ws, P, cus, st, 0, ~0ull, true, scan_pieces(Ws.n_al / kRun, cus), true);
+        }
+      }, &best);
       printf("sweep %8.1f MiB x%3d: %7.3f TB/s (best %7.3f)\n", sz / 1048576.0, reps,
              sz * (double)reps / (med * 1e9), sz * (double)reps / (best * 1e9));
       fflush(stdout);

@@ -19,20 +19,14 @@ n = int(gib * (1 << 30))
 p = _lib.params(16384, 65536, 262144, 1)
 ctx = _lib.Context(0, n + (1 << 20))
 res = {}
-for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records")):
+for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records", "binary")):
     dp = ctx.device_alloc(n)
     if kind == "random":
         ctx.fill_random(dp, n, 0x6d61706163686521)
-    elif kind == "records":  # CSV-like rows (tests/test_gpu_zcomp.py _records), 64 MiB repeated
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from test_gpu_zcomp import _records
-        base = _records(64 << 20).tobytes()
-        for o in range(0, n, len(base)):
-            ctx.h2d(dp + o, np.frombuffer(base[:min(len(base), n - o)], np.uint8))
-    else:
-        rng = np.random.default_rng(21)
-        vocab = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 11, 2000)]
-        base = b" ".join(vocab[i] for i in rng.integers(0, 2000, 12_000_000))[:64 << 20]
+    else:  # the shared synthetic corpora (tests/corpora.py), a 64 MiB pattern repeated
+        sys.path.insert(0, ROOT)
+        from tests import corpora
+        base = corpora.by_name(kind, 64 << 20).tobytes()
         for o in range(0, n, len(base)):
             ctx.h2d(dp + o, np.frombuffer(base[:min(len(base), n - o)], np.uint8))
     cap_c = n // 16383 + 2
