@@ -89,6 +89,14 @@ __device__ __forceinline__ uint32_t ht_ld(uint16_t *ht, uint32_t h) {
   return __hip_atomic_load(ht + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// A workgroup barrier that orders LDS only: __syncthreads' workgroup fence
+// waits for every outstanding global load too (vmcnt(0) on gfx9), which
+// would drain the match finder's prefetches at each of its per-tile barriers.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __global__ void k_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint32_t *err,
                              uint64_t *bound) {
@@ -128,12 +136,25 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
   }
 }
 
-// 16 bytes at p of a buffer of nbytes (zero past its end).
-__device__ __forceinline__ uint4 ld16(const uint8_t *base, uint64_t p, uint64_t nbytes) {
-  if (p + 16 <= nbytes) return *reinterpret_cast<const uint4 *>(base + p);  // (misaligned: gfx950 reads the bytes)
-  uint32_t w[4] = {0, 0, 0, 0};
-  for (uint32_t i = 0; i < 16 && p + i < nbytes; ++i) w[i >> 2] |= (uint32_t)base[p + i] << (8 * (i & 3));
-  return make_uint4(w[0], w[1], w[2], w[3]);
+// Branch-free 16-byte load for prefetching (a branch around a load makes the
+// compiler wait for it where the paths join): the 16 bytes at p, or, within
+// 16 bytes of the end of the nbytes >= 16 readable, the last 16 bytes; fix16
+// then realigns them (bytes past the end zero) where they are used.
+__device__ __forceinline__ uint4 ld16c(const uint8_t *base, uint64_t p, uint64_t nbytes) {
+  return *reinterpret_cast<const uint4 *>(base + (p + 16 <= nbytes ? p : nbytes - 16));
+}
+__device__ __forceinline__ uint4 fix16(uint4 x, uint64_t p, uint64_t nbytes) {
+  if (p + 16 <= nbytes) return x;
+  const uint32_t sh = p >= nbytes ? 16u : (uint32_t)(p - (nbytes - 16));  // bytes to drop, 1..16
+  uint64_t lo = (uint64_t)x.y << 32 | x.x, hi = (uint64_t)x.w << 32 | x.z;
+  if (sh >= 8) {
+    lo = sh >= 16 ? 0 : hi >> (8 * (sh - 8));
+    hi = 0;
+  } else {
+    lo = lo >> (8 * sh) | hi << (64 - 8 * sh);
+    hi >>= 8 * sh;
+  }
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
 // Common prefix of two 16-byte strings.
@@ -161,6 +182,7 @@ __device__ __forceinline__ bool ht_newer(uint32_t v, uint32_t t0, uint32_t p) {
 __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint64_t nbytes, const ZcBlock *blocks,
                                                        uint64_t nblk, uint32_t *words) {
   __shared__ __attribute__((aligned(16))) uint16_t hts[1u << kHsLog], htl[1u << kHlLog];
+  __shared__ uint32_t vote[3];  // "a store is pending" of the insert loop's rounds, three slots in rotation
   const uint64_t bi0 = blockIdx.x;
   if (bi0 >= nblk) return;
   const ZcBlock B0 = blocks[bi0];
@@ -176,12 +198,18 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   for (uint32_t k = tid; k < (1u << kHlLog) / 8; k += kFindTile) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
   const uint8_t *cb = base + csrc;
   const uint64_t cbytes = nbytes - csrc;  // (bytes readable from the chunk start)
-  uint4 nx = ld16(cb, prime0 + tid, cbytes);  // the next tile's bytes, loaded a tile ahead
+  if (clen < 16 || cbytes < 16) {  // (too short to match: every position a literal)
+    for (uint32_t p = seg0 + tid; p < seg1; p += kFindTile)
+      words[(bi0 + (p / (uint32_t)kZcBlock - B0.b)) * kZcBlock + p % (uint32_t)kZcBlock] = 0u;
+    return;
+  }
+  uint4 nx = ld16c(cb, prime0 + tid, cbytes);  // the next tile's bytes, loaded a tile ahead
+  if (tid < 3) vote[tid] = 0;
+  uint32_t round = 0;
   __syncthreads();
   for (uint32_t t0 = prime0; t0 < seg1; t0 += kFindTile) {
     const uint32_t p = t0 + tid;
-    const uint4 x = nx;
-    if (t0 + kFindTile < seg1) nx = ld16(cb, p + kFindTile, cbytes);
+    const uint4 x = fix16(nx, p, cbytes);
     const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert)
     const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
     const uint32_t v = (p + 1) & 0xFFFFu;
@@ -192,18 +220,30 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     // candidates (distance modulo 2^16, within the chunk) and their bytes
     const uint32_t ds = (p + 1 - cs) & 0xFFFFu, dl = (p + 1 - cl) & 0xFFFFu;
     const bool oks = cs != 0 && ds != 0 && ds <= p, okl = cl != 0 && dl != 0 && dl <= p && dl != ds;
-    uint4 ys = make_uint4(0, 0, 0, 0), yl = ys;
-    if (oks) ys = ld16(cb, p - ds, cbytes);
-    if (okl) yl = ld16(cb, p - dl, cbytes);
-    __syncthreads();  // every lookup of the tile before any insert
+    // (loaded now, used after the inserts; a missing candidate loads position 0)
+    const uint32_t qs = oks ? p - ds : 0u, ql = okl ? p - dl : 0u;
+    const uint4 ys0 = ld16c(cb, qs, cbytes), yl0 = ld16c(cb, ql, cbytes);
+    // the next tile's bytes after the candidates' (the counter retires in
+    // order: the candidates are then awaited without draining the prefetch)
+    nx = ld16c(cb, p + kFindTile, cbytes);
+    lds_sync();  // every lookup of the tile before any insert
     const bool ws = vs && v != 0, wl = vl && v != 0;
     if (ws) ht_st(hts, hs, v);
     if (wl) ht_st(htl, hl, v);
     // the latest position per slot: lanes whose store lost to an older
     // position of the tile (or that an older tile's value still holds) store
-    // again until none does
+    // again until none does.  A round's vote slot is cleared two rounds ahead
+    // (its last readers passed a barrier since), so no round needs a second
+    // barrier for it.
     bool ps = ws, pl = wl;
-    while (__syncthreads_or(ps || pl)) {
+    for (;;) {
+      const uint32_t k = round % 3;
+      if (tid == 0) __hip_atomic_store(vote + (round + 1) % 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (ps || pl) __hip_atomic_store(vote + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      lds_sync();
+      const bool any = __hip_atomic_load(vote + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+      ++round;
+      if (!any) break;
       if (ps) {
         ps = !ht_newer(ht_ld(hts, hs), t0, p);
         if (ps) ht_st(hts, hs, v);
@@ -216,6 +256,7 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     if (find) {
       const uint32_t bend = min(clen, (p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
       const uint32_t lim = min(kMlCap, bend - p);
+      const uint4 ys = fix16(ys0, qs, cbytes), yl = fix16(yl0, ql, cbytes);
       uint32_t ms = oks ? min(prefix16(x, ys), lim) : 0u, ml = okl ? min(prefix16(x, yl), lim) : 0u;
       uint32_t m = 0, d = 0;
       if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;

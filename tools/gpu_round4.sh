@@ -50,6 +50,13 @@ for stage in "$@"; do
     timeout -k 10 300 python -u tools/zc_bench.py 2 3 > $OUT/zc_bench.json 2> $OUT/zc_bench.err \
       || { echo "zc bench rc=$?"; tail -20 $OUT/zc_bench.err; exit 1; }
     cat $OUT/zc_bench.json ;;
+  zcstats)  # kernel trace + stats of the compressor only (1 GiB of text and of binary)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/zc_stats -o zc --output-format csv -- \
+      python3 $R/tools/zc_bench.py 1 2 text,binary > $OUT/zc_under_rocprof.json 2> $OUT/zc_stats.err \
+      || { echo "zc stats rc=$?"; tail -5 $OUT/zc_stats.err; exit 1; }
+    python3 $R/tools/kcsv.py $OUT/zc_stats/zc_kernel_stats.csv
+    cd $R ;;
   zcprof)  # kernel trace + stats of the compressor (1 GiB text), then PMC passes
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/zc_stats -o zc --output-format csv -- \
