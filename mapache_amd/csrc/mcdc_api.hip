@@ -1895,7 +1895,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   if ((rc = ensure(ctx, ctx->zc_tmp, tmpb))) return rc;
   if ((rc = ensure(ctx, ctx->zc_blocks, mb * sizeof(ZcBlock))) || (rc = ensure(ctx, ctx->zc_stage, mb * kZcSlot)) ||
       (rc = ensure(ctx, ctx->zc_seqs, mb * kZcSeqCap * 8)) || (rc = ensure(ctx, ctx->zc_piece, (mb + 1) * 8)) ||
-      (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)) || (rc = ensure(ctx, ctx->zc_words, mb * kZcBlock * 4)))
+      (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)) || (rc = ensure(ctx, ctx->zc_words, (mb * kZcBlock + 1024) * 4)))
     return rc;
   for (uint64_t c0 = 0; c0 < nchunks;) {  // batches of whole chunks, <= kZcBatchBlocks blocks each
     uint64_t c1 = c0 + 1;

@@ -12,16 +12,16 @@
 //   k_zc_blocks  block records of the batch's chunks (chunk, index, source)
 //   k_zc_find    ONE WORKGROUP (4 waves) PER SEGMENT of up to 8 blocks of a
 //                chunk: candidate matches for every position.  Two tables of
-//                2^15 16-bit positions in LDS (128 KiB: a 5-byte key and an
-//                8-byte key, as zstd's double-fast pair), filled 256
-//                positions at a time: a tile reads its candidates from the
-//                tables as the earlier tiles left them, then inserts its own
-//                positions (the latest position per slot kept, whichever
-//                lane's store lands: a read-back loop, so the result never
-//                depends on the hardware's choice).  A segment after a
-//                chunk's first re-inserts the 64 KiB before it (the reach).
-//                Each candidate is verified on 16 bytes; per position one
-//                word (match length <= 16 | offset << 16, 0 = none) to scratch
+//                32-bit positions in LDS (160 KiB: 2^15 slots for a 5-byte
+//                key and 2^13 for an 8-byte key, as zstd's double-fast pair),
+//                filled 256 positions at a time: a tile reads its candidates
+//                from the tables as the earlier tiles left them, then inserts
+//                its own positions with LDS max atomics (the latest position
+//                per slot, deterministically).  A segment after a chunk's
+//                first re-inserts the 128 KiB before it.  Each candidate is
+//                verified on 16 bytes, a tile later (its loads in flight
+//                meanwhile); per position one word (match length <= 16 << 24
+//                | offset, 0 = none) to scratch
 //   k_zc_parse   ONE WAVE PER BLOCK: greedy parse over the words, 256
 //                positions per window (4 ballots of "has a match"), the next
 //                match found with scalar bit scans; a match of 16 bytes is
@@ -60,33 +60,28 @@ namespace {
 
 using namespace zs;
 
-// Match finder tables: 2^15 16-bit positions each (position + 1 modulo
-// 2^16, 0 = empty), so a candidate lies at most 65535 bytes back (the
-// distance is taken modulo 2^16; a stale entry aliases to a nearer position
-// and is rejected by the byte check, or is a valid match there).
+// Match finder tables in LDS: 2^15 slots for a 5-byte key and 2^13 for an
+// 8-byte key (zstd's double-fast pair), 32-bit chunk positions (+ 1, 0 =
+// empty): 160 KiB, the whole of a CU's LDS.  Inserts are LDS max atomics, so
+// a slot ends at the latest position whichever lane's atomic lands last.
 // tools/zc_model2.cpp priced the choices on the bench's corpora (16/64/256
-// KiB chunks): one 2^14 5-byte-key table 2.44 / 3.20 / 1.74 (text / records
-// / binary) -> 2^15 + 2^15 (8-byte key) 2.63 / 3.31 / 1.79, zstd level 3
-// 2.68 / 3.23 / 1.78; 256-position tiles cost < 0.1 % against exact
-// most-recent insertion (1024: 2 % on records).
-constexpr uint32_t kHsLog = 15, kHlLog = 15;
-constexpr uint32_t kFindTile = 256;   // positions per step = threads per workgroup
-constexpr uint32_t kMlCap = 16;       // match bytes verified per candidate (longer: k_zc_parse extends)
-constexpr uint32_t kPrime = 65536;    // bytes before a segment re-inserted (the reach)
+// KiB chunks; text / records / binary): one 2^14 table 2.44 / 3.20 / 1.74;
+// 2^15 + 2^13 2.59 / 3.30 / 1.78; zstd level 3 2.68 / 3.23 / 1.78.  256
+// positions per tile cost < 0.5 % against exact most-recent insertion (512:
+// 1 % on records and binary).
+constexpr uint32_t kHsLog = 15, kHlLog = 13;
+#ifndef MCDC_ZC_TILE
+#define MCDC_ZC_TILE 256  // (compile-time A/B knob)
+#endif
+constexpr uint32_t kFindTile = MCDC_ZC_TILE;  // positions per step = threads per workgroup
+constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
+constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
 
 __device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
   return (lo * 2654435761u + (hi & 0xFFu) * 0x85EBCA77u) >> (32 - kHsLog);
 }
 __device__ __forceinline__ uint32_t hash8(uint32_t lo, uint32_t hi) {
   return ((lo * 0x9E3779B1u) ^ (hi * 0x85EBCA77u) ^ ((lo ^ hi) >> 15)) * 0xC2B2AE3Du >> (32 - kHlLog);
-}
-// (relaxed workgroup-scope atomics: LDS loads and stores the compiler may not
-// merge, forward or move across the barriers of the insert loop)
-__device__ __forceinline__ void ht_st(uint16_t *ht, uint32_t h, uint32_t v) {
-  __hip_atomic_store(ht + h, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t ht_ld(uint16_t *ht, uint32_t h) {
-  return __hip_atomic_load(ht + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 // A workgroup barrier that orders LDS only: __syncthreads' workgroup fence
@@ -144,17 +139,13 @@ __device__ __forceinline__ uint4 ld16c(const uint8_t *base, uint64_t p, uint64_t
   return *reinterpret_cast<const uint4 *>(base + (p + 16 <= nbytes ? p : nbytes - 16));
 }
 __device__ __forceinline__ uint4 fix16(uint4 x, uint64_t p, uint64_t nbytes) {
-  if (p + 16 <= nbytes) return x;
-  const uint32_t sh = p >= nbytes ? 16u : (uint32_t)(p - (nbytes - 16));  // bytes to drop, 1..16
-  uint64_t lo = (uint64_t)x.y << 32 | x.x, hi = (uint64_t)x.w << 32 | x.z;
-  if (sh >= 8) {
-    lo = sh >= 16 ? 0 : hi >> (8 * (sh - 8));
-    hi = 0;
-  } else {
-    lo = lo >> (8 * sh) | hi << (64 - 8 * sh);
-    hi >>= 8 * sh;
-  }
-  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  // (selects only: a branch here would make the compiler wait for every load at its join)
+  const uint32_t sh = p + 16 <= nbytes ? 0u : p >= nbytes ? 16u : (uint32_t)(p - (nbytes - 16));  // bytes to drop
+  const uint64_t lo = (uint64_t)x.y << 32 | x.x, hi = (uint64_t)x.w << 32 | x.z;
+  const uint32_t b = 8 * (sh & 7);
+  const uint64_t lo1 = b ? (lo >> b | hi << (64 - b)) : lo, hi1 = hi >> b;  // shifted by sh % 8 bytes
+  const uint64_t rlo = sh >= 16 ? 0 : sh >= 8 ? hi1 : lo1, rhi = sh >= 8 ? 0 : hi1;
+  return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
 }
 
 // Common prefix of two 16-byte strings.
@@ -167,22 +158,17 @@ __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
   return m;
 }
 
-// Slot value v (16-bit, position + 1) against the tile [t0, t0 + kFindTile):
-// true when v is a position of the tile at or after position p (the slot
-// already holds a position as new as p's own).
-__device__ __forceinline__ bool ht_newer(uint32_t v, uint32_t t0, uint32_t p) {
-  const uint32_t r = (v - (t0 + 1)) & 0xFFFFu;  // (its offset in the tile, if it is one of the tile's)
-  return v != 0 && r < kFindTile && t0 + r >= p;
-}
-
 // The match finder: one workgroup of kFindTile threads per segment (up to
 // kZcSegBlocks blocks of one chunk, the first record of the segment's blocks:
 // other workgroups return).  Writes words[(block - batch start) * kZcBlock +
-// position in block] for every position of the segment.
+// position in block] for every position of the segment: match length (<=
+// kMlCap) << 24 | offset, 0 = no match of 4 bytes or more.  Per tile: the
+// lookups (tables as the earlier tiles left them), the candidates' bytes
+// requested, the previous tile's candidates verified (their bytes had a
+// tile's time to arrive), then the inserts; two LDS-only barriers.
 __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint64_t nbytes, const ZcBlock *blocks,
                                                        uint64_t nblk, uint32_t *words) {
-  __shared__ __attribute__((aligned(16))) uint16_t hts[1u << kHsLog], htl[1u << kHlLog];
-  __shared__ uint32_t vote[3];  // "a store is pending" of the insert loop's rounds, three slots in rotation
+  __shared__ __attribute__((aligned(16))) uint32_t hts[1u << kHsLog], htl[1u << kHlLog];
   const uint64_t bi0 = blockIdx.x;
   if (bi0 >= nblk) return;
   const ZcBlock B0 = blocks[bi0];
@@ -194,77 +180,79 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   const uint32_t seg0 = B0.b * (uint32_t)kZcBlock;
   const uint32_t seg1 = min(clen, seg0 + kZcSegBlocks * (uint32_t)kZcBlock);
   const uint32_t prime0 = seg0 > kPrime ? seg0 - kPrime : 0u;
-  for (uint32_t k = tid; k < (1u << kHsLog) / 8; k += kFindTile) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
-  for (uint32_t k = tid; k < (1u << kHlLog) / 8; k += kFindTile) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
   const uint8_t *cb = base + csrc;
   const uint64_t cbytes = nbytes - csrc;  // (bytes readable from the chunk start)
+  auto word_at = [&](uint32_t p) -> uint32_t * {
+    return words + (bi0 + (p / (uint32_t)kZcBlock - B0.b)) * kZcBlock + p % (uint32_t)kZcBlock;
+  };
   if (clen < 16 || cbytes < 16) {  // (too short to match: every position a literal)
-    for (uint32_t p = seg0 + tid; p < seg1; p += kFindTile)
-      words[(bi0 + (p / (uint32_t)kZcBlock - B0.b)) * kZcBlock + p % (uint32_t)kZcBlock] = 0u;
+    for (uint32_t p = seg0 + tid; p < seg1; p += kFindTile) *word_at(p) = 0u;
     return;
   }
-  uint4 nx = ld16c(cb, prime0 + tid, cbytes);  // the next tile's bytes, loaded a tile ahead
-  if (tid < 3) vote[tid] = 0;
-  uint32_t round = 0;
-  __syncthreads();
-  for (uint32_t t0 = prime0; t0 < seg1; t0 += kFindTile) {
+  for (uint32_t k = tid; k < (1u << kHsLog) / 4; k += kFindTile) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = tid; k < (1u << kHlLog) / 4; k += kFindTile) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
+  // Two tiles in flight: a tile's own bytes are requested two tiles ahead,
+  // and its candidates' bytes are verified two tiles later (the counter
+  // retires in order, so waiting for a tile's own bytes leaves the newer
+  // requests in flight)
+  struct Stage {
+    bool v, ks, kl;
+    uint32_t p, qs, ql;
+    uint4 x, ys, yl;
+  };
+  Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
+  uint4 n0 = ld16c(cb, prime0 + tid, cbytes), n1 = ld16c(cb, prime0 + kFindTile + tid, cbytes);
+  // position S.p: its word (a position that is not the segment's writes to
+  // a spare word past the batch's: no branch around the store, see step)
+  auto verify = [&](const Stage &S) {
+    const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
+    const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
+    const uint4 ys = fix16(S.ys, S.qs, cbytes), yl = fix16(S.yl, S.ql, cbytes);
+    const uint32_t ms = S.ks ? min(prefix16(S.x, ys), lim) : 0u, ml = S.kl ? min(prefix16(S.x, yl), lim) : 0u;
+    const uint32_t ds = S.p - S.qs, dl = S.p - S.ql;
+    uint32_t m = 0, d = 0;
+    if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
+    else if (ml >= zs::kMinMatch) m = ml, d = dl;
+    *(S.v ? word_at(S.p) : words + nblk * kZcBlock + tid) = m ? (m << 24 | d) : 0u;
+  };
+  // one tile; n: its own bytes on entry, the bytes of the tile two ahead on
+  // exit; S: the tile two back on entry (verified here), this tile on exit.
+  // The loop below alternates two (n, S) sets, so no register with a pending
+  // load is ever copied (a copy would wait for the load)
+  auto step = [&](uint32_t t0, uint4 &n, Stage &S) {
     const uint32_t p = t0 + tid;
-    const uint4 x = fix16(nx, p, cbytes);
+    const uint4 x = fix16(n, p, cbytes);
     const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert)
     const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
-    const uint32_t v = (p + 1) & 0xFFFFu;
     const uint32_t hs = hash5(x.x, x.y), hl = hash8(x.x, x.y);
-    uint32_t cs = 0, cl = 0;
-    if (find && vs) cs = ht_ld(hts, hs);
-    if (find && vl) cl = ht_ld(htl, hl);
-    // candidates (distance modulo 2^16, within the chunk) and their bytes
-    const uint32_t ds = (p + 1 - cs) & 0xFFFFu, dl = (p + 1 - cl) & 0xFFFFu;
-    const bool oks = cs != 0 && ds != 0 && ds <= p, okl = cl != 0 && dl != 0 && dl <= p && dl != ds;
-    // (loaded now, used after the inserts; a missing candidate loads position 0)
-    const uint32_t qs = oks ? p - ds : 0u, ql = okl ? p - dl : 0u;
-    const uint4 ys0 = ld16c(cb, qs, cbytes), yl0 = ld16c(cb, ql, cbytes);
-    // the next tile's bytes after the candidates' (the counter retires in
-    // order: the candidates are then awaited without draining the prefetch)
-    nx = ld16c(cb, p + kFindTile, cbytes);
+    const uint32_t cs = find && vs ? hts[hs] : 0u, cl = find && vl ? htl[hl] : 0u;
+    // candidates within the window (a table holds positions before this tile)
+    const bool oks = cs != 0 && p - (cs - 1) <= zs::kWindow;
+    const bool okl = cl != 0 && cl != cs && p - (cl - 1) <= zs::kWindow;
+    const uint32_t qs = oks ? cs - 1 : 0u, ql = okl ? cl - 1 : 0u;
+    verify(S);
+    S.v = find;
+    S.ks = oks;
+    S.kl = okl;
+    S.p = p;
+    S.qs = qs;
+    S.ql = ql;
+    S.x = x;
+    S.ys = ld16c(cb, qs, cbytes);
+    S.yl = ld16c(cb, ql, cbytes);
+    n = ld16c(cb, p + 2 * kFindTile, cbytes);
     lds_sync();  // every lookup of the tile before any insert
-    const bool ws = vs && v != 0, wl = vl && v != 0;
-    if (ws) ht_st(hts, hs, v);
-    if (wl) ht_st(htl, hl, v);
-    // the latest position per slot: lanes whose store lost to an older
-    // position of the tile (or that an older tile's value still holds) store
-    // again until none does.  A round's vote slot is cleared two rounds ahead
-    // (its last readers passed a barrier since), so no round needs a second
-    // barrier for it.
-    bool ps = ws, pl = wl;
-    for (;;) {
-      const uint32_t k = round % 3;
-      if (tid == 0) __hip_atomic_store(vote + (round + 1) % 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (ps || pl) __hip_atomic_store(vote + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      lds_sync();
-      const bool any = __hip_atomic_load(vote + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-      ++round;
-      if (!any) break;
-      if (ps) {
-        ps = !ht_newer(ht_ld(hts, hs), t0, p);
-        if (ps) ht_st(hts, hs, v);
-      }
-      if (pl) {
-        pl = !ht_newer(ht_ld(htl, hl), t0, p);
-        if (pl) ht_st(htl, hl, v);
-      }
-    }
-    if (find) {
-      const uint32_t bend = min(clen, (p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
-      const uint32_t lim = min(kMlCap, bend - p);
-      const uint4 ys = fix16(ys0, qs, cbytes), yl = fix16(yl0, ql, cbytes);
-      uint32_t ms = oks ? min(prefix16(x, ys), lim) : 0u, ml = okl ? min(prefix16(x, yl), lim) : 0u;
-      uint32_t m = 0, d = 0;
-      if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
-      else if (ml >= zs::kMinMatch) m = ml, d = dl;
-      const uint64_t wi = (bi0 + (p / (uint32_t)kZcBlock - B0.b)) * kZcBlock + p % (uint32_t)kZcBlock;
-      words[wi] = m ? (m << 16 | d) : 0u;
-    }
+    if (vs) atomicMax(hts + hs, p + 1);
+    if (vl) atomicMax(htl + hl, p + 1);
+    lds_sync();  // every insert before the next tile's lookups
+  };
+  __syncthreads();
+  for (uint32_t t0 = prime0; t0 < seg1; t0 += 2 * kFindTile) {
+    step(t0, n0, s0);
+    if (t0 + kFindTile < seg1) step(t0 + kFindTile, n1, s1);
   }
+  verify(s0);
+  verify(s1);
 }
 
 // Copy bytes [a, a + n) of src to dst, the whole wave (64 lanes) together,
@@ -374,8 +362,8 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
       const uint32_t i = (uint32_t)__builtin_ctzll(mm);
       const uint32_t pos = wb + 64 * j + i;
       const uint32_t wd = (uint32_t)__builtin_amdgcn_readlane((int)sel4(j, v[0], v[1], v[2], v[3]), (int)i);
-      uint32_t ml = wd >> 16;
-      const uint32_t off = wd & 0xFFFFu;
+      uint32_t ml = wd >> 24;
+      const uint32_t off = wd & 0xFFFFFFu;
       if (ml == kMlCap) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
         for (;;) {
           const uint32_t q = pos + ml + lane;
