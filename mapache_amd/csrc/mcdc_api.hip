@@ -235,7 +235,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, sv_comp, sv_seal, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words;
+      sv_in, sv_pack, sv_comp, sv_seal, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs;
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -938,7 +938,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
                     &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
-                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words};
+                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_recs};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1895,14 +1895,15 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   if ((rc = ensure(ctx, ctx->zc_tmp, tmpb))) return rc;
   if ((rc = ensure(ctx, ctx->zc_blocks, mb * sizeof(ZcBlock))) || (rc = ensure(ctx, ctx->zc_stage, mb * kZcSlot)) ||
       (rc = ensure(ctx, ctx->zc_seqs, mb * kZcSeqCap * 8)) || (rc = ensure(ctx, ctx->zc_piece, (mb + 1) * 8)) ||
-      (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)) || (rc = ensure(ctx, ctx->zc_words, (mb * kZcBlock + 1024) * 4)))
+      (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)) || (rc = ensure(ctx, ctx->zc_words, (mb * kZcBlock + 1024) * 4)) ||
+      (rc = ensure(ctx, ctx->zc_recs, mb * kZcSeqCap * 8)))
     return rc;
   for (uint64_t c0 = 0; c0 < nchunks;) {  // batches of whole chunks, <= kZcBatchBlocks blocks each
     uint64_t c1 = c0 + 1;
     while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb) ++c1;
     launch_zc_batch((const uint8_t *)d_data, n, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
                     (ZcBlock *)ctx->zc_blocks.p, (uint8_t *)ctx->zc_stage.p, (uint64_t *)ctx->zc_seqs.p,
-                    (uint32_t *)ctx->zc_words.p, T,
+                    (uint32_t *)ctx->zc_words.p, (uint64_t *)ctx->zc_recs.p, T,
                     (uint64_t *)ctx->zc_piece.p, (uint64_t *)ctx->zc_poff.p, misc + 2, (uint8_t *)d_out, ext,
                     ctx->zc_tmp.p, tmpb, st, ctx->knobs.zc_huf);
     HIP_TRY(hipGetLastError());

@@ -30,13 +30,14 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
                        uint32_t *err, uint64_t *bound, void *tmp, size_t tmp_bytes, hipStream_t st);
 // Scratch per batch of nblk blocks (bytes), all device memory of the context:
 //   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot, seqs nblk x kZcSeqCap
-//   x 8, match words nblk x kZcBlock x 4 (6.1 x the batch's input in all),
+//   x 8, state records nblk x kZcSeqCap x 8, match words (nblk x kZcBlock +
+//   1024) x 4 (6.6 x the batch's input in all),
 //   piece / poff (nblk + 1) x 8.  A batch holds whole chunks, at most
 //   kZcBatchBlocks blocks unless one chunk is longer (1 GiB: 7 x 2^18 words).
 // one batch: the chunks [c0, c1), blocks [b0, b0 + nblk)
 void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
                      uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
-                     uint32_t *words,
+                     uint32_t *words, uint64_t *recs,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true);
 

@@ -25,7 +25,8 @@
 //   k_zc_parse   ONE WAVE PER BLOCK: greedy parse over the words, 256
 //                positions per window (4 ballots of "has a match"), the next
 //                match found with scalar bit scans; a match of 16 bytes is
-//                extended 64 bytes per step; literals to the block's staging
+//                extended 64 bytes per step; repeat codes where an offset
+//                repeats one the block set; literals to the block's staging
 //                slot (64 runs copied at a time), sequences to scratch
 //   k_zc_huff    ONE WAVE PER BLOCK: the block's literals (all of a block
 //                without matches) as a Huffman-coded (or RLE) literals
@@ -35,15 +36,12 @@
 //                or FSE-compressed weights) by one lane, then the streams
 //                (four above 1023 literals) by the whole wave, bit positions
 //                from wave scans, assembled in LDS
-//   k_zc_encode  ONE LANE PER BLOCK, 64 blocks per wave sharing one table
-//                set: repeat codes where an offset repeats one the block set,
-//                code histograms of the wave's blocks, per symbol type a
-//                shared table or the predefined one (seq_plan), the shared
-//                tables built by the wave in LDS; each block takes the shared
-//                table of a type only when its own sequences cost less with
-//                it (description included); then each lane writes its block's
-//                serial FSE bitstream (three interleaved state machines);
-//                block kept compressed only if smaller than raw
+//   k_zc_encode  ONE WAVE PER BLOCK: per symbol type the block's own FSE
+//                table or the predefined one (seq_plan), the three state
+//                machines on three lanes (their bits to scratch), then every
+//                sequence's bits placed by the whole wave (wave scans of bit
+//                counts, OR-ed into place); block kept compressed only if
+//                smaller than raw
 //   scan         piece sizes (frame header on a chunk's first block, block
 //                header, content) -> output offsets, frames back to back
 //   k_zc_final   ONE WAVE PER BLOCK: headers + content (staging or input)
@@ -299,6 +297,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
   uint8_t *lit = stage + bi * kZcSlot + zs::kLitHdr;
   uint64_t *sq = seqs + bi * kZcSeqCap;
   uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0;
+  zs::RepHist R{{0, 0, 0}, 0};
   uint32_t run_src = 0, run_len = 0, run_dst = 0;  // this lane's pending literal run
   // 64 bytes of each lane's run per step: four 16-byte loads in flight, then
   // byte stores
@@ -374,11 +373,13 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
           if (diff) break;
         }
       }
+      // repeat codes (the block's own history: rep_code), wave-uniform
+      const uint64_t sv = zs::rep_code(R, zs::seq_pack(pos - lit0, ml, off));
       if (lane == (nseq & 63)) {
         run_src = lit0;
         run_len = pos - lit0;
         run_dst = nlit;
-        sq[nseq] = zs::seq_pack(pos - lit0, ml, off);
+        sq[nseq] = sv;
       }
       nlit += pos - lit0;
       ++nseq;
@@ -656,114 +657,218 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
   }
 }
 
-// One lane per block, 64 blocks per wave sharing one set of tables (a
-// block's own tables would not fit 64 times in LDS, and one wave per block
-// leaves the serial bitstream 64x less parallel):
-//   plan     code histograms over the wave's blocks with 64 or more
-//            sequences; seq_plan (lane 0) picks per symbol type the shared
-//            table or the predefined one, pricing the descriptions once per
-//            block; the shared tables built by the wave, the predefined
-//            ones copied beside them, bits per code of both in LDS
-//   choose   each block prices its own sequences under both and takes the
-//            shared table for a type only if that is smaller with its
-//            description
-//   encode   each lane writes its block's serial FSE bitstream (three
-//            interleaved state machines); block kept compressed only if
-//            smaller than raw
-constexpr uint32_t kEncOwnMin = 64;  // sequences for a block to consider the shared tables
+// ONE WAVE PER BLOCK: the block's sequences section with tables of its own
+// (per symbol type the block's FSE_Compressed_Mode table or the predefined
+// one, seq_plan), the serial FSE state machines split from the bit writing:
+//   plan     code histograms (lanes over the sequences, LDS atomics);
+//            seq_plan on lane 0; the own tables built by the wave
+//   chains   the three state machines (lanes 0-2: LL, OF, ML) walk the
+//            sequences from the last to the first, 64 at a time (codes
+//            read from the batch's lanes): per sequence the state bits
+//            (count | value << 4, 16 bits each) to scratch
+//   offsets  per sequence its bits (state bits + extra bits) and, by wave
+//            scans in writing order (last sequence first), its bit offset
+//   write    the section zeroed, every sequence's bits OR-ed into place by
+//            its lane (global atomics), then the final states, the end mark
+//            and the header (count, modes, descriptions) by lane 0
+// The block stays raw when the compressed block is not smaller.
+__device__ __forceinline__ void or_bits(uint32_t *w, uint64_t bit, uint64_t lo, uint64_t hi, uint32_t nbits) {
+  // bits [bit, bit + nbits) of a little-endian stream of 32-bit words = the
+  // low nbits of hi:lo (nbits <= 96)
+  const uint32_t sh = (uint32_t)(bit & 31);
+  uint32_t *q = w + (bit >> 5);
+  const uint64_t a = lo << sh, b = (hi << sh) | (sh ? lo >> (64 - sh) : 0), c = sh ? hi >> (64 - sh) : 0;
+  const uint32_t words = (sh + nbits + 31) >> 5;
+  const uint32_t v[4] = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (k < words && v[k]) atomicOr(q + k, v[k]);
+  if (words > 4 && (uint32_t)c) atomicOr(q + 4, (uint32_t)c);
+}
 
 __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                  uint64_t *seqs, ZTables T, uint64_t *piece) {
+                                                  const uint64_t *seqs, uint64_t *recs, ZTables T, uint64_t *piece) {
   MCDC_VGPR_PAD(40);  // (not an exact fill)
-  __shared__ FseCTL t[3], pt[3];  // shared (own) and predefined tables
+  __shared__ FseCTL tb[3];  // the block's LL, OF, ML tables (own or predefined)
   __shared__ SeqPlan P;
-  __shared__ float bits[2][3][53];  // bits per code: [shared / predefined][LL, OF, ML][code]
   __shared__ uint32_t hist[3][53], cum[54], seen[54];
   const uint32_t lane = lane_id();
-  const uint64_t bi = (uint64_t)blockIdx.x * 64 + lane;
-  const bool valid = bi < nblk;
-  if (bi == nblk) piece[nblk] = 0;
-  ZcBlock B{};
-  if (valid) B = blocks[bi];
+  const uint64_t bi = blockIdx.x;
+  if (bi == 0 && lane == 0) piece[nblk] = 0;
+  if (bi >= nblk) return;
+  const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   const uint64_t *sq = seqs + bi * kZcSeqCap;
-  const FseCT *pre[3] = {&T.ll, &T.of, &T.ml};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    pt[k].state[lane] = pre[k]->state[lane];
-    if (lane < 53) {
-      pt[k].dfs[lane] = pre[k]->dfs[lane];
-      pt[k].dnb[lane] = pre[k]->dnb[lane];
-      hist[k][lane] = 0;
-    }
-    if (lane == 0) pt[k].log = pre[k]->log;
-  }
-  __syncthreads();
-  const bool cand = ns >= kEncOwnMin;
-  {  // repeat codes (the block's own history, rep_code), in place; the histograms
-    RepHist R{{0, 0, 0}, 0};
-    uint64_t *sw = seqs + bi * kZcSeqCap;
-    for (uint32_t i = 0; i < ns; ++i) {
-      const uint64_t q = rep_code(R, sq[i]);
-      sw[i] = q;
-      if (cand) {
+  uint16_t *rec = reinterpret_cast<uint16_t *>(recs + bi * kZcSeqCap);
+  uint8_t *st = stage + bi * kZcSlot;
+  uint32_t csize = 0;
+  if (ns || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
+    const uint32_t at = B.lsize ? B.lsize : kLitHdr + B.nlit;  // the literals section (k_zc_huff / raw)
+    if (!B.lsize && lane == 0) put_raw_lit_header(st, B.nlit);
+    if (ns == 0) {
+      if (lane == 0) st[at] = 0;  // Number_of_Sequences 0
+      csize = at + 1 < B.len ? at + 1 : 0;
+    } else {
+      for (uint32_t k = lane; k < 3 * 53; k += 64) (&hist[0][0])[k] = 0;
+      __syncthreads();
+      for (uint32_t i = lane; i < ns; i += 64) {
+        const uint64_t q = sq[i];
         atomicAdd(&hist[0][ll_code(seq_ll(q))], 1u);
         atomicAdd(&hist[1][highbit(seq_ov(q))], 1u);
         atomicAdd(&hist[2][ml_code(seq_ml(q) - 3)], 1u);
       }
-    }
-  }
-  const uint32_t ncand = (uint32_t)__builtin_popcountll(__ballot(cand));
-  uint32_t total = cand ? ns : 0;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) total += (uint32_t)__shfl_xor((int)total, d);
-  __syncthreads();
-  if (lane == 0) seq_plan(hist[0], hist[1], hist[2], total, P, ncand ? ncand : 1);
-  __syncthreads();
-  const int16_t *pnorm[3] = {kLLNorm, kOFNorm, kMLNorm};
-  const uint32_t npre[3] = {36, 29, 53};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    if (P.own[k]) fse_build_wave(P.norm[k], P.tl[k], t[k], cum, seen, lane);
-    if (lane < 53) {
-      const int32_t n = P.own[k] ? P.norm[k][lane] : 0;
-      bits[0][k][lane] = n > 0 ? (float)P.tl[k] - log2f((float)n) : 1e9f;
-      const int32_t m = lane < npre[k] ? (pnorm[k][lane] == -1 ? 1 : pnorm[k][lane]) : 0;
-      bits[1][k][lane] = m > 0 ? (float)pt[k].log - log2f((float)m) : 1e9f;
-    }
-  }
-  __syncthreads();
-  uint32_t modes = 0;
-  if (cand && (P.own[0] | P.own[1] | P.own[2])) {
-    float c0[3] = {0, 0, 0}, c1[3] = {0, 0, 0};
-    for (uint32_t i = 0; i < ns; ++i) {
-      const uint64_t q = sq[i];
-      const uint32_t code[3] = {ll_code(seq_ll(q)), highbit(seq_ov(q)), ml_code(seq_ml(q) - 3)};
+      __syncthreads();
+      if (lane == 0) seq_plan(hist[0], hist[1], hist[2], ns, P, 1);
+      __syncthreads();
+      const FseCT *pre[3] = {&T.ll, &T.of, &T.ml};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        c0[k] += bits[0][k][code[k]];
-        c1[k] += bits[1][k][code[k]];
+        if (P.own[k]) {
+          fse_build_wave(P.norm[k], P.tl[k], tb[k], cum, seen, lane);
+        } else {
+          tb[k].state[lane] = pre[k]->state[lane];
+          if (lane < 53) {
+            tb[k].dfs[lane] = pre[k]->dfs[lane];
+            tb[k].dnb[lane] = pre[k]->dnb[lane];
+          }
+          if (lane == 0) tb[k].log = pre[k]->log;
+        }
+        __syncthreads();
+      }
+      // chains: lane k < 3 runs type k's state machine, the last sequence first
+      const FseCTL &ct = tb[lane < 3 ? lane : 0];
+      uint32_t state = 0;
+      for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) {
+        const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
+        const int32_t i = b0 + (int32_t)lane;
+        uint32_t c0 = 0, c1 = 0, c2 = 0;
+        if (i < b1) {
+          const uint64_t q = sq[i];
+          c0 = ll_code(seq_ll(q));
+          c1 = highbit(seq_ov(q));
+          c2 = ml_code(seq_ml(q) - 3);
+        }
+        for (int32_t j = b1 - b0 - 1; j >= 0; --j) {
+          const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, j),
+                         a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, j),
+                         a2 = (uint32_t)__builtin_amdgcn_readlane((int)c2, j);
+          const uint32_t c = lane == 0 ? a0 : lane == 1 ? a1 : a2;
+          if (lane < 3) {
+            const uint32_t dnb = ct.dnb[c];
+            const int32_t dfs = ct.dfs[c];
+            uint32_t r = 0;
+            if (b0 + j == (int32_t)ns - 1) {  // the last sequence: the initial state (no bits)
+              const uint32_t nb = (dnb + (1u << 15)) >> 16;
+              state = ct.state[((((nb << 16) - dnb)) >> nb) + dfs];
+            } else {
+              const uint32_t nb = (state + dnb) >> 16;
+              r = nb | (state & ((1u << nb) - 1u)) << 4;
+              state = ct.state[(state >> nb) + dfs];
+            }
+            rec[4 * (b0 + j) + lane] = (uint16_t)r;
+          }
+        }
+      }
+      // (the records land in L2 and the CU's vector L1 is invalidated before
+      // the other lanes read them back)
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      // the section: header, then the bitstream from a 4-byte aligned word base
+      const uint32_t cnt = ns < 128 ? 1u : ns < 0x7F00 ? 2u : 3u;
+      const uint32_t hsz = cnt + 1 + P.ndesc;
+      uint8_t *bs0 = st + at + hsz;
+      const uint32_t pre_bits = (uint32_t)((uintptr_t)bs0 & 3) * 8;  // stream bit 0 inside the first word
+      uint32_t *w0 = reinterpret_cast<uint32_t *>((uintptr_t)bs0 & ~(uintptr_t)3);
+      // bits per sequence and offsets (writing order: the last sequence first)
+      uint64_t base_bits = 0;
+      const uint32_t tl0 = tb[0].log, tl1 = tb[1].log, tl2 = tb[2].log;
+      // first pass: the total, to size the zeroing and the raw / compressed choice
+      uint64_t tot = 0;
+      for (uint32_t i = lane; i < ns; i += 64) {
+        const uint64_t q = sq[i];
+        const uint64_t rr = *reinterpret_cast<const uint64_t *>(rec + 4 * i);
+        const uint32_t llc = ll_code(seq_ll(q)), mlc = ml_code(seq_ml(q) - 3), ofc = highbit(seq_ov(q));
+        tot += (rr & 15) + ((rr >> 16) & 15) + ((rr >> 32) & 15) + ll_bits(llc) + ml_bits(mlc) + ofc;
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) tot += (uint64_t)__shfl_xor((long long)tot, d);
+      const uint64_t all_bits = tot + tl0 + tl1 + tl2 + 1;  // + final states + end mark
+      const uint32_t nbytes = (uint32_t)((all_bits + 7) / 8);
+      const uint32_t total = at + hsz + nbytes;
+      if (total < B.len) {
+        // zero the stream: its head bytes up to the next word boundary one by
+        // one (the bytes before it in that word are the header's, or the
+        // literals' when the header is short), whole words after
+        const uint32_t head = pre_bits ? 4 - pre_bits / 8 : 0u;
+        if (lane < head) bs0[lane] = 0;
+        const uint32_t nw = ((uint32_t)all_bits + 31) / 32 + 1;
+        for (uint32_t k = lane; k < nw; k += 64) w0[(pre_bits ? 1 : 0) + k] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) {
+          const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
+          const int32_t i = b1 - 1 - (int32_t)lane;  // lane 0 the batch's last sequence (written first)
+          uint64_t lo = 0, hi = 0;
+          uint32_t nb = 0;
+          if (i >= b0) {
+            const uint64_t q = sq[i];
+            const uint64_t rr = *reinterpret_cast<const uint64_t *>(rec + 4 * i);
+            const uint32_t ll = seq_ll(q), mb = seq_ml(q) - 3, ob = seq_ov(q);
+            const uint32_t llc = ll_code(ll), mlc = ml_code(mb), ofc = highbit(ob);
+            auto put = [&](uint64_t v, uint32_t n) {  // append n bits (n <= 32)
+              v &= n >= 64 ? ~0ull : ((1ull << n) - 1);
+              if (nb < 64) {
+                lo |= v << nb;
+                if (nb + n > 64) hi |= v >> (64 - nb);
+              } else {
+                hi |= v << (nb - 64);
+              }
+              nb += n;
+            };
+            // states in writing order OF, ML, LL (none for the last sequence)
+            put((rr >> 20) & 0xFFF, (uint32_t)((rr >> 16) & 15));
+            put((rr >> 36) & 0xFFF, (uint32_t)((rr >> 32) & 15));
+            put((rr >> 4) & 0xFFF, (uint32_t)(rr & 15));
+            put(ll, ll_bits(llc));
+            put(mb, ml_bits(mlc));
+            put(ob, ofc);
+          }
+          uint64_t incl = nb;  // inclusive prefix in lane order = writing order
+#pragma unroll
+          for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t t = (uint64_t)__shfl_up((long long)incl, d);
+            if (lane >= d) incl += t;
+          }
+          if (nb) or_bits(w0, pre_bits + base_bits + incl - nb, lo, hi, nb);
+          base_bits += (uint64_t)__shfl((long long)incl, 63);
+        }
+        // final states (ML, OF, LL: log bits each) and the end mark, lane 0
+        const uint32_t fs = state;  // lanes 0-2: the final states of LL, OF, ML
+        const uint32_t f0 = (uint32_t)__shfl((int)fs, 0), f1 = (uint32_t)__shfl((int)fs, 1),
+                       f2 = (uint32_t)__shfl((int)fs, 2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        if (lane == 0) {
+          const uint64_t v = (uint64_t)(f2 & ((1u << tl2) - 1)) | (uint64_t)(f1 & ((1u << tl1) - 1)) << tl2 |
+                             (uint64_t)(f0 & ((1u << tl0) - 1)) << (tl2 + tl1) | 1ull << (tl2 + tl1 + tl0);
+          or_bits(w0, pre_bits + base_bits, v, 0, tl2 + tl1 + tl0 + 1);
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+          uint8_t *h = st + at;  // Number_of_Sequences, Symbol_Compression_Modes, descriptions
+          if (cnt == 1) {
+            h[0] = (uint8_t)ns;
+          } else if (cnt == 2) {
+            h[0] = (uint8_t)((ns >> 8) + 0x80);
+            h[1] = (uint8_t)ns;
+          } else {
+            h[0] = 0xFF;
+            h[1] = (uint8_t)(ns - 0x7F00);
+            h[2] = (uint8_t)((ns - 0x7F00) >> 8);
+          }
+          h[cnt] = (uint8_t)P.modes;
+          for (uint32_t k = 0; k < P.ndesc; ++k) h[cnt + 1 + k] = P.desc[k];
+        }
+        csize = total;
       }
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      if (P.own[k] && c0[k] + 8.0f * (float)P.dlen[k] < c1[k]) modes |= 2u << (6 - 2 * k);
   }
-  uint32_t csize = 0;
-  if (valid && (ns || B.lsize)) {  // (no sequences but a Huffman / RLE section: a literals-only block)
-    uint8_t *st = stage + bi * kZcSlot;
-    if (!B.lsize) put_raw_lit_header(st, B.nlit);
-    const uint32_t at = B.lsize ? B.lsize : kLitHdr + B.nlit;  // (Huffman / RLE section written by k_zc_huff)
-    const uint32_t cap = B.len > at + 1 ? B.len - at - 1 : 0;
-    const FseCTL &tll = (modes >> 6) & 3 ? t[0] : pt[0];
-    const FseCTL &tof = (modes >> 4) & 3 ? t[1] : pt[1];
-    const FseCTL &tml = (modes >> 2) & 3 ? t[2] : pt[2];
-    const uint32_t ss = cap ? encode_sequences_with(tll, tof, tml, modes, P.desc, P.doff, P.dlen,
-                                                    [&](uint32_t i) { return sq[i]; }, ns, st + at, cap)
-                            : 0;
-    if (ss) csize = at + ss;
-  }
-  if (valid) {
+  if (lane == 0) {
     blocks[bi].csize = csize;
     piece[bi] = (B.b == 0 ? kFrameHdr : 0) + kBlockHdr + (csize ? csize : B.len);
   }
@@ -832,7 +937,8 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 
 void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
                      uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
-                     uint32_t *words, const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase,
+                     uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
+                     uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf) {
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
@@ -840,8 +946,7 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindTile), 0, st, base, nbytes, blocks, nblk, words);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, words, stage, seqs);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage);
-  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)((nblk + 1 + 63) / 64)), dim3(64), 0, st, blocks, nblk, stage, seqs,
-                     T, piece);
+  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, T, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);
   hipLaunchKernelGGL(k_zc_final, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, poff, obase, out,
