@@ -423,24 +423,26 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
 // is smaller than the raw section (3-byte header + the literals), written
 // over the staging slot's raw literals; B.lsize its size, 0 = raw.  The whole
 // wave works on every step but the tree and its description (one lane):
-//   count    16 bytes per lane per step into 8 LDS histogram copies
+//   count    16 bytes per lane per step into 4 LDS histogram copies
 //   rank     the 256 symbols by count (ties by symbol), four per lane
 //   tree     huf_build on the ranked symbols, the weights' description
 //            (direct or FSE-compressed, the shorter; lane 0)
 //   sizes    bits per stream (wave sums); give up unless smaller than raw
-//   streams  64 literals per round, last first: code lengths -> wave scan ->
-//            bit positions -> codes OR-ed into the section assembled in LDS
-//   store    header, tree, jump table; the section to the slot, 16-byte stores
-__global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage) {
-  // the section under assembly; its first 8 KiB hold the histogram copies and
-  // then the tree's scratch before it is cleared
-  __shared__ __attribute__((aligned(16))) uint32_t out[kZcSlot / 4];
+//   streams  each stream cut into 64 contiguous pieces (in writing order:
+//            the last literal first), a lane per piece: its bit count, a
+//            wave scan for its offset, then its bits packed in a register
+//            and stored a word at a time into the block's match-word
+//            scratch (free after k_zc_parse; words shared with a
+//            neighbouring piece OR-ed in)
+//   store    header, tree, jump table; the section copied to the slot
+// (LDS ~9 KiB per wave: 16 waves per CU; the section itself stays in HBM.)
+__global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
+                                                uint32_t *scratch) {
+  __shared__ __attribute__((aligned(16))) uint32_t hist[4][256];
   __shared__ HufCT ct;
+  __shared__ HufWork hw;
   __shared__ uint8_t tdesc[132];
   __shared__ uint32_t tree_sz;
-  uint32_t(*hist)[256] = reinterpret_cast<uint32_t(*)[256]>(out);
-  HufWork &hw = *reinterpret_cast<HufWork *>(out + 8 * 256);
-  static_assert(8 * 256 * 4 + sizeof(HufWork) <= sizeof(out), "LDS");
   const uint64_t bi = blockIdx.x;
   if (bi >= nblk) return;
   const uint32_t lane = lane_id();
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
   if (n < 32) return;  // (lsize stays 0: raw literals)
   uint8_t *st = stage + bi * kZcSlot;
   const uint8_t *src = B.nseq ? st + kLitHdr : base + B.src;
-  for (uint32_t k = lane; k < 8 * 256; k += 64) out[k] = 0;
+  for (uint32_t k = lane; k < 4 * 256; k += 64) (&hist[0][0])[k] = 0;
   __syncthreads();
   // count (misaligned 16-byte loads: gfx950 reads the bytes at the address)
   for (uint32_t k0 = 0; k0 < n; k0 += 1024) {
@@ -468,17 +470,14 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
     }
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j)
-      if (j < m) atomicAdd(&hist[lane & 7][(w[j >> 2] >> (8 * (j & 3))) & 0xFF], 1u);
+      if (j < m) atomicAdd(&hist[lane & 3][(w[j >> 2] >> (8 * (j & 3))) & 0xFF], 1u);
   }
   __syncthreads();
   uint32_t c[4];
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const uint32_t k = lane + 64 * h;
-    uint32_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v += hist[j][k];
-    c[h] = v;
+    c[h] = hist[0][k] + hist[1][k] + hist[2][k] + hist[3][k];
   }
   __syncthreads();
 #pragma unroll
@@ -543,41 +542,46 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
   const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
   if (one && csize >= 1024) return;  // (one stream: 10-bit sizes)
   const uint32_t hdr = lit_hdr_size(n, csize, one);
-  const uint32_t nq = (total + 15) / 16;  // 16-byte units of the section
-  for (uint32_t k = lane; k < nq; k += 64) reinterpret_cast<uint4 *>(out)[k] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
+  uint32_t *sw = scratch + bi * kZcBlock;  // the section under assembly (words)
+  const uint32_t nq = (total + 3) / 4 + 1;
+  for (uint32_t k = lane; k < nq; k += 64) sw[k] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
   // the streams
   uint32_t o = hdr + tree + (one ? 0 : 6);  // byte offset of stream k in the section
   for (uint32_t k = 0; k < ns; ++k) {
     const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
-    uint32_t carry = 8 * o;  // bit position of the next round's first literal
-    for (uint32_t r0 = 0; r0 < len; r0 += 8 * 64) {
-      uint32_t x[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t q = r0 + 64 * j + lane;
-        x[j] = q < len ? (uint32_t)src[e - 1 - q] : 0x100u;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (r0 + 64 * j >= len) break;
-        const uint32_t nb = x[j] < 0x100u ? ct.nb[x[j]] : 0u;
-        const uint32_t incl = wave_incl_sum(nb, lane);
-        const uint32_t pos = carry + incl - nb;
-        if (nb) {
-          const uint32_t code = ct.code[x[j]], sft = pos & 31;
-          atomicOr(&out[pos >> 5], code << sft);
-          if (sft + nb > 32) atomicOr(&out[(pos >> 5) + 1], code >> (32 - sft));
+    // piece of lane l: writing indices [l P, (l + 1) P) = literals e - 1 - w
+    const uint32_t P = (len + 63) / 64, w0 = min(lane * P, len), w1 = min(w0 + P, len);
+    uint32_t nbits = 0;
+    for (uint32_t w = w0; w < w1; ++w) nbits += ct.nb[src[e - 1 - w]];
+    const uint32_t incl = wave_incl_sum(nbits, lane);
+    uint64_t bit = 8ull * o + (incl - nbits);
+    if (nbits) {
+      uint64_t acc = 0;
+      uint32_t accn = (uint32_t)(bit & 31), wi = (uint32_t)(bit >> 5);
+      bool first = true;
+      for (uint32_t w = w0; w < w1; ++w) {
+        const uint32_t x = src[e - 1 - w];
+        acc |= (uint64_t)ct.code[x] << accn;
+        accn += ct.nb[x];
+        if (accn >= 32) {
+          if (first) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece before)
+          else sw[wi] = (uint32_t)acc;
+          first = false;
+          acc >>= 32;
+          accn -= 32;
+          ++wi;
         }
-        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       }
+      if (accn) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece after)
     }
-    if (lane == 0) atomicOr(&out[carry >> 5], 1u << (carry & 31));  // the end mark
+    const uint32_t end = 8 * o + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (lane == 0) atomicOr(sw + (end >> 5), 1u << (end & 31));  // the end mark
     o += ssz[k];
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
   if (lane == 0) {
-    uint8_t *sec = reinterpret_cast<uint8_t *>(out);
+    uint8_t *sec = reinterpret_cast<uint8_t *>(sw);
     put_huf_lit_header(sec, n, csize, one);
     for (uint32_t i = 0; i < tree; ++i) sec[hdr + i] = tdesc[i];
     if (!one)
@@ -587,9 +591,11 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
       }
     blocks[bi].lsize = total;
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
   // (every read of the staged literals is done: the section replaces them)
-  for (uint32_t k = lane; k < nq; k += 64) reinterpret_cast<uint4 *>(st)[k] = reinterpret_cast<const uint4 *>(out)[k];
+  const uint32_t n16 = (total + 15) / 16;
+  for (uint32_t k = lane; k < n16; k += 64)
+    reinterpret_cast<uint4 *>(st)[k] = reinterpret_cast<const uint4 *>(sw)[k];
 }
 
 // Modular inverse of an odd a modulo 2^32 (Newton: each step doubles the bits).
@@ -945,7 +951,7 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      b0, blocks);
   hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindTile), 0, st, base, nbytes, blocks, nblk, words);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, words, stage, seqs);
-  if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage);
+  if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, words);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, T, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);
