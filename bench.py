@@ -66,6 +66,26 @@ def _dist():
     return world, rank, local
 
 
+def _newest_profile(name: str):
+    """(parsed JSON, relative path) of profiles/rNN[/part]/<name> of the newest round, or (None, None)."""
+    import glob
+    import re
+    cands = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", name)) + \
+            glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "*", name)):
+        rel = os.path.relpath(path, ROOT)
+        m = re.match(r"profiles/r(\d+)/", rel)
+        if m:
+            cands.append((int(m.group(1)), rel.count("/") == 2, rel))
+    for _, _, rel in sorted(cands, reverse=True):
+        try:
+            with open(os.path.join(ROOT, rel)) as f:
+                return json.load(f), rel
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
 def _pmc_traffic():
     """Calibrated PMC read traffic of the scan (profiles/rNN/pmc_traffic.json, written from
     separate rocprofv3 --pmc FETCH_SIZE passes by tools/profile_round.sh): HBM bytes per input byte.
@@ -350,6 +370,15 @@ def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_s
                                   "peak engine clock"},
              "chunk_plus_ids_ms": round(dt2 * 1e3, 3), "chunk_plus_ids_gib_s": round(n / dt2 / GIB, 2),
              "parity_probe_chunks": int(len(sel)), "parity_probe_ok": ok}
+        pmc, src = _newest_profile("b3_pmc.json")  # counters of the same kernel (separate --pmc passes)
+        if pmc and pmc.get("held_clock_ghz"):
+            # VALU-issue floor at the clock the chip holds under this kernel: the
+            # measured instructions per block at 100 % VALUBusy
+            busy = pmc.get("valu_busy_pct") or None
+            r["roofline"]["pmc"] = {"valu_busy_pct": busy, "held_clock_ghz": pmc["held_clock_ghz"],
+                                    "valu_per_wave_block": pmc.get("valu_per_wave_block"),
+                                    "floor_ms_at_held_clock": round(ids_ms * busy / 100, 3) if busy else None,
+                                    "source": src}
         # dedup index (save_blob's index check, repository_v1.rs:169-180) over these IDs in HBM:
         # into an empty index (all new) and again into the populated one (all duplicates)
         try:

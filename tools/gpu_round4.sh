@@ -72,6 +72,18 @@ for stage in "$@"; do
     done
     cd $R
     echo zcprof done ;;
+  b3pmc)  # chunk-ID kernel counters (tools/b3bench.py 16 GiB): instruction mix, VALUBusy, the held clock
+    cd /tmp && export TMPDIR=/tmp
+    i=0
+    for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" \
+                "VALUBusy GRBM_GUI_ACTIVE"; do
+      i=$((i+1))
+      timeout -s KILL 150 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/b3pmc/p$i -o run -- \
+        python3 $R/tools/b3bench.py 16 2 > $OUT/b3pmc_p$i.log 2>&1 || { echo "b3 pmc pass $i rc=$?"; exit 1; }
+    done
+    cd $R
+    echo b3pmc done ;;
   calib)  # FETCH_SIZE of the scan (tools/scanbench prod) against the bare load pattern (quadread)
     cd /tmp && export TMPDIR=/tmp
     for mode in quadread prod; do
