@@ -299,6 +299,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
   uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0;
   zs::RepHist R{{0, 0, 0}, 0};
   uint32_t run_src = 0, run_len = 0, run_dst = 0;  // this lane's pending literal run
+  uint64_t my_seq = 0;                             // and its sequence (stored 64 at a time)
   // 64 bytes of each lane's run per step: four 16-byte loads in flight, then
   // byte stores
   auto flush_runs = [&]() {
@@ -379,11 +380,14 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
         run_src = lit0;
         run_len = pos - lit0;
         run_dst = nlit;
-        sq[nseq] = sv;
+        my_seq = sv;
       }
       nlit += pos - lit0;
       ++nseq;
-      if ((nseq & 63) == 0) flush_runs();
+      if ((nseq & 63) == 0) {  // 64 sequences: one coalesced store, then their literal runs
+        sq[nseq - 64 + lane] = my_seq;
+        flush_runs();
+      }
       cur = pos + ml;
       lit0 = cur;
     }
@@ -399,6 +403,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
     load_win(wb + 256, nv);
   }
   if (nseq) {  // (no sequence: the block is stored raw from the input, nothing to stage)
+    if (lane < (nseq & 63)) sq[(nseq & ~63u) + lane] = my_seq;
     flush_runs();
     wave_copy(lit + nlit, p0 + lit0, end - lit0, lane);
     nlit += end - lit0;

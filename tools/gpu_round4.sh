@@ -65,7 +65,7 @@ for stage in "$@"; do
     i=0
     for ctrs in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES GRBM_GUI_ACTIVE" \
                 "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
-                "FETCH_SIZE WRITE_SIZE"; do
+                "FETCH_SIZE" "WRITE_SIZE"; do
       i=$((i+1))
       timeout -s KILL 150 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/zc_pmc/p$i -o run -- \
         python3 $R/tools/zc_bench.py 1 1 text > $OUT/zc_pmc_p$i.log 2>&1 || { echo "zc pmc pass $i rc=$?"; exit 1; }
