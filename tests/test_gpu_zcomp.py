@@ -124,24 +124,28 @@ def test_edge_lengths_offsets_overlaps(ctx):
 
 def test_long_chunks_segments_and_reach(ctx):
     """Chunks longer than one match-finder segment (8 blocks, 256 KiB): the
-    segment after the first re-inserts the 64 KiB before it, matches reach back
-    at most 65535 bytes (16-bit table positions, the offset check), long
-    matches (extended past the 16 verified bytes) across segment starts, an
-    8 MiB chunk; every frame decodes, and repeats within the reach compress."""
+    segment after the first re-inserts the 128 KiB before it, long matches
+    (extended past the 16 verified bytes) across segment starts, repeats 70 000
+    bytes apart (found across segment starts through the re-inserted bytes), a
+    2 MiB period (beyond the 2^20 window: never referenced), an 8 MiB chunk;
+    every frame decodes within the 2^20 window."""
     rng = np.random.default_rng(12)
     blk = O.random_bytes(40_000, 3)
     per = np.tile(blk, 60)[:2_000_000]  # period 40 000 < 64 KiB: everything after the first period matches
-    far = np.concatenate([O.random_bytes(70_000, 4)] * 10)  # period 70 000 > reach: incompressible
+    far = np.concatenate([O.random_bytes(70_000, 4)] * 10)  # period 70 000: within the re-inserted 128 KiB
+    beyond = np.concatenate([O.random_bytes(2 << 20, 6)] * 2)  # period 2 MiB > the window
     big = np.concatenate([_text(4 << 20, 8), O.random_bytes(1 << 20, 9), np.zeros(3 << 20, np.uint8)])
-    data = np.concatenate([per, far, big, _data("binary", 3 << 20, 2)])
-    offs = np.array([0, per.size, per.size + far.size, per.size + far.size + big.size], np.uint64)
-    lens = np.array([per.size, far.size, big.size, data.size - int(offs[3])], np.uint64)
+    parts = [per, far, big, _data("binary", 3 << 20, 2), beyond]
+    data = np.concatenate(parts)
+    offs = np.cumsum([0] + [x.size for x in parts[:-1]]).astype(np.uint64)
+    lens = np.array([x.size for x in parts], np.uint64)
     ch = np.zeros(len(offs), dtype=_lib.CHUNK_DTYPE)
     ch["offset"], ch["length"] = offs, lens
     fr, out, nbytes = _compress(ctx, data, ch)
     _check_frames(data, ch, fr, out, nbytes)
     assert int(fr[0, 1]) < per.size // 40  # the periodic chunk: matches across every segment start
-    assert int(fr[1, 1]) > far.size * 0.99  # beyond the reach: stored raw
+    assert int(fr[1, 1]) < far.size // 5
+    assert int(fr[4, 1]) > beyond.size * 0.99  # beyond the window: stored raw
     del rng
 
 
