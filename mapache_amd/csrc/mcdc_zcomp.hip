@@ -285,7 +285,7 @@ __device__ __forceinline__ uint64_t sel4(uint32_t j, uint64_t a, uint64_t b, uin
 // readlane.  Literal runs are copied 64 at a time: lane (k mod 64) keeps run
 // k's source, length and destination, and the wave copies the 64 runs
 // together.
-__global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *blocks, uint64_t nblk,
+__global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
                                                  const uint32_t *words, uint8_t *stage, uint64_t *seqs) {
   const uint64_t bi = blockIdx.x;
   if (bi >= nblk) return;
@@ -364,14 +364,23 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, ZcBlock *b
       const uint32_t wd = (uint32_t)__builtin_amdgcn_readlane((int)sel4(j, v[0], v[1], v[2], v[3]), (int)i);
       uint32_t ml = wd >> 24;
       const uint32_t off = wd & 0xFFFFFFu;
-      if (ml == kMlCap) {  // extend 64 bytes per step: lane k compares byte pos + ml + k
+      if (ml == kMlCap) {  // extend 1 KiB per step: lane k compares bytes [pos + ml + 16 k, + 16)
         for (;;) {
-          const uint32_t q = pos + ml + lane;
-          // (the source may lie in an earlier block of the chunk: p0 - off + q, signed)
-          const bool same = q < end && p0[q] == p0[(int64_t)q - (int64_t)off];
-          const uint64_t diff = __ballot(!same);
-          ml += diff ? (uint32_t)__builtin_ctzll(diff) : 64u;
-          if (diff) break;
+          const uint32_t q = pos + ml + 16 * lane;
+          uint32_t m = 0;
+          if (q < end) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
+            const uint64_t g = B.src + q;
+            const uint4 a = fix16(ld16c(base, g, nbytes), g, nbytes),
+                        b = fix16(ld16c(base, g - off, nbytes), g - off, nbytes);
+            m = min(prefix16(a, b), end - q);
+          }
+          const uint64_t brk = __ballot(m < 16);
+          if (brk) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(brk);
+            ml += 16 * i + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)i);
+            break;
+          }
+          ml += 1024;
         }
       }
       // repeat codes (the block's own history: rep_code), wave-uniform
@@ -955,7 +964,8 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
   hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindTile), 0, st, base, nbytes, blocks, nblk, words);
-  hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, words, stage, seqs);
+  hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
+                     seqs);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, words);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, T, piece);
   size_t b = tmp_bytes;

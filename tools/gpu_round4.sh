@@ -50,6 +50,15 @@ for stage in "$@"; do
     timeout -k 10 300 python -u tools/zc_bench.py 2 3 > $OUT/zc_bench.json 2> $OUT/zc_bench.err \
       || { echo "zc bench rc=$?"; tail -20 $OUT/zc_bench.err; exit 1; }
     cat $OUT/zc_bench.json ;;
+  zcab)  # tools/zc_bench.py with each abship/*.so variant beside the product library (2 GiB text, binary)
+    timeout -k 10 200 python -u tools/zc_bench.py 2 3 text,binary > $OUT/zcab_product.json 2>&1 || { echo "zcab product rc=$?"; exit 1; }
+    echo "product $(cat $OUT/zcab_product.json)"
+    for so in abship/*.so; do
+      b=$(basename $so .so)
+      MCDC_LIBRARY=$R/$so timeout -k 10 200 python -u tools/zc_bench.py 2 3 text,binary > $OUT/zcab_$b.json 2>&1 \
+        || { echo "zcab $b rc=$?"; exit 1; }
+      echo "$b $(cat $OUT/zcab_$b.json)"
+    done ;;
   zcstats)  # kernel trace + stats of the compressor only (1 GiB of text and of binary)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/zc_stats -o zc --output-format csv -- \
