@@ -22,12 +22,13 @@
 //                verified on 16 bytes, a tile later (its loads in flight
 //                meanwhile); per position one word (match length <= 16 << 24
 //                | offset, 0 = none) to scratch
-//   k_zc_parse   ONE WAVE PER BLOCK: greedy parse over the words, 256
-//                positions per window (4 ballots of "has a match"), the next
-//                match found with scalar bit scans; a match of 16 bytes is
-//                extended 64 bytes per step; repeat codes where an offset
-//                repeats one the block set; literals to the block's staging
-//                slot (64 runs copied at a time), sequences to scratch
+//   k_zc_parse   ONE WAVE PER BLOCK: the greedy parse over the words, 256
+//                positions per window without a serial walk: the chain from
+//                the cursor by pointer doubling in LDS, its matches, literal
+//                lengths and indices by wave scans; a match of 16 verified
+//                bytes on the chain extended 1 KiB per step; repeat code 1
+//                for an offset equal to the previous sequence's; literals to
+//                the block's staging slot, sequences to scratch
 //   k_zc_huff    ONE WAVE PER BLOCK: the block's literals (all of a block
 //                without matches) as a Huffman-coded (or RLE) literals
 //                section when smaller than raw: histogram of the 256 byte
@@ -253,175 +254,6 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   verify(s1);
 }
 
-// Copy bytes [a, a + n) of src to dst, the whole wave (64 lanes) together,
-// four bytes per lane per round loaded before any is stored.
-__device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint32_t n,
-                                          uint32_t lane) {
-  for (uint32_t k0 = 0; k0 < n; k0 += 256) {
-    uint8_t b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t k = k0 + 64 * j + lane;
-      b[j] = k < n ? src[k] : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t k = k0 + 64 * j + lane;
-      if (k < n) dst[k] = b[j];
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  return j == 0 ? a : j == 1 ? b : j == 2 ? c : d;
-}
-__device__ __forceinline__ uint64_t sel4(uint32_t j, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
-  return j == 0 ? a : j == 1 ? b : j == 2 ? c : d;
-}
-
-// The greedy parse of one block over k_zc_find's words: a window of 256
-// positions' words (4 per lane) and their "has a match" ballots; the next
-// match at or after the cursor by scalar bit scans; the match's word by
-// readlane.  Literal runs are copied 64 at a time: lane (k mod 64) keeps run
-// k's source, length and destination, and the wave copies the 64 runs
-// together.
-__global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
-                                                 const uint32_t *words, uint8_t *stage, uint64_t *seqs) {
-  const uint64_t bi = blockIdx.x;
-  if (bi >= nblk) return;
-  const uint32_t lane = lane_id();
-  const ZcBlock B = blocks[bi];
-  const uint32_t end = B.len;
-  const uint8_t *p0 = base + B.src;
-  const uint32_t *w = words + bi * kZcBlock;
-  uint8_t *lit = stage + bi * kZcSlot + zs::kLitHdr;
-  uint64_t *sq = seqs + bi * kZcSeqCap;
-  uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0;
-  zs::RepHist R{{0, 0, 0}, 0};
-  uint32_t run_src = 0, run_len = 0, run_dst = 0;  // this lane's pending literal run
-  uint64_t my_seq = 0;                             // and its sequence (stored 64 at a time)
-  // 64 bytes of each lane's run per step: four 16-byte loads in flight, then
-  // byte stores
-  auto flush_runs = [&]() {
-    uint32_t mx = run_len;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
-    for (uint32_t k0 = 0; k0 < mx; k0 += 64) {
-      uint4 q[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t k = k0 + 16 * j;
-        q[j] = make_uint4(0, 0, 0, 0);
-        if (k < run_len) {
-          if (run_src + k + 16 <= end) {
-            q[j] = *reinterpret_cast<const uint4 *>(p0 + run_src + k);
-          } else {  // (the block's last bytes: no read past them)
-            uint32_t b[4] = {0, 0, 0, 0};
-            for (uint32_t i = 0; i < 16 && run_src + k + i < end; ++i) b[i >> 2] |= (uint32_t)p0[run_src + k + i] << (8 * (i & 3));
-            q[j] = make_uint4(b[0], b[1], b[2], b[3]);
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t k = k0 + 16 * j;
-        if (k < run_len) {
-          const uint32_t n = run_len - k < 16 ? run_len - k : 16;
-          const uint32_t b[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-          uint8_t *d = lit + run_dst + k;
-#pragma unroll
-          for (uint32_t i = 0; i < 16; ++i)
-            if (i < n) d[i] = (uint8_t)(b[i >> 2] >> (8 * (i & 3)));
-        }
-      }
-    }
-    run_len = 0;
-  };
-  auto load_win = [&](uint32_t wb, uint32_t *v) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t q = wb + 64 * j + lane;
-      v[j] = q < end ? w[q] : 0u;
-    }
-  };
-  uint32_t wb = 0, v[4], nv[4];
-  load_win(0, v);
-  load_win(256, nv);
-  while (wb < end) {
-    const uint64_t m0 = __ballot(v[0] != 0), m1 = __ballot(v[1] != 0), m2 = __ballot(v[2] != 0),
-                   m3 = __ballot(v[3] != 0);
-    while (cur < wb + 256) {  // the matches of this window, in order
-      const uint32_t rel = cur - wb;
-      uint32_t j = rel >> 6;
-      uint64_t mm = sel4(j, m0, m1, m2, m3) & (~0ull << (rel & 63));
-      while (!mm && ++j < 4) mm = sel4(j, m0, m1, m2, m3);
-      if (!mm) {
-        cur = wb + 256;
-        break;
-      }
-      const uint32_t i = (uint32_t)__builtin_ctzll(mm);
-      const uint32_t pos = wb + 64 * j + i;
-      const uint32_t wd = (uint32_t)__builtin_amdgcn_readlane((int)sel4(j, v[0], v[1], v[2], v[3]), (int)i);
-      uint32_t ml = wd >> 24;
-      const uint32_t off = wd & 0xFFFFFFu;
-      if (ml == kMlCap) {  // extend 1 KiB per step: lane k compares bytes [pos + ml + 16 k, + 16)
-        for (;;) {
-          const uint32_t q = pos + ml + 16 * lane;
-          uint32_t m = 0;
-          if (q < end) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
-            const uint64_t g = B.src + q;
-            const uint4 a = fix16(ld16c(base, g, nbytes), g, nbytes),
-                        b = fix16(ld16c(base, g - off, nbytes), g - off, nbytes);
-            m = min(prefix16(a, b), end - q);
-          }
-          const uint64_t brk = __ballot(m < 16);
-          if (brk) {
-            const uint32_t i = (uint32_t)__builtin_ctzll(brk);
-            ml += 16 * i + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)i);
-            break;
-          }
-          ml += 1024;
-        }
-      }
-      // repeat codes (the block's own history: rep_code), wave-uniform
-      const uint64_t sv = zs::rep_code(R, zs::seq_pack(pos - lit0, ml, off));
-      if (lane == (nseq & 63)) {
-        run_src = lit0;
-        run_len = pos - lit0;
-        run_dst = nlit;
-        my_seq = sv;
-      }
-      nlit += pos - lit0;
-      ++nseq;
-      if ((nseq & 63) == 0) {  // 64 sequences: one coalesced store, then their literal runs
-        sq[nseq - 64 + lane] = my_seq;
-        flush_runs();
-      }
-      cur = pos + ml;
-      lit0 = cur;
-    }
-    // the next window: the prefetched one, or (after a long match) the cursor's
-    const uint32_t nb = cur & ~63u;
-    if (nb == wb + 256) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = nv[j];
-    } else {
-      load_win(nb, v);
-    }
-    wb = nb;
-    load_win(wb + 256, nv);
-  }
-  if (nseq) {  // (no sequence: the block is stored raw from the input, nothing to stage)
-    if (lane < (nseq & 63)) sq[(nseq & ~63u) + lane] = my_seq;
-    flush_runs();
-    wave_copy(lit + nlit, p0 + lit0, end - lit0, lane);
-    nlit += end - lit0;
-  }
-  if (lane == 0) {
-    blocks[bi].nlit = nlit;
-    blocks[bi].nseq = nseq;
-  }
-}
 
 // Inclusive sum over the wave's 64 lanes.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
@@ -432,6 +264,175 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
   }
   return v;
 }
+// Inclusive max over the wave's 64 lanes (values >= -1).
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const int32_t t = __shfl_up(v, d);
+    if (lane >= d) v = max(v, t);
+  }
+  return v;
+}
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
+  return v;
+}
+
+// The greedy parse of one block over k_zc_find's words, 256 positions per
+// window (position i of the window in lane i % 64, slot i / 64), without a
+// serial walk: every position's successor (+ its match length, or + 1 for a
+// literal) is known from its word, so the chain from the cursor is found by
+// pointer doubling in LDS (J_k = the 2^k-th successor, 8 levels; marking
+// S_{k+1} = S_k + J_k(S_k) from the cursor), and the chain's matches,
+// literals, literal lengths (an exclusive max-scan of match ends) and
+// sequence / literal indices (prefix counts of ballots) follow by wave scans.
+// A match of 16 verified bytes on the chain is extended (1 KiB per wave step)
+// and ends the window there.  Offsets repeat as repeat code 1 (the previous
+// sequence's offset, literal length > 0: rep[0] is always the previous
+// offset when only that code is used) after the block's first sequence.
+__global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
+                                                 const uint32_t *words, uint8_t *stage, uint64_t *seqs) {
+  __shared__ uint16_t J[8][257];
+  __shared__ uint8_t mk[260];
+  __shared__ uint32_t offl[256];
+  const uint64_t bi = blockIdx.x;
+  if (bi >= nblk) return;
+  const uint32_t lane = lane_id();
+  const ZcBlock B = blocks[bi];
+  const uint32_t end = B.len;
+  const uint8_t *p0 = base + B.src;
+  const uint32_t *w = words + bi * kZcBlock;
+  uint8_t *lit = stage + bi * kZcSlot + zs::kLitHdr;
+  uint64_t *sq = seqs + bi * kZcSeqCap;
+  uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0, last_off = 0;  // (last_off 0: no sequence yet)
+  if (lane == 0) {
+    for (int k = 0; k < 8; ++k) J[k][256] = 256;
+  }
+  uint32_t nwd[4];
+  auto load_win = [&](uint32_t wb, uint32_t *v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t q = wb + 64 * j + lane;
+      v[j] = q < end ? w[q] : 0u;
+    }
+  };
+  uint32_t nwb = 0;
+  load_win(0, nwd);
+  while (cur < end) {
+    const uint32_t wb = cur & ~63u, s0 = cur - wb;
+    uint32_t wd[4];
+    if (wb == nwb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wd[j] = nwd[j];
+    } else {
+      load_win(wb, wd);
+    }
+    nwb = wb + 256;
+    load_win(nwb, nwd);  // (the next window's words, in flight meanwhile)
+    uint32_t ml[4], nx[4];
+    bool valid[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane;
+      valid[j] = wb + i < end;
+      ml[j] = wd[j] >> 24;
+      nx[j] = valid[j] ? i + (ml[j] ? ml[j] : 1u) : 0x7FFFFFFFu;
+      J[0][i] = (uint16_t)min(nx[j], 256u);
+      offl[i] = wd[j] & 0xFFFFFFu;
+      mk[i] = (uint8_t)(i == s0);
+    }
+    for (int k = 0; k < 7; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        J[k + 1][i] = J[k][J[k][i]];
+      }
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        if (mk[i]) mk[J[k][i]] = 1;
+      }
+    bool node[4], mt[4];
+    uint64_t bc[4];
+    int32_t cap_first = 0x7FFFFFFF;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane;
+      node[j] = valid[j] && mk[i];
+      mt[j] = node[j] && ml[j] != 0;
+      bc[j] = __ballot(mt[j] && ml[j] == kMlCap);
+      if (cap_first == 0x7FFFFFFF && bc[j]) cap_first = 64 * j + (int32_t)__builtin_ctzll(bc[j]);
+    }
+    uint32_t L = 255, mlt = 0;  // nodes <= L are this window's; the capped match at L (if any) is mlt long
+    if (cap_first != 0x7FFFFFFF) {  // extend it (1 KiB per step: lane k compares bytes [.. + 16 k, + 16))
+      L = (uint32_t)cap_first;
+      const uint32_t pos = wb + L, off = offl[L];
+      mlt = kMlCap;
+      for (;;) {
+        const uint32_t q = pos + mlt + 16 * lane;
+        uint32_t m = 0;
+        if (q < end) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
+          const uint64_t g = B.src + q;
+          const uint4 x = fix16(ld16c(base, g, nbytes), g, nbytes), y = fix16(ld16c(base, g - off, nbytes), g - off, nbytes);
+          m = min(prefix16(x, y), end - q);
+        }
+        const uint64_t brk = __ballot(m < 16);
+        if (brk) {
+          const uint32_t t = (uint32_t)__builtin_ctzll(brk);
+          mlt += 16 * t + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)t);
+          break;
+        }
+        mlt += 1024;
+      }
+    }
+    // this window's matches and literals, in position order (slot-major)
+    uint32_t mcount = 0, lcount = 0;
+    int32_t pend = -1, pidx = -1;  // running exclusive max-scans: end / index of the previous match
+    uint32_t exit_pos = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane, q = wb + i;
+      const bool in = node[j] && i <= L, m = in && mt[j], l = in && !mt[j];
+      const uint32_t mlen = (i == L && mlt) ? mlt : ml[j];
+      const uint64_t bm = __ballot(m), bl = __ballot(l);
+      const uint32_t mr = mcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      const uint32_t lr = lcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+      // exclusive scans over this slot's lanes, carried from the earlier slots
+      const int32_t ie = wave_incl_max(m ? (int32_t)(q + mlen) : -1, lane), ii = wave_incl_max(m ? (int32_t)i : -1, lane);
+      int32_t pe = __shfl_up(ie, 1), pi = __shfl_up(ii, 1);
+      if (lane == 0) pe = pi = -1;
+      pe = max(pe, pend);
+      pi = max(pi, pidx);
+      if (m) {
+        const uint32_t start = pe >= 0 ? (uint32_t)pe : lit0;
+        const uint32_t ll = q - start, off = offl[i];
+        const uint32_t poff = pi >= 0 ? offl[pi] : last_off;
+        const uint32_t ov = (ll && off == poff) ? 1u : off + 3;
+        sq[nseq + mr] = zs::seq_pack_ov(ll, mlen, ov);
+      }
+      if (l) lit[nlit + lr] = p0[q];
+      pend = max(pend, __shfl(ie, 63));
+      pidx = max(pidx, __shfl(ii, 63));
+      mcount += (uint32_t)__builtin_popcountll(bm);
+      lcount += (uint32_t)__builtin_popcountll(bl);
+      if (in) exit_pos = max(exit_pos, q + (m ? mlen : 1u));
+    }
+    nseq += mcount;
+    nlit += lcount;
+    if (pidx >= 0) {
+      lit0 = (uint32_t)pend;
+      last_off = offl[pidx];
+    }
+    cur = (uint32_t)wave_max((int32_t)exit_pos);
+  }
+  if (lane == 0) {
+    blocks[bi].nlit = nlit;
+    blocks[bi].nseq = nseq;
+  }
+}
+
 
 // The literals section of a compressed block: Huffman-coded or RLE when that
 // is smaller than the raw section (3-byte header + the literals), written
