@@ -70,10 +70,10 @@ using namespace zs;
 // 1 % on records and binary).
 constexpr uint32_t kHsLog = 15, kHlLog = 13;
 #ifndef MCDC_ZC_TILE
-#define MCDC_ZC_TILE 256  // (compile-time A/B knob)
+#define MCDC_ZC_TILE 512  // (compile-time A/B knob)
 #endif
 constexpr uint32_t kFindTile = MCDC_ZC_TILE;  // positions per step = threads per workgroup
-constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
+constexpr uint32_t kMlCap = 64;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
 
 __device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
@@ -197,17 +197,28 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   struct Stage {
     bool v, ks, kl;
     uint32_t p, qs, ql;
-    uint4 x, ys, yl;
+    uint4 x[4], ys[4], yl[4];  // 64 bytes at the position and at each candidate
   };
   Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
   uint4 n0 = ld16c(cb, prime0 + tid, cbytes), n1 = ld16c(cb, prime0 + kFindTile + tid, cbytes);
   // position S.p: its word (a position that is not the segment's writes to
   // a spare word past the batch's: no branch around the store, see step)
+  auto prefix64 = [&](const uint4 *x, const uint4 *y, uint32_t px, uint32_t py) {  // (selects only)
+    uint32_t m = 0;
+    bool go = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t t = prefix16(fix16(x[k], px + 16 * k, cbytes), fix16(y[k], py + 16 * k, cbytes));
+      m += go ? t : 0u;
+      go = go && t == 16;
+    }
+    return m;
+  };
   auto verify = [&](const Stage &S) {
     const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
     const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
-    const uint4 ys = fix16(S.ys, S.qs, cbytes), yl = fix16(S.yl, S.ql, cbytes);
-    const uint32_t ms = S.ks ? min(prefix16(S.x, ys), lim) : 0u, ml = S.kl ? min(prefix16(S.x, yl), lim) : 0u;
+    const uint32_t ms = S.ks ? min(prefix64(S.x, S.ys, S.p, S.qs), lim) : 0u,
+                   ml = S.kl ? min(prefix64(S.x, S.yl, S.p, S.ql), lim) : 0u;
     const uint32_t ds = S.p - S.qs, dl = S.p - S.ql;
     uint32_t m = 0, d = 0;
     if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
@@ -236,9 +247,12 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     S.p = p;
     S.qs = qs;
     S.ql = ql;
-    S.x = x;
-    S.ys = ld16c(cb, qs, cbytes);
-    S.yl = ld16c(cb, ql, cbytes);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      S.ys[k] = ld16c(cb, qs + 16 * k, cbytes);
+      S.yl[k] = ld16c(cb, ql + 16 * k, cbytes);
+      S.x[k] = k ? ld16c(cb, p + 16 * k, cbytes) : n;  // (the first 16 as loaded: verify realigns)
+    }
     n = ld16c(cb, p + 2 * kFindTile, cbytes);
     lds_sync();  // every lookup of the tile before any insert
     if (vs) atomicMax(hts + hs, p + 1);
