@@ -73,7 +73,7 @@ constexpr uint32_t kHsLog = 15, kHlLog = 13;
 #define MCDC_ZC_TILE 512  // (compile-time A/B knob)
 #endif
 constexpr uint32_t kFindTile = MCDC_ZC_TILE;  // positions per step = threads per workgroup
-constexpr uint32_t kMlCap = 64;               // match bytes verified per candidate (longer: k_zc_parse extends)
+constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
 
 __device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
@@ -197,28 +197,17 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   struct Stage {
     bool v, ks, kl;
     uint32_t p, qs, ql;
-    uint4 x[4], ys[4], yl[4];  // 64 bytes at the position and at each candidate
+    uint4 x, ys, yl;
   };
   Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
   uint4 n0 = ld16c(cb, prime0 + tid, cbytes), n1 = ld16c(cb, prime0 + kFindTile + tid, cbytes);
   // position S.p: its word (a position that is not the segment's writes to
   // a spare word past the batch's: no branch around the store, see step)
-  auto prefix64 = [&](const uint4 *x, const uint4 *y, uint32_t px, uint32_t py) {  // (selects only)
-    uint32_t m = 0;
-    bool go = true;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t t = prefix16(fix16(x[k], px + 16 * k, cbytes), fix16(y[k], py + 16 * k, cbytes));
-      m += go ? t : 0u;
-      go = go && t == 16;
-    }
-    return m;
-  };
   auto verify = [&](const Stage &S) {
     const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
     const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
-    const uint32_t ms = S.ks ? min(prefix64(S.x, S.ys, S.p, S.qs), lim) : 0u,
-                   ml = S.kl ? min(prefix64(S.x, S.yl, S.p, S.ql), lim) : 0u;
+    const uint4 ys = fix16(S.ys, S.qs, cbytes), yl = fix16(S.yl, S.ql, cbytes);
+    const uint32_t ms = S.ks ? min(prefix16(S.x, ys), lim) : 0u, ml = S.kl ? min(prefix16(S.x, yl), lim) : 0u;
     const uint32_t ds = S.p - S.qs, dl = S.p - S.ql;
     uint32_t m = 0, d = 0;
     if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
@@ -247,12 +236,9 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     S.p = p;
     S.qs = qs;
     S.ql = ql;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      S.ys[k] = ld16c(cb, qs + 16 * k, cbytes);
-      S.yl[k] = ld16c(cb, ql + 16 * k, cbytes);
-      S.x[k] = k ? ld16c(cb, p + 16 * k, cbytes) : n;  // (the first 16 as loaded: verify realigns)
-    }
+    S.x = x;
+    S.ys = ld16c(cb, qs, cbytes);
+    S.yl = ld16c(cb, ql, cbytes);
     n = ld16c(cb, p + 2 * kFindTile, cbytes);
     lds_sync();  // every lookup of the tile before any insert
     if (vs) atomicMax(hts + hs, p + 1);
@@ -703,11 +689,13 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
 //            (count | value << 4, 16 bits each) to scratch
 //   offsets  per sequence its bits (state bits + extra bits) and, by wave
 //            scans in writing order (last sequence first), its bit offset
-//   write    the section zeroed, every sequence's bits OR-ed into place by
-//            its lane (global atomics), then the final states, the end mark
-//            and the header (count, modes, descriptions) by lane 0
+//   write    64 sequences at a time: each lane ORs its sequence's bits into
+//            an LDS buffer (LDS atomics), the buffer's whole words go out
+//            with plain stores, the partial last word carries over; then the
+//            final states, the end mark and the header (count, modes,
+//            descriptions) by lane 0
 // The block stays raw when the compressed block is not smaller.
-__device__ __forceinline__ void or_bits(uint32_t *w, uint64_t bit, uint64_t lo, uint64_t hi, uint32_t nbits) {
+__device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint64_t lo, uint64_t hi, uint32_t nbits) {
   // bits [bit, bit + nbits) of a little-endian stream of 32-bit words = the
   // low nbits of hi:lo (nbits <= 96)
   const uint32_t sh = (uint32_t)(bit & 31);
@@ -727,6 +715,8 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   __shared__ FseCTL tb[3];  // the block's LL, OF, ML tables (own or predefined)
   __shared__ SeqPlan P;
   __shared__ uint32_t hist[3][53], cum[54], seen[54];
+  constexpr uint32_t kWbWords = 64 * 96 / 32 + 4;  // a batch's bits + the carried word
+  __shared__ uint32_t wb[kWbWords];
   const uint32_t lane = lane_id();
   const uint64_t bi = blockIdx.x;
   if (bi == 0 && lane == 0) piece[nblk] = 0;
@@ -814,7 +804,6 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
       const uint32_t pre_bits = (uint32_t)((uintptr_t)bs0 & 3) * 8;  // stream bit 0 inside the first word
       uint32_t *w0 = reinterpret_cast<uint32_t *>((uintptr_t)bs0 & ~(uintptr_t)3);
       // bits per sequence and offsets (writing order: the last sequence first)
-      uint64_t base_bits = 0;
       const uint32_t tl0 = tb[0].log, tl1 = tb[1].log, tl2 = tb[2].log;
       // first pass: the total, to size the zeroing and the raw / compressed choice
       uint64_t tot = 0;
@@ -830,14 +819,20 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
       const uint32_t nbytes = (uint32_t)((all_bits + 7) / 8);
       const uint32_t total = at + hsz + nbytes;
       if (total < B.len) {
-        // zero the stream: its head bytes up to the next word boundary one by
-        // one (the bytes before it in that word are the header's, or the
-        // literals' when the header is short), whole words after
-        const uint32_t head = pre_bits ? 4 - pre_bits / 8 : 0u;
-        if (lane < head) bs0[lane] = 0;
-        const uint32_t nw = ((uint32_t)all_bits + 31) / 32 + 1;
-        for (uint32_t k = lane; k < nw; k += 64) w0[(pre_bits ? 1 : 0) + k] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        // the bitstream, 64 sequences at a time: their bits OR-ed into an LDS
+        // buffer (the batch is at most 64 x 96 bits), then its whole words
+        // stored to the slot with plain stores; the last partial word carries
+        // over.  The first word keeps the bytes before the stream (the
+        // header's, written last, or the literals' when the header is short).
+        uint32_t carry = w0[0] & (pre_bits ? (1u << pre_bits) - 1u : 0u);  // (wave-uniform load)
+        uint32_t cbits = pre_bits, wi = 0;  // bits in carry; index of carry's word
+        auto flush = [&](uint32_t tbits) {  // tbits new bits in wb[] after the carry; whole words out
+          const uint32_t nwords = (cbits + tbits) >> 5;
+          for (uint32_t k = lane; k < nwords; k += 64) w0[wi + k] = wb[k];
+          carry = wb[nwords];
+          cbits = (cbits + tbits) & 31;
+          wi += nwords;
+        };
         for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) {
           const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
           const int32_t i = b1 - 1 - (int32_t)lane;  // lane 0 the batch's last sequence (written first)
@@ -866,25 +861,38 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
             put(mb, ml_bits(mlc));
             put(ob, ofc);
           }
-          uint64_t incl = nb;  // inclusive prefix in lane order = writing order
+          uint32_t incl = nb;  // inclusive prefix in lane order = writing order
 #pragma unroll
           for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint64_t t = (uint64_t)__shfl_up((long long)incl, d);
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, d);
             if (lane >= d) incl += t;
           }
-          if (nb) or_bits(w0, pre_bits + base_bits + incl - nb, lo, hi, nb);
-          base_bits += (uint64_t)__shfl((long long)incl, 63);
+          const uint32_t tbits = (uint32_t)__shfl((int)incl, 63);
+          for (uint32_t k = lane; k < kWbWords; k += 64) wb[k] = 0;
+          if (lane == 0) wb[0] = carry;
+          __syncthreads();
+          if (nb) or_bits(wb, cbits + incl - nb, lo, hi, nb);
+          __syncthreads();
+          flush(tbits);
+          __syncthreads();
         }
-        // final states (ML, OF, LL: log bits each) and the end mark, lane 0
+        // final states (ML, OF, LL: log bits each), the end mark, the last words
         const uint32_t fs = state;  // lanes 0-2: the final states of LL, OF, ML
         const uint32_t f0 = (uint32_t)__shfl((int)fs, 0), f1 = (uint32_t)__shfl((int)fs, 1),
                        f2 = (uint32_t)__shfl((int)fs, 2);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-        if (lane == 0) {
+        {
+          const uint32_t fb = tl2 + tl1 + tl0 + 1;
           const uint64_t v = (uint64_t)(f2 & ((1u << tl2) - 1)) | (uint64_t)(f1 & ((1u << tl1) - 1)) << tl2 |
                              (uint64_t)(f0 & ((1u << tl0) - 1)) << (tl2 + tl1) | 1ull << (tl2 + tl1 + tl0);
-          or_bits(w0, pre_bits + base_bits, v, 0, tl2 + tl1 + tl0 + 1);
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+          if (lane < 4) wb[lane] = lane ? 0u : carry;
+          __syncthreads();
+          if (lane == 0) or_bits(wb, cbits, v, 0, fb);
+          __syncthreads();
+          flush(fb);
+          if (lane == 0 && cbits) w0[wi] = carry;  // (the last, partial word)
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        if (lane == 0) {
           uint8_t *h = st + at;  // Number_of_Sequences, Symbol_Compression_Modes, descriptions
           if (cnt == 1) {
             h[0] = (uint8_t)ns;
