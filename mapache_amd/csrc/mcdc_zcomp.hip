@@ -68,7 +68,13 @@ using namespace zs;
 // 2^15 + 2^13 2.59 / 3.30 / 1.78; zstd level 3 2.68 / 3.23 / 1.78.  256
 // positions per tile cost < 0.5 % against exact most-recent insertion (512:
 // 1 % on records and binary).
-constexpr uint32_t kHsLog = 15, kHlLog = 13;
+#ifndef MCDC_ZC_HS
+#define MCDC_ZC_HS 15  // (compile-time A/B knobs)
+#endif
+#ifndef MCDC_ZC_HL
+#define MCDC_ZC_HL 13
+#endif
+constexpr uint32_t kHsLog = MCDC_ZC_HS, kHlLog = MCDC_ZC_HL;
 #ifndef MCDC_ZC_TILE
 #define MCDC_ZC_TILE 512  // (compile-time A/B knob)
 #endif
@@ -76,11 +82,18 @@ constexpr uint32_t kFindTile = MCDC_ZC_TILE;  // positions per step = threads pe
 constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
 
+// Keys hashed with 24-bit multiplies (full rate; a 32-bit multiply issues at
+// a quarter of it): the key cut into 24- and 16-bit pieces, each multiplied by
+// an odd 24-bit constant, the low 32 bits of the products mixed; the index is
+// the top bits, which every bit of a piece reaches.
+__device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t k) { return (uint32_t)__umul24(a, k); }  // (HIP's returns int)
 __device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
-  return (lo * 2654435761u + (hi & 0xFFu) * 0x85EBCA77u) >> (32 - kHsLog);
+  const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFu) << 8;
+  return (mul24(a, 0x9E3779u) + mul24(b, 0xC2B2AFu)) >> (32 - kHsLog);
 }
 __device__ __forceinline__ uint32_t hash8(uint32_t lo, uint32_t hi) {
-  return ((lo * 0x9E3779B1u) ^ (hi * 0x85EBCA77u) ^ ((lo ^ hi) >> 15)) * 0xC2B2AE3Du >> (32 - kHlLog);
+  const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFFFu) << 8, c = hi >> 16;
+  return (mul24(a, 0x85EBCBu) ^ mul24(b, 0x27D4EBu) ^ mul24(c, 0x165667u)) >> (32 - kHlLog);
 }
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 // A workgroup barrier that orders LDS only: __syncthreads' workgroup fence
@@ -147,14 +160,41 @@ __device__ __forceinline__ uint4 fix16(uint4 x, uint64_t p, uint64_t nbytes) {
   return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
 }
 
+// Loads the compiler's wait-count pass does not see.  On gfx9 one counter
+// (vmcnt) covers loads and stores, and with a store pending the pass treats
+// the counter as out of order and waits for zero before any use of a load:
+// a loop that stores a result per step and prefetches two steps ahead gets
+// every prefetch drained at the next step.  The match finder issues its
+// loads here and waits itself (vm_wait*, counting only its own loads: loads
+// return in order, a store may retire early), each wait taking the loaded
+// registers as operands so that no use is scheduled before it.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 ald16c(const uint8_t *base, uint64_t p, uint64_t nbytes) {
+  const uint8_t *a = base + (p + 16 <= nbytes ? p : nbytes - 16);
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint4 to4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+// 16 bytes at base + p of the nbytes >= 16 readable there, bytes past the end zero.
+__device__ __forceinline__ u32x4 ld16z(const uint8_t *base, uint64_t p, uint64_t nbytes) {
+  const uint4 v = fix16(*reinterpret_cast<const uint4 *>(base + (p + 16 <= nbytes ? p : nbytes - 16)), p, nbytes);
+  return u32x4{v.x, v.y, v.z, v.w};
+}
+// (the same with a uniform base and a 32-bit offset: no 64-bit address math)
+__device__ __forceinline__ u32x4 ald16s(const uint8_t *sbase, uint32_t off) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(off), "s"(sbase) : "memory");
+  return v;
+}
+__device__ __forceinline__ void ast32s(uint32_t *sbase, uint32_t off, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, %2" ::"v"(off), "v"(v), "s"(sbase) : "memory");
+}
+
 // Common prefix of two 16-byte strings.
 __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
-  const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
-  uint32_t m = 16;
-#pragma unroll
-  for (int k = 3; k >= 0; --k)
-    if (d[k]) m = 4 * k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
-  return m;
+  const uint64_t d0 = (uint64_t)(x.y ^ y.y) << 32 | (x.x ^ y.x), d1 = (uint64_t)(x.w ^ y.w) << 32 | (x.z ^ y.z);
+  return d0 ? (uint32_t)__builtin_ctzll(d0) >> 3 : d1 ? 8u + ((uint32_t)__builtin_ctzll(d1) >> 3) : 16u;
 }
 
 // The match finder: one workgroup of kFindTile threads per segment (up to
@@ -181,47 +221,63 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   const uint32_t prime0 = seg0 > kPrime ? seg0 - kPrime : 0u;
   const uint8_t *cb = base + csrc;
   const uint64_t cbytes = nbytes - csrc;  // (bytes readable from the chunk start)
-  auto word_at = [&](uint32_t p) -> uint32_t * {
-    return words + (bi0 + (p / (uint32_t)kZcBlock - B0.b)) * kZcBlock + p % (uint32_t)kZcBlock;
-  };
+  // the segment's words: the chunk's blocks are consecutive records, so
+  // position p's word is wseg[p]; positions outside the segment keep nothing
+  uint32_t *wseg = words + (bi0 - B0.b) * kZcBlock;
   if (clen < 16 || cbytes < 16) {  // (too short to match: every position a literal)
-    for (uint32_t p = seg0 + tid; p < seg1; p += kFindTile) *word_at(p) = 0u;
+    for (uint32_t p = seg0 + tid; p < seg1; p += kFindTile) wseg[p] = 0u;
     return;
   }
   for (uint32_t k = tid; k < (1u << kHsLog) / 4; k += kFindTile) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
   for (uint32_t k = tid; k < (1u << kHlLog) / 4; k += kFindTile) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
+  // 16-byte loads at chunk offsets clamped to the last 16 readable bytes; a
+  // tile within 16 bytes of the end realigns them (fix16), others use them as loaded
+  const uint32_t last16 = (uint32_t)min<uint64_t>(cbytes - 16, 0xFFFFFFF0ull);
+  const uint64_t tail0 = cbytes >= kFindTile + 16 ? cbytes - (kFindTile + 16) : 0;  // tiles from here: the tail
   // Two tiles in flight: a tile's own bytes are requested two tiles ahead,
   // and its candidates' bytes are verified two tiles later (the counter
   // retires in order, so waiting for a tile's own bytes leaves the newer
   // requests in flight)
   struct Stage {
-    bool v, ks, kl;
+    bool v, ks, kl, tail;
     uint32_t p, qs, ql;
-    uint4 x, ys, yl;
+    uint4 x;
+    u32x4 ys, yl;
   };
   Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
-  uint4 n0 = ld16c(cb, prime0 + tid, cbytes), n1 = ld16c(cb, prime0 + kFindTile + tid, cbytes);
-  // position S.p: its word (a position that is not the segment's writes to
-  // a spare word past the batch's: no branch around the store, see step)
+  u32x4 n0 = ald16s(cb, min(prime0 + tid, last16)), n1 = ald16s(cb, min(prime0 + kFindTile + tid, last16));
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1)::"memory");
   auto verify = [&](const Stage &S) {
     const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
     const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
-    const uint4 ys = fix16(S.ys, S.qs, cbytes), yl = fix16(S.yl, S.ql, cbytes);
+    uint4 ys = to4(S.ys), yl = to4(S.yl);
+    if (S.tail) {
+      ys = fix16(ys, S.qs, cbytes);
+      yl = fix16(yl, S.ql, cbytes);
+    }
     const uint32_t ms = S.ks ? min(prefix16(S.x, ys), lim) : 0u, ml = S.kl ? min(prefix16(S.x, yl), lim) : 0u;
     const uint32_t ds = S.p - S.qs, dl = S.p - S.ql;
     uint32_t m = 0, d = 0;
     if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
     else if (ml >= zs::kMinMatch) m = ml, d = dl;
-    *(S.v ? word_at(S.p) : words + nblk * kZcBlock + tid) = m ? (m << 24 | d) : 0u;
+#ifdef MCDC_ZC_NOVERIFY
+    if (ds != ~0u) m = 0;
+#endif
+    if (S.v) ast32s(wseg, 4 * S.p, m ? (m << 24 | d) : 0u);
   };
   // one tile; n: its own bytes on entry, the bytes of the tile two ahead on
   // exit; S: the tile two back on entry (verified here), this tile on exit.
   // The loop below alternates two (n, S) sets, so no register with a pending
-  // load is ever copied (a copy would wait for the load)
-  auto step = [&](uint32_t t0, uint4 &n, Stage &S) {
+  // load is ever copied.  Per step the memory operations are: the verified
+  // word's store (or none), then the loads ys, yl, n; a step's loads are
+  // used two steps later, after the three loads of the step between (vmcnt(3)).
+  auto step = [&](uint32_t t0, u32x4 &n, Stage &S) {
+    asm volatile("s_waitcnt vmcnt(3)" : "+v"(n), "+v"(S.ys), "+v"(S.yl)::"memory");
     const uint32_t p = t0 + tid;
-    const uint4 x = fix16(n, p, cbytes);
-    const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert)
+    const bool tail = t0 >= tail0;
+    uint4 x = to4(n);
+    if (tail) x = fix16(x, p, cbytes);
+    const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert; tiles past the segment: nothing kept)
     const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
     const uint32_t hs = hash5(x.x, x.y), hl = hash8(x.x, x.y);
     const uint32_t cs = find && vs ? hts[hs] : 0u, cl = find && vl ? htl[hl] : 0u;
@@ -233,23 +289,34 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     S.v = find;
     S.ks = oks;
     S.kl = okl;
+    S.tail = tail;
     S.p = p;
     S.qs = qs;
     S.ql = ql;
     S.x = x;
-    S.ys = ld16c(cb, qs, cbytes);
-    S.yl = ld16c(cb, ql, cbytes);
-    n = ld16c(cb, p + 2 * kFindTile, cbytes);
+#ifdef MCDC_ZC_NOVERIFY  // (A/B: the finder without its candidate loads; no matches, see verify)
+    S.ys = S.yl = u32x4{qs, ql, ~0u, ~0u};
+    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+#else
+    S.ys = ald16s(cb, min(qs, last16));
+    S.yl = ald16s(cb, min(ql, last16));
+    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+#endif
     lds_sync();  // every lookup of the tile before any insert
     if (vs) atomicMax(hts + hs, p + 1);
     if (vl) atomicMax(htl + hl, p + 1);
     lds_sync();  // every insert before the next tile's lookups
   };
   __syncthreads();
+  // (both steps unconditional: a tile past the segment keeps nothing, and a
+  // join after a conditional step would cost the compiler's own waits)
   for (uint32_t t0 = prime0; t0 < seg1; t0 += 2 * kFindTile) {
     step(t0, n0, s0);
-    if (t0 + kFindTile < seg1) step(t0 + kFindTile, n1, s1);
+    step(t0 + kFindTile, n1, s1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(s0.ys), "+v"(s0.yl), "+v"(s1.ys), "+v"(s1.yl)::"memory");
   verify(s0);
   verify(s1);
 }
@@ -451,9 +518,10 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
 //            neighbouring piece OR-ed in)
 //   store    header, tree, jump table; the section copied to the slot
 // (LDS ~9 KiB per wave: 16 waves per CU; the section itself stays in HBM.)
-__global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                uint32_t *scratch) {
+__global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
+                                                uint8_t *stage, uint32_t *scratch) {
   __shared__ __attribute__((aligned(16))) uint32_t hist[4][256];
+  uint32_t *const ctw = hist[1];  // (after the counts are merged into hist[0])
   __shared__ HufCT ct;
   __shared__ HufWork hw;
   __shared__ uint8_t tdesc[132];
@@ -538,15 +606,46 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
   __syncthreads();
   const uint32_t tree = tree_sz;
   if (!tree) return;  // (no description applies: raw literals)
-  // bits per stream (stream k: literals [k seg, min((k + 1) seg, n)))
+  // code | length << 16 per symbol: one LDS read per literal
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const uint32_t x = lane + 64 * h;
+    ctw[x] = ct.nb[x] ? (uint32_t)ct.code[x] | (uint32_t)ct.nb[x] << 16 : 0u;
+  }
+  __syncthreads();
+  // Streams (stream k: literals [k seg, min((k + 1) seg, n))), each cut into
+  // 64 pieces in writing order (the last literal first): lane l's piece is
+  // the literals [e - w1, e - w0), w0 = l P, w1 = min(w0 + P, len), P <= 128,
+  // read with 16-byte loads into registers (bytes past what src holds read as
+  // zero) and walked from its last byte down.
   const bool one = n < 1024;
   const uint32_t seg = one ? n : (n + 3) / 4, ns = one ? 1 : 4;
-  uint32_t sb[4] = {0, 0, 0, 0};
+  const uint64_t lim = B.nseq ? (uint64_t)n + 64 : nbytes - B.src;  // bytes readable at src
+  auto piece = [&](uint32_t k, u32x4 *q, uint32_t &L, uint32_t &P) {
+    const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
+    P = (len + 63) / 64;
+    const uint32_t w0 = min(lane * P, len), w1 = min(w0 + P, len);
+    L = w1 - w0;
+    const uint32_t a0 = e - w1;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (16u * c < P) q[c] = ld16z(src, a0 + 16u * c, lim);
+  };
+  auto byte_at = [&](const u32x4 *q, const int b) -> uint32_t { return (q[b >> 4][(b >> 2) & 3] >> (8 * (b & 3))) & 0xFFu; };
+  uint32_t sb[4] = {0, 0, 0, 0}, npc[4] = {0, 0, 0, 0};
   for (uint32_t k = 0; k < ns; ++k) {
-    const uint32_t a = k * seg, e = min(a + seg, n);
+    u32x4 q[8];
+    uint32_t L, P;
+    piece(k, q, L, P);
     uint32_t b = 0;
-#pragma unroll 8
-    for (uint32_t i = a + lane; i < e; i += 64) b += ct.nb[src[i]];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (16u * c >= P) break;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (16u * c + j < L) b += ctw[byte_at(q, 16 * c + j)] >> 16;
+    }
+    npc[k] = b;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) b += (uint32_t)__shfl_xor((int)b, d);
     sb[k] = b;
@@ -561,35 +660,40 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, ZcBlock *bl
   const uint32_t nq = (total + 3) / 4 + 1;
   for (uint32_t k = lane; k < nq; k += 64) sw[k] = 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-  // the streams
+  // the streams: a piece's bits packed in a register, stored a word at a
+  // time; the words it shares with its neighbours OR-ed in
   uint32_t o = hdr + tree + (one ? 0 : 6);  // byte offset of stream k in the section
   for (uint32_t k = 0; k < ns; ++k) {
-    const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
-    // piece of lane l: writing indices [l P, (l + 1) P) = literals e - 1 - w
-    const uint32_t P = (len + 63) / 64, w0 = min(lane * P, len), w1 = min(w0 + P, len);
-    uint32_t nbits = 0;
-    for (uint32_t w = w0; w < w1; ++w) nbits += ct.nb[src[e - 1 - w]];
+    u32x4 q[8];
+    uint32_t L, P;
+    piece(k, q, L, P);
+    const uint32_t nbits = npc[k];
     const uint32_t incl = wave_incl_sum(nbits, lane);
-    uint64_t bit = 8ull * o + (incl - nbits);
-    if (nbits) {
-      uint64_t acc = 0;
-      uint32_t accn = (uint32_t)(bit & 31), wi = (uint32_t)(bit >> 5);
-      bool first = true;
-      for (uint32_t w = w0; w < w1; ++w) {
-        const uint32_t x = src[e - 1 - w];
-        acc |= (uint64_t)ct.code[x] << accn;
-        accn += ct.nb[x];
-        if (accn >= 32) {
-          if (first) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece before)
-          else sw[wi] = (uint32_t)acc;
-          first = false;
-          acc >>= 32;
-          accn -= 32;
-          ++wi;
+    const uint64_t bit = 8ull * o + (incl - nbits);
+    uint64_t acc = 0;
+    uint32_t accn = (uint32_t)(bit & 31), wi = (uint32_t)(bit >> 5);
+    bool first = true;
+#pragma unroll
+    for (int c = 7; c >= 0; --c) {
+      if (16u * c >= P) continue;
+#pragma unroll
+      for (int j = 15; j >= 0; --j) {
+        if (16u * c + j < L) {
+          const uint32_t t = ctw[byte_at(q, 16 * c + j)];
+          acc |= (uint64_t)(t & 0xFFFFu) << accn;
+          accn += t >> 16;
+          if (accn >= 32) {
+            if (first) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece before)
+            else sw[wi] = (uint32_t)acc;
+            first = false;
+            acc >>= 32;
+            accn -= 32;
+            ++wi;
+          }
         }
       }
-      if (accn) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece after)
     }
+    if (nbits && accn) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece after)
     const uint32_t end = 8 * o + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (lane == 0) atomicOr(sw + (end >> 5), 1u << (end & 31));  // the end mark
     o += ssz[k];
@@ -989,7 +1093,7 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindTile), 0, st, base, nbytes, blocks, nblk, words);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
                      seqs);
-  if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, words);
+  if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, T, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);

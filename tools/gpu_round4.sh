@@ -59,6 +59,16 @@ for stage in "$@"; do
         || { echo "zcab $b rc=$?"; exit 1; }
       echo "$b $(cat $OUT/zcab_$b.json)"
     done ;;
+  zcabs)  # kernel stats of the compressor with each abship/*.so variant (1 GiB text)
+    cd /tmp && export TMPDIR=/tmp
+    for so in $R/abship/*.so; do
+      b=$(basename $so .so)
+      MCDC_LIBRARY=$so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/zcabs_$b -o zc --output-format csv -- \
+        python3 $R/tools/zc_bench.py 1 2 text > $OUT/zcabs_$b.json 2> $OUT/zcabs_$b.err || { echo "zcabs $b rc=$?"; exit 1; }
+      echo "== $b $(cat $OUT/zcabs_$b.json)"
+      python3 $R/tools/kcsv.py $OUT/zcabs_$b/zc_kernel_stats.csv
+    done
+    cd $R ;;
   zcstats)  # kernel trace + stats of the compressor only (1 GiB of text and of binary)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/zc_stats -o zc --output-format csv -- \
@@ -74,7 +84,10 @@ for stage in "$@"; do
     i=0
     for ctrs in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES GRBM_GUI_ACTIVE" \
                 "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
-                "FETCH_SIZE" "WRITE_SIZE"; do
+                "FETCH_SIZE" "WRITE_SIZE" \
+                "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                "VALUBusy GRBM_GUI_ACTIVE" \
+                "SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE"; do
       i=$((i+1))
       timeout -s KILL 150 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/zc_pmc/p$i -o run -- \
         python3 $R/tools/zc_bench.py 1 1 text > $OUT/zc_pmc_p$i.log 2>&1 || { echo "zc pmc pass $i rc=$?"; exit 1; }

@@ -69,10 +69,23 @@ int main(int argc, char **argv) {
   std::vector<uint8_t> lits, buf(1 << 21), zbuf(1 << 20);
   double tot = 0, tot_z = 0;
   uint64_t nseq_all = 0, nlit_all = 0, nrep = 0;
+  const int hk = getenv("ZC_HASH") ? atoi(getenv("ZC_HASH")) : 0;  // 1: the GPU's 32-bit forms
+  auto u24 = [](uint32_t x, uint32_t k) { return (uint32_t)((uint64_t)(x & 0xFFFFFF) * k); };
   auto hshort = [&](const uint8_t *q) {
+    const uint64_t v = rd64(q);
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    if (hk == 1) return (u24(lo & 0xFFFFFF, 0x9E3779u) + u24(lo >> 24 | (hi & 0xFF) << 8, 0xC2B2AFu)) >> (32 - hlog);
+    if (hk == 2) return (lo * 2654435761u + (hi & 0xFFu) * 0x85EBCA77u) >> (32 - hlog);
     return (uint32_t)(((rd64(q) << (64 - 8 * hb)) * 0xCF1BBCDCB7A56463ull) >> (64 - hlog));
   };
-  auto hlong = [&](const uint8_t *q) { return (uint32_t)((rd64(q) * 0x9E3779B185EBCA87ull) >> (64 - llog)); };
+  auto hlong = [&](const uint8_t *q) {
+    const uint64_t v = rd64(q);
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    if (hk == 1)
+      return (u24(lo & 0xFFFFFF, 0x85EBCBu) ^ u24(lo >> 24 | (hi & 0xFFFF) << 8, 0x27D4EBu) ^ u24(hi >> 16, 0x165667u)) >>
+             (32 - llog);
+    return (uint32_t)((rd64(q) * 0x9E3779B185EBCA87ull) >> (64 - llog));
+  };
   for (size_t c = 0; c < nch; ++c) {
     const uint8_t *p = d.data() + ch[c].offset;
     const uint32_t clen = (uint32_t)ch[c].length;

@@ -48,6 +48,12 @@ def main(tag, out=None):
             e["lds_bank_conflict_cycles_per_lds_active"] = round(m.get("SQ_LDS_BANK_CONFLICT", 0) / m["SQ_LDS_IDX_ACTIVE"], 3)
         if m.get("SQ_INSTS_LDS"):
             e["lds_bank_conflict_cycles_per_lds_instr"] = round(m.get("SQ_LDS_BANK_CONFLICT", 0) / m["SQ_INSTS_LDS"], 3)
+        for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_LDS",
+                  "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM"):
+            if c in m and m.get("SQ_WAVE_CYCLES"):
+                e[c.lower() + "_per_wave_cycle"] = round(m[c] / m["SQ_WAVE_CYCLES"], 3)
+        if "VALUBusy" in m:
+            e["valu_busy_pct"] = round(m["VALUBusy"], 2)
         if "FETCH_SIZE" in m:
             e["fetch_bytes_x2_per_input_byte"] = round(m["FETCH_SIZE"] * 1024 * 2 / batch, 3)
         if "WRITE_SIZE" in m:
