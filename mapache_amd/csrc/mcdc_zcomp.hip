@@ -78,6 +78,9 @@ constexpr uint32_t kHsLog = MCDC_ZC_HS, kHlLog = MCDC_ZC_HL;
 #ifndef MCDC_ZC_TILE
 #define MCDC_ZC_TILE 512  // (compile-time A/B knob)
 #endif
+#ifndef MCDC_ZC_LOOK
+#define MCDC_ZC_LOOK 2  // tiles of look-ahead for a tile's own bytes (2 or 4; compile-time A/B knob)
+#endif
 constexpr uint32_t kFindTile = MCDC_ZC_TILE;  // positions per step = threads per workgroup
 constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
@@ -245,8 +248,14 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     u32x4 ys, yl;
   };
   Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
+#if MCDC_ZC_LOOK == 4
+  u32x4 n0 = ald16s(cb, min(prime0 + tid, last16)), n1 = ald16s(cb, min(prime0 + kFindTile + tid, last16)),
+        n2 = ald16s(cb, min(prime0 + 2 * kFindTile + tid, last16)), n3 = ald16s(cb, min(prime0 + 3 * kFindTile + tid, last16));
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3)::"memory");
+#else
   u32x4 n0 = ald16s(cb, min(prime0 + tid, last16)), n1 = ald16s(cb, min(prime0 + kFindTile + tid, last16));
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1)::"memory");
+#endif
   auto verify = [&](const Stage &S) {
     const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
     const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
@@ -271,8 +280,21 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   // load is ever copied.  Per step the memory operations are: the verified
   // word's store (or none), then the loads ys, yl, n; a step's loads are
   // used two steps later, after the three loads of the step between (vmcnt(3)).
+#ifdef MCDC_ZC_TIMING  // (A/B: cycles per phase of wave 0 in some workgroups, printed)
+  uint64_t tm[5] = {0, 0, 0, 0, 0}, tstart = __builtin_amdgcn_s_memtime(), tnow = 0;
+  uint32_t nsteps = 0;
+#define ZC_TICK(k) (tnow = __builtin_amdgcn_s_memtime(), tm[k] += tnow - tstart, tstart = tnow)
+#else
+#define ZC_TICK(k) ((void)0)
+#endif
   auto step = [&](uint32_t t0, u32x4 &n, Stage &S) {
+    ZC_TICK(4);
+#if MCDC_ZC_LOOK == 4
+    asm volatile("s_waitcnt vmcnt(4)" : "+v"(n), "+v"(S.ys), "+v"(S.yl)::"memory");
+#else
     asm volatile("s_waitcnt vmcnt(3)" : "+v"(n), "+v"(S.ys), "+v"(S.yl)::"memory");
+#endif
+    ZC_TICK(0);
     const uint32_t p = t0 + tid;
     const bool tail = t0 >= tail0;
     uint4 x = to4(n);
@@ -286,6 +308,7 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     const bool okl = cl != 0 && cl != cs && p - (cl - 1) <= zs::kWindow;
     const uint32_t qs = oks ? cs - 1 : 0u, ql = okl ? cl - 1 : 0u;
     verify(S);
+    ZC_TICK(1);
     S.v = find;
     S.ks = oks;
     S.kl = okl;
@@ -296,29 +319,50 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     S.x = x;
 #ifdef MCDC_ZC_NOVERIFY  // (A/B: the finder without its candidate loads; no matches, see verify)
     S.ys = S.yl = u32x4{qs, ql, ~0u, ~0u};
-    n = ald16s(cb, min(p + 2 * kFindTile, last16));
-    n = ald16s(cb, min(p + 2 * kFindTile, last16));
-    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
+    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
+    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
 #else
     S.ys = ald16s(cb, min(qs, last16));
     S.yl = ald16s(cb, min(ql, last16));
-    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
 #endif
     lds_sync();  // every lookup of the tile before any insert
+    ZC_TICK(2);
     if (vs) atomicMax(hts + hs, p + 1);
     if (vl) atomicMax(htl + hl, p + 1);
     lds_sync();  // every insert before the next tile's lookups
+    ZC_TICK(3);
+#ifdef MCDC_ZC_TIMING
+    ++nsteps;
+#endif
   };
   __syncthreads();
   // (both steps unconditional: a tile past the segment keeps nothing, and a
   // join after a conditional step would cost the compiler's own waits)
+#if MCDC_ZC_LOOK == 4
+  for (uint32_t t0 = prime0; t0 < seg1; t0 += 4 * kFindTile) {
+    step(t0, n0, s0);
+    step(t0 + kFindTile, n1, s1);
+    step(t0 + 2 * kFindTile, n2, s0);
+    step(t0 + 3 * kFindTile, n3, s1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3), "+v"(s0.ys), "+v"(s0.yl), "+v"(s1.ys),
+               "+v"(s1.yl)::"memory");
+#else
   for (uint32_t t0 = prime0; t0 < seg1; t0 += 2 * kFindTile) {
     step(t0, n0, s0);
     step(t0 + kFindTile, n1, s1);
   }
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(s0.ys), "+v"(s0.yl), "+v"(s1.ys), "+v"(s1.yl)::"memory");
+#endif
   verify(s0);
   verify(s1);
+#ifdef MCDC_ZC_TIMING
+  if (tid == 0 && bi0 % 509 == 0)
+    printf("ZCT wg %lu steps %u wait %lu calc %lu bar1 %lu bar2 %lu loop %lu\n", (unsigned long)bi0, nsteps,
+           (unsigned long)tm[0], (unsigned long)tm[1], (unsigned long)tm[2], (unsigned long)tm[3], (unsigned long)tm[4]);
+#endif
 }
 
 
@@ -362,7 +406,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
                                                  const uint32_t *words, uint8_t *stage, uint64_t *seqs) {
   __shared__ uint16_t J[8][257];
   __shared__ uint8_t mk[260];
-  __shared__ uint32_t offl[256];
+  __shared__ uint32_t offl[256], wbyt[64];
   const uint64_t bi = blockIdx.x;
   if (bi >= nblk) return;
   const uint32_t lane = lane_id();
@@ -376,27 +420,49 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   if (lane == 0) {
     for (int k = 0; k < 8; ++k) J[k][256] = 256;
   }
-  uint32_t nwd[4];
-  auto load_win = [&](uint32_t wb, uint32_t *v) {
+  // A window's words and source bytes (lane l: bytes [wb + 4 l, + 4)) are
+  // requested a window ahead with loads outside the compiler's wait counting
+  // (see ald16c: the literal and sequence stores would otherwise drain them),
+  // and waited for at the next window's start, used or not.
+  const uint64_t lim = nbytes - B.src;                                          // bytes readable at p0
+  const bool wide = lim >= 4;                                                   // (else byte loads)
+  const uint32_t lim4 = wide ? (uint32_t)min<uint64_t>(lim - 4, 0xFFFFFFFCull) : 0u;
+  auto issue = [&](uint32_t wb, uint32_t *v, uint32_t &by) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t q = wb + 64 * j + lane;
-      v[j] = q < end ? w[q] : 0u;
+      const uint32_t q = min(wb + 64 * j + lane, (uint32_t)kZcBlock - 1);
+      asm volatile("global_load_dword %0, %1, %2" : "=v"(v[j]) : "v"(4 * q), "s"(w) : "memory");
     }
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(by) : "v"(min(wb + 4 * lane, lim4)), "s"(p0) : "memory");
   };
+  auto wait_all = [&](uint32_t *v, uint32_t &by) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(by)::"memory");
+  };
+  uint32_t nwd[4], nby;
   uint32_t nwb = 0;
-  load_win(0, nwd);
+  issue(0, nwd, nby);
   while (cur < end) {
     const uint32_t wb = cur & ~63u, s0 = cur - wb;
-    uint32_t wd[4];
-    if (wb == nwb) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wd[j] = nwd[j];
-    } else {
-      load_win(wb, wd);
+    wait_all(nwd, nby);
+    uint32_t wd[4], by;
+    if (wb != nwb) {  // (a long match skipped the prefetched window)
+      issue(wb, nwd, nby);
+      wait_all(nwd, nby);
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wd[j] = wb + 64 * j + lane < end ? nwd[j] : 0u;
+    {
+      const uint32_t a = wb + 4 * lane, c = min(a, lim4);
+      by = a - c < 4 ? nby >> (8 * (a - c)) : 0u;  // (clamped at the end of the input: realigned)
+      if (!wide) {  // (fewer than 4 bytes readable)
+        by = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+          if (a + k < lim) by |= (uint32_t)p0[a + k] << (8 * k);
+      }
+    }
+    wbyt[lane] = by;
     nwb = wb + 256;
-    load_win(nwb, nwd);  // (the next window's words, in flight meanwhile)
+    issue(nwb, nwd, nby);  // (the next window's, in flight meanwhile)
     uint32_t ml[4], nx[4];
     bool valid[4];
 #pragma unroll
@@ -479,7 +545,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         const uint32_t ov = (ll && off == poff) ? 1u : off + 3;
         sq[nseq + mr] = zs::seq_pack_ov(ll, mlen, ov);
       }
-      if (l) lit[nlit + lr] = p0[q];
+      if (l) lit[nlit + lr] = reinterpret_cast<const uint8_t *>(wbyt)[i];
       pend = max(pend, __shfl(ie, 63));
       pidx = max(pidx, __shfl(ii, 63));
       mcount += (uint32_t)__builtin_popcountll(bm);
@@ -494,6 +560,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     }
     cur = (uint32_t)wave_max((int32_t)exit_pos);
   }
+  wait_all(nwd, nby);  // (no load may land in a register after its last use)
   if (lane == 0) {
     blocks[bi].nlit = nlit;
     blocks[bi].nseq = nseq;
