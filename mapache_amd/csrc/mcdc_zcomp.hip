@@ -366,6 +366,19 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
 }
 
 
+#ifdef MCDC_ZC_TIMING  // (A/B: cycles per phase of one wave, some blocks, printed)
+#define ZT_DECL uint64_t zt_[6] = {0, 0, 0, 0, 0, 0}, zt0_ = __builtin_amdgcn_s_memtime(), zt1_ = 0
+#define ZT(k) (zt1_ = __builtin_amdgcn_s_memtime(), zt_[k] += zt1_ - zt0_, zt0_ = zt1_)
+#define ZT_PRINT(name, cond)                                                                                      \
+  if ((cond) && lane_id() == 0)                                                                                  \
+  printf("ZCT %s blk %lu t0 %lu t1 %lu t2 %lu t3 %lu t4 %lu\n", name, (unsigned long)blockIdx.x,                   \
+         (unsigned long)zt_[0], (unsigned long)zt_[1], (unsigned long)zt_[2], (unsigned long)zt_[3], (unsigned long)zt_[4])
+#else
+#define ZT_DECL
+#define ZT(k) ((void)0)
+#define ZT_PRINT(name, cond)
+#endif
+
 // Inclusive sum over the wave's 64 lanes.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
 #pragma unroll
@@ -440,9 +453,11 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   };
   uint32_t nwd[4], nby;
   uint32_t nwb = 0;
+  ZT_DECL;
   issue(0, nwd, nby);
   while (cur < end) {
     const uint32_t wb = cur & ~63u, s0 = cur - wb;
+    ZT(4);
     wait_all(nwd, nby);
     uint32_t wd[4], by;
     if (wb != nwb) {  // (a long match skipped the prefetched window)
@@ -463,6 +478,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     wbyt[lane] = by;
     nwb = wb + 256;
     issue(nwb, nwd, nby);  // (the next window's, in flight meanwhile)
+    ZT(0);
     uint32_t ml[4], nx[4];
     bool valid[4];
 #pragma unroll
@@ -487,6 +503,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         const uint32_t i = 64 * j + lane;
         if (mk[i]) mk[J[k][i]] = 1;
       }
+    ZT(1);
     bool node[4], mt[4];
     uint64_t bc[4];
     int32_t cap_first = 0x7FFFFFFF;
@@ -520,6 +537,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         mlt += 1024;
       }
     }
+    ZT(2);
     // this window's matches and literals, in position order (slot-major)
     uint32_t mcount = 0, lcount = 0;
     int32_t pend = -1, pidx = -1;  // running exclusive max-scans: end / index of the previous match
@@ -559,8 +577,10 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       last_off = offl[pidx];
     }
     cur = (uint32_t)wave_max((int32_t)exit_pos);
+    ZT(3);
   }
   wait_all(nwd, nby);  // (no load may land in a register after its last use)
+  ZT_PRINT("parse", bi % 509 == 0);
   if (lane == 0) {
     blocks[bi].nlit = nlit;
     blocks[bi].nseq = nseq;
@@ -591,6 +611,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   uint32_t *const ctw = hist[1];  // (after the counts are merged into hist[0])
   __shared__ HufCT ct;
   __shared__ HufWork hw;
+  __shared__ HufDescWork dw;
   __shared__ uint8_t tdesc[132];
   __shared__ uint32_t tree_sz;
   const uint64_t bi = blockIdx.x;
@@ -602,6 +623,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   if (n < 32) return;  // (lsize stays 0: raw literals)
   uint8_t *st = stage + bi * kZcSlot;
   const uint8_t *src = B.nseq ? st + kLitHdr : base + B.src;
+  ZT_DECL;
   for (uint32_t k = lane; k < 4 * 256; k += 64) (&hist[0][0])[k] = 0;
   __syncthreads();
   // count (misaligned 16-byte loads: gfx950 reads the bytes at the address)
@@ -666,11 +688,13 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   for (int h = 0; h < 4; ++h)
     if (c[h]) hw.sym[r[h]] = (uint16_t)(lane + 64 * h);
   __syncthreads();
-  if (lane == 0) {
-    huf_build(hist[0], ct, hw, true);
-    tree_sz = huf_tree_desc(ct, tdesc);
-  }
+  ZT(0);
+  if (lane == 0) huf_build(hist[0], ct, hw, true);
   __syncthreads();
+  ZT(4);
+  if (lane == 0) tree_sz = huf_tree_desc(ct, tdesc, dw);
+  __syncthreads();
+  ZT(1);
   const uint32_t tree = tree_sz;
   if (!tree) return;  // (no description applies: raw literals)
   // code | length << 16 per symbol: one LDS read per literal
@@ -717,6 +741,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
     for (int d = 32; d >= 1; d >>= 1) b += (uint32_t)__shfl_xor((int)b, d);
     sb[k] = b;
   }
+  ZT(2);
   uint32_t ssz[4];
   const uint32_t total = huf_section_size(tree, n, sb, one, ssz);
   if (total >= kLitHdr + n) return;  // not smaller than raw
@@ -782,6 +807,8 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   const uint32_t n16 = (total + 15) / 16;
   for (uint32_t k = lane; k < n16; k += 64)
     reinterpret_cast<uint4 *>(st)[k] = reinterpret_cast<const uint4 *>(sw)[k];
+  ZT(3);
+  ZT_PRINT("huff", bi % 509 == 0);
 }
 
 // Modular inverse of an odd a modulo 2^32 (Newton: each step doubles the bits).
@@ -849,23 +876,196 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
   }
 }
 
-// ONE WAVE PER BLOCK: the block's sequences section with tables of its own
-// (per symbol type the block's FSE_Compressed_Mode table or the predefined
-// one, seq_plan), the serial FSE state machines split from the bit writing:
-//   plan     code histograms (lanes over the sequences, LDS atomics);
-//            seq_plan on lane 0; the own tables built by the wave
-//   chains   the three state machines (lanes 0-2: LL, OF, ML) walk the
-//            sequences from the last to the first, 64 at a time (codes
-//            read from the batch's lanes): per sequence the state bits
-//            (count | value << 4, 16 bits each) to scratch
-//   offsets  per sequence its bits (state bits + extra bits) and, by wave
-//            scans in writing order (last sequence first), its bit offset
-//   write    64 sequences at a time: each lane ORs its sequence's bits into
-//            an LDS buffer (LDS atomics), the buffer's whole words go out
-//            with plain stores, the partial last word carries over; then the
-//            final states, the end mark and the header (count, modes,
-//            descriptions) by lane 0
+// The sequences section of a block, in three kernels (the serial FSE state
+// machines split from the rest, and run for many blocks per wave):
+//   k_zc_plan    ONE WAVE PER BLOCK: code histograms (lanes over the
+//                sequences, LDS atomics), seq_plan on lane 0 (per symbol type
+//                the block's own FSE_Compressed_Mode table or the predefined
+//                one), the own tables built by the wave; plan and tables to
+//                the block's match-word scratch (free after k_zc_huff)
+//   k_zc_chain   ONE LANE PER STATE MACHINE, 9 blocks x 3 types per wave:
+//                the wave's 27 tables in LDS, each lane walks its block's
+//                sequences from the last to the first, per sequence the state
+//                bits (count | value << 4, 16 bits) to scratch, then the final
+//                state; codes prefetched 8 sequences ahead
+//   k_zc_encode  ONE WAVE PER BLOCK: per sequence its bits (state bits + extra
+//                bits), 64 sequences at a time OR-ed into an LDS buffer at
+//                offsets from wave scans in writing order (last sequence
+//                first), the buffer's whole words out with plain stores, the
+//                partial last word carried; then the final states, the end
+//                mark and the header (count, modes, descriptions)
 // The block stays raw when the compressed block is not smaller.
+struct ZcSeqTab {  // (in the block's match-word scratch)
+  FseCTL t[3];     // LL, OF, ML: own or predefined
+  uint32_t fin[3]; // final states (k_zc_chain)
+  SeqPlan P;
+};
+static_assert(sizeof(ZcSeqTab) <= kZcBlock * 4, "sequence tables exceed the block's scratch");
+__device__ __forceinline__ ZcSeqTab *seq_tab(uint32_t *words, uint64_t bi) {
+  return reinterpret_cast<ZcSeqTab *>(words + bi * kZcBlock);
+}
+// After the tables: per symbol type the sequences' codes, one byte each, the
+// last sequence first (k_zc_chain's walking order), + 8 bytes of slack.
+constexpr uint32_t kSeqTabBytes = (sizeof(ZcSeqTab) + 15) / 16 * 16;
+static_assert(kSeqTabBytes + 3 * (kZcSeqCap + 8) <= kZcBlock * 4, "sequence codes exceed the block's scratch");
+__device__ __forceinline__ uint8_t *seq_codes(uint32_t *words, uint64_t bi, uint32_t k) {
+  return reinterpret_cast<uint8_t *>(words + bi * kZcBlock) + kSeqTabBytes + k * (kZcSeqCap + 8);
+}
+
+__global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t nblk, const uint64_t *seqs,
+                                                uint32_t *words, ZTables T) {
+  __shared__ FseCTL tb[3];
+  __shared__ SeqPlan P;
+  __shared__ uint32_t hist[3][53], cum[54], seen[54];
+  const uint32_t lane = lane_id();
+  const uint64_t bi = blockIdx.x;
+  if (bi >= nblk) return;
+  const ZcBlock B = blocks[bi];
+  const uint32_t ns = B.nseq;
+  if (ns == 0) return;
+  const uint64_t *sq = seqs + bi * kZcSeqCap;
+  ZT_DECL;
+  for (uint32_t k = lane; k < 3 * 53; k += 64) (&hist[0][0])[k] = 0;
+  __syncthreads();
+  uint8_t *cd0 = seq_codes(words, bi, 0), *cd1 = seq_codes(words, bi, 1), *cd2 = seq_codes(words, bi, 2);
+  for (uint32_t i = lane; i < ns; i += 64) {
+    const uint64_t q = sq[i];
+    const uint32_t c0 = ll_code(seq_ll(q)), c1 = highbit(seq_ov(q)), c2 = ml_code(seq_ml(q) - 3);
+    atomicAdd(&hist[0][c0], 1u);
+    atomicAdd(&hist[1][c1], 1u);
+    atomicAdd(&hist[2][c2], 1u);
+    cd0[ns - 1 - i] = (uint8_t)c0;
+    cd1[ns - 1 - i] = (uint8_t)c1;
+    cd2[ns - 1 - i] = (uint8_t)c2;
+  }
+  __syncthreads();
+  ZT(3);
+  if (lane == 0) seq_plan(hist[0], hist[1], hist[2], ns, P, 1);
+  __syncthreads();
+  ZT(4);
+  const FseCT *pre[3] = {&T.ll, &T.of, &T.ml};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (P.own[k]) {
+      fse_build_wave(P.norm[k], P.tl[k], tb[k], cum, seen, lane);
+    } else {
+      tb[k].state[lane] = pre[k]->state[lane];
+      if (lane < 53) {
+        tb[k].dfs[lane] = pre[k]->dfs[lane];
+        tb[k].dnb[lane] = pre[k]->dnb[lane];
+      }
+      if (lane == 0) tb[k].log = pre[k]->log;
+    }
+    __syncthreads();
+  }
+  ZcSeqTab *tab = seq_tab(words, bi);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {  // (the states in use, then dfs, dnb, log)
+    const uint32_t nst = 1u << tb[k].log;
+    for (uint32_t u = lane; u < nst; u += 64) tab->t[k].state[u] = tb[k].state[u];
+    if (lane < 53) {
+      tab->t[k].dfs[lane] = tb[k].dfs[lane];
+      tab->t[k].dnb[lane] = tb[k].dnb[lane];
+    }
+    if (lane == 0) tab->t[k].log = tb[k].log;
+  }
+  constexpr uint32_t kPw = sizeof(SeqPlan) / 4;
+  static_assert(sizeof(SeqPlan) % 4 == 0, "SeqPlan copy by words");
+  for (uint32_t u = lane; u < kPw; u += 64) reinterpret_cast<uint32_t *>(&tab->P)[u] = reinterpret_cast<const uint32_t *>(&P)[u];
+  ZT(0);
+  ZT_PRINT("plan", bi % 509 == 0);
+}
+
+// Blocks per wave: 27 state machines, one per lane; 39 KiB of tables, 4
+// waves per CU, so that a batch of 8192 blocks is one round of waves on 256
+// CUs.  The machines are VALU-bound (one wave per SIMD): k_zc_plan hands
+// them their codes, one byte per sequence, in walking order.
+constexpr uint32_t kChainBlocks = 9;
+__global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t nblk, uint64_t *recs,
+                                                 uint32_t *words) {
+  __shared__ FseCTL tb[3 * kChainBlocks];
+  const uint32_t lane = lane_id();
+  const uint64_t g0 = (uint64_t)blockIdx.x * kChainBlocks;
+  ZT_DECL;
+  for (uint32_t j = 0; j < kChainBlocks && g0 + j < nblk; ++j) {
+    const uint64_t b = g0 + j;
+    if (blocks[b].nseq == 0) continue;
+    const ZcSeqTab *tab = seq_tab(words, b);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      FseCTL &d = tb[3 * j + k];
+      const uint32_t lg = tab->t[k].log, nst = 1u << lg;
+      for (uint32_t u = lane; u < nst / 2; u += 64)
+        reinterpret_cast<uint32_t *>(d.state)[u] = reinterpret_cast<const uint32_t *>(tab->t[k].state)[u];
+      if (lane < 53) {
+        d.dfs[lane] = tab->t[k].dfs[lane];
+        d.dnb[lane] = tab->t[k].dnb[lane];
+      }
+    }
+  }
+  __syncthreads();
+  ZT(0);
+  const uint32_t j = min(lane / 3, kChainBlocks - 1), k = lane % 3;
+  const uint64_t b = g0 + j;
+  const bool act = lane < 3 * kChainBlocks && b < nblk;
+  const uint32_t ns = act ? blocks[b].nseq : 0u;
+  const FseCTL &ct = tb[3 * j + k];
+  uint16_t *rec = reinterpret_cast<uint16_t *>(recs + (act ? b : 0) * kZcSeqCap);
+  const uint8_t *cd = seq_codes(words, act ? b : 0, k);  // codes in walking order: cd[m] = sequence ns - 1 - m
+  // 8 sequences per batch: codes of batch t in a register pair, of batch
+  // t + 1 in flight (a load outside the compiler's wait counting, waited
+  // for after the batch's steps, before its records are stored)
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto issue = [&](uint32_t m0) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(cd + m0) : "memory");
+    return v;
+  };
+  const int32_t top = wave_max((int32_t)ns);  // (the wave's longest block sets the batch count)
+  uint32_t state = 0;
+  if (ns) {  // the last sequence: the initial state (no bits)
+    const uint32_t c = cd[0], dnb = ct.dnb[c];
+    const uint32_t nb = (dnb + (1u << 15)) >> 16;
+    state = ct.state[((((nb << 16) - dnb)) >> nb) + ct.dfs[c]];
+    rec[4 * (ns - 1) + k] = 0;
+  }
+  // one batch: the codes in cq (waited for), the next batch's requested into
+  // nq; the loop alternates two register pairs, so that no register with a
+  // load in flight is ever copied
+  auto batch = [&](int32_t m0, u32x2 &cq, u32x2 &nq) {
+    uint32_t dn[8];
+    int32_t df[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t c = (cq[u >> 2] >> (8 * (u & 3))) & 63u;
+      dn[u] = ct.dnb[c];
+      df[u] = ct.dfs[c];
+    }
+    nq = issue((uint32_t)m0 + 8);
+    uint32_t r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t nb = (state + dn[u]) >> 16;
+      r[u] = nb | (state & ((1u << nb) - 1u)) << 4;
+      const uint32_t nxt = ct.state[((state >> nb) + (uint32_t)df[u]) & 511u];
+      state = m0 + u < (int32_t)ns ? nxt : state;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(nq)::"memory");
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (m0 + u < (int32_t)ns) rec[4 * (ns - 1 - (uint32_t)(m0 + u)) + k] = (uint16_t)r[u];
+  };
+  u32x2 qa = issue(1), qb;
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa)::"memory");
+  for (int32_t m0 = 1; m0 < top; m0 += 16) {  // m: sequence ns - 1 - m
+    batch(m0, qa, qb);
+    batch(m0 + 8, qb, qa);
+  }
+  if (act && ns) seq_tab(words, b)->fin[k] = state;
+  ZT(1);
+  ZT_PRINT("chain", blockIdx.x % 97 == 0);
+}
+
 __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint64_t lo, uint64_t hi, uint32_t nbits) {
   // bits [bit, bit + nbits) of a little-endian stream of 32-bit words = the
   // low nbits of hi:lo (nbits <= 96)
@@ -881,11 +1081,9 @@ __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint64_t lo, 
 }
 
 __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                  const uint64_t *seqs, uint64_t *recs, ZTables T, uint64_t *piece) {
+                                                  const uint64_t *seqs, const uint64_t *recs, uint32_t *words,
+                                                  uint64_t *piece) {
   MCDC_VGPR_PAD(40);  // (not an exact fill)
-  __shared__ FseCTL tb[3];  // the block's LL, OF, ML tables (own or predefined)
-  __shared__ SeqPlan P;
-  __shared__ uint32_t hist[3][53], cum[54], seen[54];
   constexpr uint32_t kWbWords = 64 * 96 / 32 + 4;  // a batch's bits + the carried word
   __shared__ uint32_t wb[kWbWords];
   const uint32_t lane = lane_id();
@@ -895,7 +1093,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   const uint64_t *sq = seqs + bi * kZcSeqCap;
-  uint16_t *rec = reinterpret_cast<uint16_t *>(recs + bi * kZcSeqCap);
+  const uint16_t *rec = reinterpret_cast<const uint16_t *>(recs + bi * kZcSeqCap);
   uint8_t *st = stage + bi * kZcSlot;
   uint32_t csize = 0;
   if (ns || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
@@ -905,77 +1103,17 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
       if (lane == 0) st[at] = 0;  // Number_of_Sequences 0
       csize = at + 1 < B.len ? at + 1 : 0;
     } else {
-      for (uint32_t k = lane; k < 3 * 53; k += 64) (&hist[0][0])[k] = 0;
-      __syncthreads();
-      for (uint32_t i = lane; i < ns; i += 64) {
-        const uint64_t q = sq[i];
-        atomicAdd(&hist[0][ll_code(seq_ll(q))], 1u);
-        atomicAdd(&hist[1][highbit(seq_ov(q))], 1u);
-        atomicAdd(&hist[2][ml_code(seq_ml(q) - 3)], 1u);
-      }
-      __syncthreads();
-      if (lane == 0) seq_plan(hist[0], hist[1], hist[2], ns, P, 1);
-      __syncthreads();
-      const FseCT *pre[3] = {&T.ll, &T.of, &T.ml};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (P.own[k]) {
-          fse_build_wave(P.norm[k], P.tl[k], tb[k], cum, seen, lane);
-        } else {
-          tb[k].state[lane] = pre[k]->state[lane];
-          if (lane < 53) {
-            tb[k].dfs[lane] = pre[k]->dfs[lane];
-            tb[k].dnb[lane] = pre[k]->dnb[lane];
-          }
-          if (lane == 0) tb[k].log = pre[k]->log;
-        }
-        __syncthreads();
-      }
-      // chains: lane k < 3 runs type k's state machine, the last sequence first
-      const FseCTL &ct = tb[lane < 3 ? lane : 0];
-      uint32_t state = 0;
-      for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) {
-        const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
-        const int32_t i = b0 + (int32_t)lane;
-        uint32_t c0 = 0, c1 = 0, c2 = 0;
-        if (i < b1) {
-          const uint64_t q = sq[i];
-          c0 = ll_code(seq_ll(q));
-          c1 = highbit(seq_ov(q));
-          c2 = ml_code(seq_ml(q) - 3);
-        }
-        for (int32_t j = b1 - b0 - 1; j >= 0; --j) {
-          const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, j),
-                         a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, j),
-                         a2 = (uint32_t)__builtin_amdgcn_readlane((int)c2, j);
-          const uint32_t c = lane == 0 ? a0 : lane == 1 ? a1 : a2;
-          if (lane < 3) {
-            const uint32_t dnb = ct.dnb[c];
-            const int32_t dfs = ct.dfs[c];
-            uint32_t r = 0;
-            if (b0 + j == (int32_t)ns - 1) {  // the last sequence: the initial state (no bits)
-              const uint32_t nb = (dnb + (1u << 15)) >> 16;
-              state = ct.state[((((nb << 16) - dnb)) >> nb) + dfs];
-            } else {
-              const uint32_t nb = (state + dnb) >> 16;
-              r = nb | (state & ((1u << nb) - 1u)) << 4;
-              state = ct.state[(state >> nb) + dfs];
-            }
-            rec[4 * (b0 + j) + lane] = (uint16_t)r;
-          }
-        }
-      }
-      // (the records land in L2 and the CU's vector L1 is invalidated before
-      // the other lanes read them back)
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      ZT_DECL;
+      const ZcSeqTab *tab = seq_tab(words, bi);
+      const uint32_t ndesc = tab->P.ndesc;
       // the section: header, then the bitstream from a 4-byte aligned word base
       const uint32_t cnt = ns < 128 ? 1u : ns < 0x7F00 ? 2u : 3u;
-      const uint32_t hsz = cnt + 1 + P.ndesc;
+      const uint32_t hsz = cnt + 1 + ndesc;
       uint8_t *bs0 = st + at + hsz;
       const uint32_t pre_bits = (uint32_t)((uintptr_t)bs0 & 3) * 8;  // stream bit 0 inside the first word
       uint32_t *w0 = reinterpret_cast<uint32_t *>((uintptr_t)bs0 & ~(uintptr_t)3);
       // bits per sequence and offsets (writing order: the last sequence first)
-      const uint32_t tl0 = tb[0].log, tl1 = tb[1].log, tl2 = tb[2].log;
+      const uint32_t tl0 = tab->t[0].log, tl1 = tab->t[1].log, tl2 = tab->t[2].log;
       // first pass: the total, to size the zeroing and the raw / compressed choice
       uint64_t tot = 0;
       for (uint32_t i = lane; i < ns; i += 64) {
@@ -1048,9 +1186,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
           __syncthreads();
         }
         // final states (ML, OF, LL: log bits each), the end mark, the last words
-        const uint32_t fs = state;  // lanes 0-2: the final states of LL, OF, ML
-        const uint32_t f0 = (uint32_t)__shfl((int)fs, 0), f1 = (uint32_t)__shfl((int)fs, 1),
-                       f2 = (uint32_t)__shfl((int)fs, 2);
+        const uint32_t f0 = tab->fin[0], f1 = tab->fin[1], f2 = tab->fin[2];  // final states of LL, OF, ML
         {
           const uint32_t fb = tl2 + tl1 + tl0 + 1;
           const uint64_t v = (uint64_t)(f2 & ((1u << tl2) - 1)) | (uint64_t)(f1 & ((1u << tl1) - 1)) << tl2 |
@@ -1075,11 +1211,13 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
             h[1] = (uint8_t)(ns - 0x7F00);
             h[2] = (uint8_t)((ns - 0x7F00) >> 8);
           }
-          h[cnt] = (uint8_t)P.modes;
-          for (uint32_t k = 0; k < P.ndesc; ++k) h[cnt + 1 + k] = P.desc[k];
+          h[cnt] = (uint8_t)tab->P.modes;
+          for (uint32_t k = 0; k < ndesc; ++k) h[cnt + 1 + k] = tab->P.desc[k];
         }
         csize = total;
       }
+      ZT(2);
+      ZT_PRINT("encode", bi % 509 == 0);
     }
   }
   if (lane == 0) {
@@ -1161,7 +1299,10 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
                      seqs);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words);
-  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, T, piece);
+  hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, seqs, words, T);
+  hipLaunchKernelGGL(k_zc_chain, dim3((unsigned)((nblk + kChainBlocks - 1) / kChainBlocks)), dim3(64), 0, st, blocks,
+                     nblk, recs, words);
+  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, words, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);
   hipLaunchKernelGGL(k_zc_final, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, poff, obase, out,

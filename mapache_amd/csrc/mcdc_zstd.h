@@ -112,12 +112,13 @@ constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
 constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
                                  1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
+// (sym: S bytes, cumul: 54 entries of workspace; the GPU passes LDS, since a
+// dynamically indexed local array would live in scratch memory)
 template <uint32_t S>
-__host__ __device__ inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCTN<S> &ct) {
+__host__ __device__ inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCTN<S> &ct, uint8_t *sym,
+                                          uint32_t *cumul) {
   const uint32_t size = 1u << tlog;
   uint32_t high = size - 1;
-  uint8_t sym[S];
-  uint32_t cumul[54];
   cumul[0] = 0;
   for (int u = 1; u <= nsym; ++u) {
     if (norm[u - 1] == -1) {
@@ -155,6 +156,12 @@ __host__ __device__ inline void fse_build(const int16_t *norm, int nsym, uint32_
     }
   }
   ct.log = tlog;
+}
+template <uint32_t S>
+__host__ __device__ inline void fse_build(const int16_t *norm, int nsym, uint32_t tlog, FseCTN<S> &ct) {
+  uint8_t sym[S];
+  uint32_t cumul[54];
+  fse_build(norm, nsym, tlog, ct, sym, cumul);
 }
 
 inline ZTables build_tables() {
@@ -700,6 +707,16 @@ __host__ __device__ inline uint32_t huf_tree_direct(const HufCT &ct, uint8_t *ds
   return 1 + (nw + 1) / 2;
 }
 
+// Workspace of the tree descriptions (LDS on the GPU, see fse_build).
+struct HufDescWork {
+  uint32_t cnt[13];
+  uint32_t cumul[54];
+  int16_t norm[53];
+  uint8_t sym[64];
+  uint8_t tmp[130];
+  FseCTN<64> t;
+};
+
 // The weights FSE-compressed (RFC 8878 §4.2.1.2, as zstd's HUF_compressWeights
 // writes them): an FSE table description of the weight histogram (accuracy
 // log <= 6), then one bitstream with two interleaved states -- weights at even
@@ -708,10 +725,11 @@ __host__ __device__ inline uint32_t huf_tree_direct(const HufCT &ct, uint8_t *ds
 // weights as the initial states.  headerByte = the compressed size (< 128).
 // Returns the description's size (1 + compressed size), or 0 when the weights
 // do not FSE-compress (a single distinct weight, or 128 bytes or more).
-__host__ __device__ inline uint32_t huf_tree_fse(const HufCT &ct, uint8_t *dst) {
+__host__ __device__ inline uint32_t huf_tree_fse(const HufCT &ct, uint8_t *dst, HufDescWork &ws) {
   const uint32_t nw = ct.last;  // 1 .. 255
   if (nw < 2) return 0;
-  uint32_t cnt[13] = {0};
+  uint32_t *cnt = ws.cnt;
+  for (uint32_t w = 0; w < 13; ++w) cnt[w] = 0;
   uint32_t maxw = 0;
   for (uint32_t i = 0; i < nw; ++i) {
     const uint32_t w = huf_weight(ct, i);
@@ -721,13 +739,13 @@ __host__ __device__ inline uint32_t huf_tree_fse(const HufCT &ct, uint8_t *dst) 
   for (uint32_t w = 0; w <= maxw; ++w)
     if (cnt[w] == nw) return 0;  // (one distinct weight: zstd's "rle", not FSE-coded)
   const uint32_t tl = fse_table_log(nw, maxw, 6);
-  int16_t norm[53];
+  int16_t *norm = ws.norm;
   if (!fse_normalize(cnt, maxw + 1, nw, tl, norm)) return 0;
   for (uint32_t w = maxw + 1; w < 53; ++w) norm[w] = 0;
   uint8_t *o = dst + 1;
   const uint32_t nd = fse_write_ncount(norm, maxw + 1, tl, o);
-  FseCTN<64> t;
-  fse_build(norm, (int)(maxw + 1), tl, t);
+  FseCTN<64> &t = ws.t;
+  fse_build(norm, (int)(maxw + 1), tl, t, ws.sym, ws.cumul);
   BitW bw{o + nd, dst + 128, 0, 0, false};
   FseState s1, s2;
   uint32_t i = nw;
@@ -754,15 +772,19 @@ __host__ __device__ inline uint32_t huf_tree_fse(const HufCT &ct, uint8_t *dst) 
 
 // The shorter of the two descriptions (direct only for last <= 128); 0 when
 // neither applies (the literals then stay raw).  dst holds 130 bytes.
-__host__ __device__ inline uint32_t huf_tree_desc(const HufCT &ct, uint8_t *dst) {
-  uint8_t tmp[130];
-  const uint32_t f = huf_tree_fse(ct, tmp);
+__host__ __device__ inline uint32_t huf_tree_desc(const HufCT &ct, uint8_t *dst, HufDescWork &ws) {
+  uint8_t *tmp = ws.tmp;
+  const uint32_t f = huf_tree_fse(ct, tmp, ws);
   const uint32_t d = ct.last <= 128 ? 1 + (ct.last + 1) / 2 : 0xFFFFFFFFu;
   if (f && f < d) {
     for (uint32_t i = 0; i < f; ++i) dst[i] = tmp[i];
     return f;
   }
   return d != 0xFFFFFFFFu ? huf_tree_direct(ct, dst) : 0u;
+}
+inline uint32_t huf_tree_desc(const HufCT &ct, uint8_t *dst) {
+  HufDescWork ws;
+  return huf_tree_desc(ct, dst, ws);
 }
 
 // Bits of one Huffman stream of n literals (without the end mark).
