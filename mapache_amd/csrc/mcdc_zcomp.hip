@@ -75,13 +75,8 @@ using namespace zs;
 #define MCDC_ZC_HL 13
 #endif
 constexpr uint32_t kHsLog = MCDC_ZC_HS, kHlLog = MCDC_ZC_HL;
-#ifndef MCDC_ZC_TILE
-#define MCDC_ZC_TILE 512  // (compile-time A/B knob)
-#endif
-#ifndef MCDC_ZC_LOOK
-#define MCDC_ZC_LOOK 2  // tiles of look-ahead for a tile's own bytes (2 or 4; compile-time A/B knob)
-#endif
-constexpr uint32_t kFindTile = MCDC_ZC_TILE;  // positions per step = threads per workgroup
+constexpr uint32_t kFindThreads = 512;   // threads per workgroup (8 waves)
+constexpr uint32_t kFindTile = kFindThreads;  // positions per step
 constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
 
@@ -93,6 +88,15 @@ __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t k) { return (uint
 __device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
   const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFu) << 8;
   return (mul24(a, 0x9E3779u) + mul24(b, 0xC2B2AFu)) >> (32 - kHsLog);
+}
+// 13-bit tags of the same keys (other multipliers: independent of the index)
+__device__ __forceinline__ uint32_t tag5(uint32_t lo, uint32_t hi) {
+  const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFu) << 8;
+  return (mul24(a, 0xA54FF5u) + mul24(b, 0x6C8E95u)) >> (32 - 13);
+}
+__device__ __forceinline__ uint32_t tag8(uint32_t lo, uint32_t hi) {
+  const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFFFu) << 8, c = hi >> 16;
+  return (mul24(a, 0x4F1BBDu) ^ mul24(b, 0x9E3B75u) ^ mul24(c, 0x2C1B3Du)) >> (32 - 13);
 }
 __device__ __forceinline__ uint32_t hash8(uint32_t lo, uint32_t hi) {
   const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFFFu) << 8, c = hi >> 16;
@@ -200,16 +204,21 @@ __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
   return d0 ? (uint32_t)__builtin_ctzll(d0) >> 3 : d1 ? 8u + ((uint32_t)__builtin_ctzll(d1) >> 3) : 16u;
 }
 
-// The match finder: one workgroup of kFindTile threads per segment (up to
+// The match finder: one workgroup of kFindThreads threads per segment (up to
 // kZcSegBlocks blocks of one chunk, the first record of the segment's blocks:
 // other workgroups return).  Writes words[(block - batch start) * kZcBlock +
 // position in block] for every position of the segment: match length (<=
-// kMlCap) << 24 | offset, 0 = no match of 4 bytes or more.  Per tile: the
-// lookups (tables as the earlier tiles left them), the candidates' bytes
-// requested, the previous tile's candidates verified (their bytes had a
-// tile's time to arrive), then the inserts; two LDS-only barriers.
-__global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint64_t nbytes, const ZcBlock *blocks,
-                                                       uint64_t nblk, uint32_t *words) {
+// kMlCap) << 24 | offset, 0 = no match of 4 bytes or more.  Table entries
+// are (position - prime0 + 1) << 13 | a 13-bit tag of the key (0 = empty),
+// so a lookup knows whether the stored key is (almost surely) its own, and
+// each position verifies ONE candidate: the long table's when its tag
+// matches, else the short table's when that one does (tools/zc_model2.cpp:
+// no ratio change against verifying both).  Per tile: the lookups (tables as
+// the earlier tiles left them), the candidate's bytes requested, the tile
+// two back verified (its bytes had two tiles' time to arrive), then the
+// inserts; two LDS-only barriers per tile.
+__global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, uint64_t nbytes,
+                                                          const ZcBlock *blocks, uint64_t nblk, uint32_t *words) {
   __shared__ __attribute__((aligned(16))) uint32_t hts[1u << kHsLog], htl[1u << kHlLog];
   const uint64_t bi0 = blockIdx.x;
   if (bi0 >= nblk) return;
@@ -222,64 +231,43 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   const uint32_t seg0 = B0.b * (uint32_t)kZcBlock;
   const uint32_t seg1 = min(clen, seg0 + kZcSegBlocks * (uint32_t)kZcBlock);
   const uint32_t prime0 = seg0 > kPrime ? seg0 - kPrime : 0u;
+  static_assert(kPrime + kZcSegBlocks * kZcBlock < (1u << 19), "entry positions take 19 bits");
   const uint8_t *cb = base + csrc;
   const uint64_t cbytes = nbytes - csrc;  // (bytes readable from the chunk start)
   // the segment's words: the chunk's blocks are consecutive records, so
   // position p's word is wseg[p]; positions outside the segment keep nothing
   uint32_t *wseg = words + (bi0 - B0.b) * kZcBlock;
   if (clen < 16 || cbytes < 16) {  // (too short to match: every position a literal)
-    for (uint32_t p = seg0 + tid; p < seg1; p += kFindTile) wseg[p] = 0u;
+    for (uint32_t p = seg0 + tid; p < seg1; p += kFindThreads) wseg[p] = 0u;
     return;
   }
-  for (uint32_t k = tid; k < (1u << kHsLog) / 4; k += kFindTile) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
-  for (uint32_t k = tid; k < (1u << kHlLog) / 4; k += kFindTile) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = tid; k < (1u << kHsLog) / 4; k += kFindThreads) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = tid; k < (1u << kHlLog) / 4; k += kFindThreads) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
   // 16-byte loads at chunk offsets clamped to the last 16 readable bytes; a
   // tile within 16 bytes of the end realigns them (fix16), others use them as loaded
   const uint32_t last16 = (uint32_t)min<uint64_t>(cbytes - 16, 0xFFFFFFF0ull);
   const uint64_t tail0 = cbytes >= kFindTile + 16 ? cbytes - (kFindTile + 16) : 0;  // tiles from here: the tail
   // Two tiles in flight: a tile's own bytes are requested two tiles ahead,
-  // and its candidates' bytes are verified two tiles later (the counter
+  // and its candidate's bytes are verified two tiles later (the counter
   // retires in order, so waiting for a tile's own bytes leaves the newer
   // requests in flight)
   struct Stage {
-    bool v, ks, kl, tail;
-    uint32_t p, qs, ql;
+    bool v, k, tail;
+    uint32_t p, q;
     uint4 x;
-    u32x4 ys, yl;
+    u32x4 y;
   };
   Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
-#if MCDC_ZC_LOOK == 4
-  u32x4 n0 = ald16s(cb, min(prime0 + tid, last16)), n1 = ald16s(cb, min(prime0 + kFindTile + tid, last16)),
-        n2 = ald16s(cb, min(prime0 + 2 * kFindTile + tid, last16)), n3 = ald16s(cb, min(prime0 + 3 * kFindTile + tid, last16));
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3)::"memory");
-#else
   u32x4 n0 = ald16s(cb, min(prime0 + tid, last16)), n1 = ald16s(cb, min(prime0 + kFindTile + tid, last16));
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1)::"memory");
-#endif
   auto verify = [&](const Stage &S) {
     const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
     const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
-    uint4 ys = to4(S.ys), yl = to4(S.yl);
-    if (S.tail) {
-      ys = fix16(ys, S.qs, cbytes);
-      yl = fix16(yl, S.ql, cbytes);
-    }
-    const uint32_t ms = S.ks ? min(prefix16(S.x, ys), lim) : 0u, ml = S.kl ? min(prefix16(S.x, yl), lim) : 0u;
-    const uint32_t ds = S.p - S.qs, dl = S.p - S.ql;
-    uint32_t m = 0, d = 0;
-    if (ms >= zs::kMinMatch && (ms > ml || (ms == ml && ds < dl))) m = ms, d = ds;
-    else if (ml >= zs::kMinMatch) m = ml, d = dl;
-#ifdef MCDC_ZC_NOVERIFY
-    if (ds != ~0u) m = 0;
-#endif
-    if (S.v) ast32s(wseg, 4 * S.p, m ? (m << 24 | d) : 0u);
+    uint4 y = to4(S.y);
+    if (S.tail) y = fix16(y, S.q, cbytes);
+    const uint32_t m = S.k ? min(prefix16(S.x, y), lim) : 0u;
+    if (S.v) ast32s(wseg, 4 * S.p, m >= zs::kMinMatch ? (m << 24 | (S.p - S.q)) : 0u);
   };
-  // one tile; n: its own bytes on entry, the bytes of the tile two ahead on
-  // exit; S: the tile two back on entry (verified here), this tile on exit.
-  // The loop below alternates two (n, S) sets, so no register with a pending
-  // load is ever copied.  Per step the memory operations are: the verified
-  // word's store (or none), then the loads ys, yl, n; a step's loads are
-  // used two steps later, after the three loads of the step between (vmcnt(3)).
 #ifdef MCDC_ZC_TIMING  // (A/B: cycles per phase of wave 0 in some workgroups, printed)
   uint64_t tm[5] = {0, 0, 0, 0, 0}, tstart = __builtin_amdgcn_s_memtime(), tnow = 0;
   uint32_t nsteps = 0;
@@ -287,13 +275,17 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
 #else
 #define ZC_TICK(k) ((void)0)
 #endif
+  // one tile; n: its own bytes on entry, the bytes of the tile two ahead on
+  // exit; S: the tile two back on entry (verified here), this tile on exit.
+  // The loop below alternates two (n, S) sets, so no register with a pending
+  // load is ever copied.  Per step the memory operations are: the verified
+  // word's store (or none), then the loads y (every lane: a lane without a
+  // candidate reads its own position, so the count is fixed) and n; a
+  // step's loads are used two steps later, after the 2 loads of the step
+  // between.
   auto step = [&](uint32_t t0, u32x4 &n, Stage &S) {
     ZC_TICK(4);
-#if MCDC_ZC_LOOK == 4
-    asm volatile("s_waitcnt vmcnt(4)" : "+v"(n), "+v"(S.ys), "+v"(S.yl)::"memory");
-#else
-    asm volatile("s_waitcnt vmcnt(3)" : "+v"(n), "+v"(S.ys), "+v"(S.yl)::"memory");
-#endif
+    asm volatile("s_waitcnt vmcnt(2)" : "+v"(n), "+v"(S.y)::"memory");
     ZC_TICK(0);
     const uint32_t p = t0 + tid;
     const bool tail = t0 >= tail0;
@@ -301,36 +293,28 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
     if (tail) x = fix16(x, p, cbytes);
     const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert; tiles past the segment: nothing kept)
     const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
-    const uint32_t hs = hash5(x.x, x.y), hl = hash8(x.x, x.y);
-    const uint32_t cs = find && vs ? hts[hs] : 0u, cl = find && vl ? htl[hl] : 0u;
-    // candidates within the window (a table holds positions before this tile)
-    const bool oks = cs != 0 && p - (cs - 1) <= zs::kWindow;
-    const bool okl = cl != 0 && cl != cs && p - (cl - 1) <= zs::kWindow;
-    const uint32_t qs = oks ? cs - 1 : 0u, ql = okl ? cl - 1 : 0u;
+    const uint32_t hs = hash5(x.x, x.y), hl = hash8(x.x, x.y), gs = tag5(x.x, x.y), gl = tag8(x.x, x.y);
+    const uint32_t es = find && vs ? hts[hs] : 0u, el = find && vl ? htl[hl] : 0u;
     verify(S);
     ZC_TICK(1);
+    // the candidate: the long key's if its tag matches, else the short key's
+    const uint32_t cl = prime0 + (el >> 13) - 1, cs = prime0 + (es >> 13) - 1;
+    const bool okl = el != 0 && (el & 0x1FFFu) == gl && p - cl <= zs::kWindow;
+    const bool oks = es != 0 && (es & 0x1FFFu) == gs && p - cs <= zs::kWindow;
+    const uint32_t q = okl ? cl : oks ? cs : p;
     S.v = find;
-    S.ks = oks;
-    S.kl = okl;
+    S.k = okl || oks;
     S.tail = tail;
     S.p = p;
-    S.qs = qs;
-    S.ql = ql;
+    S.q = q;
     S.x = x;
-#ifdef MCDC_ZC_NOVERIFY  // (A/B: the finder without its candidate loads; no matches, see verify)
-    S.ys = S.yl = u32x4{qs, ql, ~0u, ~0u};
-    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
-    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
-    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
-#else
-    S.ys = ald16s(cb, min(qs, last16));
-    S.yl = ald16s(cb, min(ql, last16));
-    n = ald16s(cb, min(p + MCDC_ZC_LOOK * kFindTile, last16));
-#endif
+    S.y = ald16s(cb, min(q, last16));
+    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+    const uint32_t r = (p - prime0 + 1) << 13;
     lds_sync();  // every lookup of the tile before any insert
     ZC_TICK(2);
-    if (vs) atomicMax(hts + hs, p + 1);
-    if (vl) atomicMax(htl + hl, p + 1);
+    if (vs) atomicMax(hts + hs, r | gs);
+    if (vl) atomicMax(htl + hl, r | gl);
     lds_sync();  // every insert before the next tile's lookups
     ZC_TICK(3);
 #ifdef MCDC_ZC_TIMING
@@ -340,22 +324,11 @@ __global__ __launch_bounds__(kFindTile) void k_zc_find(const uint8_t *base, uint
   __syncthreads();
   // (both steps unconditional: a tile past the segment keeps nothing, and a
   // join after a conditional step would cost the compiler's own waits)
-#if MCDC_ZC_LOOK == 4
-  for (uint32_t t0 = prime0; t0 < seg1; t0 += 4 * kFindTile) {
-    step(t0, n0, s0);
-    step(t0 + kFindTile, n1, s1);
-    step(t0 + 2 * kFindTile, n2, s0);
-    step(t0 + 3 * kFindTile, n3, s1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3), "+v"(s0.ys), "+v"(s0.yl), "+v"(s1.ys),
-               "+v"(s1.yl)::"memory");
-#else
   for (uint32_t t0 = prime0; t0 < seg1; t0 += 2 * kFindTile) {
     step(t0, n0, s0);
     step(t0 + kFindTile, n1, s1);
   }
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(s0.ys), "+v"(s0.yl), "+v"(s1.ys), "+v"(s1.yl)::"memory");
-#endif
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(s0.y), "+v"(s1.y)::"memory");
   verify(s0);
   verify(s1);
 #ifdef MCDC_ZC_TIMING
@@ -1295,7 +1268,7 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
-  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindTile), 0, st, base, nbytes, blocks, nblk, words);
+  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
                      seqs);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words);

@@ -64,7 +64,7 @@ for stage in "$@"; do
     for so in $R/abship/*.so; do
       b=$(basename $so .so)
       MCDC_LIBRARY=$so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/zcabs_$b -o zc --output-format csv -- \
-        python3 $R/tools/zc_bench.py 1 2 text > $OUT/zcabs_$b.json 2> $OUT/zcabs_$b.err || { echo "zcabs $b rc=$?"; exit 1; }
+        python3 $R/tools/zc_bench.py 1 2 ${ZCAB_KIND:-text} > $OUT/zcabs_$b.json 2> $OUT/zcabs_$b.err || { echo "zcabs $b rc=$?"; exit 1; }
       echo "== $b $(cat $OUT/zcabs_$b.json)"
       python3 $R/tools/kcsv.py $OUT/zcabs_$b/zc_kernel_stats.csv
     done

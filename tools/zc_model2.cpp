@@ -109,8 +109,22 @@ int main(int argc, char **argv) {
           if (m > best) best = m, bo = q - cc;
         };
         const uint32_t hs = hshort(p + q);
-        try_c(st[hs]);
-        if (llog) try_c(lt[hlong(p + q)]);
+        static const int single = getenv("ZC_SINGLE") ? atoi(getenv("ZC_SINGLE")) : 0;
+        if (single == 2 && llog) {  // tags: the long candidate if its 8-byte key matches, else the short if its 5 bytes do
+          const uint32_t cl = lt[hlong(p + q)], cs = st[hs];
+          auto keyeq = [&](uint32_t c, uint32_t nbk) {
+            return c && c - 1 < q && q - (c - 1) <= reach && std::memcmp(p + c - 1, p + q, nbk) == 0;
+          };
+          if (keyeq(cl, 8)) try_c(cl);
+          else if (keyeq(cs, 5)) try_c(cs);
+        } else if (single && llog) {  // one candidate verified: the long table's if it has one in reach, else the short's
+          const uint32_t cl = lt[hlong(p + q)];
+          if (cl && cl - 1 < q && q - (cl - 1) <= reach) try_c(cl);
+          else try_c(st[hs]);
+        } else {
+          try_c(st[hs]);
+          if (llog) try_c(lt[hlong(p + q)]);
+        }
         if (intra) {
           st[hs] = q + 1;
           if (llog) lt[hlong(p + q)] = q + 1;
