@@ -352,29 +352,35 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
 #define ZT_PRINT(name, cond)
 #endif
 
-// Inclusive sum over the wave's 64 lanes.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)v, d);
-    if (lane >= d) v += t;
-  }
+// Wave scans with DPP (row shifts within 16-lane rows, then the row
+// broadcasts of lanes 15 and 31): VALU operand modifiers, where __shfl_up /
+// __shfl_xor go through the LDS crossbar (ds_bpermute) at LDS latency per step.
+#define MCDC_DPP(old, v, ctrl, rm) ((uint32_t)__builtin_amdgcn_update_dpp((int)(old), (int)(v), ctrl, rm, 0xf, false))
+// Inclusive sum over the wave's 64 lanes (all lanes active).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t) {
+  v += MCDC_DPP(0, v, 0x111, 0xf);  // row_shr:1
+  v += MCDC_DPP(0, v, 0x112, 0xf);  // row_shr:2
+  v += MCDC_DPP(0, v, 0x114, 0xf);  // row_shr:4
+  v += MCDC_DPP(0, v, 0x118, 0xf);  // row_shr:8
+  v += MCDC_DPP(0, v, 0x142, 0xa);  // row_bcast:15 into rows 1, 3
+  v += MCDC_DPP(0, v, 0x143, 0xc);  // row_bcast:31 into rows 2, 3
   return v;
 }
 // Inclusive max over the wave's 64 lanes (values >= -1).
-__device__ __forceinline__ int32_t wave_incl_max(int32_t v, uint32_t lane) {
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const int32_t t = __shfl_up(v, d);
-    if (lane >= d) v = max(v, t);
-  }
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v, uint32_t) {
+  v = max(v, (int32_t)MCDC_DPP(-1, v, 0x111, 0xf));
+  v = max(v, (int32_t)MCDC_DPP(-1, v, 0x112, 0xf));
+  v = max(v, (int32_t)MCDC_DPP(-1, v, 0x114, 0xf));
+  v = max(v, (int32_t)MCDC_DPP(-1, v, 0x118, 0xf));
+  v = max(v, (int32_t)MCDC_DPP(-1, v, 0x142, 0xa));
+  v = max(v, (int32_t)MCDC_DPP(-1, v, 0x143, 0xc));
   return v;
 }
-__device__ __forceinline__ int32_t wave_max(int32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
-  return v;
-}
+// The value of the lane below (wave_shr:1); lane 0 gets old.
+__device__ __forceinline__ int32_t wave_shr1(int32_t v, int32_t old) { return (int32_t)MCDC_DPP(old, v, 0x138, 0xf); }
+__device__ __forceinline__ int32_t lane63(int32_t v) { return __builtin_amdgcn_readlane(v, 63); }
+__device__ __forceinline__ int32_t wave_max(int32_t v) { return lane63(wave_incl_max(v, 0)); }
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane63((int32_t)wave_incl_sum(v, 0)); }
 
 // The greedy parse of one block over k_zc_find's words, 256 positions per
 // window (position i of the window in lane i % 64, slot i / 64), without a
@@ -524,9 +530,12 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       const uint32_t mr = mcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       const uint32_t lr = lcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
       // exclusive scans over this slot's lanes, carried from the earlier slots
-      const int32_t ie = wave_incl_max(m ? (int32_t)(q + mlen) : -1, lane), ii = wave_incl_max(m ? (int32_t)i : -1, lane);
-      int32_t pe = __shfl_up(ie, 1), pi = __shfl_up(ii, 1);
-      if (lane == 0) pe = pi = -1;
+      // (one scan: the match index in the high half, its end - wb in the low;
+      // the last match at or before a lane has both the largest index and end)
+      const int32_t key = wave_incl_max(m ? (int32_t)(i << 16 | (i + mlen)) : -1, lane);
+      const int32_t pk = wave_shr1(key, -1);
+      const int32_t ie = key >= 0 ? (int32_t)(wb + (key & 0xFFFF)) : -1, ii = key >= 0 ? key >> 16 : -1;
+      int32_t pe = pk >= 0 ? (int32_t)(wb + (pk & 0xFFFF)) : -1, pi = pk >= 0 ? pk >> 16 : -1;
       pe = max(pe, pend);
       pi = max(pi, pidx);
       if (m) {
@@ -537,8 +546,8 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         sq[nseq + mr] = zs::seq_pack_ov(ll, mlen, ov);
       }
       if (l) lit[nlit + lr] = reinterpret_cast<const uint8_t *>(wbyt)[i];
-      pend = max(pend, __shfl(ie, 63));
-      pidx = max(pidx, __shfl(ii, 63));
+      pend = max(pend, lane63(ie));
+      pidx = max(pidx, lane63(ii));
       mcount += (uint32_t)__builtin_popcountll(bm);
       lcount += (uint32_t)__builtin_popcountll(bl);
       if (in) exit_pos = max(exit_pos, q + (m ? mlen : 1u));
@@ -710,8 +719,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
         if (16u * c + j < L) b += ctw[byte_at(q, 16 * c + j)] >> 16;
     }
     npc[k] = b;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) b += (uint32_t)__shfl_xor((int)b, d);
+    b = wave_sum(b);
     sb[k] = b;
   }
   ZT(2);
@@ -1095,8 +1103,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
         const uint32_t llc = ll_code(seq_ll(q)), mlc = ml_code(seq_ml(q) - 3), ofc = highbit(seq_ov(q));
         tot += (rr & 15) + ((rr >> 16) & 15) + ((rr >> 32) & 15) + ll_bits(llc) + ml_bits(mlc) + ofc;
       }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) tot += (uint64_t)__shfl_xor((long long)tot, d);
+      tot = wave_sum((uint32_t)tot);  // (< 2^32 bits: a block's sequences)
       const uint64_t all_bits = tot + tl0 + tl1 + tl2 + 1;  // + final states + end mark
       const uint32_t nbytes = (uint32_t)((all_bits + 7) / 8);
       const uint32_t total = at + hsz + nbytes;
@@ -1143,13 +1150,8 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
             put(mb, ml_bits(mlc));
             put(ob, ofc);
           }
-          uint32_t incl = nb;  // inclusive prefix in lane order = writing order
-#pragma unroll
-          for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += t;
-          }
-          const uint32_t tbits = (uint32_t)__shfl((int)incl, 63);
+          const uint32_t incl = wave_incl_sum(nb, lane);  // inclusive prefix in lane order = writing order
+          const uint32_t tbits = (uint32_t)lane63((int32_t)incl);
           for (uint32_t k = lane; k < kWbWords; k += 64) wb[k] = 0;
           if (lane == 0) wb[0] = carry;
           __syncthreads();
