@@ -589,11 +589,17 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
 // (LDS ~9 KiB per wave: 16 waves per CU; the section itself stays in HBM.)
 __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
                                                 uint8_t *stage, uint32_t *scratch) {
-  __shared__ __attribute__((aligned(16))) uint32_t hist[4][256];
-  uint32_t *const ctw = hist[1];  // (after the counts are merged into hist[0])
+  // LDS: the counts (4 copies while counting, merged into the first), then
+  // in the place of copies 1-3, one after another: huf_build's work, the
+  // description's work, the code table ctw (6.4 KiB in all: 25 waves per CU)
+  constexpr uint32_t kRegion = (sizeof(HufWork) > 768 * 4 ? sizeof(HufWork) : 768 * 4) / 4;
+  static_assert(sizeof(HufDescWork) <= kRegion * 4 && sizeof(HufWork) % 4 == 0, "huff LDS layout");
+  __shared__ __attribute__((aligned(16))) uint32_t pool[256 + kRegion];
+  uint32_t(*const hist)[256] = reinterpret_cast<uint32_t(*)[256]>(pool);
+  HufWork &hw = *reinterpret_cast<HufWork *>(pool + 256);
+  HufDescWork &dw = *reinterpret_cast<HufDescWork *>(pool + 256);
+  uint32_t *const ctw = pool + 256;
   __shared__ HufCT ct;
-  __shared__ HufWork hw;
-  __shared__ HufDescWork dw;
   __shared__ uint8_t tdesc[132];
   __shared__ uint32_t tree_sz;
   const uint64_t bi = blockIdx.x;
@@ -694,29 +700,36 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   const bool one = n < 1024;
   const uint32_t seg = one ? n : (n + 3) / 4, ns = one ? 1 : 4;
   const uint64_t lim = B.nseq ? (uint64_t)n + 64 : nbytes - B.src;  // bytes readable at src
-  auto piece = [&](uint32_t k, u32x4 *q, uint32_t &L, uint32_t &P) {
+  // (chunk c of the piece in q[c], or in q[nc - 1 - c] with rev; the loops
+  // below take q[0] and shift the rest down, so the code is not unrolled
+  // over the whole piece: the instruction cache holds it)
+  auto piece = [&](uint32_t k, u32x4 *q, uint32_t &L, uint32_t &P, bool rev) {
     const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
     P = (len + 63) / 64;
     const uint32_t w0 = min(lane * P, len), w1 = min(w0 + P, len);
     L = w1 - w0;
-    const uint32_t a0 = e - w1;
+    const uint32_t a0 = e - w1, nc = (P + 15) / 16;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      if (16u * c < P) q[c] = ld16z(src, a0 + 16u * c, lim);
+      if ((uint32_t)c < nc) q[c] = ld16z(src, a0 + 16u * (rev ? nc - 1 - c : c), lim);
   };
-  auto byte_at = [&](const u32x4 *q, const int b) -> uint32_t { return (q[b >> 4][(b >> 2) & 3] >> (8 * (b & 3))) & 0xFFu; };
+  auto shift_down = [&](u32x4 *q) {
+#pragma unroll
+    for (int c = 0; c < 7; ++c) q[c] = q[c + 1];
+  };
+  auto byte_of = [&](u32x4 v, const int j) -> uint32_t { return (v[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
   uint32_t sb[4] = {0, 0, 0, 0}, npc[4] = {0, 0, 0, 0};
   for (uint32_t k = 0; k < ns; ++k) {
     u32x4 q[8];
     uint32_t L, P;
-    piece(k, q, L, P);
+    piece(k, q, L, P, false);
     uint32_t b = 0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      if (16u * c >= P) break;
+    for (uint32_t c = 0; 16u * c < P; ++c) {
+      const u32x4 v = q[0];
 #pragma unroll
       for (int j = 0; j < 16; ++j)
-        if (16u * c + j < L) b += ctw[byte_at(q, 16 * c + j)] >> 16;
+        if (16u * c + j < L) b += ctw[byte_of(v, j)] >> 16;
+      shift_down(q);
     }
     npc[k] = b;
     b = wave_sum(b);
@@ -739,20 +752,20 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   for (uint32_t k = 0; k < ns; ++k) {
     u32x4 q[8];
     uint32_t L, P;
-    piece(k, q, L, P);
+    piece(k, q, L, P, true);
     const uint32_t nbits = npc[k];
     const uint32_t incl = wave_incl_sum(nbits, lane);
     const uint64_t bit = 8ull * o + (incl - nbits);
     uint64_t acc = 0;
     uint32_t accn = (uint32_t)(bit & 31), wi = (uint32_t)(bit >> 5);
     bool first = true;
-#pragma unroll
-    for (int c = 7; c >= 0; --c) {
-      if (16u * c >= P) continue;
+    const uint32_t nc = (P + 15) / 16;
+    for (uint32_t cc = nc; cc-- > 0;) {  // chunk cc of the piece is q[0] here
+      const u32x4 v = q[0];
 #pragma unroll
       for (int j = 15; j >= 0; --j) {
-        if (16u * c + j < L) {
-          const uint32_t t = ctw[byte_at(q, 16 * c + j)];
+        if (16u * cc + j < L) {
+          const uint32_t t = ctw[byte_of(v, j)];
           acc |= (uint64_t)(t & 0xFFFFu) << accn;
           accn += t >> 16;
           if (accn >= 32) {
@@ -765,6 +778,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
           }
         }
       }
+      shift_down(q);
     }
     if (nbits && accn) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece after)
     const uint32_t end = 8 * o + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
