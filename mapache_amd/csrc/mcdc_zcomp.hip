@@ -458,29 +458,38 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     nwb = wb + 256;
     issue(nwb, nwd, nby);  // (the next window's, in flight meanwhile)
     ZT(0);
-    uint32_t ml[4], nx[4];
+    uint32_t ml[4], cj[4];
     bool valid[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane;
       valid[j] = wb + i < end;
       ml[j] = wd[j] >> 24;
-      nx[j] = valid[j] ? i + (ml[j] ? ml[j] : 1u) : 0x7FFFFFFFu;
-      J[0][i] = (uint16_t)min(nx[j], 256u);
+      cj[j] = valid[j] ? min(i + (ml[j] ? ml[j] : 1u), 256u) : 256u;
+      J[0][i] = (uint16_t)cj[j];
       offl[i] = wd[j] & 0xFFFFFFu;
       mk[i] = (uint8_t)(i == s0);
     }
-    for (int k = 0; k < 7; ++k)
+    // J_k of the lane's own positions stay in registers (16 bits each): a
+    // doubling round reads only J_k(J_k(i)), marking reads only mk
+    uint32_t jr[8][2];
+    jr[0][0] = cj[0] | cj[1] << 16;
+    jr[0][1] = cj[2] | cj[3] << 16;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 64 * j + lane;
-        J[k + 1][i] = J[k][J[k][i]];
-      }
+    for (int k = 0; k < 7; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cj[j] = J[k][cj[j]];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) J[k + 1][64 * j + lane] = (uint16_t)cj[j];
+      jr[k + 1][0] = cj[0] | cj[1] << 16;
+      jr[k + 1][1] = cj[2] | cj[3] << 16;
+    }
+#pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t i = 64 * j + lane;
-        if (mk[i]) mk[J[k][i]] = 1;
+        if (mk[i]) mk[(jr[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = 1;
       }
     ZT(1);
     bool node[4], mt[4];
