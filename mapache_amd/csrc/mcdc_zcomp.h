@@ -13,7 +13,10 @@ constexpr uint64_t kZcBlock = 32768;               // zstd block: 32 KiB of one 
 constexpr uint32_t kZcSeqCap = kZcBlock / 4;       // sequences per block: every match is >= 4 bytes
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
 constexpr uint32_t kZcSegBlocks = 8;               // blocks of a chunk one match-finder workgroup covers
-constexpr uint64_t kZcBatchBlocks = 8192;          // blocks per batch (256 MiB; more for a longer chunk)
+#ifndef MCDC_ZC_BATCH
+#define MCDC_ZC_BATCH 16384  // (compile-time A/B knob)
+#endif
+constexpr uint64_t kZcBatchBlocks = MCDC_ZC_BATCH;  // blocks per batch (512 MiB; more for a longer chunk)
 
 struct ZcBlock {
   uint64_t src;                 // chunk bytes [src, src + len) of the input
@@ -31,7 +34,7 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 // Scratch per batch of nblk blocks (bytes), all device memory of the context:
 //   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot, seqs nblk x kZcSeqCap
 //   x 8, state records nblk x kZcSeqCap x 8, match words (nblk x kZcBlock +
-//   1024) x 4 (6.6 x the batch's input in all),
+//   1024) x 4 (9 x the batch's input in all: 4.5 GiB for a full batch),
 //   piece / poff (nblk + 1) x 8.  A batch holds whole chunks, at most
 //   kZcBatchBlocks blocks unless one chunk is longer (1 GiB: 7 x 2^18 words).
 // one batch: the chunks [c0, c1), blocks [b0, b0 + nblk)
