@@ -3,28 +3,30 @@
 // (/root/reference/src/repository/storage.rs:74-84) on the GPU, so the save
 // path chunk -> IDs -> compress -> seal never leaves HBM.  One zstd frame per
 // chunk (the blob mapache stores), in the crate's frame layout (magic, no
-// content size, window 2^20, no checksum); blocks of 16 KiB, each either
+// content size, window 2^20, no checksum); blocks of 32 KiB, each either
 // compressed (Huffman / RLE / raw literals + FSE sequences, predefined or per-block tables,
 // mcdc_zstd.h) or raw when that is not smaller.  Decodes with mapache's decoder (storage.rs:87-94).
 //
-// Per batch of blocks (a block = 32 KiB of one chunk; batches bound the
-// scratch):
+// Per batch of blocks (a block = 32 KiB of one chunk; batches of whole chunks
+// bound the scratch, mcdc_zcomp.h):
 //   k_zc_blocks  block records of the batch's chunks (chunk, index, source)
-//   k_zc_find    ONE WORKGROUP (4 waves) PER SEGMENT of up to 8 blocks of a
-//                chunk: candidate matches for every position.  Two tables of
-//                32-bit positions in LDS (160 KiB: 2^15 slots for a 5-byte
-//                key and 2^13 for an 8-byte key, as zstd's double-fast pair),
-//                filled 256 positions at a time: a tile reads its candidates
-//                from the tables as the earlier tiles left them, then inserts
-//                its own positions with LDS max atomics (the latest position
-//                per slot, deterministically).  A segment after a chunk's
-//                first re-inserts the 128 KiB before it.  Each candidate is
-//                verified on 16 bytes, a tile later (its loads in flight
-//                meanwhile); per position one word (match length <= 16 << 24
-//                | offset, 0 = none) to scratch
+//   k_zc_find    ONE WORKGROUP (8 waves) PER SEGMENT of up to 8 blocks of a
+//                chunk: candidate matches for every position.  Two LDS tables
+//                (160 KiB: 2^15 slots for a 5-byte key and 2^13 for an 8-byte
+//                key, as zstd's double-fast pair) of 32-bit entries: a
+//                segment-relative position and a 13-bit tag of the key.
+//                Filled 512 positions at a time: a tile reads the tables as
+//                the earlier tiles left them, then inserts its own positions
+//                with LDS max atomics (the latest position per slot,
+//                deterministically).  One candidate per position, the long
+//                key's when its tag matches, else the short key's, verified
+//                on 16 bytes two tiles later (its loads in flight meanwhile);
+//                per position one word (match length <= 16 << 24 | offset,
+//                0 = none) to scratch.  A segment after a chunk's first
+//                re-inserts the 128 KiB before it.
 //   k_zc_parse   ONE WAVE PER BLOCK: the greedy parse over the words, 256
 //                positions per window without a serial walk: the chain from
-//                the cursor by pointer doubling in LDS, its matches, literal
+//                the cursor by pointer doubling, its matches, literal
 //                lengths and indices by wave scans; a match of 16 verified
 //                bytes on the chain extended 1 KiB per step; repeat code 1
 //                for an offset equal to the previous sequence's; literals to
@@ -35,14 +37,12 @@
 //                values in LDS, symbols ranked by the wave, the
 //                length-limited canonical code and its description (direct
 //                or FSE-compressed weights) by one lane, then the streams
-//                (four above 1023 literals) by the whole wave, bit positions
-//                from wave scans, assembled in LDS
-//   k_zc_encode  ONE WAVE PER BLOCK: per symbol type the block's own FSE
-//                table or the predefined one (seq_plan), the three state
-//                machines on three lanes (their bits to scratch), then every
-//                sequence's bits placed by the whole wave (wave scans of bit
-//                counts, OR-ed into place); block kept compressed only if
-//                smaller than raw
+//                (four above 1023 literals) by the whole wave in lane pieces
+//   k_zc_plan    ONE WAVE PER BLOCK: per symbol type the block's own FSE
+//   k_zc_chain   table or the predefined one (seq_plan); the three state
+//   k_zc_encode  machines of 9 blocks per wave, one per lane (their bits to
+//                scratch); then every sequence's bits placed by the block's
+//                wave; the block kept compressed only if smaller than raw
 //   scan         piece sizes (frame header on a chunk's first block, block
 //                header, content) -> output offsets, frames back to back
 //   k_zc_final   ONE WAVE PER BLOCK: headers + content (staging or input)
@@ -60,14 +60,14 @@ namespace {
 using namespace zs;
 
 // Match finder tables in LDS: 2^15 slots for a 5-byte key and 2^13 for an
-// 8-byte key (zstd's double-fast pair), 32-bit chunk positions (+ 1, 0 =
-// empty): 160 KiB, the whole of a CU's LDS.  Inserts are LDS max atomics, so
-// a slot ends at the latest position whichever lane's atomic lands last.
+// 8-byte key (zstd's double-fast pair), 32-bit entries (position << 13 | tag,
+// 0 = empty): 160 KiB, the whole of a CU's LDS.  Inserts are LDS max atomics,
+// so a slot ends at the latest position whichever lane's atomic lands last.
 // tools/zc_model2.cpp priced the choices on the bench's corpora (16/64/256
 // KiB chunks; text / records / binary): one 2^14 table 2.44 / 3.20 / 1.74;
-// 2^15 + 2^13 2.59 / 3.30 / 1.78; zstd level 3 2.68 / 3.23 / 1.78.  256
-// positions per tile cost < 0.5 % against exact most-recent insertion (512:
-// 1 % on records and binary).
+// 2^15 + 2^13 2.59 / 3.30 / 1.78; zstd level 3 2.68 / 3.23 / 1.78.  Tiles of
+// 512 positions cost ~1 % on records and binary against exact most-recent
+// insertion.
 #ifndef MCDC_ZC_HS
 #define MCDC_ZC_HS 15  // (compile-time A/B knobs)
 #endif
