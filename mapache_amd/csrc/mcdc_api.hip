@@ -235,7 +235,8 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, sv_comp, sv_seal, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs;
+      sv_in, sv_pack, sv_comp, sv_seal, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs,
+      zc_blocks2, zc_stage2, zc_seqs2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_recs2;  // (the second batch set)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -938,7 +939,9 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
                     &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
-                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_recs};
+                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_recs,
+                    &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_seqs2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
+                    &ctx->zc_words2, &ctx->zc_recs2};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1890,25 +1893,59 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   const uint64_t total_blocks = hfirst[nchunks];
   uint64_t longest = 0;  // a batch holds whole chunks
   for (size_t i = 0; i < nchunks; ++i) longest = std::max<uint64_t>(longest, hfirst[i + 1] - hfirst[i]);
-  const uint64_t mb = std::max(std::min<uint64_t>(total_blocks, kZcBatchBlocks), longest);
+  // Batches alternate between two scratch sets on the context's two streams,
+  // so one batch's kernels run into the other's tails; only the final copies
+  // (output offsets carried from batch to batch) are ordered across streams.
+  // One set when a single batch of kZcBatchBlocks / 2 holds everything.
+  const bool two = total_blocks > kZcBatchBlocks / 2 && longest <= kZcBatchBlocks / 2;
+  const uint64_t mb = two ? kZcBatchBlocks / 2 : std::max(std::min<uint64_t>(total_blocks, kZcBatchBlocks), longest);
   tmpb = std::max(tmpb, zc_tmp_bytes(mb));
-  if ((rc = ensure(ctx, ctx->zc_tmp, tmpb))) return rc;
-  if ((rc = ensure(ctx, ctx->zc_blocks, mb * sizeof(ZcBlock))) || (rc = ensure(ctx, ctx->zc_stage, mb * kZcSlot)) ||
-      (rc = ensure(ctx, ctx->zc_seqs, mb * kZcSeqCap * 8)) || (rc = ensure(ctx, ctx->zc_piece, (mb + 1) * 8)) ||
-      (rc = ensure(ctx, ctx->zc_poff, (mb + 1) * 8)) || (rc = ensure(ctx, ctx->zc_words, (mb * kZcBlock + 1024) * 4)) ||
-      (rc = ensure(ctx, ctx->zc_recs, mb * kZcSeqCap * 8)))
-    return rc;
-  for (uint64_t c0 = 0; c0 < nchunks;) {  // batches of whole chunks, <= kZcBatchBlocks blocks each
+  struct Set {
+    DevBuf *blocks, *stage, *seqs, *piece, *poff, *tmp, *words, *recs;
+  } sets[2] = {{&ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs, &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_tmp,
+                &ctx->zc_words, &ctx->zc_recs},
+               {&ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_seqs2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
+                &ctx->zc_words2, &ctx->zc_recs2}};
+  for (int k = 0; k < (two ? 2 : 1); ++k) {
+    const Set &z = sets[k];
+    if ((rc = ensure(ctx, *z.tmp, tmpb)) || (rc = ensure(ctx, *z.blocks, mb * sizeof(ZcBlock))) ||
+        (rc = ensure(ctx, *z.stage, mb * kZcSlot)) || (rc = ensure(ctx, *z.seqs, mb * kZcSeqCap * 8)) ||
+        (rc = ensure(ctx, *z.piece, (mb + 1) * 8)) || (rc = ensure(ctx, *z.poff, (mb + 1) * 8)) ||
+        (rc = ensure(ctx, *z.words, (mb * kZcBlock + 1024) * 4)) || (rc = ensure(ctx, *z.recs, mb * kZcSeqCap * 8)))
+      return rc;
+  }
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // [0] setup done on st; [1 + k] set k's last final copy
+  auto destroy = [&]() {
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (auto &e : ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return e = nullptr, destroy(), fail(MCDC_E_DEVICE, "event creation failed");
+  hipStream_t ss[2] = {st, ctx->stream2};
+  if (two) {
+    rc = hipEventRecord(ev[0], st) == hipSuccess && hipStreamWaitEvent(ss[1], ev[0], 0) == hipSuccess
+             ? MCDC_OK
+             : fail(MCDC_E_DEVICE, "stream ordering failed");
+    if (rc) return destroy(), rc;
+  }
+  int k = 0, prev = -1;  // set of the batch, set of the batch before
+  for (uint64_t c0 = 0; c0 < nchunks; k ^= two ? 1 : 0) {  // batches of whole chunks, <= mb blocks each
     uint64_t c1 = c0 + 1;
     while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb) ++c1;
+    const Set &z = sets[k];
     launch_zc_batch((const uint8_t *)d_data, n, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
-                    (ZcBlock *)ctx->zc_blocks.p, (uint8_t *)ctx->zc_stage.p, (uint64_t *)ctx->zc_seqs.p,
-                    (uint32_t *)ctx->zc_words.p, (uint64_t *)ctx->zc_recs.p, T,
-                    (uint64_t *)ctx->zc_piece.p, (uint64_t *)ctx->zc_poff.p, misc + 2, (uint8_t *)d_out, ext,
-                    ctx->zc_tmp.p, tmpb, st, ctx->knobs.zc_huf);
-    HIP_TRY(hipGetLastError());
+                    (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
+                    (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
+                    ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
+                    two ? ev[1 + k] : nullptr);
+    if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
+    prev = k;
     c0 = c1;
   }
+  if (two && prev == 1 && hipStreamWaitEvent(st, ev[2], 0) != hipSuccess)
+    return destroy(), fail(MCDC_E_DEVICE, "stream ordering failed");
+  destroy();
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
   uint64_t total = 0;
   HIP_TRY(hipMemcpyAsync(&total, misc + 2, 8, hipMemcpyDeviceToHost, st));

@@ -42,6 +42,9 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
                      uint32_t *words, uint64_t *recs,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
-                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true);
+                     uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true,
+                     hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr);
+// (final_after: the output offsets' previous update, on another stream, is
+// waited for before this batch's final copy; final_done: recorded after it)
 
 }  // namespace mcdc

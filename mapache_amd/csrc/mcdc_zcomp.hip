@@ -1289,7 +1289,8 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
                      uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
-                     uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf) {
+                     uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
+                     hipEvent_t final_after, hipEvent_t final_done) {
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
@@ -1303,9 +1304,11 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, words, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);
+  if (final_after) (void)hipStreamWaitEvent(st, final_after, 0);
   hipLaunchKernelGGL(k_zc_final, dim3((unsigned)nblk), dim3(64), 0, st, base, blocks, nblk, stage, poff, obase, out,
                      ext);
   hipLaunchKernelGGL(k_zc_advance, dim3(1), dim3(64), 0, st, obase, poff, nblk);
+  if (final_done) (void)hipEventRecord(final_done, st);
 }
 
 }  // namespace mcdc
