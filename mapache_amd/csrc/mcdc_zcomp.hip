@@ -75,7 +75,10 @@ using namespace zs;
 #define MCDC_ZC_HL 13
 #endif
 constexpr uint32_t kHsLog = MCDC_ZC_HS, kHlLog = MCDC_ZC_HL;
-constexpr uint32_t kFindThreads = 512;   // threads per workgroup (8 waves)
+#ifndef MCDC_ZC_FT
+#define MCDC_ZC_FT 1024  // (compile-time A/B knob)
+#endif
+constexpr uint32_t kFindThreads = MCDC_ZC_FT;  // threads per workgroup (16 waves)
 constexpr uint32_t kFindTile = kFindThreads;  // positions per step
 constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
@@ -85,23 +88,17 @@ constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inser
 // an odd 24-bit constant, the low 32 bits of the products mixed; the index is
 // the top bits, which every bit of a piece reaches.
 __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t k) { return (uint32_t)__umul24(a, k); }  // (HIP's returns int)
-__device__ __forceinline__ uint32_t hash5(uint32_t lo, uint32_t hi) {
+// The index is the top bits of the mixed value, the 13-bit tag the bits
+// below them (kHsLog + 13 <= 32): one mix per key for both.
+__device__ __forceinline__ uint32_t mix5(uint32_t lo, uint32_t hi) {
   const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFu) << 8;
-  return (mul24(a, 0x9E3779u) + mul24(b, 0xC2B2AFu)) >> (32 - kHsLog);
+  return mul24(a, 0x9E3779u) + mul24(b, 0xC2B2AFu);
 }
-// 13-bit tags of the same keys (other multipliers: independent of the index)
-__device__ __forceinline__ uint32_t tag5(uint32_t lo, uint32_t hi) {
-  const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFu) << 8;
-  return (mul24(a, 0xA54FF5u) + mul24(b, 0x6C8E95u)) >> (32 - 13);
-}
-__device__ __forceinline__ uint32_t tag8(uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ uint32_t mix8(uint32_t lo, uint32_t hi) {
   const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFFFu) << 8, c = hi >> 16;
-  return (mul24(a, 0x4F1BBDu) ^ mul24(b, 0x9E3B75u) ^ mul24(c, 0x2C1B3Du)) >> (32 - 13);
+  return mul24(a, 0x85EBCBu) ^ mul24(b, 0x27D4EBu) ^ mul24(c, 0x165667u);
 }
-__device__ __forceinline__ uint32_t hash8(uint32_t lo, uint32_t hi) {
-  const uint32_t a = lo & 0xFFFFFFu, b = lo >> 24 | (hi & 0xFFFFu) << 8, c = hi >> 16;
-  return (mul24(a, 0x85EBCBu) ^ mul24(b, 0x27D4EBu) ^ mul24(c, 0x165667u)) >> (32 - kHlLog);
-}
+static_assert(kHsLog + 13 <= 32 && kHlLog + 13 <= 32, "index and tag bits of one mixed value");
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 // A workgroup barrier that orders LDS only: __syncthreads' workgroup fence
 // waits for every outstanding global load too (vmcnt(0) on gfx9), which
@@ -293,7 +290,9 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     if (tail) x = fix16(x, p, cbytes);
     const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert; tiles past the segment: nothing kept)
     const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
-    const uint32_t hs = hash5(x.x, x.y), hl = hash8(x.x, x.y), gs = tag5(x.x, x.y), gl = tag8(x.x, x.y);
+    const uint32_t m5 = mix5(x.x, x.y), m8 = mix8(x.x, x.y);
+    const uint32_t hs = m5 >> (32 - kHsLog), hl = m8 >> (32 - kHlLog);
+    const uint32_t gs = (m5 >> (32 - kHsLog - 13)) & 0x1FFFu, gl = (m8 >> (32 - kHlLog - 13)) & 0x1FFFu;
     const uint32_t es = find && vs ? hts[hs] : 0u, el = find && vl ? htl[hl] : 0u;
     verify(S);
     ZC_TICK(1);
