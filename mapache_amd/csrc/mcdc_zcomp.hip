@@ -164,28 +164,19 @@ __device__ __forceinline__ uint4 fix16(uint4 x, uint64_t p, uint64_t nbytes) {
   return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
 }
 
-// Loads the compiler's wait-count pass does not see.  On gfx9 one counter
+// Loads the compiler's wait-count pass does not see (ald16s and the inline
+// loads of the parse, Huffman and chain kernels).  On gfx9 one counter
 // (vmcnt) covers loads and stores, and with a store pending the pass treats
 // the counter as out of order and waits for zero before any use of a load:
 // a loop that stores a result per step and prefetches two steps ahead gets
-// every prefetch drained at the next step.  The match finder issues its
-// loads here and waits itself (vm_wait*, counting only its own loads: loads
-// return in order, a store may retire early), each wait taking the loaded
-// registers as operands so that no use is scheduled before it.
+// every prefetch drained at the next step.  These kernels issue such loads
+// themselves and wait with explicit s_waitcnt (counting only their own loads
+// where the count is exact: loads return in order, a store may retire
+// early), each wait taking the loaded registers as operands so that no use
+// is scheduled before it; devaudit checks no such register is read early.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 ald16c(const uint8_t *base, uint64_t p, uint64_t nbytes) {
-  const uint8_t *a = base + (p + 16 <= nbytes ? p : nbytes - 16);
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(a) : "memory");
-  return v;
-}
 __device__ __forceinline__ uint4 to4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
-// 16 bytes at base + p of the nbytes >= 16 readable there, bytes past the end zero.
-__device__ __forceinline__ u32x4 ld16z(const uint8_t *base, uint64_t p, uint64_t nbytes) {
-  const uint4 v = fix16(*reinterpret_cast<const uint4 *>(base + (p + 16 <= nbytes ? p : nbytes - 16)), p, nbytes);
-  return u32x4{v.x, v.y, v.z, v.w};
-}
-// (the same with a uniform base and a 32-bit offset: no 64-bit address math)
+// 16 bytes at sbase + off (a uniform base and a 32-bit offset: no 64-bit address math)
 __device__ __forceinline__ u32x4 ald16s(const uint8_t *sbase, uint32_t off) {
   u32x4 v;
   asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(off), "s"(sbase) : "memory");
@@ -413,7 +404,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   }
   // A window's words and source bytes (lane l: bytes [wb + 4 l, + 4)) are
   // requested a window ahead with loads outside the compiler's wait counting
-  // (see ald16c: the literal and sequence stores would otherwise drain them),
+  // (see ald16s: the literal and sequence stores would otherwise drain them),
   // and waited for at the next window's start, used or not.
   const uint64_t lim = nbytes - B.src;                                          // bytes readable at p0
   const bool wide = lim >= 4;                                                   // (else byte loads)
@@ -622,7 +613,13 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   ZT_DECL;
   for (uint32_t k = lane; k < 4 * 256; k += 64) (&hist[0][0])[k] = 0;
   __syncthreads();
-  // count (misaligned 16-byte loads: gfx950 reads the bytes at the address)
+  // streams: stream k holds literals [k seg, min((k + 1) seg, n)); four of
+  // them above 1023 literals
+  const bool one = n < 1024;
+  const uint32_t seg = one ? n : (n + 3) / 4, ns = one ? 1 : 4;
+  // count per stream (hist[k]), 16 bytes per lane per step (misaligned
+  // 16-byte loads: gfx950 reads the bytes at the address); a lane's 16 bytes
+  // cross at most one stream boundary (seg >= 256)
   for (uint32_t k0 = 0; k0 < n; k0 += 1024) {
     const uint32_t k = k0 + 16 * lane;
     uint32_t w[4] = {0, 0, 0, 0}, m = 0;
@@ -636,16 +633,20 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
       for (uint32_t j = 0; j < 16; ++j)
         if (j < m) w[j >> 2] |= (uint32_t)src[k + j] << (8 * (j & 3));
     }
+    const uint32_t s0 = one ? 0u : (k >= seg) + (k >= 2 * seg) + (k >= 3 * seg), nb0 = (s0 + 1) * seg;
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j)
-      if (j < m) atomicAdd(&hist[lane & 3][(w[j >> 2] >> (8 * (j & 3))) & 0xFF], 1u);
+      if (j < m) atomicAdd(&hist[s0 + (k + j >= nb0 ? 1u : 0u)][(w[j >> 2] >> (8 * (j & 3))) & 0xFF], 1u);
   }
   __syncthreads();
-  uint32_t c[4];
+  uint32_t c[4], cs[3][4];  // totals; streams 0-2's counts (stream 3's = total - the rest)
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const uint32_t k = lane + 64 * h;
-    c[h] = hist[0][k] + hist[1][k] + hist[2][k] + hist[3][k];
+    cs[0][h] = hist[0][k];
+    cs[1][h] = hist[1][k];
+    cs[2][h] = hist[2][k];
+    c[h] = cs[0][h] + cs[1][h] + cs[2][h] + hist[3][k];
   }
   __syncthreads();
 #pragma unroll
@@ -693,56 +694,22 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   ZT(1);
   const uint32_t tree = tree_sz;
   if (!tree) return;  // (no description applies: raw literals)
-  // code | length << 16 per symbol: one LDS read per literal
+  // code | length << 16 per symbol: one LDS read per literal; bits per stream
+  // from the per-stream counts
+  uint32_t sb[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
-    const uint32_t x = lane + 64 * h;
-    ctw[x] = ct.nb[x] ? (uint32_t)ct.code[x] | (uint32_t)ct.nb[x] << 16 : 0u;
+    const uint32_t x = lane + 64 * h, nb = ct.nb[x];
+    ctw[x] = nb ? (uint32_t)ct.code[x] | nb << 16 : 0u;
+    sb[0] += cs[0][h] * nb;
+    sb[1] += cs[1][h] * nb;
+    sb[2] += cs[2][h] * nb;
+    sb[3] += (c[h] - cs[0][h] - cs[1][h] - cs[2][h]) * nb;
   }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sb[k] = wave_sum(sb[k]);
+  if (one) sb[0] += sb[1] + sb[2] + sb[3];  // (one stream: every count is stream 0's)
   __syncthreads();
-  // Streams (stream k: literals [k seg, min((k + 1) seg, n))), each cut into
-  // 64 pieces in writing order (the last literal first): lane l's piece is
-  // the literals [e - w1, e - w0), w0 = l P, w1 = min(w0 + P, len), P <= 128,
-  // read with 16-byte loads into registers (bytes past what src holds read as
-  // zero) and walked from its last byte down.
-  const bool one = n < 1024;
-  const uint32_t seg = one ? n : (n + 3) / 4, ns = one ? 1 : 4;
-  const uint64_t lim = B.nseq ? (uint64_t)n + 64 : nbytes - B.src;  // bytes readable at src
-  // (chunk c of the piece in q[c], or in q[nc - 1 - c] with rev; the loops
-  // below take q[0] and shift the rest down, so the code is not unrolled
-  // over the whole piece: the instruction cache holds it)
-  auto piece = [&](uint32_t k, u32x4 *q, uint32_t &L, uint32_t &P, bool rev) {
-    const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
-    P = (len + 63) / 64;
-    const uint32_t w0 = min(lane * P, len), w1 = min(w0 + P, len);
-    L = w1 - w0;
-    const uint32_t a0 = e - w1, nc = (P + 15) / 16;
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if ((uint32_t)c < nc) q[c] = ld16z(src, a0 + 16u * (rev ? nc - 1 - c : c), lim);
-  };
-  auto shift_down = [&](u32x4 *q) {
-#pragma unroll
-    for (int c = 0; c < 7; ++c) q[c] = q[c + 1];
-  };
-  auto byte_of = [&](u32x4 v, const int j) -> uint32_t { return (v[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
-  uint32_t sb[4] = {0, 0, 0, 0}, npc[4] = {0, 0, 0, 0};
-  for (uint32_t k = 0; k < ns; ++k) {
-    u32x4 q[8];
-    uint32_t L, P;
-    piece(k, q, L, P, false);
-    uint32_t b = 0;
-    for (uint32_t c = 0; 16u * c < P; ++c) {
-      const u32x4 v = q[0];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (16u * c + j < L) b += ctw[byte_of(v, j)] >> 16;
-      shift_down(q);
-    }
-    npc[k] = b;
-    b = wave_sum(b);
-    sb[k] = b;
-  }
   ZT(2);
   uint32_t ssz[4];
   const uint32_t total = huf_section_size(tree, n, sb, one, ssz);
@@ -754,43 +721,85 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   const uint32_t nq = (total + 3) / 4 + 1;
   for (uint32_t k = lane; k < nq; k += 64) sw[k] = 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-  // the streams: a piece's bits packed in a register, stored a word at a
-  // time; the words it shares with its neighbours OR-ed in
+  // The streams, 256 literals per step in writing order (the last literal
+  // first): lane l takes writing indices 4 l .. 4 l + 3 of the step (one
+  // 4-byte load, read from its top byte down), a wave scan of the lanes' bit
+  // counts places them, their codes are OR-ed into an LDS ring of 512 words,
+  // and the ring's completed words go out with plain stores (a stream's first
+  // and last word, shared with its neighbours, OR-ed in).
+  uint32_t *const ring = pool + 512;
+  constexpr uint32_t kRing = 512;
+  static_assert(512 + kRing <= 256 + kRegion, "huff ring in the LDS pool");
   uint32_t o = hdr + tree + (one ? 0 : 6);  // byte offset of stream k in the section
   for (uint32_t k = 0; k < ns; ++k) {
-    u32x4 q[8];
-    uint32_t L, P;
-    piece(k, q, L, P, true);
-    const uint32_t nbits = npc[k];
-    const uint32_t incl = wave_incl_sum(nbits, lane);
-    const uint64_t bit = 8ull * o + (incl - nbits);
-    uint64_t acc = 0;
-    uint32_t accn = (uint32_t)(bit & 31), wi = (uint32_t)(bit >> 5);
-    bool first = true;
-    const uint32_t nc = (P + 15) / 16;
-    for (uint32_t cc = nc; cc-- > 0;) {  // chunk cc of the piece is q[0] here
-      const u32x4 v = q[0];
-#pragma unroll
-      for (int j = 15; j >= 0; --j) {
-        if (16u * cc + j < L) {
-          const uint32_t t = ctw[byte_of(v, j)];
-          acc |= (uint64_t)(t & 0xFFFFu) << accn;
-          accn += t >> 16;
-          if (accn >= 32) {
-            if (first) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece before)
-            else sw[wi] = (uint32_t)acc;
-            first = false;
-            acc >>= 32;
-            accn -= 32;
-            ++wi;
-          }
-        }
+    const uint32_t a = k * seg, e = min(a + seg, n), len = e - a;
+    const uint32_t fw = (8 * o) >> 5;  // the stream's first word
+    uint32_t bitp = 8 * o, ff = fw;    // next bit; first word not yet flushed
+    for (uint32_t u = lane; u < kRing; u += 64) ring[u] = 0;
+    auto flush = [&](uint32_t upto) {  // words [ff, upto) out, their ring slots zeroed
+      for (uint32_t i = ff + lane; i < upto; i += 64) {
+        const uint32_t v = ring[i & (kRing - 1)];
+        if (i == fw) atomicOr(sw + i, v);
+        else sw[i] = v;
+        ring[i & (kRing - 1)] = 0;
       }
-      shift_down(q);
+      ff = upto;
+    };
+    // lane's 4 bytes of the step at r0: literals e - 1 - w0 down to e - 4 - w0
+    // (w0 = r0 + 4 lane) are the 4 bytes at e - 4 - w0, clamped to the
+    // stream's first literal (the bytes below it shifted out); requested a
+    // step ahead, outside the compiler's wait counting (see ald16s)
+    auto issue = [&](uint32_t r0) {
+      const int32_t at = (int32_t)e - 4 - (int32_t)(r0 + 4 * lane);
+      const uint8_t *p = src + (at < (int32_t)a ? a : (uint32_t)at);
+      uint32_t v;
+      asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+      return v;
+    };
+    // (each step waits for everything outstanding first: its own bytes,
+    // requested two steps back, the next step's, requested one step back,
+    // and the previous flushes' stores)
+    auto step = [&](uint32_t r0, uint32_t &q) {
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
+      const uint32_t w0 = r0 + 4 * lane;
+      const uint32_t cnt = w0 < len ? min(len - w0, 4u) : 0u;
+      const int32_t at = (int32_t)e - 4 - (int32_t)w0;
+      const uint32_t below = at < (int32_t)a ? (uint32_t)((int32_t)a - at) : 0u;  // bytes below the stream (cnt < 4)
+      const uint32_t dw = below >= 4 ? 0u : q << (8 * below);
+      q = issue(r0 + 512);
+      uint32_t t[4], lb = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[j] = (uint32_t)j < cnt ? ctw[(dw >> (8 * (3 - j))) & 0xFFu] : 0u;
+        lb += t[j] >> 16;
+      }
+      const uint32_t incl = wave_incl_sum(lb, lane);
+      uint32_t off = bitp + incl - lb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t nb = t[j] >> 16;
+        if (nb) {
+          const uint32_t sh = off & 31, wd = off >> 5;
+          const uint64_t v = (uint64_t)(t[j] & 0xFFFFu) << sh;
+          atomicOr(ring + (wd & (kRing - 1)), (uint32_t)v);
+          if (sh + nb > 32) atomicOr(ring + ((wd + 1) & (kRing - 1)), (uint32_t)(v >> 32));
+        }
+        off += nb;
+      }
+      bitp += (uint32_t)lane63((int32_t)incl);
+      if ((bitp >> 5) - ff >= 128) flush(bitp >> 5);
+    };
+    uint32_t da = issue(0), db = issue(256);
+    for (uint32_t r0 = 0; r0 < len; r0 += 512) {  // (two registers alternate: no copy of a loading register)
+      step(r0, da);
+      if (r0 + 256 < len) step(r0 + 256, db);
     }
-    if (nbits && accn) atomicOr(sw + wi, (uint32_t)acc);  // (shared with the piece after)
-    const uint32_t end = 8 * o + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (lane == 0) atomicOr(sw + (end >> 5), 1u << (end & 31));  // the end mark
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(da), "+v"(db)::"memory");
+    // the end mark, then every word the stream touched (the last one OR-ed)
+    if (lane == 0) atomicOr(ring + ((bitp >> 5) & (kRing - 1)), 1u << (bitp & 31));
+    const uint32_t last = bitp >> 5;
+    flush(last);
+    if (lane == 0) atomicOr(sw + last, ring[last & (kRing - 1)]);
     o += ssz[k];
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
