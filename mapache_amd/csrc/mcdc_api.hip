@@ -1897,7 +1897,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   // so one batch's kernels run into the other's tails; only the final copies
   // (output offsets carried from batch to batch) are ordered across streams.
   // One set when a single batch of kZcBatchBlocks / 2 holds everything.
-  const bool two = total_blocks > kZcBatchBlocks / 2 && longest <= kZcBatchBlocks / 2;
+  const bool two = ctx->knobs.zc_two && total_blocks > kZcBatchBlocks / 2 && longest <= kZcBatchBlocks / 2;
   const uint64_t mb = two ? kZcBatchBlocks / 2 : std::max(std::min<uint64_t>(total_blocks, kZcBatchBlocks), longest);
   tmpb = std::max(tmpb, zc_tmp_bytes(mb));
   struct Set {

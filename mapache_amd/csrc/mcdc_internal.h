@@ -160,6 +160,7 @@ struct Knobs {
   int lane_walk = 1;      // MCDC_LANE_WALK: 0 group walk only, 1 lane walk when max <= 64 runs, 2 always
   int lane_seg_chunks = 4;// MCDC_LANE_SEG_CHUNKS: expected chunks per segment on the lane walk
   bool zc_huf = true;      // MCDC_ZC_HUF: Huffman / RLE literals in the GPU zstd compressor
+  bool zc_two = true;      // MCDC_ZC_TWO: compressor batches alternate between two streams
   bool test_fail_after_index = false;  // MCDC_TEST_FAIL_AFTER_INDEX: mcdc_save_files fails after its index
                                        // add (test hook: the rollback path, tests/test_gpu_save.py)
   // A/B builds only

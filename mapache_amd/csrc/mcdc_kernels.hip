@@ -2142,6 +2142,7 @@ Knobs read_knobs() {
   k.lane_walk = std::min(std::max(env("MCDC_LANE_WALK", k.lane_walk), 0), 2);
   k.lane_seg_chunks = std::max(env("MCDC_LANE_SEG_CHUNKS", k.lane_seg_chunks), 1);
   k.zc_huf = env("MCDC_ZC_HUF", k.zc_huf ? 1 : 0) != 0;
+  k.zc_two = env("MCDC_ZC_TWO", k.zc_two ? 1 : 0) != 0;
   k.test_fail_after_index = env("MCDC_TEST_FAIL_AFTER_INDEX", 0) != 0;
 #ifdef MCDC_AB_KNOBS
   k.group = env("MCDC_GROUP", k.group);

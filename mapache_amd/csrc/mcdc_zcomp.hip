@@ -907,9 +907,11 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
 //                partial last word carried; then the final states, the end
 //                mark and the header (count, modes, descriptions)
 // The block stays raw when the compressed block is not smaller.
-struct ZcSeqTab {  // (in the block's match-word scratch)
-  FseCTL t[3];     // LL, OF, ML: own or predefined
-  uint32_t fin[3]; // final states (k_zc_chain)
+struct ZcSeqTab {    // (in the block's match-word scratch)
+  FseCTL t[3];       // LL, OF, ML: own or predefined
+  uint32_t fin[3];   // final states (k_zc_chain)
+  uint32_t sbits[3]; // state bits of each machine's sequences (k_zc_chain)
+  uint32_t xbits;    // extra bits of the block's sequences (k_zc_plan)
   SeqPlan P;
 };
 static_assert(sizeof(ZcSeqTab) <= kZcBlock * 4, "sequence tables exceed the block's scratch");
@@ -940,15 +942,32 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
   for (uint32_t k = lane; k < 3 * 53; k += 64) (&hist[0][0])[k] = 0;
   __syncthreads();
   uint8_t *cd0 = seq_codes(words, bi, 0), *cd1 = seq_codes(words, bi, 1), *cd2 = seq_codes(words, bi, 2);
-  for (uint32_t i = lane; i < ns; i += 64) {
-    const uint64_t q = sq[i];
-    const uint32_t c0 = ll_code(seq_ll(q)), c1 = highbit(seq_ov(q)), c2 = ml_code(seq_ml(q) - 3);
-    atomicAdd(&hist[0][c0], 1u);
-    atomicAdd(&hist[1][c1], 1u);
-    atomicAdd(&hist[2][c2], 1u);
-    cd0[ns - 1 - i] = (uint8_t)c0;
-    cd1[ns - 1 - i] = (uint8_t)c1;
-    cd2[ns - 1 - i] = (uint8_t)c2;
+  uint32_t xb = 0;  // extra bits
+  // (64 sequences per step, the next step's requested meanwhile outside the
+  // compiler's wait counting: see ald16s)
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto issue = [&](uint32_t i) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(sq + min(i, ns - 1)) : "memory");
+    return v;
+  };
+  u32x2 qv = issue(lane);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(qv)::"memory");
+  for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint64_t q = (uint64_t)qv.y << 32 | qv.x;
+    qv = issue(i + 64);
+    if (i < ns) {
+      const uint32_t c0 = ll_code(seq_ll(q)), c1 = highbit(seq_ov(q)), c2 = ml_code(seq_ml(q) - 3);
+      xb += ll_bits(c0) + c1 + ml_bits(c2);
+      atomicAdd(&hist[0][c0], 1u);
+      atomicAdd(&hist[1][c1], 1u);
+      atomicAdd(&hist[2][c2], 1u);
+      cd0[ns - 1 - i] = (uint8_t)c0;
+      cd1[ns - 1 - i] = (uint8_t)c1;
+      cd2[ns - 1 - i] = (uint8_t)c2;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(qv)::"memory");
   }
   __syncthreads();
   ZT(3);
@@ -971,6 +990,8 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
     __syncthreads();
   }
   ZcSeqTab *tab = seq_tab(words, bi);
+  xb = wave_sum(xb);
+  if (lane == 0) tab->xbits = xb;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {  // (the states in use, then dfs, dnb, log)
     const uint32_t nst = 1u << tb[k].log;
@@ -1044,6 +1065,7 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   // one batch: the codes in cq (waited for), the next batch's requested into
   // nq; the loop alternates two register pairs, so that no register with a
   // load in flight is ever copied
+  uint32_t sbits = 0;
   auto batch = [&](int32_t m0, u32x2 &cq, u32x2 &nq) {
     uint32_t dn[8];
     int32_t df[8];
@@ -1060,7 +1082,9 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
       const uint32_t nb = (state + dn[u]) >> 16;
       r[u] = nb | (state & ((1u << nb) - 1u)) << 4;
       const uint32_t nxt = ct.state[((state >> nb) + (uint32_t)df[u]) & 511u];
-      state = m0 + u < (int32_t)ns ? nxt : state;
+      const bool in = m0 + u < (int32_t)ns;
+      state = in ? nxt : state;
+      sbits += in ? nb : 0u;
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(nq)::"memory");
 #pragma unroll
@@ -1073,7 +1097,10 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
     batch(m0, qa, qb);
     batch(m0 + 8, qb, qa);
   }
-  if (act && ns) seq_tab(words, b)->fin[k] = state;
+  if (act && ns) {
+    seq_tab(words, b)->fin[k] = state;
+    seq_tab(words, b)->sbits[k] = sbits;
+  }
   ZT(1);
   ZT_PRINT("chain", blockIdx.x % 97 == 0);
 }
@@ -1096,7 +1123,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
                                                   const uint64_t *seqs, const uint64_t *recs, uint32_t *words,
                                                   uint64_t *piece) {
   MCDC_VGPR_PAD(40);  // (not an exact fill)
-  constexpr uint32_t kWbWords = 64 * 96 / 32 + 4;  // a batch's bits + the carried word
+  constexpr uint32_t kWbWords = 512 + 64 * 96 / 32 + 8;  // 512 words + a batch's bits + slack
   __shared__ uint32_t wb[kWbWords];
   const uint32_t lane = lane_id();
   const uint64_t bi = blockIdx.x;
@@ -1126,41 +1153,52 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
       uint32_t *w0 = reinterpret_cast<uint32_t *>((uintptr_t)bs0 & ~(uintptr_t)3);
       // bits per sequence and offsets (writing order: the last sequence first)
       const uint32_t tl0 = tab->t[0].log, tl1 = tab->t[1].log, tl2 = tab->t[2].log;
-      // first pass: the total, to size the zeroing and the raw / compressed choice
-      uint64_t tot = 0;
-      for (uint32_t i = lane; i < ns; i += 64) {
-        const uint64_t q = sq[i];
-        const uint64_t rr = *reinterpret_cast<const uint64_t *>(rec + 4 * i);
-        const uint32_t llc = ll_code(seq_ll(q)), mlc = ml_code(seq_ml(q) - 3), ofc = highbit(seq_ov(q));
-        tot += (rr & 15) + ((rr >> 16) & 15) + ((rr >> 32) & 15) + ll_bits(llc) + ml_bits(mlc) + ofc;
-      }
-      tot = wave_sum((uint32_t)tot);  // (< 2^32 bits: a block's sequences)
+      // the total (state bits from k_zc_chain, extra bits from k_zc_plan), to
+      // size the stream and choose raw or compressed
+      const uint64_t tot = (uint64_t)tab->xbits + tab->sbits[0] + tab->sbits[1] + tab->sbits[2];
       const uint64_t all_bits = tot + tl0 + tl1 + tl2 + 1;  // + final states + end mark
       const uint32_t nbytes = (uint32_t)((all_bits + 7) / 8);
       const uint32_t total = at + hsz + nbytes;
       if (total < B.len) {
-        // the bitstream, 64 sequences at a time: their bits OR-ed into an LDS
-        // buffer (the batch is at most 64 x 96 bits), then its whole words
-        // stored to the slot with plain stores; the last partial word carries
-        // over.  The first word keeps the bytes before the stream (the
-        // header's, written last, or the literals' when the header is short).
-        uint32_t carry = w0[0] & (pre_bits ? (1u << pre_bits) - 1u : 0u);  // (wave-uniform load)
-        uint32_t cbits = pre_bits, wi = 0;  // bits in carry; index of carry's word
-        auto flush = [&](uint32_t tbits) {  // tbits new bits in wb[] after the carry; whole words out
-          const uint32_t nwords = (cbits + tbits) >> 5;
+        // The bitstream, 64 sequences at a time: their bits OR-ed into an LDS
+        // buffer at offsets from a wave scan (a batch is at most 64 x 96
+        // bits); when the buffer holds 512 words they go out with plain
+        // stores and the partial last word moves to its front.  The first
+        // word keeps the bytes before the stream (the header's, written
+        // last, or the literals' when the header is short).  A batch's
+        // sequences and records are requested during the batch before,
+        // outside the compiler's wait counting (see ald16s).
+        for (uint32_t k = lane; k < kWbWords; k += 64) wb[k] = 0;
+        __syncthreads();
+        if (lane == 0) wb[0] = w0[0] & (pre_bits ? (1u << pre_bits) - 1u : 0u);
+        uint32_t cb = pre_bits, wi = 0;  // bits in the buffer; the buffer's first word in the slot
+        auto flush = [&](bool all) {     // whole words out (all: the partial last one too)
+          const uint32_t nwords = all ? (cb + 31) >> 5 : cb >> 5;
+          __syncthreads();
           for (uint32_t k = lane; k < nwords; k += 64) w0[wi + k] = wb[k];
-          carry = wb[nwords];
-          cbits = (cbits + tbits) & 31;
+          if (all) return;
+          const uint32_t part = wb[nwords];
+          __syncthreads();
+          for (uint32_t k = lane; k <= nwords; k += 64) wb[k] = 0;
+          __syncthreads();
+          if (lane == 0) wb[0] = part;
+          cb &= 31;
           wi += nwords;
         };
-        for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        auto issue = [&](int32_t b1, u32x2 &q, u32x2 &r) {
+          const int32_t i = b1 - 1 - (int32_t)lane, ic = i >= 0 ? i : 0;
+          asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(q) : "v"(sq + ic) : "memory");
+          asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(rec + 4 * ic) : "memory");
+        };
+        auto batch = [&](int32_t b1, u32x2 &qv, u32x2 &rv) {
           const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
           const int32_t i = b1 - 1 - (int32_t)lane;  // lane 0 the batch's last sequence (written first)
+          const uint64_t q = (uint64_t)qv.y << 32 | qv.x, rr = (uint64_t)rv.y << 32 | rv.x;
+          issue(b1 - 64, qv, rv);  // the next batch's, waited for at this one's end
           uint64_t lo = 0, hi = 0;
           uint32_t nb = 0;
           if (i >= b0) {
-            const uint64_t q = sq[i];
-            const uint64_t rr = *reinterpret_cast<const uint64_t *>(rec + 4 * i);
             const uint32_t ll = seq_ll(q), mb = seq_ml(q) - 3, ob = seq_ov(q);
             const uint32_t llc = ll_code(ll), mlc = ml_code(mb), ofc = highbit(ob);
             auto put = [&](uint64_t v, uint32_t n) {  // append n bits (n <= 32)
@@ -1182,27 +1220,25 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
             put(ob, ofc);
           }
           const uint32_t incl = wave_incl_sum(nb, lane);  // inclusive prefix in lane order = writing order
-          const uint32_t tbits = (uint32_t)lane63((int32_t)incl);
-          for (uint32_t k = lane; k < kWbWords; k += 64) wb[k] = 0;
-          if (lane == 0) wb[0] = carry;
-          __syncthreads();
-          if (nb) or_bits(wb, cbits + incl - nb, lo, hi, nb);
-          __syncthreads();
-          flush(tbits);
-          __syncthreads();
-        }
+          if (nb) or_bits(wb, cb + incl - nb, lo, hi, nb);
+          cb += (uint32_t)lane63((int32_t)incl);
+          if (cb >= 512 * 32) flush(false);
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(qv), "+v"(rv)::"memory");
+        };
+        u32x2 qa, ra;
+        issue((int32_t)ns, qa, ra);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa), "+v"(ra)::"memory");
+        for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) batch(b1, qa, ra);
         // final states (ML, OF, LL: log bits each), the end mark, the last words
         const uint32_t f0 = tab->fin[0], f1 = tab->fin[1], f2 = tab->fin[2];  // final states of LL, OF, ML
         {
           const uint32_t fb = tl2 + tl1 + tl0 + 1;
           const uint64_t v = (uint64_t)(f2 & ((1u << tl2) - 1)) | (uint64_t)(f1 & ((1u << tl1) - 1)) << tl2 |
                              (uint64_t)(f0 & ((1u << tl0) - 1)) << (tl2 + tl1) | 1ull << (tl2 + tl1 + tl0);
-          if (lane < 4) wb[lane] = lane ? 0u : carry;
           __syncthreads();
-          if (lane == 0) or_bits(wb, cbits, v, 0, fb);
-          __syncthreads();
-          flush(fb);
-          if (lane == 0 && cbits) w0[wi] = carry;  // (the last, partial word)
+          if (lane == 0) or_bits(wb, cb, v, 0, fb);
+          cb += fb;
+          flush(true);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
         if (lane == 0) {
