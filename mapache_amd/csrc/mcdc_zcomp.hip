@@ -686,6 +686,9 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
     if (c[h]) hw.sym[r[h]] = (uint16_t)(lane + 64 * h);
   __syncthreads();
   ZT(0);
+#if MCDC_ZC_HCUT == 1  // (A/B timing: stop after the counts)
+  return;
+#endif
   if (lane == 0) huf_build(hist[0], ct, hw, true);
   __syncthreads();
   ZT(4);
@@ -694,6 +697,9 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   ZT(1);
   const uint32_t tree = tree_sz;
   if (!tree) return;  // (no description applies: raw literals)
+#if MCDC_ZC_HCUT == 2  // (A/B timing: stop after the tree)
+  return;
+#endif
   // code | length << 16 per symbol: one LDS read per literal; bits per stream
   // from the per-stream counts
   uint32_t sb[4] = {0, 0, 0, 0};
@@ -720,7 +726,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   uint32_t *sw = scratch + bi * kZcBlock;  // the section under assembly (words)
   const uint32_t nq = (total + 3) / 4 + 1;
   for (uint32_t k = lane; k < nq; k += 64) sw[k] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (same wave: agent scope would write back the L2)
   // The streams, 256 literals per step in writing order (the last literal
   // first): lane l takes writing indices 4 l .. 4 l + 3 of the step (one
   // 4-byte load, read from its top byte down), a wave scan of the lanes' bit
@@ -739,8 +745,10 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
     auto flush = [&](uint32_t upto) {  // words [ff, upto) out, their ring slots zeroed
       for (uint32_t i = ff + lane; i < upto; i += 64) {
         const uint32_t v = ring[i & (kRing - 1)];
+#if MCDC_ZC_HCUT != 3  // (A/B timing: no stores)
         if (i == fw) atomicOr(sw + i, v);
         else sw[i] = v;
+#endif
         ring[i & (kRing - 1)] = 0;
       }
       ff = upto;
@@ -756,43 +764,51 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
       asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
       return v;
     };
-    // (each step waits for everything outstanding first: its own bytes,
-    // requested two steps back, the next step's, requested one step back,
-    // and the previous flushes' stores)
+    // (each step waits for its own bytes, requested two steps back: the
+    // step between issued one load after them, so vmcnt(1) -- a flush's
+    // stores, which may retire out of order, only make it wait longer)
     auto step = [&](uint32_t r0, uint32_t &q) {
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
+      asm volatile("s_waitcnt vmcnt(1)" : "+v"(q)::"memory");
       const uint32_t w0 = r0 + 4 * lane;
       const uint32_t cnt = w0 < len ? min(len - w0, 4u) : 0u;
       const int32_t at = (int32_t)e - 4 - (int32_t)w0;
       const uint32_t below = at < (int32_t)a ? (uint32_t)((int32_t)a - at) : 0u;  // bytes below the stream (cnt < 4)
       const uint32_t dw = below >= 4 ? 0u : q << (8 * below);
       q = issue(r0 + 512);
-      uint32_t t[4], lb = 0;
+      // the lane's 4 codes packed (<= 44 bits), then placed: the first and
+      // last word of its span may be shared with the neighbouring lanes (LDS
+      // OR), a middle word is its own (plain store)
+      uint64_t acc = 0;
+      uint32_t lb = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        t[j] = (uint32_t)j < cnt ? ctw[(dw >> (8 * (3 - j))) & 0xFFu] : 0u;
-        lb += t[j] >> 16;
+        const uint32_t t = (uint32_t)j < cnt ? ctw[(dw >> (8 * (3 - j))) & 0xFFu] : 0u;
+        acc |= (uint64_t)(t & 0xFFFFu) << lb;
+        lb += t >> 16;
       }
       const uint32_t incl = wave_incl_sum(lb, lane);
-      uint32_t off = bitp + incl - lb;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t nb = t[j] >> 16;
-        if (nb) {
-          const uint32_t sh = off & 31, wd = off >> 5;
-          const uint64_t v = (uint64_t)(t[j] & 0xFFFFu) << sh;
-          atomicOr(ring + (wd & (kRing - 1)), (uint32_t)v);
-          if (sh + nb > 32) atomicOr(ring + ((wd + 1) & (kRing - 1)), (uint32_t)(v >> 32));
+      if (lb) {
+        const uint32_t off = bitp + incl - lb, sh = off & 31, wd = off >> 5;
+        const uint64_t lo = acc << sh;
+        const uint32_t top = sh ? (uint32_t)(acc >> (64 - sh)) : 0u;  // bits 64.. of the shifted span
+        const uint32_t nw = (sh + lb + 31) >> 5;                        // words spanned (1..3)
+        atomicOr(ring + (wd & (kRing - 1)), (uint32_t)lo);
+        if (nw == 2) atomicOr(ring + ((wd + 1) & (kRing - 1)), (uint32_t)(lo >> 32));
+        if (nw == 3) {
+          ring[(wd + 1) & (kRing - 1)] = (uint32_t)(lo >> 32);
+          atomicOr(ring + ((wd + 2) & (kRing - 1)), top);
         }
-        off += nb;
       }
       bitp += (uint32_t)lane63((int32_t)incl);
       if ((bitp >> 5) - ff >= 128) flush(bitp >> 5);
     };
     uint32_t da = issue(0), db = issue(256);
-    for (uint32_t r0 = 0; r0 < len; r0 += 512) {  // (two registers alternate: no copy of a loading register)
-      step(r0, da);
-      if (r0 + 256 < len) step(r0 + 256, db);
+#if MCDC_ZC_HCUT == 5  // (A/B timing: no stream steps)
+    if (len > 0) break;
+#endif
+    for (uint32_t r0 = 0; r0 < len; r0 += 512) {  // (two registers alternate: no copy of a loading
+      step(r0, da);                                 // register; a step at or past len adds nothing)
+      step(r0 + 256, db);
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(da), "+v"(db)::"memory");
     // the end mark, then every word the stream touched (the last one OR-ed)
@@ -802,7 +818,10 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
     if (lane == 0) atomicOr(sw + last, ring[last & (kRing - 1)]);
     o += ssz[k];
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+#if MCDC_ZC_HCUT == 4  // (A/B timing: stop after the streams)
+  return;
+#endif
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (same wave: agent scope would write back the L2)
   if (lane == 0) {
     uint8_t *sec = reinterpret_cast<uint8_t *>(sw);
     put_huf_lit_header(sec, n, csize, one);
@@ -814,7 +833,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
       }
     blocks[bi].lsize = total;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (same wave: agent scope would write back the L2)
   // (every read of the staged literals is done: the section replaces them)
   const uint32_t n16 = (total + 15) / 16;
   for (uint32_t k = lane; k < n16; k += 64)
@@ -1240,7 +1259,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
           cb += fb;
           flush(true);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (same wave: agent scope would write back the L2)
         if (lane == 0) {
           uint8_t *h = st + at;  // Number_of_Sequences, Symbol_Compression_Modes, descriptions
           if (cnt == 1) {
