@@ -38,7 +38,15 @@ def main(tag, out=None):
             continue
         m = {c: statistics.median(v) for c, v in per.items()}
         e = {"counters_median_per_dispatch": m, "dispatch_ms_median_under_pmc": round(statistics.median(ds) * 1e3, 3)}
-        batch = 512 << 20  # bytes per dispatch (one batch of kZcBatchBlocks = 16384 blocks of 32 KiB)
+        # bytes per dispatch: each pass runs tools/zc_bench.py 1 1 text = one
+        # warm-up + one timed call over 1 GiB; a kernel's dispatches per pass
+        # are the batches of those two calls
+        per_pass = defaultdict(int)
+        for key in acc:
+            if key[0] == k:
+                per_pass[key[1]] += 1
+        batch = 2 * (1 << 30) / statistics.median(per_pass.values())
+        e["input_bytes_per_dispatch"] = int(batch)
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM"):
             if c in m:
                 e[c.lower() + "_per_input_byte"] = round(m[c] / batch, 3)
@@ -59,7 +67,7 @@ def main(tag, out=None):
         if "WRITE_SIZE" in m:
             e["write_bytes_per_input_byte"] = round(m["WRITE_SIZE"] * 1024 / batch, 3)
         res[k] = e
-    doc = {"workload": "tools/zc_bench.py 1 1 text (1 GiB of text in 16/64/256 KiB chunks, batches of 512 MiB); "
+    doc = {"workload": "tools/zc_bench.py 1 1 text (1 GiB of text in 16/64/256 KiB chunks; per-byte rates over each dispatch's share of the input); "
                        "one counter group per rocprofv3 --pmc pass (tools/gpu_round4.sh zcprof)",
            "source": f"gpurun_out/{tag}/zc_pmc", "kernels": res}
     if out:
