@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_zc_find", "k_zc_parse", "k_zc_huff", "k_zc_encode", "k_zc_final")
+KERNELS = ("k_zc_find", "k_zc_parse", "k_zc_huff", "k_zc_plan", "k_zc_chain", "k_zc_encode", "k_zc_final")
 
 
 def main(tag, out=None):
