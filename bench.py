@@ -628,7 +628,7 @@ def gpu_encode_text(ctx, data: np.ndarray, ch: np.ndarray, nz: np.ndarray, steps
                 "compress_device_ms": round(zdev, 3), "compressed_bytes": int(zb), "ratio": round(n / zb, 3),
                 "encode_ms": round(dte * 1e3, 3), "encode_gib_s": round(n / dte / GIB, 2),
                 "sealed_bytes": int(oo[-1]), "encode_ratio": round(n / int(oo[-1]), 3), "parity_probe_ok": bool(ok),
-                "note": "mcdc_zstd_compress_device (greedy LZ, Huffman literals, FSE sequences with per-block or predefined tables, 16 KiB blocks) "
+                "note": "mcdc_zstd_compress_device (greedy LZ, Huffman literals, FSE sequences with per-block or predefined tables, 32 KiB blocks) "
                         "+ mcdc_seal_device, all in HBM; ratio vs the host level-3 ratio of the same blobs above"}
     finally:
         for x in (d_off, d_seal, d_nz, d_fr, d_ch, d_z, dp):

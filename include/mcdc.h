@@ -256,7 +256,7 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
 /* SecureStorage::compress (storage.rs:74-84) of every chunk of a boundary
  * list on the GPU: frame i is a zstd frame of chunk i in the crate's layout
  * (magic, Frame_Header_Descriptor 0x00: no content size, no checksum; window
- * 2^20 = storage.rs:31) of 16 KiB blocks, each compressed (Huffman / RLE /
+ * 2^20 = storage.rs:31) of 32 KiB blocks, each compressed (Huffman / RLE /
  * raw literals; sequences with per-block or predefined FSE tables) or raw
  * when that is not smaller.
  * mapache's decoder (zstd, window_log_max 20, :87-94) reads them; the bytes
@@ -264,7 +264,7 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
  * the bench).  Frames are written back to back from d_out (no alignment);
  * frames[i] (host or device) receives (offset, length).  *out_bytes: the bytes
  * written; on MCDC_E_CAPACITY the capacity that always suffices (the raw
- * frames: sum of length + 6 + 3 per 16 KiB block).  chunks: host or device;
+ * frames: sum of length + 6 + 3 per 32 KiB block).  chunks: host or device;
  * a chunk outside [0, n) or of 2 GiB or more -> MCDC_E_INVALID. */
 int mcdc_zstd_compress_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
                               size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,

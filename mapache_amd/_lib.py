@@ -431,9 +431,9 @@ class Context:
     @staticmethod
     def zstd_compress_bound(lengths) -> int:
         """Output capacity that always suffices for zstd_compress: the raw frames
-        of 16 KiB blocks (length + 6 + 3 per block)."""
+        of 32 KiB blocks (length + 6 + 3 per block)."""
         ln = np.asarray(lengths, dtype=np.uint64)
-        nb = np.maximum((ln + np.uint64(16383)) // np.uint64(16384), np.uint64(1))
+        nb = np.maximum((ln + np.uint64(32767)) // np.uint64(32768), np.uint64(1))
         return int((ln + np.uint64(6) + np.uint64(3) * nb).sum())
 
     @_locked

@@ -1881,7 +1881,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   HIP_TRY(hipMemcpyAsync(hfirst.data(), first, (nchunks + 1) * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (hm[0]) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer or is 2 GiB or longer", n);
-  if (out_bytes) *out_bytes = hm[1];  // the capacity that always suffices (raw frames of 16 KiB blocks)
+  if (out_bytes) *out_bytes = hm[1];  // the capacity that always suffices (raw frames of 32 KiB blocks)
   if (hm[1] > out_cap || !d_out)
     return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", out_cap, (unsigned long long)hm[1]);
   uint64_t *ext = (uint64_t *)direct_out(ctx, frames);
