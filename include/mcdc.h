@@ -265,7 +265,12 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
  * frames[i] (host or device) receives (offset, length).  *out_bytes: the bytes
  * written; on MCDC_E_CAPACITY the capacity that always suffices (the raw
  * frames: sum of length + 6 + 3 per 32 KiB block).  chunks: host or device;
- * a chunk outside [0, n) or of 2 GiB or more -> MCDC_E_INVALID. */
+ * a chunk outside [0, n) or of 2 GiB or more -> MCDC_E_INVALID.
+ * Scratch: device memory of the context, grown on first use and kept (not
+ * counted against max_bytes): about 9 bytes per byte of a batch of whole
+ * chunks, a batch holding up to 8192 blocks of 32 KiB (2.3 GiB), two batch
+ * sets once the input exceeds one (4.5 GiB); a chunk longer than a batch
+ * takes a batch of its own size. */
 int mcdc_zstd_compress_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
                               size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,
                               mcdc_blob *frames);

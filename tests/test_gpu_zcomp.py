@@ -171,6 +171,33 @@ def test_deterministic_and_device_lists(ctx):
     assert nb == a[2] and (fr == a[0]).all() and out.tobytes() == a[1].tobytes()
 
 
+def test_two_streams_match_one_stream(ctx, monkeypatch):
+    """Above one batch set (4096 blocks) batches alternate between two scratch
+    sets on two streams (only the final copies are ordered across them): the
+    output is byte-identical to one stream's (MCDC_ZC_TWO=0, read at context
+    creation) and decodes."""
+    data = np.tile(_data("text", 16 << 20, 7), 10)  # (160 MiB: ~6500 blocks)
+    ch = O.chunk(O.Params(*P16), data)
+    a = _compress(ctx, data, ch)
+    monkeypatch.setenv("MCDC_ZC_TWO", "0")
+    one = _lib.Context(0, 1 << 30)
+    try:
+        b = _compress(one, data, ch)
+    finally:
+        one.close()
+    assert a[2] == b[2] and (a[0] == b[0]).all() and a[1].tobytes() == b[1].tobytes()
+    pick = np.arange(0, len(ch), 97)
+    _check_frames_subset(data, ch, a[0], a[1], pick)
+
+
+def _check_frames_subset(data, chunks, fr, out, pick):
+    z = O.Zstd()
+    for i in pick:
+        o, ln = int(fr[i, 0]), int(fr[i, 1])
+        src = data[int(chunks["offset"][i]):int(chunks["offset"][i] + chunks["length"][i])].tobytes()
+        assert z.decompress(out[o:o + ln].tobytes(), len(src) + 64) == src, i
+
+
 def test_seal_and_decode_round_trip(ctx):
     """compress -> seal (AES-256-GCM-SIV, mcdc_seal_device over the frames'
     extents) -> mapache's decode (mcdc_decode_blobs: open, zstd decompress)."""
