@@ -945,6 +945,74 @@ __device__ __forceinline__ uint8_t *seq_codes(uint32_t *words, uint64_t bi, uint
   return reinterpret_cast<uint8_t *>(words + bi * kZcBlock) + kSeqTabBytes + k * (kZcSeqCap + 8);
 }
 
+// Float sum over the wave's 64 lanes (DPP, as wave_incl_sum), the total in every lane.
+__device__ __forceinline__ float wave_sum_f(float v) {
+#define MCDC_FADD(ctrl, rm) v += __int_as_float((int)MCDC_DPP(0, __float_as_int(v), ctrl, rm))
+  MCDC_FADD(0x111, 0xf);
+  MCDC_FADD(0x112, 0xf);
+  MCDC_FADD(0x114, 0xf);
+  MCDC_FADD(0x118, 0xf);
+  MCDC_FADD(0x142, 0xa);
+  MCDC_FADD(0x143, 0xc);
+#undef MCDC_FADD
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// seq_plan (mcdc_zstd.h) by the whole wave: lane s holds symbol s of a type,
+// the normalization, its largest count and both costs by wave reductions;
+// only the table description is written by one lane.  (The decisions are
+// seq_plan's; a cost sum in another order may round differently, which can
+// only move a near tie between two valid encodings.)
+__device__ void seq_plan_wave(uint32_t (*cnt)[53], uint32_t nseq, SeqPlan &P, uint32_t lane) {
+  const int16_t *pre[3] = {kLLNorm, kOFNorm, kMLNorm};
+  const uint32_t npre[3] = {36, 29, 53}, tpre[3] = {6, 5, 6}, shift[3] = {6, 4, 2};
+  uint32_t ndesc = 0, modes = 0;
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = lane < kSeqNSym[k] ? cnt[k][lane] : 0u;
+    const uint64_t nz = __ballot(c != 0);
+    const uint32_t distinct = (uint32_t)__builtin_popcountll(nz), maxsym = nz ? 63u - (uint32_t)__builtin_clzll(nz) : 0u;
+    bool own = false;
+    uint32_t tl = tpre[k], nd = 0;
+    if (nseq >= 32 && distinct >= 2) {
+      tl = fse_table_log(nseq, maxsym, kSeqMaxLog[k]);
+      const uint32_t scale = 1u << tl;
+      uint32_t v = c ? (c * scale + nseq / 2) / nseq : 0u;
+      if (c && v == 0) v = 1;
+      const uint32_t sum = wave_sum(v);
+      const uint32_t bc = (uint32_t)wave_max((int32_t)c);
+      const uint32_t big = (uint32_t)__builtin_ctzll(__ballot(c == bc));  // (the first largest count)
+      const int32_t fixed = (int32_t)__builtin_amdgcn_readlane((int)v, (int)big) + (int32_t)scale - (int32_t)sum;
+      if (fixed >= 1) {
+        const int32_t nrm = lane == big ? fixed : (int32_t)v;
+        if (lane < 53) P.norm[k][lane] = (int16_t)(lane <= maxsym ? nrm : 0);
+        __syncthreads();
+        if (lane == 0) nd = fse_write_ncount(P.norm[k], maxsym + 1, tl, P.desc + ndesc);
+        nd = (uint32_t)__builtin_amdgcn_readlane((int)nd, 0);
+        const int32_t pn0 = lane < npre[k] ? pre[k][lane] : 0, pn = pn0 == -1 ? 1 : pn0;
+        const float oc = c ? (float)c * ((float)tl - log2f((float)nrm)) : 0.0f;
+        const float pc = c ? (pn <= 0 ? 1e30f : (float)c * ((float)tpre[k] - log2f((float)pn))) : 0.0f;
+        const float ownc = wave_sum_f(oc) + 8.0f * (float)nd, predc = wave_sum_f(pc);
+        own = ownc < predc;
+      }
+    }
+    if (lane == 0) {
+      P.own[k] = own ? 1u : 0u;
+      P.tl[k] = own ? tl : tpre[k];
+      P.doff[k] = ndesc;
+      P.dlen[k] = own ? nd : 0u;
+    }
+    if (own) {
+      ndesc += nd;
+      modes |= 2u << shift[k];
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    P.ndesc = ndesc;
+    P.modes = modes;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t nblk, const uint64_t *seqs,
                                                 uint32_t *words, ZTables T) {
   __shared__ FseCTL tb[3];
@@ -990,7 +1058,7 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
   }
   __syncthreads();
   ZT(3);
-  if (lane == 0) seq_plan(hist[0], hist[1], hist[2], ns, P, 1);
+  seq_plan_wave(hist, ns, P, lane);
   __syncthreads();
   ZT(4);
   const FseCT *pre[3] = {&T.ll, &T.of, &T.ml};
