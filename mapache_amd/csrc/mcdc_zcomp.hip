@@ -147,6 +147,43 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
   }
 }
 
+// The finder's segments by cost, longest first: a segment's blocks (<=
+// kZcSegBlocks) plus, after a chunk's first segment, the kPrime bytes it
+// re-inserts (4 blocks' worth); order[i] = the record starting the i-th
+// segment, then nblk (no segment).  One workgroup: a counting sort in LDS
+// (the order within a bucket follows the atomics; it changes no output).
+__global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uint64_t nblk, uint32_t *order) {
+  constexpr uint32_t kKeys = kZcSegBlocks + kPrime / kZcBlock + 1;
+  __shared__ uint32_t cnt[kKeys], at[kKeys];
+  const uint32_t tid = threadIdx.x;
+  if (tid < kKeys) cnt[tid] = 0;
+  __syncthreads();
+  auto key = [&](const ZcBlock &B) {  // (descending cost: bucket 0 = the costliest)
+    const uint32_t nsb = min<uint32_t>(kZcSegBlocks, B.nb - B.b);
+    return kKeys - 1 - (nsb + (B.b ? kPrime / kZcBlock : 0u));
+  };
+  for (uint64_t r = tid; r < nblk; r += 1024) {
+    const ZcBlock B = blocks[r];
+    if (B.b % kZcSegBlocks == 0) atomicAdd(&cnt[key(B)], 1u);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t a = 0;
+    for (uint32_t k = 0; k < kKeys; ++k) {
+      at[k] = a;
+      a += cnt[k];
+    }
+    cnt[0] = a;  // (the number of segments)
+  }
+  __syncthreads();
+  const uint32_t nseg = cnt[0];
+  for (uint64_t r = tid; r < nblk; r += 1024) {
+    const ZcBlock B = blocks[r];
+    if (B.b % kZcSegBlocks == 0) order[atomicAdd(&at[key(B)], 1u)] = (uint32_t)r;
+  }
+  for (uint64_t i = nseg + tid; i < nblk; i += 1024) order[i] = (uint32_t)nblk;
+}
+
 // Branch-free 16-byte load for prefetching (a branch around a load makes the
 // compiler wait for it where the paths join): the 16 bytes at p, or, within
 // 16 bytes of the end of the nbytes >= 16 readable, the last 16 bytes; fix16
@@ -205,10 +242,15 @@ __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
 // the earlier tiles left them), the candidate's bytes requested, the tile
 // two back verified (its bytes had two tiles' time to arrive), then the
 // inserts; two LDS-only barriers per tile.
+//
+// Workgroups take the segments longest first (order[], k_zc_segorder): one
+// workgroup fills a CU (its tables are the whole LDS), and a segment of 8
+// blocks that started last would run on alone at the end of the launch.
 __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, uint64_t nbytes,
-                                                          const ZcBlock *blocks, uint64_t nblk, uint32_t *words) {
+                                                          const ZcBlock *blocks, uint64_t nblk, uint32_t *words,
+                                                          const uint32_t *order) {
   __shared__ __attribute__((aligned(16))) uint32_t hts[1u << kHsLog], htl[1u << kHlLog];
-  const uint64_t bi0 = blockIdx.x;
+  const uint64_t bi0 = order[blockIdx.x];
   if (bi0 >= nblk) return;
   const ZcBlock B0 = blocks[bi0];
   if (B0.b % kZcSegBlocks) return;
@@ -289,8 +331,13 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     ZC_TICK(1);
     // the candidate: the long key's if its tag matches, else the short key's
     const uint32_t cl = prime0 + (el >> 13) - 1, cs = prime0 + (es >> 13) - 1;
+#ifdef MCDC_ZC_NOBAR
+    const bool okl = el != 0 && (el & 0x1FFFu) == gl && cl < p && p - cl <= zs::kWindow;
+    const bool oks = es != 0 && (es & 0x1FFFu) == gs && cs < p && p - cs <= zs::kWindow;
+#else
     const bool okl = el != 0 && (el & 0x1FFFu) == gl && p - cl <= zs::kWindow;
     const bool oks = es != 0 && (es & 0x1FFFu) == gs && p - cs <= zs::kWindow;
+#endif
     const uint32_t q = okl ? cl : oks ? cs : p;
     S.v = find;
     S.k = okl || oks;
@@ -298,14 +345,25 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     S.p = p;
     S.q = q;
     S.x = x;
+#if defined(MCDC_ZC_NOGATHER)  // (A/B timing only: no candidate gathers, every position a literal)
+    S.k = false;
+    S.y = ald16s(cb, min(p, last16));
+#else
     S.y = ald16s(cb, min(q, last16));
+#endif
     n = ald16s(cb, min(p + 2 * kFindTile, last16));
     const uint32_t r = (p - prime0 + 1) << 13;
+#ifndef MCDC_ZC_NOBAR  // (A/B timing only: no barriers, racy lookups)
     lds_sync();  // every lookup of the tile before any insert
+#endif
     ZC_TICK(2);
+#ifndef MCDC_ZC_NOINS  // (A/B timing only: no inserts, no candidates)
     if (vs) atomicMax(hts + hs, r | gs);
     if (vl) atomicMax(htl + hl, r | gl);
+#endif
+#ifndef MCDC_ZC_NOBAR
     lds_sync();  // every insert before the next tile's lookups
+#endif
     ZC_TICK(3);
 #ifdef MCDC_ZC_TIMING
     ++nsteps;
@@ -569,6 +627,159 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
 }
 
 
+// huf_build (mcdc_zstd.h) by the wave, from the counts and ranks of the
+// lane's four symbols (lane + 64 h): the same code.  Lane 0 runs only the
+// two-queue merge (register heads, one LDS read per step); the depths by
+// pointer jumping (d += d[anc], anc = anc[anc]: a few rounds for the <= 511
+// nodes, 8 per lane); the lengths by rank from the per-depth counts; the
+// canonical codes from ballots per length, in symbol order.
+__device__ void huf_build_wave(const uint32_t (&c)[4], const uint32_t (&r)[4], uint32_t n, HufCT &ct, HufWork &w,
+                               uint32_t lane) {
+  __shared__ uint32_t s_maxd;
+  uint32_t *const f = w.f, *const bl = w.bl;
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+    if (c[h]) f[r[h]] = c[h];
+  bl[lane] = 0;
+  __syncthreads();
+  const uint32_t m = 2 * n - 1, root = m - 1;
+  if (lane == 0) {
+    constexpr uint32_t kInf = 0xFFFFFFFFu;
+    uint32_t li = 0, ni = n, fl = f[0], fn = kInf;
+    for (uint32_t nn = n; nn < m; ++nn) {
+      uint32_t ab[2], wab[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (fl <= fn) {  // (a leaf on a tie: the serial queue's order)
+          ab[t] = li++;
+          wab[t] = fl;
+          fl = li < n ? f[li] : kInf;
+        } else {
+          ab[t] = ni++;
+          wab[t] = fn;
+          fn = ni < nn ? f[ni] : kInf;
+        }
+      }
+      const uint32_t sum = wab[0] + wab[1];
+      f[nn] = sum;
+      w.par[ab[0]] = w.par[ab[1]] = (uint16_t)nn;
+      if (fn == kInf) fn = sum;  // (the internal queue was empty: ni == nn)
+    }
+  }
+  __syncthreads();
+  // depths: node i = lane + 64 j
+  uint32_t an[8], dn[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t i = lane + 64 * j;
+    an[j] = i < root ? w.par[i] : root;
+    dn[j] = i < root ? 1u : 0u;
+  }
+  for (;;) {
+    bool more = false;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) more |= lane + 64 * j < m && an[j] != root;
+    if (!__ballot(more)) break;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (lane + 64 * j < m) {
+        w.par[lane + 64 * j] = (uint16_t)an[j];
+        w.dep[lane + 64 * j] = (uint8_t)dn[j];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (lane + 64 * j < m && an[j] != root) {
+        dn[j] += w.dep[an[j]];
+        an[j] = w.par[an[j]];
+      }
+    __syncthreads();
+  }
+  // leaves 0 .. n - 1 per depth (capped at 63, as huf_build)
+  uint32_t maxd = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (lane + 64 * j < n) {
+      const uint32_t d = min(dn[j], 63u);
+      atomicAdd(&bl[d], 1u);
+      maxd = max(maxd, d);
+    }
+  maxd = (uint32_t)wave_max((int32_t)maxd);
+  __syncthreads();
+  if (lane == 0) {  // the length limit (huf_build's steps)
+    if (maxd > kHufMaxBits) {
+      for (uint32_t d = kHufMaxBits + 1; d <= maxd; ++d) {
+        bl[kHufMaxBits] += bl[d];
+        bl[d] = 0;
+      }
+      uint64_t kraft = 0;
+      for (uint32_t d = 1; d <= kHufMaxBits; ++d) kraft += (uint64_t)bl[d] << (kHufMaxBits - d);
+      while (kraft > (1ull << kHufMaxBits)) {
+        uint32_t d = kHufMaxBits - 1;
+        while (bl[d] == 0) --d;
+        --bl[d];
+        bl[d + 1] += 2;
+        --bl[kHufMaxBits];
+        --kraft;
+      }
+      maxd = kHufMaxBits;
+    }
+    s_maxd = maxd;
+  }
+  __syncthreads();
+  maxd = s_maxd;
+  // lengths: the j-th most frequent symbol (j = n - 1 - rank) takes the
+  // shortest depth d with bl[1] + .. + bl[d] > j
+  uint32_t L[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    L[h] = 0;
+    if (c[h]) {
+      const uint32_t j = n - 1 - r[h];
+      uint32_t cum = 0;
+      for (uint32_t d = 1; d <= maxd; ++d) {
+        cum += bl[d];
+        if (cum > j) {
+          L[h] = d;
+          break;
+        }
+      }
+    }
+    ct.nb[lane + 64 * h] = (uint8_t)L[h];
+  }
+  uint32_t last = 0;
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+    if (c[h]) last = lane + 64 * h;
+  last = (uint32_t)wave_max((int32_t)last);
+  // canonical codes: per length from the longest down, start 0, next
+  // length's start (start + count) >> 1; within a length in symbol order
+  uint32_t start[kHufMaxBits + 1];
+  {
+    uint32_t mn = 0;
+#pragma unroll
+    for (int d = kHufMaxBits; d >= 1; --d) {
+      start[d] = mn;
+      if ((uint32_t)d <= maxd) mn = (mn + bl[d]) >> 1;
+    }
+  }
+  const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int d = 1; d <= (int)kHufMaxBits; ++d) {
+    uint32_t base = start[d];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint64_t mk = __ballot(L[h] == (uint32_t)d);
+      if (L[h] == (uint32_t)d) ct.code[lane + 64 * h] = (uint16_t)(base + (uint32_t)__builtin_popcountll(mk & lt));
+      base += (uint32_t)__builtin_popcountll(mk);
+    }
+  }
+  if (lane == 0) {
+    ct.maxb = maxd;
+    ct.last = last;
+  }
+}
+
 // The literals section of a compressed block: Huffman-coded or RLE when that
 // is smaller than the raw section (3-byte header + the literals), written
 // over the staging slot's raw literals; B.lsize its size, 0 = raw.  The whole
@@ -681,15 +892,11 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
       for (int h = 0; h < 4; ++h)
         r[h] += (qs[j] && (qs[j] < c[h] || (qs[j] == c[h] && t + j < lane + 64 * h))) ? 1u : 0u;
   }
-#pragma unroll
-  for (int h = 0; h < 4; ++h)
-    if (c[h]) hw.sym[r[h]] = (uint16_t)(lane + 64 * h);
-  __syncthreads();
   ZT(0);
 #if MCDC_ZC_HCUT == 1  // (A/B timing: stop after the counts)
   return;
 #endif
-  if (lane == 0) huf_build(hist[0], ct, hw, true);
+  huf_build_wave(c, r, distinct, ct, hw, lane);
   __syncthreads();
   ZT(4);
   if (lane == 0) tree_sz = huf_tree_desc(ct, tdesc, dw);
@@ -1425,7 +1632,11 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
-  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words);
+  // (piece is free until k_zc_encode: the finder's segment order)
+  uint32_t *order = reinterpret_cast<uint32_t *>(piece);
+  hipLaunchKernelGGL(k_zc_segorder, dim3(1), dim3(1024), 0, st, blocks, nblk, order);
+  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
+                     order);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
                      seqs);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words);

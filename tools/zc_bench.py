@@ -46,7 +46,10 @@ for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text",
     ok = True
     for i in range(8):
         src = ctx.d2h_bytes(dp + int(ch["offset"][i]), int(ch["length"][i])).tobytes()
-        ok &= z.decompress(ctx.d2h_bytes(d_out + int(fr[i, 0]), int(fr[i, 1])).tobytes(), len(src) + 64) == src
+        try:
+            ok &= z.decompress(ctx.d2h_bytes(d_out + int(fr[i, 0]), int(fr[i, 1])).tobytes(), len(src) + 64) == src
+        except AssertionError:  # (A/B timing variants may not decode)
+            ok = False
     res[kind] = {"gib_s": round(n / dt / (1 << 30), 2), "device_ms": round(dev, 3), "ratio": round(n / nb, 4),
                  "chunks": int(k), "probe_ok": bool(ok)}
     for x in (d_fr, d_out, d_ch, dp):
