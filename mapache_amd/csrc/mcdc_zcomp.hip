@@ -1339,13 +1339,13 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   const FseCTL &ct = tb[3 * j + k];
   uint16_t *rec = reinterpret_cast<uint16_t *>(recs + (act ? b : 0) * kZcSeqCap);
   const uint8_t *cd = seq_codes(words, act ? b : 0, k);  // codes in walking order: cd[m] = sequence ns - 1 - m
-  // 8 sequences per batch: codes of batch t in a register pair, of batch
+  // 16 sequences per batch: codes of batch t in a register quad, of batch
   // t + 1 in flight (a load outside the compiler's wait counting, waited
-  // for after the batch's steps, before its records are stored)
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  // for after the batch's steps, before its records are stored; 16 steps of
+  // the chain cover the load's latency, 8 did not)
   auto issue = [&](uint32_t m0) {
-    u32x2 v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(cd + m0) : "memory");
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(cd + m0) : "memory");
     return v;
   };
   const int32_t top = wave_max((int32_t)ns);  // (the wave's longest block sets the batch count)
@@ -1357,22 +1357,22 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
     rec[4 * (ns - 1) + k] = 0;
   }
   // one batch: the codes in cq (waited for), the next batch's requested into
-  // nq; the loop alternates two register pairs, so that no register with a
+  // nq; the loop alternates two register quads, so that no register with a
   // load in flight is ever copied
   uint32_t sbits = 0;
-  auto batch = [&](int32_t m0, u32x2 &cq, u32x2 &nq) {
-    uint32_t dn[8];
-    int32_t df[8];
+  auto batch = [&](int32_t m0, u32x4 &cq, u32x4 &nq) {
+    uint32_t dn[16];
+    int32_t df[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const uint32_t c = (cq[u >> 2] >> (8 * (u & 3))) & 63u;
       dn[u] = ct.dnb[c];
       df[u] = ct.dfs[c];
     }
-    nq = issue((uint32_t)m0 + 8);
-    uint32_t r[8];
+    nq = issue((uint32_t)m0 + 16);
+    uint32_t r[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const uint32_t nb = (state + dn[u]) >> 16;
       r[u] = nb | (state & ((1u << nb) - 1u)) << 4;
       const uint32_t nxt = ct.state[((state >> nb) + (uint32_t)df[u]) & 511u];
@@ -1382,14 +1382,14 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(nq)::"memory");
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 16; ++u)
       if (m0 + u < (int32_t)ns) rec[4 * (ns - 1 - (uint32_t)(m0 + u)) + k] = (uint16_t)r[u];
   };
-  u32x2 qa = issue(1), qb;
+  u32x4 qa = issue(1), qb;
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa)::"memory");
-  for (int32_t m0 = 1; m0 < top; m0 += 16) {  // m: sequence ns - 1 - m
+  for (int32_t m0 = 1; m0 < top; m0 += 32) {  // m: sequence ns - 1 - m
     batch(m0, qa, qb);
-    batch(m0 + 8, qb, qa);
+    batch(m0 + 16, qb, qa);
   }
   if (act && ns) {
     seq_tab(words, b)->fin[k] = state;
