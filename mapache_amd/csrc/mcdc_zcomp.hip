@@ -150,21 +150,28 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
 // The finder's segments by cost, longest first: a segment's blocks (<=
 // kZcSegBlocks) plus, after a chunk's first segment, the kPrime bytes it
 // re-inserts (4 blocks' worth); order[i] = the record starting the i-th
-// segment, then nblk (no segment).  One workgroup: a counting sort in LDS
-// (the order within a bucket follows the atomics; it changes no output).
-__global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uint64_t nblk, uint32_t *order) {
+// segment, then nblk (no segment).  And the blocks for k_zc_parse, longest
+// first by 4 KiB steps: porder[i] = the i-th block.  One workgroup: counting
+// sorts in LDS (the order within a bucket follows the atomics; it changes no
+// output).
+__global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uint64_t nblk, uint32_t *order,
+                                                      uint32_t *porder) {
   constexpr uint32_t kKeys = kZcSegBlocks + kPrime / kZcBlock + 1;
-  __shared__ uint32_t cnt[kKeys], at[kKeys];
+  constexpr uint32_t kPKeys = kZcBlock / 4096 + 1;
+  __shared__ uint32_t cnt[kKeys], at[kKeys], pcnt[kPKeys], pat[kPKeys];
   const uint32_t tid = threadIdx.x;
   if (tid < kKeys) cnt[tid] = 0;
+  if (tid < kPKeys) pcnt[tid] = 0;
   __syncthreads();
   auto key = [&](const ZcBlock &B) {  // (descending cost: bucket 0 = the costliest)
     const uint32_t nsb = min<uint32_t>(kZcSegBlocks, B.nb - B.b);
     return kKeys - 1 - (nsb + (B.b ? kPrime / kZcBlock : 0u));
   };
+  auto pkey = [&](const ZcBlock &B) { return kPKeys - 1 - min<uint32_t>(kPKeys - 1, B.len / 4096); };
   for (uint64_t r = tid; r < nblk; r += 1024) {
     const ZcBlock B = blocks[r];
     if (B.b % kZcSegBlocks == 0) atomicAdd(&cnt[key(B)], 1u);
+    atomicAdd(&pcnt[pkey(B)], 1u);
   }
   __syncthreads();
   if (tid == 0) {
@@ -174,12 +181,18 @@ __global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uin
       a += cnt[k];
     }
     cnt[0] = a;  // (the number of segments)
+    a = 0;
+    for (uint32_t k = 0; k < kPKeys; ++k) {
+      pat[k] = a;
+      a += pcnt[k];
+    }
   }
   __syncthreads();
   const uint32_t nseg = cnt[0];
   for (uint64_t r = tid; r < nblk; r += 1024) {
     const ZcBlock B = blocks[r];
     if (B.b % kZcSegBlocks == 0) order[atomicAdd(&at[key(B)], 1u)] = (uint32_t)r;
+    porder[atomicAdd(&pat[pkey(B)], 1u)] = (uint32_t)r;
   }
   for (uint64_t i = nseg + tid; i < nblk; i += 1024) order[i] = (uint32_t)nblk;
 }
@@ -443,12 +456,13 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane
 // sequence's offset, literal length > 0: rep[0] is always the previous
 // offset when only that code is used) after the block's first sequence.
 __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
-                                                 const uint32_t *words, uint8_t *stage, uint64_t *seqs) {
+                                                 const uint32_t *words, uint8_t *stage, uint64_t *seqs,
+                                                 const uint32_t *porder) {
   __shared__ uint16_t J[8][257];
   __shared__ uint8_t mk[260];
   __shared__ uint32_t offl[256], wbyt[64];
-  const uint64_t bi = blockIdx.x;
-  if (bi >= nblk) return;
+  if (blockIdx.x >= nblk) return;
+  const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
   const ZcBlock B = blocks[bi];
   const uint32_t end = B.len;
@@ -1632,13 +1646,14 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
-  // (piece is free until k_zc_encode: the finder's segment order)
-  uint32_t *order = reinterpret_cast<uint32_t *>(piece);
-  hipLaunchKernelGGL(k_zc_segorder, dim3(1), dim3(1024), 0, st, blocks, nblk, order);
+  // (piece, nblk + 1 words of 8 bytes, is free until k_zc_encode: the
+  // finder's segment order and the parse's block order)
+  uint32_t *order = reinterpret_cast<uint32_t *>(piece), *porder = order + nblk;
+  hipLaunchKernelGGL(k_zc_segorder, dim3(1), dim3(1024), 0, st, blocks, nblk, order, porder);
   hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
                      order);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
-                     seqs);
+                     seqs, porder);
   if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words);
   hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, seqs, words, T);
   hipLaunchKernelGGL(k_zc_chain, dim3((unsigned)((nblk + kChainBlocks - 1) / kChainBlocks)), dim3(64), 0, st, blocks,
