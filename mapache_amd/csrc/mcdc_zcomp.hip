@@ -812,7 +812,7 @@ __device__ void huf_build_wave(const uint32_t (&c)[4], const uint32_t (&r)[4], u
 //   store    header, tree, jump table; the section copied to the slot
 // (LDS ~9 KiB per wave: 16 waves per CU; the section itself stays in HBM.)
 __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
-                                                uint8_t *stage, uint32_t *scratch) {
+                                                uint8_t *stage, uint32_t *scratch, const uint32_t *porder) {
   // LDS: the counts (4 copies while counting, merged into the first), then
   // in the place of copies 1-3, one after another: huf_build's work, the
   // description's work, the code table ctw (6.4 KiB in all: 25 waves per CU)
@@ -826,8 +826,8 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   __shared__ HufCT ct;
   __shared__ uint8_t tdesc[132];
   __shared__ uint32_t tree_sz;
-  const uint64_t bi = blockIdx.x;
-  if (bi >= nblk) return;
+  if (blockIdx.x >= nblk) return;
+  const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
   const ZcBlock B = blocks[bi];
   // a block without sequences: all of it literals, read from the input (k_zc_parse staged nothing)
@@ -1235,13 +1235,13 @@ __device__ void seq_plan_wave(uint32_t (*cnt)[53], uint32_t nseq, SeqPlan &P, ui
 }
 
 __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t nblk, const uint64_t *seqs,
-                                                uint32_t *words, ZTables T) {
+                                                uint32_t *words, ZTables T, const uint32_t *porder) {
   __shared__ FseCTL tb[3];
   __shared__ SeqPlan P;
   __shared__ uint32_t hist[3][53], cum[54], seen[54];
   const uint32_t lane = lane_id();
-  const uint64_t bi = blockIdx.x;
-  if (bi >= nblk) return;
+  if (blockIdx.x >= nblk) return;
+  const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   if (ns == 0) return;
@@ -1654,8 +1654,10 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      order);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
                      seqs, porder);
-  if (huf) hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words);
-  hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, seqs, words, T);
+  if (huf)
+    hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words,
+                       porder);
+  hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, seqs, words, T, porder);
   hipLaunchKernelGGL(k_zc_chain, dim3((unsigned)((nblk + kChainBlocks - 1) / kChainBlocks)), dim3(64), 0, st, blocks,
                      nblk, recs, words);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, words, piece);
