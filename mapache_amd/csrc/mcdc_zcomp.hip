@@ -149,28 +149,30 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
 
 // The finder's segments by cost, longest first: a segment's blocks (<=
 // kZcSegBlocks) plus, after a chunk's first segment, the kPrime bytes it
-// re-inserts (4 blocks' worth); order[i] = the record starting the i-th
+// re-inserts, by 4 KiB; order[i] = the record starting the i-th
 // segment, then nblk (no segment).  And the blocks for k_zc_parse, longest
 // first by 4 KiB steps: porder[i] = the i-th block.  One workgroup: counting
 // sorts in LDS (the order within a bucket follows the atomics; it changes no
 // output).
 __global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uint64_t nblk, uint32_t *order,
                                                       uint32_t *porder) {
-  constexpr uint32_t kKeys = kZcSegBlocks + kPrime / kZcBlock + 1;
+  constexpr uint32_t kKeys = (kZcSegBlocks * kZcBlock + kPrime) / 4096 + 1;
   constexpr uint32_t kPKeys = kZcBlock / 4096 + 1;
   __shared__ uint32_t cnt[kKeys], at[kKeys], pcnt[kPKeys], pat[kPKeys];
+  MCDC_VGPR_PAD(24);  // (not an exact fill)
   const uint32_t tid = threadIdx.x;
   if (tid < kKeys) cnt[tid] = 0;
   if (tid < kPKeys) pcnt[tid] = 0;
   __syncthreads();
-  auto key = [&](const ZcBlock &B) {  // (descending cost: bucket 0 = the costliest)
+  auto key = [&](const ZcBlock &B, uint64_t r) {  // (descending cost by 4 KiB: bucket 0 = the costliest)
     const uint32_t nsb = min<uint32_t>(kZcSegBlocks, B.nb - B.b);
-    return kKeys - 1 - (nsb + (B.b ? kPrime / kZcBlock : 0u));
+    const uint32_t bytes = (nsb - 1) * kZcBlock + blocks[r + nsb - 1].len + (B.b ? kPrime : 0u);
+    return kKeys - 1 - min(kKeys - 1, bytes / 4096);
   };
   auto pkey = [&](const ZcBlock &B) { return kPKeys - 1 - min<uint32_t>(kPKeys - 1, B.len / 4096); };
   for (uint64_t r = tid; r < nblk; r += 1024) {
     const ZcBlock B = blocks[r];
-    if (B.b % kZcSegBlocks == 0) atomicAdd(&cnt[key(B)], 1u);
+    if (B.b % kZcSegBlocks == 0) atomicAdd(&cnt[key(B, r)], 1u);
     atomicAdd(&pcnt[pkey(B)], 1u);
   }
   __syncthreads();
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uin
   const uint32_t nseg = cnt[0];
   for (uint64_t r = tid; r < nblk; r += 1024) {
     const ZcBlock B = blocks[r];
-    if (B.b % kZcSegBlocks == 0) order[atomicAdd(&at[key(B)], 1u)] = (uint32_t)r;
+    if (B.b % kZcSegBlocks == 0) order[atomicAdd(&at[key(B, r)], 1u)] = (uint32_t)r;
     porder[atomicAdd(&pat[pkey(B)], 1u)] = (uint32_t)r;
   }
   for (uint64_t i = nseg + tid; i < nblk; i += 1024) order[i] = (uint32_t)nblk;
