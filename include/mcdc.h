@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MCDC_ABI_VERSION 4
+#define MCDC_ABI_VERSION 5
 
 /* status codes */
 #define MCDC_OK 0
@@ -432,10 +432,19 @@ const char *mcdc_last_error(void);
 /* Device / pinned-host allocation on the context's device. */
 int mcdc_device_alloc(struct mcdc_ctx *ctx, size_t bytes, void **d_ptr);
 int mcdc_device_free(struct mcdc_ctx *ctx, void *d_ptr);
-/* Wait until all work on the context's device has finished (the timed
+/* Wait until all work enqueued by this context has finished: its streams
+ * and the null stream; other contexts' work is not waited for (the timed
  * region's device-side bracket in bench.py: the bench never initialises a
  * second HIP runtime, e.g. torch's, in the libmcdc process). */
 int mcdc_ctx_synchronize(struct mcdc_ctx *ctx);
+/* Per-context settings for tests and tuning (not reference interface):
+ *   "zc_batch_blocks"        blocks per GPU compressor batch (default 16384,
+ *                            512 MiB; two streams take half each), >= 8
+ *   "zc_two"                 0: compressor batches on one stream
+ *   "test_fail_after_index"  1: mcdc_save_files fails after its index add
+ *                            (exercises the rollback)
+ * Unknown name -> MCDC_E_INVALID. */
+int mcdc_ctx_set_option(struct mcdc_ctx *ctx, const char *name, long long value);
 int mcdc_host_alloc(struct mcdc_ctx *ctx, size_t bytes, void **h_ptr);
 int mcdc_host_free(struct mcdc_ctx *ctx, void *h_ptr);
 int mcdc_memcpy_h2d(struct mcdc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);

@@ -38,7 +38,7 @@ EXPORTS = (
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
     "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device", "mcdc_save_files",
-    "mcdc_zstd_compress_device", "mcdc_ctx_synchronize",
+    "mcdc_zstd_compress_device", "mcdc_ctx_synchronize", "mcdc_ctx_set_option",
 )
 
 
@@ -114,6 +114,7 @@ def load():
     L.mcdc_device_alloc.argtypes = [vp, sz, P(vp)]
     L.mcdc_device_free.argtypes = [vp, vp]
     L.mcdc_ctx_synchronize.argtypes = [vp]
+    L.mcdc_ctx_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
     L.mcdc_host_alloc.argtypes = [vp, sz, P(vp)]
     L.mcdc_host_free.argtypes = [vp, vp]
     L.mcdc_memcpy_h2d.argtypes = [vp, vp, vp, sz]
@@ -620,8 +621,15 @@ class Context:
 
     @_locked
     def synchronize(self) -> None:
-        """Wait for all work on the context's device (mcdc_ctx_synchronize)."""
+        """Wait for all work of this context (mcdc_ctx_synchronize: its streams
+        and the null stream, not other contexts')."""
         check(load().mcdc_ctx_synchronize(self._h))
+
+    @_locked
+    def set_option(self, name: str, value: int) -> None:
+        """mcdc_ctx_set_option: "zc_batch_blocks", "zc_two",
+        "test_fail_after_index" (test and tuning settings of this context)."""
+        check(load().mcdc_ctx_set_option(self._h, name.encode(), int(value)))
 
     @_locked
     def timing(self) -> dict:

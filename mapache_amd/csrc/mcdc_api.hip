@@ -1157,7 +1157,31 @@ int mcdc_device_free(mcdc_ctx *ctx, void *d_ptr) {
 int mcdc_ctx_synchronize(mcdc_ctx *ctx) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  HIP_TRY(hipDeviceSynchronize());
+  // the context's own streams (every call of the library enqueues on them),
+  // then the null stream (the plain copies of the utilities): other
+  // contexts' work on the device is not waited for
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream2));
+  HIP_TRY(hipStreamSynchronize(nullptr));
+  return MCDC_OK;
+}
+
+int mcdc_ctx_set_option(mcdc_ctx *ctx, const char *name, long long value) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!name) return fail(MCDC_E_INVALID, "option name is NULL");
+  const std::string n(name);
+  if (n == "zc_batch_blocks") {
+    if (value < (long long)kZcSegBlocks || value > (1ll << 24))
+      return fail(MCDC_E_INVALID, "zc_batch_blocks %lld outside [%u, 2^24]", value, kZcSegBlocks);
+    ctx->knobs.zc_batch = (uint64_t)value;
+  } else if (n == "zc_two") {
+    ctx->knobs.zc_two = value != 0;
+  } else if (n == "test_fail_after_index") {
+    ctx->knobs.test_fail_after_index = value != 0;
+  } else {
+    return fail(MCDC_E_INVALID, "unknown option '%s'", name);
+  }
   return MCDC_OK;
 }
 
@@ -1830,7 +1854,7 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   };
   rc = rest();
   if (rc == MCDC_OK && ctx->knobs.test_fail_after_index)  // test hook (tests/test_gpu_save.py)
-    rc = fail(MCDC_E_DEVICE, "injected failure after the index add (MCDC_TEST_FAIL_AFTER_INDEX)");
+    rc = fail(MCDC_E_DEVICE, "injected failure after the index add (option test_fail_after_index)");
   if (rc) {
     if (nb) {  // rollback: the index as before the call
       ix->cur ^= 1;
@@ -1896,9 +1920,10 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   // Batches alternate between two scratch sets on the context's two streams,
   // so one batch's kernels run into the other's tails; only the final copies
   // (output offsets carried from batch to batch) are ordered across streams.
-  // One set when a single batch of kZcBatchBlocks / 2 holds everything.
-  const bool two = ctx->knobs.zc_two && total_blocks > kZcBatchBlocks / 2 && longest <= kZcBatchBlocks / 2;
-  const uint64_t mb = two ? kZcBatchBlocks / 2 : std::max(std::min<uint64_t>(total_blocks, kZcBatchBlocks), longest);
+  // One set when a single batch of zc_batch / 2 blocks holds everything.
+  const uint64_t zb = ctx->knobs.zc_batch;
+  const bool two = ctx->knobs.zc_two && total_blocks > zb / 2 && longest <= zb / 2;
+  const uint64_t mb = two ? zb / 2 : std::max(std::min<uint64_t>(total_blocks, zb), longest);
   tmpb = std::max(tmpb, zc_tmp_bytes(mb));
   struct Set {
     DevBuf *blocks, *stage, *seqs, *piece, *poff, *tmp, *words, *recs;
@@ -1938,7 +1963,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
                     (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
                     (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
                     ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
-                    two ? ev[1 + k] : nullptr);
+                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks);
     if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
     prev = k;
     c0 = c1;

@@ -2143,7 +2143,6 @@ Knobs read_knobs() {
   k.lane_seg_chunks = std::max(env("MCDC_LANE_SEG_CHUNKS", k.lane_seg_chunks), 1);
   k.zc_huf = env("MCDC_ZC_HUF", k.zc_huf ? 1 : 0) != 0;
   k.zc_two = env("MCDC_ZC_TWO", k.zc_two ? 1 : 0) != 0;
-  k.test_fail_after_index = env("MCDC_TEST_FAIL_AFTER_INDEX", 0) != 0;
 #ifdef MCDC_AB_KNOBS
   k.group = env("MCDC_GROUP", k.group);
   if (k.group != 8 && k.group != 16 && k.group != 32) k.group = kGroup;

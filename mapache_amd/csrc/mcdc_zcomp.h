@@ -13,6 +13,7 @@ constexpr uint64_t kZcBlock = 32768;               // zstd block: 32 KiB of one 
 constexpr uint32_t kZcSeqCap = kZcBlock / 4;       // sequences per block: every match is >= 4 bytes
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
 constexpr uint32_t kZcSegBlocks = 8;               // blocks of a chunk one match-finder workgroup covers
+constexpr uint32_t kZcPrime = 65536;               // bytes before a segment the finder re-inserts
 #ifndef MCDC_ZC_BATCH
 #define MCDC_ZC_BATCH 16384  // (compile-time A/B knob)
 #endif
@@ -23,7 +24,15 @@ struct ZcBlock {
   uint32_t len, chunk, b, nb;   // block b of nb of chunk
   uint32_t nlit, nseq, csize;   // parse result; csize 0 = stored raw
   uint32_t lsize;               // literals section already in the staging slot (Huffman / RLE), 0 = raw literals
+  uint32_t flags;               // kZcRaw: k_zc_probe found the block hopeless (stored raw, no finder / parse)
 };
+constexpr uint32_t kZcRaw = 1u;
+// Far matches (k_zc_probe / k_zc_far): per block record kZcFarSlots table
+// entries (a segment of kZcSegBlocks records owns kZcSegBlocks x kZcFarSlots
+// slots) and kZcBlock / 1024 anchor ballots, carved from the batch's `recs`
+// scratch (free until k_zc_chain).
+constexpr uint32_t kZcFarSlots = 512;
+constexpr uint32_t kZcFarBallots = (uint32_t)(kZcBlock / 1024);
 
 size_t zc_tmp_bytes(uint64_t n);
 // cnt[i] = blocks of chunk i (n + 1 entries), first = exclusive prefix; chunks
@@ -43,8 +52,9 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint32_t *words, uint64_t *recs,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true,
-                     hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr);
+                     hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr, bool far = true);
 // (final_after: the output offsets' previous update, on another stream, is
-// waited for before this batch's final copy; final_done: recorded after it)
+// waited for before this batch's final copy; final_done: recorded after it;
+// far: some chunk is longer than one finder segment, k_zc_far runs)
 
 }  // namespace mcdc

@@ -81,7 +81,10 @@ constexpr uint32_t kHsLog = MCDC_ZC_HS, kHlLog = MCDC_ZC_HL;
 constexpr uint32_t kFindThreads = MCDC_ZC_FT;  // threads per workgroup (16 waves)
 constexpr uint32_t kFindTile = kFindThreads;  // positions per step
 constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
-constexpr uint32_t kPrime = 131072;           // bytes before a segment re-inserted (its reach into earlier segments)
+constexpr uint32_t kPrime = kZcPrime;         // bytes before a segment re-inserted (farther: k_zc_far)
+// Match words: length (<= kMlCap) << 24 | offset; bit 31 marks a verified
+// kMlCap match of the finder's own (readers take the length as (w >> 24) & 31)
+constexpr uint32_t kZcLocalCap = 1u << 31;
 
 // Keys hashed with 24-bit multiplies (full rate; a 32-bit multiply issues at
 // a quarter of it): the key cut into 24- and 16-bit pieces, each multiplied by
@@ -142,7 +145,7 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
     z.chunk = (uint32_t)c;
     z.b = (uint32_t)b;
     z.nb = (uint32_t)nb;
-    z.nlit = z.nseq = z.csize = z.lsize = 0;
+    z.nlit = z.nseq = z.csize = z.lsize = z.flags = 0;
     blocks[f + b - b0] = z;
   }
 }
@@ -282,6 +285,14 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
   // the segment's words: the chunk's blocks are consecutive records, so
   // position p's word is wseg[p]; positions outside the segment keep nothing
   uint32_t *wseg = words + (bi0 - B0.b) * kZcBlock;
+  // (word stores: a 32-bit offset from the segment's first word; from the
+  // chunk's, 4 p wraps for chunks of 1 GiB or more)
+  uint32_t *const wseg0 = wseg + seg0;
+  {  // a segment whose blocks k_zc_probe found hopeless: nothing to find
+    bool all_raw = true;
+    for (uint32_t k = 0; k * (uint32_t)kZcBlock < seg1 - seg0; ++k) all_raw &= (blocks[bi0 + k].flags & kZcRaw) != 0;
+    if (all_raw) return;
+  }
   if (clen < 16 || cbytes < 16) {  // (too short to match: every position a literal)
     for (uint32_t p = seg0 + tid; p < seg1; p += kFindThreads) wseg[p] = 0u;
     return;
@@ -311,7 +322,10 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     uint4 y = to4(S.y);
     if (S.tail) y = fix16(y, S.q, cbytes);
     const uint32_t m = S.k ? min(prefix16(S.x, y), lim) : 0u;
-    if (S.v) ast32s(wseg, 4 * S.p, m >= zs::kMinMatch ? (m << 24 | (S.p - S.q)) : 0u);
+    // (a full kMlCap match carries kZcLocalCap: k_zc_far's atomicMax keeps it)
+    if (S.v)
+      ast32s(wseg0, 4 * (S.p - seg0),
+             m >= zs::kMinMatch ? (m << 24 | (S.p - S.q) | (m == kMlCap ? kZcLocalCap : 0u)) : 0u);
   };
 #ifdef MCDC_ZC_TIMING  // (A/B: cycles per phase of wave 0 in some workgroups, printed)
   uint64_t tm[5] = {0, 0, 0, 0, 0}, tstart = __builtin_amdgcn_s_memtime(), tnow = 0;
@@ -402,6 +416,255 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
 }
 
 
+// ---- the probe and the far matches --------------------------------------
+// Anchors: positions whose 8-byte key mixes (mix8) to a value with its top
+// bits clear, so that a repeated stretch has anchors at the same places in
+// both copies.  Slots from the mix's next bits, 13-bit tags from the 5-byte
+// key's mix (mix5).  Near anchors (1 position in 32) feed k_zc_probe's repeat
+// test, far anchors (1 in 128, a subset) the far tables of k_zc_far.
+constexpr uint32_t kNearLog = 14;
+__device__ __forceinline__ bool near_anchor(uint32_t m8) { return m8 < (1u << 27); }
+__device__ __forceinline__ bool far_anchor(uint32_t m8) { return m8 < (1u << 25); }
+__device__ __forceinline__ uint32_t near_slot(uint32_t m8) { return (m8 >> 13) & ((1u << kNearLog) - 1u); }
+__device__ __forceinline__ uint32_t far_slot(uint32_t m8) { return (m8 >> 13) & (kZcSegBlocks * kZcFarSlots - 1u); }
+__device__ __forceinline__ uint32_t anchor_tag(uint32_t m5) { return m5 >> 19; }
+static_assert(kZcSegBlocks * kZcFarSlots == 4096, "far slots: bits 13..24 of a far anchor's mix");
+// Bits per byte (order 0) at or above which a block without repeats is stored
+// raw: Huffman coding could save at most (8 - 7.9) / 8 of it, less its table.
+constexpr float kRawEntropy = 7.9f;
+constexpr uint32_t kProbeThreads = 1024, kProbeTile = 16 * kProbeThreads;
+static_assert(kPrime % kProbeTile == 0 && kZcBlock % kProbeTile == 0, "probe tiles start at segments and blocks");
+constexpr uint32_t kFarBack = 256;  // bytes a far match is extended backwards
+
+// bytes j .. j + 3 of the words w (little endian)
+__device__ __forceinline__ uint32_t byte_window(const uint32_t *w, int j) {
+  return (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2];
+}
+// equal bytes at the end of two 16-byte strings
+__device__ __forceinline__ uint32_t suffix16(uint4 x, uint4 y) {
+  const uint64_t d0 = (uint64_t)(x.y ^ y.y) << 32 | (x.x ^ y.x), d1 = (uint64_t)(x.w ^ y.w) << 32 | (x.z ^ y.z);
+  return d1 ? (uint32_t)__builtin_clzll(d1) >> 3 : d0 ? 8u + ((uint32_t)__builtin_clzll(d0) >> 3) : 16u;
+}
+
+// The probe: one workgroup per finder segment (the segments longest first,
+// as k_zc_find).  Pass 1 over the segment: a byte histogram of each of its
+// blocks (8 of every 16 bytes: a 16 KiB sample, whose plug-in entropy of
+// uniform bytes is 7.99 bits); in a chunk of more than one segment, its far
+// anchors into its far table in HBM (latest per slot; not for a chunk's last
+// segment: no later segment reads it) and their ballots (a bit per 16
+// positions, a word per 1024) for k_zc_far.  Only if a block carries
+// kRawEntropy bits per byte or more: pass 2, every near anchor of the
+// re-inserted bytes and the segment up to the last such block into an LDS
+// table (earliest per slot), and pass 3, such a block is hopeless if none of
+// its near anchors finds an earlier anchor with its key -- kZcRaw, stored raw
+// without the finder, the parse or the entropy coders (random, compressed or
+// encrypted data).  k_zc_far's rescue mode then clears kZcRaw of a block
+// with a far match.
+__global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks,
+                                                            uint64_t nblk, const uint32_t *order, uint32_t *ftab,
+                                                            uint64_t *fbits) {
+  __shared__ uint32_t near[1u << kNearLog];
+  __shared__ uint32_t hist[kZcSegBlocks][256];
+  __shared__ uint32_t rep[kZcSegBlocks], high[kZcSegBlocks];
+  const uint64_t bi0 = order[blockIdx.x];
+  if (bi0 >= nblk) return;
+  const ZcBlock B0 = blocks[bi0];
+  if (B0.b % kZcSegBlocks) return;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / 64;
+  const uint64_t csrc = B0.src - (uint64_t)B0.b * kZcBlock;
+  const uint32_t clen = (B0.nb - 1) * (uint32_t)kZcBlock + blocks[bi0 + (B0.nb - 1 - B0.b)].len;
+  const uint32_t seg0 = B0.b * (uint32_t)kZcBlock;
+  const uint32_t seg1 = min(clen, seg0 + kZcSegBlocks * (uint32_t)kZcBlock);
+  const uint32_t prime0 = seg0 > kPrime ? seg0 - kPrime : 0u;
+  const uint32_t nsb = (seg1 - seg0 + (uint32_t)kZcBlock - 1) / (uint32_t)kZcBlock;
+  const bool far_out = seg1 < clen;  // a later segment reads this one's far table
+  const bool far_in = seg0 > 0;      // k_zc_far reads this segment's ballots
+  const uint8_t *cb = base + csrc;
+  const uint64_t cbytes = nbytes - csrc;
+  if (clen < 16 || cbytes < 16) return;  // (flags stay 0)
+  uint32_t *ft = ftab + bi0 * kZcFarSlots;
+  for (uint32_t k = tid; k < kZcSegBlocks * 256; k += kProbeThreads) (&hist[0][0])[k] = 0;
+  if (tid < kZcSegBlocks) rep[tid] = high[tid] = 0;
+  if (far_out)
+    for (uint32_t k = tid; k < kZcSegBlocks * kZcFarSlots; k += kProbeThreads) ft[k] = 0;
+  __syncthreads();  // (the far table's zeros stored before any atomic of the workgroup)
+  auto load6 = [&](uint32_t p, uint32_t(&w)[6]) {  // bytes p .. p + 23 (zero past the buffer)
+    const uint4 a = fix16(ld16c(cb, p, cbytes), p, cbytes), b = fix16(ld16c(cb, p + 16, cbytes), p + 16, cbytes);
+    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
+  };
+  const bool hash1 = far_out || far_in;
+  for (uint32_t t0 = seg0; t0 < seg1; t0 += kProbeTile) {
+    const uint32_t p = t0 + 16 * tid;
+    uint32_t fm = 0;
+    if (p < seg1) {
+      uint32_t w[6];
+      if (hash1) {
+        load6(p, w);
+      } else {
+        const uint4 a = fix16(ld16c(cb, p, cbytes), p, cbytes);
+        w[0] = a.x, w[1] = a.y;
+      }
+      const uint32_t hb = (p - seg0) >> 15;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (p + j < seg1) atomicAdd(&hist[hb][(w[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+      if (hash1) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t q = p + j;
+          if (q >= seg1 || q + 8 > clen) continue;
+          const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
+          if (!far_anchor(m8)) continue;
+          fm |= 1u << j;
+          if (far_out) atomicMax(&ft[far_slot(m8)], (q - seg0 + 1) << 14 | anchor_tag(mix5(lo, hi)));
+        }
+      }
+    }
+    if (far_in) {  // (uniform)
+      const uint64_t bal = __ballot(fm != 0);
+      const uint32_t qw = t0 + 1024 * wv;
+      if (lane == 0 && qw < seg1) fbits[(bi0 - B0.b) * kZcFarBallots + qw / 1024] = bal;
+    }
+  }
+  __syncthreads();
+  if (wv < nsb) {  // order-0 entropy of block wv's sample: n log2 n - sum c log2 c >= kRawEntropy n
+    float sc = 0.f;
+    uint32_t n = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint32_t c = hist[wv][lane + 64 * h];
+      sc += c ? (float)c * __log2f((float)c) : 0.f;
+      n += c;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      sc += __shfl_xor(sc, o);
+      n += __shfl_xor(n, o);
+    }
+    if (lane == 0) high[wv] = n >= 1024 && (float)n * __log2f((float)n) - sc >= kRawEntropy * (float)n ? 1u : 0u;
+  }
+  __syncthreads();
+  uint32_t hend = 0;  // the end of the last high-entropy block
+  for (uint32_t k = 0; k < nsb; ++k)
+    if (high[k]) hend = min(seg1, seg0 + (k + 1) * (uint32_t)kZcBlock);
+  if (!hend) return;
+  for (uint32_t k = tid; k < (1u << kNearLog); k += kProbeThreads) near[k] = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t t0 = prime0; t0 < hend; t0 += kProbeTile) {
+    const uint32_t p = t0 + 16 * tid;
+    if (p >= hend) continue;
+    uint32_t w[6];
+    load6(p, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t q = p + j;
+      if (q >= hend || q + 8 > clen) continue;
+      const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
+      if (near_anchor(m8)) atomicMin(&near[near_slot(m8)], (q - prime0 + 1) << 13 | anchor_tag(mix5(lo, hi)));
+    }
+  }
+  __syncthreads();
+  for (uint32_t t0 = seg0; t0 < hend; t0 += kProbeTile) {
+    const uint32_t p = t0 + 16 * tid;
+    if (p >= hend || !high[(p - seg0) >> 15]) continue;
+    uint32_t w[6];
+    load6(p, w);
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t q = p + j;
+      if (q >= hend || q + 8 > clen) continue;
+      const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
+      if (!near_anchor(m8)) continue;
+      const uint32_t e = near[near_slot(m8)];
+      hit |= (e & 0x1FFFu) == anchor_tag(mix5(lo, hi)) && (e >> 13) - 1 + prime0 < q;
+    }
+    if (hit) rep[(p - seg0) >> 15] = 1;  // (any writer sets it)
+  }
+  __syncthreads();
+  if (tid < nsb && high[tid] && !rep[tid]) blocks[bi0 + tid].flags = kZcRaw;
+}
+
+// Far matches: the 2^20 window of SecureStorage::compress (storage.rs:74-84)
+// beyond the finder's reach (its segment and the kPrime bytes before it).
+// One wave per 1024 positions of a block in a chunk's second or later
+// segment.  Each far anchor (k_zc_probe's ballots) looks up the far tables of
+// the 5 segments before its own, nearest first (the latest anchor per slot of
+// each); a tagged entry within the window is verified on 16 bytes, extended
+// backwards (up to kFarBack bytes, 16 at a time), and every position from the
+// extension's start to the anchor gets the far match's word -- unless the
+// finder verified a full match there itself (atomicMax: kZcLocalCap words
+// win, then the longer match, then the larger offset, so the result does not
+// depend on the order).  k_zc_parse extends the full matches.
+//
+// Rescue mode (before the finder): the same lookups for the blocks
+// k_zc_probe found hopeless (its repeat test sees only the segment and the
+// re-inserted bytes); a verified far match clears the block's kZcRaw.
+__global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
+                                                const uint32_t *ftab, const uint64_t *fbits, uint32_t *words,
+                                                bool rescue) {
+  MCDC_VGPR_PAD(40);  // (not an exact fill)
+  const uint64_t g = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  const uint64_t bi = g / kZcFarBallots;
+  const uint32_t j = (uint32_t)(g % kZcFarBallots), lane = lane_id();
+  if (bi >= nblk) return;
+  const ZcBlock B = blocks[bi];
+  if (B.b < kZcSegBlocks || ((B.flags & kZcRaw) != 0) != rescue || j * 1024 >= B.len) return;
+  const uint64_t bal = fbits[bi * kZcFarBallots + j];
+  if (!((bal >> lane) & 1)) return;
+  const uint64_t rec0 = bi - B.b;
+  const uint64_t csrc = B.src - (uint64_t)B.b * kZcBlock;
+  const uint32_t clen = (B.nb - 1) * (uint32_t)kZcBlock + blocks[bi + (B.nb - 1 - B.b)].len;
+  const uint8_t *cb = base + csrc;
+  const uint64_t cbytes = nbytes - csrc;
+  uint32_t *wc = words + rec0 * kZcBlock;  // the chunk's words
+  const uint32_t s = B.b / kZcSegBlocks;
+  const uint32_t p = B.b * (uint32_t)kZcBlock + j * 1024 + 16 * lane;
+  const uint32_t bend = min(clen, (B.b + 1) * (uint32_t)kZcBlock);
+  uint32_t am = 0;  // far anchors among p .. p + 15
+  {
+    uint32_t w[6];
+    const uint4 a = fix16(ld16c(cb, p, cbytes), p, cbytes), b = fix16(ld16c(cb, p + 16, cbytes), p + 16, cbytes);
+    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj)
+      if (p + jj + 8 <= clen && far_anchor(mix8(byte_window(w, jj), byte_window(w, jj + 4)))) am |= 1u << jj;
+  }
+  while (am) {
+    const uint32_t q = p + (uint32_t)__builtin_ctz(am);
+    am &= am - 1;
+    if (q + kMlCap > bend || (!rescue && (wc[q] & kZcLocalCap))) continue;
+    const uint4 x = fix16(ld16c(cb, q, cbytes), q, cbytes);
+    const uint32_t m8 = mix8(x.x, x.y), tag = anchor_tag(mix5(x.x, x.y)), slot = far_slot(m8);
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t k = 1; k <= 5 && k <= s; ++k) {
+      const uint32_t e = ftab[(rec0 + (uint64_t)(s - k) * kZcSegBlocks) * kZcFarSlots + slot];
+      if (e && (e & 0x3FFFu) == tag) {
+        const uint32_t cc = (s - k) * kZcSegBlocks * (uint32_t)kZcBlock + (e >> 14) - 1;
+        if (q - cc <= zs::kWindow) c = cc;
+        break;
+      }
+    }
+    if (c == 0xFFFFFFFFu) continue;
+    if (prefix16(x, fix16(ld16c(cb, c, cbytes), c, cbytes)) < kMlCap) continue;
+    if (rescue) {
+      atomicAnd(&blocks[bi].flags, ~kZcRaw);
+      return;
+    }
+    uint32_t bk = 0;
+    while (bk < kFarBack && c >= bk + 16) {
+      const uint32_t sf = suffix16(*reinterpret_cast<const uint4 *>(cb + (q - bk - 16)),
+                                   *reinterpret_cast<const uint4 *>(cb + (c - bk - 16)));
+      bk += sf;
+      if (sf < 16) break;
+    }
+    const uint32_t off = q - c;
+    for (uint32_t x0 = q - bk; x0 <= q; ++x0) {
+      const uint32_t lim = min(kMlCap, min(clen, (x0 / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock) - x0);
+      if (lim >= zs::kMinMatch) atomicMax(wc + x0, lim << 24 | off);
+    }
+  }
+}
+
 #ifdef MCDC_ZC_TIMING  // (A/B: cycles per phase of one wave, some blocks, printed)
 #define ZT_DECL uint64_t zt_[6] = {0, 0, 0, 0, 0, 0}, zt0_ = __builtin_amdgcn_s_memtime(), zt1_ = 0
 #define ZT(k) (zt1_ = __builtin_amdgcn_s_memtime(), zt_[k] += zt1_ - zt0_, zt0_ = zt1_)
@@ -467,6 +730,10 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
   const ZcBlock B = blocks[bi];
+  if (B.flags & kZcRaw) {  // (hopeless, k_zc_probe: stored raw)
+    if (lane == 0) blocks[bi].nlit = blocks[bi].nseq = 0;
+    return;
+  }
   const uint32_t end = B.len;
   const uint8_t *p0 = base + B.src;
   const uint32_t *w = words + bi * kZcBlock;
@@ -528,7 +795,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane;
       valid[j] = wb + i < end;
-      ml[j] = wd[j] >> 24;
+      ml[j] = (wd[j] >> 24) & 31u;
       cj[j] = valid[j] ? min(i + (ml[j] ? ml[j] : 1u), 256u) : 256u;
       J[0][i] = (uint16_t)cj[j];
       offl[i] = wd[j] & 0xFFFFFFu;
@@ -834,7 +1101,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   const ZcBlock B = blocks[bi];
   // a block without sequences: all of it literals, read from the input (k_zc_parse staged nothing)
   const uint32_t n = B.nseq ? B.nlit : B.len;
-  if (n < 32) return;  // (lsize stays 0: raw literals)
+  if (n < 32 || (B.flags & kZcRaw)) return;  // (lsize stays 0: raw literals; hopeless blocks stored raw)
   uint8_t *st = stage + bi * kZcSlot;
   const uint8_t *src = B.nseq ? st + kLitHdr : base + B.src;
   ZT_DECL;
@@ -1644,7 +1911,7 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
-                     hipEvent_t final_after, hipEvent_t final_done) {
+                     hipEvent_t final_after, hipEvent_t final_done, bool far) {
   if (nblk == 0) return;
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
@@ -1652,8 +1919,17 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   // finder's segment order and the parse's block order)
   uint32_t *order = reinterpret_cast<uint32_t *>(piece), *porder = order + nblk;
   hipLaunchKernelGGL(k_zc_segorder, dim3(1), dim3(1024), 0, st, blocks, nblk, order, porder);
+  // (the far tables and ballots live in recs, free until k_zc_chain)
+  uint32_t *ftab = reinterpret_cast<uint32_t *>(recs);
+  uint64_t *fbits = reinterpret_cast<uint64_t *>(ftab + nblk * kZcFarSlots);
+  hipLaunchKernelGGL(k_zc_probe, dim3((unsigned)nblk), dim3(kProbeThreads), 0, st, base, nbytes, blocks, nblk, order,
+                     ftab, fbits);
+  const dim3 gfar((unsigned)((nblk * kZcFarBallots + 3) / 4));
+  if (far)
+    hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, true);
   hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
                      order);
+  if (far) hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, false);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
                      seqs, porder);
   if (huf)

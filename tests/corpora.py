@@ -92,6 +92,29 @@ def binary(n: int, seed: int = 5) -> np.ndarray:
     return np.frombuffer(b"".join(parts)[:n], np.uint8).copy()
 
 
+def far(n: int, seed: int = 31) -> np.ndarray:
+    """Long repeats at 256 KiB - 1 MiB distances (the 2^20 window of
+    SecureStorage::compress, storage.rs:74-84, at mapache's 512K/1M/8M
+    chunks): a base of 32 KiB pieces taken in turn from text, records and
+    binary, then, every 4-64 KiB, a 1-32 KiB stretch overwritten by a copy of
+    the bytes 256 KiB - 1 MiB before it (about a third of the bytes), as in a
+    tree of near-duplicate files."""
+    rng = np.random.default_rng(seed)
+    src = [text(n, seed + 1), records(n, seed + 2), binary(n, seed + 3)]
+    out = np.empty(n, np.uint8)
+    for k, o in enumerate(range(0, n, 32768)):
+        out[o:o + 32768] = src[k % 3][o:o + 32768]
+    pos = 256 << 10
+    while pos < n:
+        pos += int(rng.integers(4 << 10, 64 << 10))
+        ln, d = int(rng.integers(1 << 10, 32 << 10)), int(rng.integers(256 << 10, 1 << 20))
+        if pos - d < 0 or pos + ln > n:
+            continue
+        out[pos:pos + ln] = out[pos - d:pos - d + ln]
+        pos += ln
+    return out
+
+
 def by_name(kind: str, n: int, seed: int | None = None) -> np.ndarray:
-    f = {"text": text, "records": records, "binary": binary}[kind]
+    f = {"text": text, "records": records, "binary": binary, "far": far}[kind]
     return f(n) if seed is None else f(n, seed)

@@ -59,7 +59,7 @@ def test_digest_matches_oracle_digest():
 
 
 def test_abi_version():
-    assert _lib.load().mcdc_abi_version() == 4
+    assert _lib.load().mcdc_abi_version() == 5
 
 
 def test_no_device_fails_loudly():

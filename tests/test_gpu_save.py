@@ -113,18 +113,18 @@ def test_gate_is_min_chunk_size_not_the_chunkers_min(ctx):
             assert len(got[0][f]) == len(O.chunk(O.Params(*P16), files[f])) > 1, f
 
 
-def test_failure_after_index_add_rolls_back(monkeypatch):
+def test_failure_after_index_add_rolls_back():
     """Every failure after the dedup step leaves the index as it was (ADVICE
-    r03): a context built with the test hook MCDC_TEST_FAIL_AFTER_INDEX fails
-    each call after its encode and pack steps have run; the index keeps its
-    size and a later call on a normal context stores the same blobs."""
+    r03): a context with the test option "test_fail_after_index" (set through
+    mcdc_ctx_set_option: no environment variable reaches the shipping library)
+    fails each call after its encode and pack steps have run; the index keeps
+    its size and a later call on a normal context stores the same blobs."""
     files = _files(8)
     data, offs, lens = _arena(files)
     p = _lib.params(*P16)
     nonces, hn, pad = _rand(14, 4000, 12), _rand(15, 64, 12), _rand(16, 64 * 63, 36)
-    monkeypatch.setenv("MCDC_TEST_FAIL_AFTER_INDEX", "1")
     bad = _lib.Context(0, 64 << 20)
-    monkeypatch.delenv("MCDC_TEST_FAIL_AFTER_INDEX")
+    bad.set_option("test_fail_after_index", 1)
     good = _lib.Context(0, 64 << 20)
     try:
         with bad.index_create() as ix:

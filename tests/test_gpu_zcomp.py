@@ -92,18 +92,68 @@ def test_chunks_of_a_stream_decode(ctx, kind, p):
         assert nbytes <= data.size + 6 * len(ch) + 3 * (data.size // 16384 + len(ch))  # raw blocks, no growth
 
 
-@pytest.mark.parametrize("kind", ["text", "records", "binary"])
-def test_ratio_beside_level3(ctx, kind):
-    """The compressed size against libzstd level 3 (the crate's setting,
-    storage.rs:74-84) on the same 16/64/256 KiB chunks: within 5 % of its
-    ratio on every corpus (tools/zc_model2.cpp: text 98 %, records 103 %,
-    binary 101 %)."""
-    data = _data(kind, 16 << 20, 5)
-    ch = O.chunk(O.Params(*P16), data)
-    fr, out, nbytes = _compress(ctx, data, ch)
+def _level3(data, ch):
     z = O.Zstd()
-    lvl3 = sum(len(z.compress(data[int(o):int(o + n)].tobytes(), False)) for o, n in zip(ch["offset"], ch["length"]))
+    return sum(len(z.compress(data[int(o):int(o + n)].tobytes(), False)) for o, n in zip(ch["offset"], ch["length"]))
+
+
+@pytest.mark.parametrize("kind", ["text", "records", "binary", "far"])
+@pytest.mark.parametrize("p", [P16, P512], ids=["P16", "P512"])
+def test_ratio_beside_level3(ctx, kind, p):
+    """The compressed size against libzstd level 3 (the crate's setting,
+    storage.rs:74-84: the streaming encoder, window log 20) on the same chunks,
+    at the bench's 16/64/256 KiB and at mapache's own 512K/1M/8M
+    (defaults.rs:35-40): within 5 % of its ratio on every corpus.  `far`
+    repeats 1-32 KiB stretches 256 KiB - 1 MiB back: at P512 only the far
+    tables (k_zc_far) reach them (tools/zc_model3.cpp: 82 % of level 3
+    without them, 98 % with)."""
+    data = corpora.by_name(kind, (16 << 20) if p == P16 else (40 << 20), 5)
+    ch = O.chunk(O.Params(*p), data)
+    fr, out, nbytes = _compress(ctx, data, ch)
+    _check_frames_subset(data, ch, fr, out, np.arange(0, len(ch), 7))
+    lvl3 = _level3(data, ch)
     assert data.size / nbytes >= 0.95 * data.size / lvl3, (data.size / nbytes, data.size / lvl3)
+
+
+def _hopeless_mix(n, seed):
+    """64 KiB stretches in turn: random bytes, text, random bytes, a copy of
+    the random stretch 192 KiB back (across a finder segment start or within
+    one), a copy of the random stretch 640 KiB back (the far tables only), text."""
+    txt = _text(n, seed)
+    out = np.empty(n, np.uint8)
+    for k, o in enumerate(range(0, n, 65536)):
+        e, r = min(n, o + 65536), k % 6
+        if r in (1, 5):
+            out[o:e] = txt[o:e]
+        elif r == 3:
+            out[o:e] = out[o - 3 * 65536:e - 3 * 65536]
+        elif r == 4 and k >= 10:
+            out[o:e] = out[o - 10 * 65536:e - 10 * 65536]
+        else:
+            out[o:e] = O.random_bytes(e - o, seed * 1000 + k)
+    return out
+
+
+@pytest.mark.parametrize("p", [P16, P512], ids=["P16", "P512"])
+def test_hopeless_blocks_and_repeats(ctx, p):
+    """The early-out (k_zc_probe): blocks of random bytes (order-0 entropy >=
+    7.9 bits, no repeated anchors) are stored raw without the finder and the
+    entropy coders; repeated random stretches are not hopeless (near: an
+    earlier anchor with the same key; far: k_zc_far's tables) and compress;
+    text compresses.  Every frame decodes, and the ratio is within 5 % of level
+    3's on the same chunks."""
+    data = _hopeless_mix(24 << 20, 7)
+    ch = O.chunk(O.Params(*p), data)
+    fr, out, nbytes = _compress(ctx, data, ch)
+    _check_frames(data, ch, fr, out, nbytes)
+    lvl3 = _level3(data, ch)
+    assert data.size / nbytes >= 0.95 * data.size / lvl3, (data.size / nbytes, data.size / lvl3)
+    allrand = O.random_bytes(8 << 20, 3)
+    ch2 = O.chunk(O.Params(*p), allrand)
+    fr2, out2, nb2 = _compress(ctx, allrand, ch2)
+    _check_frames(allrand, ch2, fr2, out2, nb2)
+    nblk = sum((int(n) + 32767) // 32768 for n in ch2["length"])
+    assert nb2 == allrand.size + 6 * len(ch2) + 3 * nblk  # every block raw
 
 
 def test_edge_lengths_offsets_overlaps(ctx):
@@ -124,11 +174,12 @@ def test_edge_lengths_offsets_overlaps(ctx):
 
 def test_long_chunks_segments_and_reach(ctx):
     """Chunks longer than one match-finder segment (8 blocks, 256 KiB): the
-    segment after the first re-inserts the 128 KiB before it, long matches
+    segment after the first re-inserts the 64 KiB before it, long matches
     (extended past the 16 verified bytes) across segment starts, repeats 70 000
-    bytes apart (found across segment starts through the re-inserted bytes), a
-    2 MiB period (beyond the 2^20 window: never referenced), an 8 MiB chunk;
-    every frame decodes within the 2^20 window."""
+    bytes apart (across segment starts: the re-inserted bytes and the far
+    tables), a 2 MiB period (beyond the 2^20 window: never referenced, every
+    block hopeless), an 8 MiB chunk; every frame decodes within the 2^20
+    window."""
     rng = np.random.default_rng(12)
     blk = O.random_bytes(40_000, 3)
     per = np.tile(blk, 60)[:2_000_000]  # period 40 000 < 64 KiB: everything after the first period matches
@@ -171,23 +222,53 @@ def test_deterministic_and_device_lists(ctx):
     assert nb == a[2] and (fr == a[0]).all() and out.tobytes() == a[1].tobytes()
 
 
-def test_two_streams_match_one_stream(ctx, monkeypatch):
-    """Above one batch set (4096 blocks) batches alternate between two scratch
-    sets on two streams (only the final copies are ordered across them): the
-    output is byte-identical to one stream's (MCDC_ZC_TWO=0, read at context
-    creation) and decodes."""
-    data = np.tile(_data("text", 16 << 20, 7), 10)  # (160 MiB: ~6500 blocks)
-    ch = O.chunk(O.Params(*P16), data)
-    a = _compress(ctx, data, ch)
-    monkeypatch.setenv("MCDC_ZC_TWO", "0")
-    one = _lib.Context(0, 1 << 30)
-    try:
-        b = _compress(one, data, ch)
-    finally:
-        one.close()
-    assert a[2] == b[2] and (a[0] == b[0]).all() and a[1].tobytes() == b[1].tobytes()
-    pick = np.arange(0, len(ch), 97)
-    _check_frames_subset(data, ch, a[0], a[1], pick)
+@pytest.mark.parametrize("p,odd", [(P16, 0), (P16, 1), (P512, 0), (P512, 1)],
+                         ids=["P16-even", "P16-odd", "P512-even", "P512-odd"])
+def test_two_streams_match_one_stream(ctx, p, odd):
+    """Batches alternate between two scratch sets on two streams (only the
+    final copies are ordered across them) when the call holds more than half a
+    batch.  With a small batch (mcdc_ctx_set_option "zc_batch_blocks": dozens
+    of alternating batches, odd and even block counts per set) the output is
+    byte-identical to one stream's ("zc_two" 0) and to the default batch's,
+    and decodes."""
+    data = np.concatenate([_text(12 << 20, 7), corpora.far(12 << 20 if p == P16 else 52 << 20, 8)])
+    ch = O.chunk(O.Params(*p), data)
+    per = (ch["length"].astype(np.int64) + 32767) // 32768
+    batch = 2 * max(32, int(per.max())) + 2 * odd  # (a set holds the longest chunk)
+    ref = _compress(ctx, data, ch)
+    got = []
+    for two in (1, 0):
+        c = _lib.Context(0, 1 << 30)
+        try:
+            c.set_option("zc_batch_blocks", batch)
+            c.set_option("zc_two", two)
+            got.append(_compress(c, data, ch))
+        finally:
+            c.close()
+    assert int(per.sum()) > 4 * batch  # (several batches on each stream)
+    for a in got:
+        assert a[2] == ref[2] and (a[0] == ref[0]).all() and a[1].tobytes() == ref[1].tobytes()
+    _check_frames_subset(data, ch, ref[0], ref[1], np.arange(0, len(ch), 5))
+    with pytest.raises(_lib.McdcError):
+        ctx.set_option("zc_batch_blocks", 4)
+    with pytest.raises(_lib.McdcError):
+        ctx.set_option("no_such_option", 1)
+
+
+def test_chunk_over_1gib_decodes(ctx):
+    """A chunk just over 1 GiB (the finder's match-word stores
+    used a 32-bit byte offset from the chunk's first word, which wraps at 4 p
+    >= 2^32): its frame decodes to the chunk."""
+    n = (1 << 30) + 4097
+    base = _text(1 << 20, 11)
+    data = np.resize(base, n)
+    data[::65536] = np.arange(len(data[::65536]), dtype=np.uint32).astype(np.uint8)  # (not a pure period)
+    ch = np.zeros(1, dtype=_lib.CHUNK_DTYPE)
+    ch["length"] = n
+    fr, out, nbytes = _compress(ctx, data, ch)
+    assert nbytes < n // 50
+    z = O.Zstd()
+    assert z.decompress(out[:nbytes].tobytes(), n + 64) == data.tobytes()
 
 
 def _check_frames_subset(data, chunks, fr, out, pick):

@@ -1,6 +1,7 @@
 """GPU zstd compression throughput and ratio (mcdc_zstd_compress_device) on a
-random stream and on the bench's synthetic text, chunked at 16/64/256 KiB;
-device-resident in and out.  Usage: python tools/zc_bench.py [GiB] [steps]"""
+random stream and on the bench's synthetic corpora, chunked at 16/64/256 KiB
+(or mapache's 512K/1M/8M: P512); device-resident in and out.
+Usage: python tools/zc_bench.py [GiB] [steps] [kinds,...] [P16|P512]"""
 import json
 import os
 import sys
@@ -16,10 +17,11 @@ from oracle import oracle as O  # noqa: E402
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 4
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 n = int(gib * (1 << 30))
-p = _lib.params(16384, 65536, 262144, 1)
+p = _lib.params(524288, 1048576, 8388608, 1) if len(sys.argv) > 4 and sys.argv[4] == "P512" else \
+    _lib.params(16384, 65536, 262144, 1)
 ctx = _lib.Context(0, n + (1 << 20))
 res = {}
-for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records", "binary")):
+for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records", "binary", "far")):
     dp = ctx.device_alloc(n)
     if kind == "random":
         ctx.fill_random(dp, n, 0x6d61706163686521)
@@ -50,8 +52,16 @@ for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text",
             ok &= z.decompress(ctx.d2h_bytes(d_out + int(fr[i, 0]), int(fr[i, 1])).tobytes(), len(src) + 64) == src
         except AssertionError:  # (A/B timing variants may not decode)
             ok = False
+    lv3 = 0  # libzstd level 3 (the crate's streaming encoder) on the first 32 MiB of chunks
+    k3 = int(np.searchsorted(np.cumsum(ch["length"].astype(np.int64)), 32 << 20)) + 1
+    for i in range(min(k3, k)):
+        lv3 += len(z.compress(ctx.d2h_bytes(dp + int(ch["offset"][i]), int(ch["length"][i])).tobytes(), False))
+    fr3 = ctx.d2h_bytes(d_fr, 16 * min(k3, k)).view(np.uint64).reshape(-1, 2)
+    gpu3 = int(fr3[:, 1].sum())
     res[kind] = {"gib_s": round(n / dt / (1 << 30), 2), "device_ms": round(dev, 3), "ratio": round(n / nb, 4),
-                 "chunks": int(k), "probe_ok": bool(ok)}
+                 "chunks": int(k), "probe_ok": bool(ok),
+                 "ratio_32mib": round(float(ch["length"][:min(k3, k)].sum()) / gpu3, 4),
+                 "level3_ratio_32mib": round(float(ch["length"][:min(k3, k)].sum()) / lv3, 4)}
     for x in (d_fr, d_out, d_ch, dp):
         ctx.device_free(x)
 print(json.dumps(res))
