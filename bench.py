@@ -27,7 +27,9 @@ Prints ONE JSON line (rank 0).  Extra objects:
   e2e_host        - pinned host input -> H2D -> kernels -> boundaries to host
   e2e_pageable    - pageable host input (the Archiver's Vec<u8>), staged
   batch_files     - BASELINE configs[2]: 10 000 independent 8 MiB files, one call
-  small_files     - BASELINE configs[3] stand-in: synthetic kernel-tree-like mix
+  small_files     - BASELINE configs[3] size mix (80 000 log-normal files) of random bytes, chunker only
+  kernel_tree     - BASELINE configs[3] stand-in through the composed save path (mcdc_save_files at
+                    512K/1M/8M, gate, IDs, dedup, encode, packs): C-like text, ~10 % duplicate files
   chunk_ids       - SURVEY.md §8(f) next stage: BLAKE3 chunk IDs of the same 64 GiB
                     boundary list in HBM (ID::from_content, processor.rs:184), and
                     the chunk + ID pipeline
@@ -323,6 +325,80 @@ def small_files(ctx, p, nfiles: int, steps: int) -> dict:
     finally:
         ctx.device_free(d_out)
         ctx.device_free(arena)
+
+
+def kernel_tree(ctx, nfiles: int, steps: int) -> dict:
+    """BASELINE configs[3] ("extracted Linux kernel source tree, ~80 k small
+    files, dedup-heavy realistic mix") through the composed save path
+    (mcdc_save_files) at mapache's own 512K/1M/8M with the 512 KiB size gate:
+    most files take processor::save_file's whole-file branch
+    (/root/reference/src/archiver/processor.rs:144-153), the rest are chunked
+    (:160-205); IDs, the dedup index (repository_v1.rs:169-180), SecureStorage
+    encode with a key, packs.  Stand-in corpus (tests/corpora.kernel_tree: no
+    tree here or on the box): log-normal sizes, median 8 KiB, C-like text, ~10 %
+    duplicate files.  Device input, fresh index per call, packs D2H into a
+    reused pinned buffer; host_zstd (level 3 on host threads) vs gpu_compress.
+    Also the chunker alone over the same files (BASELINE's 16/64/256 KiB, no
+    gate: configs[3]'s chunking metric on text-like files)."""
+    from mapache_amd import _lib
+    from tests import corpora
+    from oracle import oracle as O
+    data, offs, lens, dup = corpora.kernel_tree(nfiles)
+    n = int(data.size)
+    p512 = _lib.params(512 << 10, 1 << 20, 8 << 20, 1)
+    key = bytes(range(32))
+    rng = np.random.default_rng(9)
+    nonces = rng.integers(0, 256, (nfiles + n // (512 << 10) + 64, 12), dtype=np.uint8)
+    hn, pad = rng.integers(0, 256, (4096, 12), dtype=np.uint8), rng.integers(0, 256, (4096 * 63, 36), dtype=np.uint8)
+    dp = ctx.device_alloc(n + 16)
+    ob = ctx.pinned_bytes(int(n * 1.01) + 4096 * nfiles + (1 << 16))
+    out = {"files": nfiles, "bytes": n, "median_file_bytes": int(np.median(lens)), "duplicate_files": int((dup >= 0).sum()),
+           "files_at_or_above_gate": int((lens >= (512 << 10)).sum())}
+    try:
+        ctx.h2d(dp, data)
+        p16 = _lib.params(*PARAMS)
+        cap = int(sum(int(s) // (p16.min_size - 1) + 2 for s in lens))
+        d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
+        try:
+            dt, (total, counts) = _timed(lambda: ctx.chunk_batch_device_to_device(p16, dp, offs, lens, d_out, cap),
+                                         steps, 1)
+            g = ctx.d2h_chunks(d_out, total)
+            pick = np.arange(0, nfiles, 997)
+            ends = np.cumsum(counts)
+            ok = True
+            for f in pick:  # sampled files against the oracle
+                r = O.chunk(O.Params(*PARAMS), data[int(offs[f]):int(offs[f] + lens[f])])
+                gf = g[int(ends[f] - counts[f]):int(ends[f])]
+                ok &= _same(gf, r)
+            out["chunk_only_p16"] = {"ms": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
+                                     "files_per_s": round(nfiles / dt, 1), "chunks": int(total),
+                                     "parity_probe_files": int(len(pick)), "parity_probe_ok": bool(ok)}
+        finally:
+            ctx.device_free(d_out)
+        for mode in ("host_zstd", "gpu_compress"):
+            def call():
+                with ctx.index_create() as ix:
+                    return ctx.save_files(p512, ix, dp, offs, lens, key, nonces, hn, pad, n=n,
+                                          gpu_compress=mode == "gpu_compress", out_buf=ob)
+            dt, (ids, new, packed, packs) = _timed(call, steps, 1)
+            t = ctx.timing()
+            distinct = len({x.tobytes() for f in ids for x in f})
+            body = packed[int(packs[0]["offset"]):int(packs[0]["offset"] + packs[0]["length"])].tobytes()
+            hdr = O.parse_header(body, key)
+            okd = all(O.blake3(np.frombuffer(O.storage_decode(body[o:o + ln], key, 16 << 20), np.uint8)) == b
+                      for b, _, o, ln in hdr[:64])
+            out[mode] = {"ms": round(dt * 1e3, 1), "gib_s": round(n / dt / GIB, 2), "files_per_s": round(nfiles / dt, 1),
+                         "blobs": int(new.size), "stored": int(new.sum()), "distinct_ids": distinct,
+                         "packs": int(len(packs)), "packed_bytes": int(packed.size), "ratio": round(n / packed.size, 3),
+                         "device_ms": round(t.get("device_ms", 0.0), 2), "decode_probe_ok": bool(okd and
+                                                                                               int(new.sum()) == distinct)}
+    finally:
+        ctx.device_free(dp)
+    out["note"] = ("mcdc_save_files from device memory at 512K/1M/8M (gate 512 KiB), key, fresh index per call, "
+                   "packs D2H into a reused pinned buffer; decode probe: the first pack's first 64 blobs decoded "
+                   "and BLAKE3-checked, stored == distinct IDs; full parity: tests/test_gpu_configs3.py")
+    out["data"] = "synthetic kernel-tree stand-in (tests/corpora.kernel_tree)"
+    return out
 
 
 def chunk_ids(ctx, p, dp: int, n: int, d_out: int, count: int, steps: int, cpu_sample_gib: float,
@@ -842,6 +918,8 @@ def main() -> int:
     ap.add_argument("--e2e-gib", type=float, default=8.0)
     ap.add_argument("--batch-files", type=int, default=10000, help="configs[2] file count (0: skip)")
     ap.add_argument("--small-files", type=int, default=80000, help="configs[3] file count (0: skip)")
+    ap.add_argument("--kernel-tree", type=int, default=80000,
+                    help="configs[3] kernel-tree stand-in through the save path: file count (0: skip)")
     ap.add_argument("--corpus-files-per-gpu", type=int, default=8192, help="configs[4]: 8 MiB files per GPU (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the files-in-parallel CPU baseline "
@@ -1067,7 +1145,8 @@ def main() -> int:
         threads = max(1, min(a.cpu_threads, _cpus()))
         for key, fn in (("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3, cpu_files, threads)
                          if a.batch_files > 0 else None),
-                        ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None)):
+                        ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None),
+                        ("kernel_tree", lambda: kernel_tree(ctx, a.kernel_tree, 3) if a.kernel_tree > 0 else None)):
             try:
                 result[key] = fn()
             except Exception as ex:  # reported, never silently dropped

@@ -1956,14 +1956,17 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   }
   int k = 0, prev = -1;  // set of the batch, set of the batch before
   for (uint64_t c0 = 0; c0 < nchunks; k ^= two ? 1 : 0) {  // batches of whole chunks, <= mb blocks each
-    uint64_t c1 = c0 + 1;
-    while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb) ++c1;
+    uint64_t c1 = c0 + 1, nseg = (hfirst[c0 + 1] - hfirst[c0] + kZcSegBlocks - 1) / kZcSegBlocks;
+    while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb) {
+      nseg += (hfirst[c1 + 1] - hfirst[c1] + kZcSegBlocks - 1) / kZcSegBlocks;
+      ++c1;
+    }
     const Set &z = sets[k];
     launch_zc_batch((const uint8_t *)d_data, n, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
                     (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
                     (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
                     ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
-                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks);
+                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks, nseg);
     if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
     prev = k;
     c0 = c1;

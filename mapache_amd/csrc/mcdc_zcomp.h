@@ -52,9 +52,12 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint32_t *words, uint64_t *recs,
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true,
-                     hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr, bool far = true);
+                     hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr, bool far = true,
+                     uint64_t nseg = 0);
 // (final_after: the output offsets' previous update, on another stream, is
 // waited for before this batch's final copy; final_done: recorded after it;
-// far: some chunk is longer than one finder segment, k_zc_far runs)
+// far: some chunk is longer than one finder segment, k_zc_far runs; nseg:
+// the batch's finder segments, sum of ceil(blocks / kZcSegBlocks) over its
+// chunks -- the probe's and the finder's grids; 0 = one workgroup per block)
 
 }  // namespace mcdc

@@ -423,11 +423,17 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
 // key's mix (mix5).  Near anchors (1 position in 32) feed k_zc_probe's repeat
 // test, far anchors (1 in 128, a subset) the far tables of k_zc_far.
 constexpr uint32_t kNearLog = 14;
-__device__ __forceinline__ bool near_anchor(uint32_t m8) { return m8 < (1u << 27); }
 __device__ __forceinline__ bool far_anchor(uint32_t m8) { return m8 < (1u << 25); }
-__device__ __forceinline__ uint32_t near_slot(uint32_t m8) { return (m8 >> 13) & ((1u << kNearLog) - 1u); }
 __device__ __forceinline__ uint32_t far_slot(uint32_t m8) { return (m8 >> 13) & (kZcSegBlocks * kZcFarSlots - 1u); }
 __device__ __forceinline__ uint32_t anchor_tag(uint32_t m5) { return m5 >> 19; }
+// The probe's near anchors (high-entropy blocks only, where no byte pattern
+// dominates): 1 position in 32 by one 24-bit product of bytes 0..2 (two
+// VALU), the slot from its next bits, the tag from a product of bytes 4..6;
+// a hit is verified on the 8 bytes.
+__device__ __forceinline__ uint32_t near_mix(uint32_t lo) { return mul24(lo & 0xFFFFFFu, 0x9E3779u); }
+__device__ __forceinline__ bool near_anchor(uint32_t nm) { return nm < (1u << 27); }
+__device__ __forceinline__ uint32_t near_slot(uint32_t nm) { return (nm >> 13) & ((1u << kNearLog) - 1u); }
+__device__ __forceinline__ uint32_t near_tag(uint32_t hi) { return mul24(hi & 0xFFFFFFu, 0xC2B2AFu) >> 19; }
 static_assert(kZcSegBlocks * kZcFarSlots == 4096, "far slots: bits 13..24 of a far anchor's mix");
 // Bits per byte (order 0) at or above which a block without repeats is stored
 // raw: Huffman coding could save at most (8 - 7.9) / 8 of it, less its table.
@@ -435,6 +441,7 @@ constexpr float kRawEntropy = 7.9f;
 constexpr uint32_t kProbeThreads = 1024, kProbeTile = 16 * kProbeThreads;
 static_assert(kPrime % kProbeTile == 0 && kZcBlock % kProbeTile == 0, "probe tiles start at segments and blocks");
 constexpr uint32_t kFarBack = 256;  // bytes a far match is extended backwards
+constexpr uint32_t kFarStride = 4;  // positions between the far words written over a backward extension
 
 // bytes j .. j + 3 of the words w (little endian)
 __device__ __forceinline__ uint32_t byte_window(const uint32_t *w, int j) {
@@ -448,24 +455,26 @@ __device__ __forceinline__ uint32_t suffix16(uint4 x, uint4 y) {
 
 // The probe: one workgroup per finder segment (the segments longest first,
 // as k_zc_find).  Pass 1 over the segment: a byte histogram of each of its
-// blocks (8 of every 16 bytes: a 16 KiB sample, whose plug-in entropy of
-// uniform bytes is 7.99 bits); in a chunk of more than one segment, its far
-// anchors into its far table in HBM (latest per slot; not for a chunk's last
-// segment: no later segment reads it) and their ballots (a bit per 16
+// blocks (4 of every 16 bytes: an 8 KiB sample, whose plug-in entropy of
+// uniform bytes is 7.98 bits); in a chunk of more than one segment, its far
+// anchors into its far table (latest per slot, built in LDS -- repeated keys
+// would serialise on one L2 address -- and stored to HBM; not for a chunk's
+// last segment: no later segment reads it) and their ballots (a bit per 16
 // positions, a word per 1024) for k_zc_far.  Only if a block carries
 // kRawEntropy bits per byte or more: pass 2, every near anchor of the
 // re-inserted bytes and the segment up to the last such block into an LDS
 // table (earliest per slot), and pass 3, such a block is hopeless if none of
-// its near anchors finds an earlier anchor with its key -- kZcRaw, stored raw
-// without the finder, the parse or the entropy coders (random, compressed or
-// encrypted data).  k_zc_far's rescue mode then clears kZcRaw of a block
-// with a far match.
+// its near anchors finds an earlier anchor with the same 8 bytes -- kZcRaw,
+// stored raw without the finder, the parse or the entropy coders (random,
+// compressed or encrypted data).  k_zc_far's rescue mode then clears kZcRaw
+// of a block with a far match.
 __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks,
                                                             uint64_t nblk, const uint32_t *order, uint32_t *ftab,
                                                             uint64_t *fbits) {
-  __shared__ uint32_t near[1u << kNearLog];
+  __shared__ uint32_t tab[1u << kNearLog];  // pass 1: the far table (its first slots); passes 2, 3: the near table
   __shared__ uint32_t hist[kZcSegBlocks][256];
   __shared__ uint32_t rep[kZcSegBlocks], high[kZcSegBlocks];
+  static_assert(kZcSegBlocks * kZcFarSlots <= (1u << kNearLog), "the far table fits the near table's place");
   const uint64_t bi0 = order[blockIdx.x];
   if (bi0 >= nblk) return;
   const ZcBlock B0 = blocks[bi0];
@@ -482,12 +491,11 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
   const uint8_t *cb = base + csrc;
   const uint64_t cbytes = nbytes - csrc;
   if (clen < 16 || cbytes < 16) return;  // (flags stay 0)
-  uint32_t *ft = ftab + bi0 * kZcFarSlots;
   for (uint32_t k = tid; k < kZcSegBlocks * 256; k += kProbeThreads) (&hist[0][0])[k] = 0;
   if (tid < kZcSegBlocks) rep[tid] = high[tid] = 0;
   if (far_out)
-    for (uint32_t k = tid; k < kZcSegBlocks * kZcFarSlots; k += kProbeThreads) ft[k] = 0;
-  __syncthreads();  // (the far table's zeros stored before any atomic of the workgroup)
+    for (uint32_t k = tid; k < kZcSegBlocks * kZcFarSlots; k += kProbeThreads) tab[k] = 0;
+  __syncthreads();
   auto load6 = [&](uint32_t p, uint32_t(&w)[6]) {  // bytes p .. p + 23 (zero past the buffer)
     const uint4 a = fix16(ld16c(cb, p, cbytes), p, cbytes), b = fix16(ld16c(cb, p + 16, cbytes), p + 16, cbytes);
     w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
@@ -502,12 +510,12 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
         load6(p, w);
       } else {
         const uint4 a = fix16(ld16c(cb, p, cbytes), p, cbytes);
-        w[0] = a.x, w[1] = a.y;
+        w[0] = a.x;
       }
       const uint32_t hb = (p - seg0) >> 15;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (p + j < seg1) atomicAdd(&hist[hb][(w[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+      for (int j = 0; j < 4; ++j)
+        if (p + j < seg1) atomicAdd(&hist[hb][(w[0] >> (8 * j)) & 0xFFu], 1u);
       if (hash1) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -516,7 +524,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
           const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
           if (!far_anchor(m8)) continue;
           fm |= 1u << j;
-          if (far_out) atomicMax(&ft[far_slot(m8)], (q - seg0 + 1) << 14 | anchor_tag(mix5(lo, hi)));
+          if (far_out) atomicMax(&tab[far_slot(m8)], (q - seg0 + 1) << 14 | anchor_tag(mix5(lo, hi)));
         }
       }
     }
@@ -527,6 +535,10 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
     }
   }
   __syncthreads();
+  if (far_out) {
+    uint32_t *ft = ftab + bi0 * kZcFarSlots;
+    for (uint32_t k = tid; k < kZcSegBlocks * kZcFarSlots; k += kProbeThreads) ft[k] = tab[k];
+  }
   if (wv < nsb) {  // order-0 entropy of block wv's sample: n log2 n - sum c log2 c >= kRawEntropy n
     float sc = 0.f;
     uint32_t n = 0;
@@ -547,7 +559,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
   for (uint32_t k = 0; k < nsb; ++k)
     if (high[k]) hend = min(seg1, seg0 + (k + 1) * (uint32_t)kZcBlock);
   if (!hend) return;
-  for (uint32_t k = tid; k < (1u << kNearLog); k += kProbeThreads) near[k] = 0xFFFFFFFFu;
+  for (uint32_t k = tid; k < (1u << kNearLog); k += kProbeThreads) tab[k] = 0xFFFFFFFFu;
   __syncthreads();
   for (uint32_t t0 = prime0; t0 < hend; t0 += kProbeTile) {
     const uint32_t p = t0 + 16 * tid;
@@ -556,10 +568,9 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
     load6(p, w);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const uint32_t q = p + j;
-      if (q >= hend || q + 8 > clen) continue;
-      const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
-      if (near_anchor(m8)) atomicMin(&near[near_slot(m8)], (q - prime0 + 1) << 13 | anchor_tag(mix5(lo, hi)));
+      const uint32_t q = p + j, nm = near_mix(byte_window(w, j));
+      if (near_anchor(nm) && q < hend && q + 8 <= clen)
+        atomicMin(&tab[near_slot(nm)], (q - prime0 + 1) << 13 | near_tag(byte_window(w, j + 4)));
     }
   }
   __syncthreads();
@@ -571,12 +582,14 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
     bool hit = false;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const uint32_t q = p + j;
-      if (q >= hend || q + 8 > clen) continue;
-      const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
-      if (!near_anchor(m8)) continue;
-      const uint32_t e = near[near_slot(m8)];
-      hit |= (e & 0x1FFFu) == anchor_tag(mix5(lo, hi)) && (e >> 13) - 1 + prime0 < q;
+      const uint32_t q = p + j, lo = byte_window(w, j), nm = near_mix(lo);
+      if (!near_anchor(nm) || q >= hend || q + 8 > clen) continue;
+      const uint32_t e = tab[near_slot(nm)], hi = byte_window(w, j + 4);
+      const uint32_t c = prime0 + (e >> 13) - 1;
+      if ((e & 0x1FFFu) == near_tag(hi) && c < q) {  // (rare: verify the 8 bytes)
+        const uint2 y = *reinterpret_cast<const uint2 *>(cb + c);  // (c + 8 < q + 8 <= clen)
+        hit |= y.x == lo && y.y == hi;
+      }
     }
     if (hit) rep[(p - seg0) >> 15] = 1;  // (any writer sets it)
   }
@@ -602,7 +615,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
 __global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
                                                 const uint32_t *ftab, const uint64_t *fbits, uint32_t *words,
                                                 bool rescue) {
-  MCDC_VGPR_PAD(40);  // (not an exact fill)
+  MCDC_VGPR_PAD(48);  // (not an exact fill)
   const uint64_t g = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
   const uint64_t bi = g / kZcFarBallots;
   const uint32_t j = (uint32_t)(g % kZcFarBallots), lane = lane_id();
@@ -635,16 +648,18 @@ __global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nb
     if (q + kMlCap > bend || (!rescue && (wc[q] & kZcLocalCap))) continue;
     const uint4 x = fix16(ld16c(cb, q, cbytes), q, cbytes);
     const uint32_t m8 = mix8(x.x, x.y), tag = anchor_tag(mix5(x.x, x.y)), slot = far_slot(m8);
+    uint32_t e[5];  // (the five tables' entries requested together)
+#pragma unroll
+    for (uint32_t k = 1; k <= 5; ++k)
+      e[k - 1] = k <= s ? ftab[(rec0 + (uint64_t)(s - k) * kZcSegBlocks) * kZcFarSlots + slot] : 0u;
     uint32_t c = 0xFFFFFFFFu;
-    for (uint32_t k = 1; k <= 5 && k <= s; ++k) {
-      const uint32_t e = ftab[(rec0 + (uint64_t)(s - k) * kZcSegBlocks) * kZcFarSlots + slot];
-      if (e && (e & 0x3FFFu) == tag) {
-        const uint32_t cc = (s - k) * kZcSegBlocks * (uint32_t)kZcBlock + (e >> 14) - 1;
-        if (q - cc <= zs::kWindow) c = cc;
-        break;
+#pragma unroll
+    for (uint32_t k = 1; k <= 5; ++k)
+      if (c == 0xFFFFFFFFu && e[k - 1] && (e[k - 1] & 0x3FFFu) == tag) {
+        const uint32_t cc = (s - k) * kZcSegBlocks * (uint32_t)kZcBlock + (e[k - 1] >> 14) - 1;
+        c = q - cc <= zs::kWindow ? cc : 0xFFFFFFFEu;  // (the nearest tagged entry decides)
       }
-    }
-    if (c == 0xFFFFFFFFu) continue;
+    if (c >= 0xFFFFFFFEu) continue;
     if (prefix16(x, fix16(ld16c(cb, c, cbytes), c, cbytes)) < kMlCap) continue;
     if (rescue) {
       atomicAnd(&blocks[bi].flags, ~kZcRaw);
@@ -657,10 +672,15 @@ __global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nb
       bk += sf;
       if (sf < 16) break;
     }
+    // the words of the extension's start and every kFarStride-th position
+    // after it up to the anchor (the parse's chain meets one within
+    // kFarStride positions of wherever it enters the stretch)
     const uint32_t off = q - c;
-    for (uint32_t x0 = q - bk; x0 <= q; ++x0) {
+    for (uint32_t x0 = q - bk;; x0 += kFarStride) {
+      x0 = min(x0, q);
       const uint32_t lim = min(kMlCap, min(clen, (x0 / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock) - x0);
       if (lim >= zs::kMinMatch) atomicMax(wc + x0, lim << 24 | off);
+      if (x0 == q) break;
     }
   }
 }
@@ -835,25 +855,34 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       if (cap_first == 0x7FFFFFFF && bc[j]) cap_first = 64 * j + (int32_t)__builtin_ctzll(bc[j]);
     }
     uint32_t L = 255, mlt = 0;  // nodes <= L are this window's; the capped match at L (if any) is mlt long
-    if (cap_first != 0x7FFFFFFF) {  // extend it (1 KiB per step: lane k compares bytes [.. + 16 k, + 16))
+    if (cap_first != 0x7FFFFFFF) {  // extend it (4 KiB per step: lane k compares bytes [.. + 64 k, + 64))
       L = (uint32_t)cap_first;
       const uint32_t pos = wb + L, off = offl[L];
       mlt = kMlCap;
       for (;;) {
-        const uint32_t q = pos + mlt + 16 * lane;
+        const uint32_t q = pos + mlt + 64 * lane;
         uint32_t m = 0;
-        if (q < end) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
-          const uint64_t g = B.src + q;
-          const uint4 x = fix16(ld16c(base, g, nbytes), g, nbytes), y = fix16(ld16c(base, g - off, nbytes), g - off, nbytes);
-          m = min(prefix16(x, y), end - q);
+        uint4 x[4], y[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
+          const uint64_t g = B.src + q + 16 * u;
+          x[u] = ld16c(base, g, nbytes);
+          y[u] = ld16c(base, g - off, nbytes);
         }
-        const uint64_t brk = __ballot(m < 16);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t qu = q + 16 * u;
+          const uint64_t g = B.src + qu;
+          const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
+          m += m == 16 * (uint32_t)u ? mu : 0u;
+        }
+        const uint64_t brk = __ballot(m < 64);
         if (brk) {
           const uint32_t t = (uint32_t)__builtin_ctzll(brk);
-          mlt += 16 * t + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)t);
+          mlt += 64 * t + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)t);
           break;
         }
-        mlt += 1024;
+        mlt += 4096;
       }
     }
     ZT(2);
@@ -902,6 +931,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     ZT(3);
   }
   wait_all(nwd, nby);  // (no load may land in a register after its last use)
+  MCDC_VGPR_PAD(80);  // (not an exact fill)
   ZT_PRINT("parse", bi % 509 == 0);
   if (lane == 0) {
     blocks[bi].nlit = nlit;
@@ -1911,8 +1941,9 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
-                     hipEvent_t final_after, hipEvent_t final_done, bool far) {
+                     hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg) {
   if (nblk == 0) return;
+  if (nseg == 0 || nseg > nblk) nseg = nblk;  // (every segment's first record is in order[0, nseg))
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
   // (piece, nblk + 1 words of 8 bytes, is free until k_zc_encode: the
@@ -1922,12 +1953,12 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   // (the far tables and ballots live in recs, free until k_zc_chain)
   uint32_t *ftab = reinterpret_cast<uint32_t *>(recs);
   uint64_t *fbits = reinterpret_cast<uint64_t *>(ftab + nblk * kZcFarSlots);
-  hipLaunchKernelGGL(k_zc_probe, dim3((unsigned)nblk), dim3(kProbeThreads), 0, st, base, nbytes, blocks, nblk, order,
+  hipLaunchKernelGGL(k_zc_probe, dim3((unsigned)nseg), dim3(kProbeThreads), 0, st, base, nbytes, blocks, nblk, order,
                      ftab, fbits);
   const dim3 gfar((unsigned)((nblk * kZcFarBallots + 3) / 4));
   if (far)
     hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, true);
-  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nblk), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
+  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nseg), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
                      order);
   if (far) hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, false);
   hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,

@@ -558,8 +558,13 @@ class Zstd:
     window_log_max 20).  Compressed bytes depend on the version: parity on
     compressed data is decode-equality."""
 
+    _lib = None  # (the loaded library, set up once per process)
+
     def __init__(self):
         import ctypes
+        if Zstd._lib is not None:
+            self.z, self.ct = Zstd._lib, ctypes
+            return
         z = ctypes.CDLL("libzstd.so.1")
         z.ZSTD_createCCtx.restype = ctypes.c_void_p
         z.ZSTD_createDCtx.restype = ctypes.c_void_p
@@ -581,6 +586,7 @@ class Zstd:
         z.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
         z.ZSTD_freeDCtx.argtypes = [ctypes.c_void_p]
         self.z, self.ct = z, ctypes
+        Zstd._lib = z
 
     def compress(self, data: bytes, content_size: bool, level: int = 3) -> bytes:
         """content_size=True: one-shot ZSTD_compress2 (size known: content size in
@@ -729,13 +735,16 @@ def save_files(params: Params, files, index=None, key=None, nonces=None, header_
             ch["length"] = a.size
         else:
             ch = chunk(params, a)
-        ids = chunk_ids(a, ch, threads=threads)
+        ids = chunk_ids(a, ch, threads=threads if a.size >= (4 << 20) else 1)
         per_file.append(ids)
         blob_bytes += [a[int(o):int(o + n)].tobytes() for o, n in zip(ch["offset"], ch["length"])]
     all_ids = np.concatenate(per_file) if per_file else np.zeros((0, 32), np.uint8)
     is_new = index.add(all_ids) if len(all_ids) else np.zeros(0, bool)
     stored = [(all_ids[i].tobytes(), blob_bytes[i]) for i in np.nonzero(is_new)[0]]
-    enc = [storage_encode(b, key, None if key is None else bytes(nonces[k])) for k, (_, b) in enumerate(stored)]
+    from concurrent.futures import ThreadPoolExecutor  # (libzstd and the AES oracle run outside the GIL)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        enc = list(ex.map(lambda kb: storage_encode(kb[1][1], key, None if key is None else bytes(nonces[kb[0]])),
+                          enumerate(stored)))
     packs, pad_at = [], 0
     for j, (f0, f1) in enumerate(pack_plan([len(e) for e in enc], max_pack_size)):
         cnt = f1 - f0

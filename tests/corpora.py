@@ -4,6 +4,8 @@ tools/ (test and benchmark data, not product code).  All deterministic.
 * text     a 2 000-word vocabulary of random lowercase words, words drawn
            uniformly, space separated (the bench's encode corpus)
 * records  CSV-like rows: ids, two names from 300, amounts, dates
+* far      long repeats 256 KiB - 1 MiB back over a text / records / binary base
+* code     C-source-like text (kernel_tree: the configs[3] file mix built on it)
 * binary   a mix of the byte shapes a backup holds besides text: fixed-width
            little-endian structs (incrementing ids, small counters, float32
            measurements with shared exponents, zero-padded name fields, flag
@@ -115,6 +117,77 @@ def far(n: int, seed: int = 31) -> np.ndarray:
     return out
 
 
+_KW = [b"static", b"int", b"unsigned", b"long", b"void", b"struct", b"const", b"return", b"if", b"else", b"for",
+       b"while", b"goto", b"break", b"case", b"switch", b"sizeof", b"u32", b"u64", b"bool", b"NULL", b"err", b"ret"]
+
+
+def code(n: int, seed: int = 41) -> np.ndarray:
+    """C-source-like text: functions of indented statements over a Zipf-skewed
+    identifier vocabulary (kernel-tree-like bytes for configs[3])."""
+    rng = np.random.default_rng(seed)
+    idents = [b"_".join(bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(2, 7, int(w)))
+              for w in rng.integers(1, 4, 5000)]
+    m = n // 24 + 64  # lines drawn (>= 25 bytes each on average)
+    z = np.minimum(rng.zipf(1.3, (m, 4)) - 1, len(idents) - 1)
+    kw, hdr, close = rng.integers(0, len(_KW), (m, 2)), rng.random(m) < 0.08, rng.random(m) < 0.1
+    depth, nk, op = rng.integers(1, 4, m), rng.integers(1, 4, m), rng.integers(0, 9, (m, 3))
+    ops = [b" = ", b" + ", b" & ", b" == ", b" != ", b"->", b", ", b" | ", b" < "]
+    tabs = [b"\t" * d for d in range(4)]
+    out, at, i = [], 0, 0
+    while at < n:
+        zi, ki = z[i % m], kw[i % m]
+        if hdr[i % m]:  # a function header
+            line = b"\n%s %s(struct %s *%s, %s %s)\n{\n" % (_KW[ki[0] % 6], idents[zi[0]], idents[zi[1]],
+                                                           idents[zi[2]], _KW[ki[1] % 6], idents[zi[3]])
+        else:
+            d, k, oi = int(depth[i % m]), int(nk[i % m]), op[i % m]
+            expr = idents[zi[0]] + b"".join(ops[oi[t]] + idents[zi[t + 1]] for t in range(k))
+            line = tabs[d] + (_KW[ki[0]] + b" (" + expr + b")\n" if ki[0] < 11 else expr + b";\n")
+            if close[i % m]:
+                line += tabs[d - 1] + b"}\n"
+        out.append(line)
+        at += len(line)
+        i += 1
+    return np.frombuffer(b"".join(out)[:n], np.uint8).copy()
+
+
+def kernel_tree(nfiles: int = 80000, seed: int = 2025):
+    """BASELINE configs[3] stand-in ("extracted Linux kernel source tree, ~80 k
+    small files, dedup-heavy realistic mix"; no tree here or on the GPU box):
+    file sizes log-normal (median 8 KiB, sigma 1.2, at most 64 MiB: ~1.3 GB for
+    80 000 files), each file a license line, its own name line, then C-like
+    text (`code`) taken from a 16 MiB base at a random offset; about 10 % of
+    the files are exact copies of an earlier file (dedup at blob level).
+    Returns (arena, offsets, lengths, duplicate_of: -1 or the copied file)."""
+    rng = np.random.default_rng(seed)
+    sizes = np.minimum(np.exp(rng.normal(np.log(8192), 1.2, nfiles)).astype(np.int64) + 1, 64 << 20)
+    dup = np.where(rng.random(nfiles) < 0.1, (rng.random(nfiles) * np.arange(nfiles)).astype(np.int64), -1)
+    dup[0] = -1
+    for f in np.nonzero(dup >= 0)[0]:  # (in file order: a copy of a copy has its final size)
+        sizes[f] = sizes[dup[f]]
+    base = code(16 << 20, seed)
+    bb = np.concatenate([base, base])
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    out = np.empty(int(sizes.sum()), np.uint8)
+    starts = rng.integers(0, base.size, nfiles)
+    for f in range(nfiles):
+        o, ln = int(offs[f]), int(sizes[f])
+        if dup[f] >= 0:
+            d = int(dup[f])
+            out[o:o + ln] = out[int(offs[d]):int(offs[d]) + ln]
+            continue
+        hdr = (b"// SPDX-License-Identifier: GPL-2.0\n/* drivers/%d/%d.c */\n" % (f % 977, f))[:ln]
+        h = len(hdr)
+        out[o:o + h] = np.frombuffer(hdr, np.uint8)
+        rest = ln - h
+        while rest > 0:  # (files above 32 MiB wrap the base)
+            s0 = int(starts[f]) % base.size
+            k = min(rest, base.size)
+            out[o + ln - rest:o + ln - rest + k] = bb[s0:s0 + k]
+            rest -= k
+    return out, offs.astype(np.uint64), sizes.astype(np.uint64), dup
+
+
 def by_name(kind: str, n: int, seed: int | None = None) -> np.ndarray:
-    f = {"text": text, "records": records, "binary": binary, "far": far}[kind]
+    f = {"text": text, "records": records, "binary": binary, "far": far, "code": code}[kind]
     return f(n) if seed is None else f(n, seed)
