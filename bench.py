@@ -962,7 +962,8 @@ def main() -> int:
     if a.headline_only:
         a.corpus_files_per_gpu = 0
     corpus_bytes = a.corpus_files_per_gpu * (8 << 20)
-    max_bytes = max(n + PARAMS[2], corpus_bytes, a.batch_files * (8 << 20) if extras else 0)
+    max_bytes = max(n + PARAMS[2], corpus_bytes, a.batch_files * (8 << 20) if extras else 0,
+                    (2 << 30) if extras and a.kernel_tree else 0)  # (the kernel-tree arena: ~1.3 GB)
     ctx = _lib.Context(local, max_bytes)
 
     def barrier():

@@ -24,5 +24,5 @@ with _lib.Context(0, 2 << 30) as ctx:
             for _ in range(3):
                 ctx.chunk_batch_device_to_device(p, arena, o, l, d_out, cap)
             t = ctx.timing()
-            print(f"{name:10s} scan {t['scan_ms']:.3f} ms  device {t['device_ms']:.3f} ms  call {t['total_ms']:.3f} ms",
-                  flush=True)
+            print(f"{name:10s} scan {t['scan_ms']:.3f} ms  device {t['device_ms']:.3f} ms  call {t['total_ms']:.3f} ms"
+                  f"  d2h+sync {t['d2h_ms']:.3f} ms", flush=True)
