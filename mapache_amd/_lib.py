@@ -71,7 +71,8 @@ class McdcTiming(ctypes.Structure):
                 ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
                 ("scan_launches", ctypes.c_uint64), ("fallback_files", ctypes.c_uint64),
                 ("ids_ms", ctypes.c_double), ("aead_ms", ctypes.c_double),
-                ("lane_walk", ctypes.c_uint64), ("handed_back", ctypes.c_uint64)]
+                ("lane_walk", ctypes.c_uint64), ("handed_back", ctypes.c_uint64),
+                ("host_pre_ms", ctypes.c_double), ("host_post_ms", ctypes.c_double)]
 
 
 class McdcBatcherStats(ctypes.Structure):

@@ -255,7 +255,8 @@ struct mcdc_ctx {
   // previous one reuses the uploaded tables.
   std::vector<uint64_t> plan_key;
   bool plan_valid = false;
-  std::vector<uint64_t> bx_fs, bx_fe;  // mcdc_chunk_batch_device's file ranges (reused: no page faults per call)
+  std::vector<uint64_t> bx_fs, bx_fe;
+  double call_t0 = 0;  // host entry time of the running call (host_pre_ms)  // mcdc_chunk_batch_device's file ranges (reused: no page faults per call)
   uint64_t *h_res = nullptr;  // pinned call summary written by k_finish
   uint64_t *h_fcnt = nullptr;  // pinned chunks-per-file, written by k_file_counts
   uint64_t *d_fcnt = nullptr;  // its device alias
@@ -390,12 +391,22 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const DevParams P = make_dev_params(params, ms, ml);
   const Knobs &kn = ctx->knobs;
   const uint64_t Z = segment_bytes(params, kn);
-  void *out_dev = direct_out(ctx, out);
-  if (!out_dev && is_device_ptr(out))
-    return fail(MCDC_E_INVALID, "out is a device pointer of another device");
-  // pinned host `out`: k_emit writes it over PCIe (default) or, with
-  // MCDC_PINNED_DIRECT=0, emits into HBM and one DMA copies the list
-  if (out_dev && !is_device_ptr(out) && !kn.pinned_direct) out_dev = nullptr;
+  // one attribute query classifies `out`: device memory of this device
+  // (used in place), pinned host memory (k_emit writes it over PCIe by
+  // default; with MCDC_PINNED_DIRECT=0 the list is emitted into HBM and one
+  // DMA copies it), pageable host memory (one D2H copy)
+  void *out_dev = nullptr;
+  if (out) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, out) != hipSuccess) {
+      (void)hipGetLastError();
+    } else if (a.type == hipMemoryTypeDevice) {
+      if (a.device != ctx->device) return fail(MCDC_E_INVALID, "out is a device pointer of another device");
+      out_dev = out;
+    } else if (a.type == hipMemoryTypeHost && a.devicePointer && kn.pinned_direct) {
+      out_dev = a.devicePointer;
+    }
+  }
 
   // ---- scan workspace, and the scan itself for a single-part call ----
   // The scan reads none of the segment tables, so a single-part call enqueues
@@ -431,6 +442,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // through the tile counter
   const uint64_t bw0 = nruns / 64 >= 2 ? nruns / 64 - 2 : 0;
   const size_t zero_bytes = (nbitw - bw0) * 16 + 8;
+  const double t_pre = now_ms();
   if (early) {
     HIP_TRY(hipEventRecord(ctx->ev_start, st));
     HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
@@ -681,6 +693,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   launch_finish(W, ctx->d_res, rs);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(rs));
+  const double t_dev = now_ms();
   if (((volatile uint64_t *)ctx->h_res)[3]) {
     // some continuation did not merge into the next segment: resolve the whole
     // call with the general path (serial fallback / serial walk), which
@@ -729,6 +742,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->timing.fallback_files = nfallback;
   ctx->timing.lane_walk = lane_all ? 1 : 0;
   ctx->timing.handed_back = lane_all ? ((volatile uint64_t *)ctx->h_res)[4] : 0;
+  ctx->timing.host_pre_ms = ctx->call_t0 > 0 ? t_pre - ctx->call_t0 : 0;
+  ctx->call_t0 = 0;
+  ctx->timing.host_post_ms = now_ms() - t_dev;
   return MCDC_OK;
 }
 
@@ -998,6 +1014,7 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
   if (rc) return rc;
   if (nbufs && (!d_arena || !offsets || !lens)) return fail(MCDC_E_INVALID, "NULL argument");
   const double t0 = now_ms();
+  ctx->call_t0 = t0;
   const uintptr_t addr = (uintptr_t)d_arena;
   const uint8_t *base = (const uint8_t *)(addr & ~(uintptr_t)15);
   const uint64_t delta = addr & 15;
@@ -1005,15 +1022,18 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
   // overflow test), the scan enqueued, then the per-file ranges and their
   // overlap check built while it runs (the host loop over 80 000 files took
   // ~0.1 ms before the first launch, tools/small_probe.py)
-  uint64_t span = 0, bad = 0;
-  for (size_t i = 0; i < nbufs; ++i) {
-    const uint64_t o = offsets[i], l = lens[i];
-    bad |= (uint64_t)(o > UINT64_MAX - 32 - l);
-    span = std::max(span, l ? o + l : 0);
-  }
-  if (bad)
-    for (size_t i = 0; i < nbufs; ++i)
-      if (offsets[i] > UINT64_MAX - 32 - lens[i]) return fail(MCDC_E_INVALID, "buffer %zu: offset + length overflows", i);
+  // (four independent maxima, branch-free: 4x faster than one max chain;
+  // an extent whose end wraps is rejected by ranges() below, and the span
+  // computed here only ever bounds what the scan reads)
+  uint64_t sm[4] = {0, 0, 0, 0};
+  size_t i4 = 0;
+  for (; i4 + 4 <= nbufs; i4 += 4)
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t l = lens[i4 + k];
+      sm[k] = std::max(sm[k], (offsets[i4 + k] + l) & (0 - (uint64_t)(l != 0)));
+    }
+  for (; i4 < nbufs; ++i4) sm[0] = std::max(sm[0], (offsets[i4] + lens[i4]) & (0 - (uint64_t)(lens[i4] != 0)));
+  const uint64_t span = std::max(std::max(sm[0], sm[1]), std::max(sm[2], sm[3]));
   // the workspace is sized from the arena span (gaps included), so the span is
   // what the context bound limits
   if (span > ctx->max_bytes)
@@ -1026,6 +1046,8 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
     uint64_t hi = 0;
     bool sorted = true;
     for (size_t i = 0; i < nbufs; ++i) {
+      if (offsets[i] > UINT64_MAX - 32 - lens[i])
+        return fail(MCDC_E_INVALID, "buffer %zu: offset + length overflows", i);
       fs[i] = delta + offsets[i];
       fe[i] = fs[i] + lens[i];
       if (lens[i] == 0) continue;

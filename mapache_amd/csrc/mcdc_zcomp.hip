@@ -736,8 +736,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane
 // S_{k+1} = S_k + J_k(S_k) from the cursor), and the chain's matches,
 // literals, literal lengths (an exclusive max-scan of match ends) and
 // sequence / literal indices (prefix counts of ballots) follow by wave scans.
-// A match of 16 verified bytes on the chain is extended (1 KiB per wave step)
-// and ends the window there.  Offsets repeat as repeat code 1 (the previous
+// A match of 16 verified bytes on the chain is extended (4 KiB per wave step);
+// the chain continues after it inside the window, or the window ends there
+// when it leaves the window.  Offsets repeat as repeat code 1 (the previous
 // sequence's offset, literal length > 0: rep[0] is always the previous
 // offset when only that code is used) after the block's first sequence.
 __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
@@ -843,22 +844,25 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         if (mk[i]) mk[(jr[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = 1;
       }
     ZT(1);
-    bool node[4], mt[4];
-    uint64_t bc[4];
-    int32_t cap_first = 0x7FFFFFFF;
+    // The chain's capped matches (kMlCap verified bytes), first to last: each
+    // is extended (4 KiB per wave step: lane k compares bytes [.. + 64 k,
+    // + 64)) to its true length T; if it ends inside the window the chain
+    // continues there (the marks after it cleared, the chain re-marked from
+    // its end over the same J tables), else the window ends at it.  (Before,
+    // every capped match ended the window: text-like data with many 16-byte
+    // repeats paid a window reload per match.)
+    uint32_t L = 255, tl[4] = {0u, 0u, 0u, 0u};  // nodes <= L are this window's; extended lengths of the lane's nodes
+    for (uint32_t from = 0;;) {
+      int32_t c = 0x7FFFFFFF;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = 64 * j + lane;
-      node[j] = valid[j] && mk[i];
-      mt[j] = node[j] && ml[j] != 0;
-      bc[j] = __ballot(mt[j] && ml[j] == kMlCap);
-      if (cap_first == 0x7FFFFFFF && bc[j]) cap_first = 64 * j + (int32_t)__builtin_ctzll(bc[j]);
-    }
-    uint32_t L = 255, mlt = 0;  // nodes <= L are this window's; the capped match at L (if any) is mlt long
-    if (cap_first != 0x7FFFFFFF) {  // extend it (4 KiB per step: lane k compares bytes [.. + 64 k, + 64))
-      L = (uint32_t)cap_first;
-      const uint32_t pos = wb + L, off = offl[L];
-      mlt = kMlCap;
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        const uint64_t bc = __ballot(valid[j] && i >= from && mk[i] && ml[j] == kMlCap);
+        if (c == 0x7FFFFFFF && bc) c = 64 * j + (int32_t)__builtin_ctzll(bc);
+      }
+      if (c == 0x7FFFFFFF) break;
+      const uint32_t pos = wb + (uint32_t)c, off = offl[c];
+      uint32_t mlt = kMlCap;
       for (;;) {
         const uint32_t q = pos + mlt + 64 * lane;
         uint32_t m = 0;
@@ -884,6 +888,33 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         }
         mlt += 4096;
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (64 * j + lane == (uint32_t)c) tl[j] = mlt;
+      const uint32_t e = (uint32_t)c + mlt;
+      if (e >= 256 || wb + e >= end) {  // (it leaves the window: the next window starts at its end)
+        L = (uint32_t)c;
+        break;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        if (i > (uint32_t)c) mk[i] = (uint8_t)(i == e);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t i = 64 * j + lane;
+          if (i >= e && mk[i]) mk[(jr[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = 1;
+        }
+      from = e;
+    }
+    bool node[4], mt[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      node[j] = valid[j] && mk[64 * j + lane];
+      mt[j] = node[j] && ml[j] != 0;
     }
     ZT(2);
     // this window's matches and literals, in position order (slot-major)
@@ -894,7 +925,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane, q = wb + i;
       const bool in = node[j] && i <= L, m = in && mt[j], l = in && !mt[j];
-      const uint32_t mlen = (i == L && mlt) ? mlt : ml[j];
+      const uint32_t mlen = tl[j] ? tl[j] : ml[j];
       const uint64_t bm = __ballot(m), bl = __ballot(l);
       const uint32_t mr = mcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       const uint32_t lr = lcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
@@ -931,7 +962,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     ZT(3);
   }
   wait_all(nwd, nby);  // (no load may land in a register after its last use)
-  MCDC_VGPR_PAD(80);  // (not an exact fill)
+  MCDC_VGPR_PAD(120);  // (not an exact fill)
   ZT_PRINT("parse", bi % 509 == 0);
   if (lane == 0) {
     blocks[bi].nlit = nlit;
