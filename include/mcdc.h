@@ -93,6 +93,8 @@ typedef struct {
   double aead_ms;      /* sealing kernels of mcdc_seal_device / mcdc_open_device */
   uint64_t lane_walk;  /* 1: the chains were walked one lane per chain */
   uint64_t handed_back; /* lane walk: segments handed to the group walk (spec + link) */
+  double host_pre_ms;  /* host time from the call's entry to the first kernel enqueued */
+  double host_post_ms; /* host time from the last device event to the return (results, copies) */
 } mcdc_timing;
 
 /* ------------------------------------------------------------------ API -- */
@@ -270,10 +272,17 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
  * counted against max_bytes): about 9 bytes per byte of a batch of whole
  * chunks, a batch holding up to 8192 blocks of 32 KiB (2.3 GiB), two batch
  * sets once the input exceeds one (4.5 GiB); a chunk longer than a batch
- * takes a batch of its own size. */
+ * takes a batch of its own size.  mcdc_zstd_compress_scratch reports the
+ * exact amount for a chunk list before the call. */
 int mcdc_zstd_compress_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
                               size_t nchunks, void *d_out, size_t out_cap, size_t *out_bytes,
                               mcdc_blob *frames);
+/* The device scratch (bytes) mcdc_zstd_compress_device allocates on this
+ * context for the chunk list `chunks` (host memory, nchunks records; only
+ * the lengths are read), with the context's batch settings: a caller sizing
+ * HBM adds it to max_bytes.  The context keeps the scratch until it is
+ * destroyed (a later call with a smaller list allocates nothing). */
+int mcdc_zstd_compress_scratch(struct mcdc_ctx *ctx, const mcdc_chunk *chunks, size_t nchunks, size_t *bytes);
 
 /* Packer::add_blob + flush (/root/reference/src/repository/packer.rs:101-186;
  * flushed when the packer holds more than max_pack_size bytes,

@@ -38,7 +38,7 @@ EXPORTS = (
     "mcdc_batcher_chunk", "mcdc_batcher_stats", "mcdc_seal_device", "mcdc_open_device", "mcdc_seal_chunks_device",
     "mcdc_index_create", "mcdc_index_destroy", "mcdc_index_size", "mcdc_index_add",
     "mcdc_encode_blobs", "mcdc_decode_blobs", "mcdc_pack_blobs", "mcdc_zstd_frames_device", "mcdc_save_files",
-    "mcdc_zstd_compress_device", "mcdc_ctx_synchronize", "mcdc_ctx_set_option",
+    "mcdc_zstd_compress_device", "mcdc_ctx_synchronize", "mcdc_ctx_set_option", "mcdc_zstd_compress_scratch",
 )
 
 
@@ -116,6 +116,7 @@ def load():
     L.mcdc_device_free.argtypes = [vp, vp]
     L.mcdc_ctx_synchronize.argtypes = [vp]
     L.mcdc_ctx_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_longlong]
+    L.mcdc_zstd_compress_scratch.argtypes = [vp, vp, sz, P(sz)]
     L.mcdc_host_alloc.argtypes = [vp, sz, P(vp)]
     L.mcdc_host_free.argtypes = [vp, vp]
     L.mcdc_memcpy_h2d.argtypes = [vp, vp, vp, sz]
@@ -625,6 +626,16 @@ class Context:
         """Wait for all work of this context (mcdc_ctx_synchronize: its streams
         and the null stream, not other contexts')."""
         check(load().mcdc_ctx_synchronize(self._h))
+
+    @_locked
+    def zstd_compress_scratch(self, chunks) -> int:
+        """Device scratch (bytes) mcdc_zstd_compress_device allocates for this
+        chunk list (mcdc_zstd_compress_scratch)."""
+        arr = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+        b = ctypes.c_size_t()
+        check(load().mcdc_zstd_compress_scratch(self._h, arr.ctypes.data if arr.size else None, arr.size,
+                                                ctypes.byref(b)))
+        return b.value
 
     @_locked
     def set_option(self, name: str, value: int) -> None:

@@ -2034,6 +2034,29 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   return MCDC_OK;
 }
 
+int mcdc_zstd_compress_scratch(mcdc_ctx *ctx, const mcdc_chunk *chunks, size_t nchunks, size_t *bytes) {
+  if (!ctx || !bytes || (nchunks && !chunks)) return fail(MCDC_E_INVALID, "NULL argument");
+  if (is_device_ptr(chunks)) return fail(MCDC_E_INVALID, "chunks must be host memory");
+  *bytes = 0;
+  if (nchunks == 0) return MCDC_OK;
+  uint64_t total_blocks = 0, longest = 0;
+  for (size_t i = 0; i < nchunks; ++i) {
+    const uint64_t nb = chunks[i].length ? (chunks[i].length + kZcBlock - 1) / kZcBlock : 1;
+    total_blocks += nb;
+    longest = std::max(longest, nb);
+  }
+  // as mcdc_zstd_compress_device sizes its batch sets
+  const uint64_t zb = ctx->knobs.zc_batch;
+  const bool two = ctx->knobs.zc_two && total_blocks > zb / 2 && longest <= zb / 2;
+  const uint64_t mb = two ? zb / 2 : std::max(std::min<uint64_t>(total_blocks, zb), longest);
+  const uint64_t tmpb = std::max(zc_tmp_bytes(nchunks), zc_tmp_bytes(mb));
+  const uint64_t set = tmpb + mb * sizeof(ZcBlock) + mb * kZcSlot + 2 * mb * kZcSeqCap * 8 + 2 * (mb + 1) * 8 +
+                       (mb * kZcBlock + 1024) * 4;
+  const uint64_t call = nchunks * sizeof(mcdc_chunk) + 2 * (nchunks + 1) * 8 + 32 + nchunks * 16;
+  *bytes = (size_t)(set * (two ? 2 : 1) + call);
+  return MCDC_OK;
+}
+
 // ------------------------------------------------------- zstd raw frames --
 int mcdc_zstd_frames_device(mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks, size_t nchunks,
                             void *d_out, size_t out_cap, size_t *out_bytes, mcdc_blob *frames) {

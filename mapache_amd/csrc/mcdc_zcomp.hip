@@ -10,25 +10,39 @@
 // Per batch of blocks (a block = 32 KiB of one chunk; batches of whole chunks
 // bound the scratch, mcdc_zcomp.h):
 //   k_zc_blocks  block records of the batch's chunks (chunk, index, source)
-//   k_zc_find    ONE WORKGROUP (8 waves) PER SEGMENT of up to 8 blocks of a
-//                chunk: candidate matches for every position.  Two LDS tables
-//                (160 KiB: 2^15 slots for a 5-byte key and 2^13 for an 8-byte
-//                key, as zstd's double-fast pair) of 32-bit entries: a
-//                segment-relative position and a 13-bit tag of the key.
-//                Filled 512 positions at a time: a tile reads the tables as
-//                the earlier tiles left them, then inserts its own positions
-//                with LDS max atomics (the latest position per slot,
-//                deterministically).  One candidate per position, the long
-//                key's when its tag matches, else the short key's, verified
-//                on 16 bytes two tiles later (its loads in flight meanwhile);
-//                per position one word (match length <= 16 << 24 | offset,
-//                0 = none) to scratch.  A segment after a chunk's first
-//                re-inserts the 128 KiB before it.
+//   k_zc_segorder the finder segments and the parse blocks, longest first
+//   k_zc_probe   ONE WORKGROUP (16 waves) PER SEGMENT: order-0 entropy of each
+//                block (a sample) and, for high-entropy blocks, a repeat test
+//                over content-defined anchors: hopeless blocks (random,
+//                compressed, encrypted data) are stored raw, every later
+//                kernel skips them; the segment's far anchors into its far
+//                table (chunks longer than a segment)
+//   k_zc_far     (rescue) a hopeless block with a far match is not hopeless
+//   k_zc_find    ONE WORKGROUP (16 waves, 1024 threads) PER SEGMENT of up to
+//                8 blocks of a chunk: candidate matches for every position.
+//                Two LDS tables (160 KiB: 2^15 slots for a 5-byte key and
+//                2^13 for an 8-byte key, as zstd's double-fast pair) of
+//                32-bit entries: a segment-relative position and a 13-bit tag
+//                of the key.  Filled 1024 positions at a time: a tile reads
+//                the tables as the earlier tiles left them, then inserts its
+//                own positions with LDS max atomics (the latest position per
+//                slot, deterministically).  One candidate per position, the
+//                long key's when its tag matches, else the short key's,
+//                verified on 16 bytes two tiles later (its loads in flight
+//                meanwhile); per position one word (match length <= 16 << 24
+//                | offset, 0 = none) to scratch.  A segment after a chunk's
+//                first re-inserts the 64 KiB before it.
+//   k_zc_far     far matches: anchors of a chunk's later segments look up the
+//                latest anchors of the 5 segments before (the 2^20 window),
+//                verified, extended backwards, written into the words
 //   k_zc_parse   ONE WAVE PER BLOCK: the greedy parse over the words, 256
-//                positions per window without a serial walk: the chain from
-//                the cursor by pointer doubling, its matches, literal
-//                lengths and indices by wave scans; a match of 16 verified
-//                bytes on the chain extended 1 KiB per step; repeat code 1
+//                positions per window without a serial walk: capped matches
+//                (16 verified bytes) get their true lengths per run of one
+//                repeat (its last position extended, the end handed back by
+//                pointer jumping); the chain from the cursor by pointer
+//                doubling, its matches, literal lengths and indices by wave
+//                scans; a match longer than 48 bytes on the chain extended
+//                2 KiB per wave step, ending the window; repeat code 1
 //                for an offset equal to the previous sequence's; literals to
 //                the block's staging slot, sequences to scratch
 //   k_zc_huff    ONE WAVE PER BLOCK: the block's literals (all of a block
@@ -85,6 +99,9 @@ constexpr uint32_t kPrime = kZcPrime;         // bytes before a segment re-inser
 // Match words: length (<= kMlCap) << 24 | offset; bit 31 marks a verified
 // kMlCap match of the finder's own (readers take the length as (w >> 24) & 31)
 constexpr uint32_t kZcLocalCap = 1u << 31;
+// The parse's run ends (ends[]): kEndNext = take the next position's,
+// kEndLong = still matching kRunExt bytes after kMlCap (the wave extends it)
+constexpr uint32_t kRunExt = 32, kEndNext = 0xFFFFu, kEndLong = 0xFFFEu;
 
 // Keys hashed with 24-bit multiplies (full rate; a 32-bit multiply issues at
 // a quarter of it): the key cut into 24- and 16-bit pieces, each multiplied by
@@ -736,16 +753,18 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane
 // S_{k+1} = S_k + J_k(S_k) from the cursor), and the chain's matches,
 // literals, literal lengths (an exclusive max-scan of match ends) and
 // sequence / literal indices (prefix counts of ballots) follow by wave scans.
-// A match of 16 verified bytes on the chain is extended (4 KiB per wave step);
-// the chain continues after it inside the window, or the window ends there
-// when it leaves the window.  Offsets repeat as repeat code 1 (the previous
+// Capped matches (16 verified bytes) get their true lengths before the walk
+// (see the window loop); the first long one on the chain (more than kRunExt
+// bytes past the 16) is extended by the wave (2 KiB per step) and ends the
+// window.  Offsets repeat as repeat code 1 (the previous
 // sequence's offset, literal length > 0: rep[0] is always the previous
 // offset when only that code is used) after the block's first sequence.
 __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
                                                  const uint32_t *words, uint8_t *stage, uint64_t *seqs,
                                                  const uint32_t *porder) {
   __shared__ uint16_t J[8][257];
-  __shared__ uint8_t mk[260];
+  __shared__ uint16_t ends[257], jp[256];
+  __shared__ uint8_t mk[260], capl[256];
   __shared__ uint32_t offl[256], wbyt[64];
   if (blockIdx.x >= nblk) return;
   const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
@@ -763,6 +782,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0, last_off = 0;  // (last_off 0: no sequence yet)
   if (lane == 0) {
     for (int k = 0; k < 8; ++k) J[k][256] = 256;
+    ends[256] = 256;
   }
   // A window's words and source bytes (lane l: bytes [wb + 4 l, + 4)) are
   // requested a window ahead with loads outside the compiler's wait counting
@@ -807,20 +827,83 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       }
     }
     wbyt[lane] = by;
-    nwb = wb + 256;
-    issue(nwb, nwd, nby);  // (the next window's, in flight meanwhile)
     ZT(0);
-    uint32_t ml[4], cj[4];
-    bool valid[4];
+    // Match lengths first.  A word of fewer than kMlCap bytes is exact; a
+    // capped word (kMlCap verified bytes) is extended here, all of them at
+    // once: consecutive capped positions with the same offset form a run of
+    // one repeat, whose positions all end where it ends, so only each run's
+    // last position is extended (per lane, up to kRunExt more bytes in one
+    // round of loads) and the end is handed back through the run by pointer
+    // jumping in LDS (ends[i] = ends[i + 1]).  A run still matching after
+    // kRunExt bytes is long: the chain stops at it (J = 256), and the first
+    // long match on the chain is extended by the whole wave (2 KiB per step)
+    // and ends the window -- short repeats (identifiers, keywords, indents of
+    // source code) no longer cost a memory round trip each.
+    uint32_t ml[4], cj[4], en[4];
+    bool valid[4], cap[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane;
       valid[j] = wb + i < end;
       ml[j] = (wd[j] >> 24) & 31u;
-      cj[j] = valid[j] ? min(i + (ml[j] ? ml[j] : 1u), 256u) : 256u;
-      J[0][i] = (uint16_t)cj[j];
+      cap[j] = valid[j] && ml[j] == kMlCap;
       offl[i] = wd[j] & 0xFFFFFFu;
+      capl[i] = (uint8_t)cap[j];
       mk[i] = (uint8_t)(i == s0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane;
+      const bool same = i < 255 && capl[i + 1] && offl[i + 1] == offl[i];
+      en[j] = !valid[j] ? 256u : !cap[j] ? i + (ml[j] ? ml[j] : 1u) : same ? kEndNext : 0u;
+      if (cap[j] && !same) {  // a run's last position: kRunExt bytes after its kMlCap
+        const uint32_t q = wb + i + kMlCap, off = offl[i];
+        uint4 x[kRunExt / 16], y[kRunExt / 16];
+#pragma unroll
+        for (int u = 0; u < (int)(kRunExt / 16); ++u) {
+          const uint64_t g = B.src + q + 16 * u;
+          x[u] = ld16c(base, g, nbytes);
+          y[u] = ld16c(base, g - off, nbytes);
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int u = 0; u < (int)(kRunExt / 16); ++u) {
+          const uint32_t qu = q + 16 * u;
+          const uint64_t g = B.src + qu;
+          const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
+          m += m == 16 * (uint32_t)u ? mu : 0u;
+        }
+        en[j] = m == kRunExt ? kEndLong : i + kMlCap + m;
+      }
+      ends[i] = (uint16_t)en[j];
+      jp[i] = (uint16_t)(i + 1);
+    }
+    // the next window's words and bytes, in flight meanwhile (requested after
+    // the run ends' loads: the compiler's wait for those counts every older
+    // load, and would drain this prefetch with them)
+    nwb = wb + 256;
+    issue(nwb, nwd, nby);
+    // the run's end to every position of the run (pointer jumping)
+    for (int r = 0; r < 8 && __ballot(en[0] == kEndNext || en[1] == kEndNext || en[2] == kEndNext ||
+                                     en[3] == kEndNext); ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        if (en[j] == kEndNext) {
+          const uint32_t p = jp[i], e2 = ends[p];
+          if (e2 != kEndNext) {
+            en[j] = e2;
+            ends[i] = (uint16_t)e2;
+          } else {
+            jp[i] = jp[p];
+          }
+        }
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane;
+      cj[j] = en[j] == kEndLong ? 256u : min(en[j], 256u);  // (a long run stops the chain)
+      J[0][i] = (uint16_t)cj[j];
     }
     // J_k of the lane's own positions stay in registers (16 bits each): a
     // doubling round reads only J_k(J_k(i)), marking reads only mk
@@ -844,77 +927,46 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         if (mk[i]) mk[(jr[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = 1;
       }
     ZT(1);
-    // The chain's capped matches (kMlCap verified bytes), first to last: each
-    // is extended (4 KiB per wave step: lane k compares bytes [.. + 64 k,
-    // + 64)) to its true length T; if it ends inside the window the chain
-    // continues there (the marks after it cleared, the chain re-marked from
-    // its end over the same J tables), else the window ends at it.  (Before,
-    // every capped match ended the window: text-like data with many 16-byte
-    // repeats paid a window reload per match.)
-    uint32_t L = 255, tl[4] = {0u, 0u, 0u, 0u};  // nodes <= L are this window's; extended lengths of the lane's nodes
-    for (uint32_t from = 0;;) {
-      int32_t c = 0x7FFFFFFF;
+    bool node[4], mt[4];
+    int32_t long_first = 0x7FFFFFFF;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 64 * j + lane;
-        const uint64_t bc = __ballot(valid[j] && i >= from && mk[i] && ml[j] == kMlCap);
-        if (c == 0x7FFFFFFF && bc) c = 64 * j + (int32_t)__builtin_ctzll(bc);
-      }
-      if (c == 0x7FFFFFFF) break;
-      const uint32_t pos = wb + (uint32_t)c, off = offl[c];
-      uint32_t mlt = kMlCap;
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane;
+      node[j] = valid[j] && mk[i];
+      mt[j] = node[j] && ml[j] != 0;
+      const uint64_t bl = __ballot(mt[j] && en[j] == kEndLong);
+      if (long_first == 0x7FFFFFFF && bl) long_first = 64 * j + (int32_t)__builtin_ctzll(bl);
+    }
+    uint32_t L = 255, mlt = 0;  // nodes <= L are this window's; the long match at L (if any) is mlt long
+    if (long_first != 0x7FFFFFFF) {  // extend it (2 KiB per step: lane k compares bytes [.. + 32 k, + 32))
+      L = (uint32_t)long_first;
+      const uint32_t pos = wb + L, off = offl[L];
+      mlt = kMlCap;
       for (;;) {
-        const uint32_t q = pos + mlt + 64 * lane;
+        const uint32_t q = pos + mlt + 32 * lane;
         uint32_t m = 0;
-        uint4 x[4], y[4];
+        uint4 x[2], y[2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
+        for (int u = 0; u < 2; ++u) {  // (the source may lie in an earlier block of the chunk: B.src + q - off)
           const uint64_t g = B.src + q + 16 * u;
           x[u] = ld16c(base, g, nbytes);
           y[u] = ld16c(base, g - off, nbytes);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 2; ++u) {
           const uint32_t qu = q + 16 * u;
           const uint64_t g = B.src + qu;
           const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
           m += m == 16 * (uint32_t)u ? mu : 0u;
         }
-        const uint64_t brk = __ballot(m < 64);
+        const uint64_t brk = __ballot(m < 32);
         if (brk) {
           const uint32_t t = (uint32_t)__builtin_ctzll(brk);
-          mlt += 64 * t + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)t);
+          mlt += 32 * t + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)t);
           break;
         }
-        mlt += 4096;
+        mlt += 2048;
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (64 * j + lane == (uint32_t)c) tl[j] = mlt;
-      const uint32_t e = (uint32_t)c + mlt;
-      if (e >= 256 || wb + e >= end) {  // (it leaves the window: the next window starts at its end)
-        L = (uint32_t)c;
-        break;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 64 * j + lane;
-        if (i > (uint32_t)c) mk[i] = (uint8_t)(i == e);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t i = 64 * j + lane;
-          if (i >= e && mk[i]) mk[(jr[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = 1;
-        }
-      from = e;
-    }
-    bool node[4], mt[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      node[j] = valid[j] && mk[64 * j + lane];
-      mt[j] = node[j] && ml[j] != 0;
     }
     ZT(2);
     // this window's matches and literals, in position order (slot-major)
@@ -925,7 +977,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane, q = wb + i;
       const bool in = node[j] && i <= L, m = in && mt[j], l = in && !mt[j];
-      const uint32_t mlen = tl[j] ? tl[j] : ml[j];
+      const uint32_t mlen = (i == L && mlt) ? mlt : cap[j] ? en[j] - i : ml[j];
       const uint64_t bm = __ballot(m), bl = __ballot(l);
       const uint32_t mr = mcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       const uint32_t lr = lcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
@@ -962,7 +1014,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     ZT(3);
   }
   wait_all(nwd, nby);  // (no load may land in a register after its last use)
-  MCDC_VGPR_PAD(120);  // (not an exact fill)
+  MCDC_VGPR_PAD(88);  // (not an exact fill)
   ZT_PRINT("parse", bi % 509 == 0);
   if (lane == 0) {
     blocks[bi].nlit = nlit;

@@ -320,3 +320,19 @@ def test_errors(ctx):
     finally:
         ctx.device_free(d_out)
         ctx.device_free(dp)
+
+
+def test_scratch_query(ctx):
+    """mcdc_zstd_compress_scratch: the device scratch a call allocates (not
+    counted against max_bytes), from the chunk lengths and the context's batch
+    settings: one batch set for a small list, two alternating sets (each half
+    a batch) above half a batch."""
+    small = np.zeros(3, dtype=_lib.CHUNK_DTYPE)
+    small["length"] = [100_000, 65_536, 1]
+    s = ctx.zstd_compress_scratch(small)
+    assert 9 * 6 * 32768 < s < 16 * 6 * 32768 + (1 << 20)  # (6 blocks: ~9-10 bytes of scratch per byte)
+    big = np.zeros(20_000, dtype=_lib.CHUNK_DTYPE)
+    big["length"] = 65_536
+    b = ctx.zstd_compress_scratch(big)
+    assert 9 * 16384 * 32768 < b < 11 * 16384 * 32768  # (two sets of 8192 blocks)
+    assert ctx.zstd_compress_scratch(big[:0]) == 0

@@ -25,4 +25,4 @@ with _lib.Context(0, 2 << 30) as ctx:
                 ctx.chunk_batch_device_to_device(p, arena, o, l, d_out, cap)
             t = ctx.timing()
             print(f"{name:10s} scan {t['scan_ms']:.3f} ms  device {t['device_ms']:.3f} ms  call {t['total_ms']:.3f} ms"
-                  f"  d2h+sync {t['d2h_ms']:.3f} ms", flush=True)
+                  f"  host pre {t['host_pre_ms']:.3f} post {t['host_post_ms']:.3f} ms", flush=True)
