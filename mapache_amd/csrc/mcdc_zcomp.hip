@@ -478,10 +478,10 @@ __device__ __forceinline__ uint32_t suffix16(uint4 x, uint4 y) {
 // would serialise on one L2 address -- and stored to HBM; not for a chunk's
 // last segment: no later segment reads it) and their ballots (a bit per 16
 // positions, a word per 1024) for k_zc_far.  Only if a block carries
-// kRawEntropy bits per byte or more: pass 2, every near anchor of the
-// re-inserted bytes and the segment up to the last such block into an LDS
-// table (earliest per slot), and pass 3, such a block is hopeless if none of
-// its near anchors finds an earlier anchor with the same 8 bytes -- kZcRaw,
+// kRawEntropy bits per byte or more: pass 2 over the re-inserted bytes and
+// the segment up to the last such block, every near anchor into an LDS table
+// (earliest per slot) tile by tile; such a block is hopeless if none of its
+// near anchors finds an earlier anchor with the same 8 bytes -- kZcRaw,
 // stored raw without the finder, the parse or the entropy coders (random,
 // compressed or encrypted data).  k_zc_far's rescue mode then clears kZcRaw
 // of a block with a far match.
@@ -492,6 +492,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
   __shared__ uint32_t hist[kZcSegBlocks][256];
   __shared__ uint32_t rep[kZcSegBlocks], high[kZcSegBlocks];
   static_assert(kZcSegBlocks * kZcFarSlots <= (1u << kNearLog), "the far table fits the near table's place");
+  MCDC_VGPR_PAD(32);  // (not an exact fill)
   const uint64_t bi0 = order[blockIdx.x];
   if (bi0 >= nblk) return;
   const ZcBlock B0 = blocks[bi0];
@@ -578,37 +579,41 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
   if (!hend) return;
   for (uint32_t k = tid; k < (1u << kNearLog); k += kProbeThreads) tab[k] = 0xFFFFFFFFu;
   __syncthreads();
+  // one pass, tile by tile: a tile's near anchors into the table (earliest
+  // per slot), barrier, then each anchor of a high-entropy block looks for an
+  // earlier anchor with its key among the tiles so far (a later tile's
+  // inserts only ever fill empty slots with later positions: no second
+  // barrier)
   for (uint32_t t0 = prime0; t0 < hend; t0 += kProbeTile) {
     const uint32_t p = t0 + 16 * tid;
-    if (p >= hend) continue;
-    uint32_t w[6];
-    load6(p, w);
+    uint32_t w[6] = {0, 0, 0, 0, 0, 0}, am = 0;
+    if (p < hend) {
+      load6(p, w);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t q = p + j, nm = near_mix(byte_window(w, j));
-      if (near_anchor(nm) && q < hend && q + 8 <= clen)
-        atomicMin(&tab[near_slot(nm)], (q - prime0 + 1) << 13 | near_tag(byte_window(w, j + 4)));
-    }
-  }
-  __syncthreads();
-  for (uint32_t t0 = seg0; t0 < hend; t0 += kProbeTile) {
-    const uint32_t p = t0 + 16 * tid;
-    if (p >= hend || !high[(p - seg0) >> 15]) continue;
-    uint32_t w[6];
-    load6(p, w);
-    bool hit = false;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t q = p + j, lo = byte_window(w, j), nm = near_mix(lo);
-      if (!near_anchor(nm) || q >= hend || q + 8 > clen) continue;
-      const uint32_t e = tab[near_slot(nm)], hi = byte_window(w, j + 4);
-      const uint32_t c = prime0 + (e >> 13) - 1;
-      if ((e & 0x1FFFu) == near_tag(hi) && c < q) {  // (rare: verify the 8 bytes)
-        const uint2 y = *reinterpret_cast<const uint2 *>(cb + c);  // (c + 8 < q + 8 <= clen)
-        hit |= y.x == lo && y.y == hi;
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t q = p + j, nm = near_mix(byte_window(w, j));
+        if (near_anchor(nm) && q < hend && q + 8 <= clen) {
+          am |= 1u << j;
+          atomicMin(&tab[near_slot(nm)], (q - prime0 + 1) << 13 | near_tag(byte_window(w, j + 4)));
+        }
       }
     }
-    if (hit) rep[(p - seg0) >> 15] = 1;  // (any writer sets it)
+    __syncthreads();
+    if (am && p >= seg0 && high[(p - seg0) >> 15]) {
+      bool hit = false;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (!((am >> j) & 1)) continue;
+        const uint32_t q = p + j, lo = byte_window(w, j), hi = byte_window(w, j + 4);
+        const uint32_t e = tab[near_slot(near_mix(lo))];
+        const uint32_t c = prime0 + (e >> 13) - 1;
+        if ((e & 0x1FFFu) == near_tag(hi) && c < q) {  // (rare: verify the 8 bytes)
+          const uint2 y = *reinterpret_cast<const uint2 *>(cb + c);  // (c + 8 < q + 8 <= clen)
+          hit |= y.x == lo && y.y == hi;
+        }
+      }
+      if (hit) rep[(p - seg0) >> 15] = 1;  // (any writer sets it)
+    }
   }
   __syncthreads();
   if (tid < nsb && high[tid] && !rep[tid]) blocks[bi0 + tid].flags = kZcRaw;
@@ -848,35 +853,40 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       ml[j] = (wd[j] >> 24) & 31u;
       cap[j] = valid[j] && ml[j] == kMlCap;
       offl[i] = wd[j] & 0xFFFFFFu;
-      capl[i] = (uint8_t)cap[j];
       mk[i] = (uint8_t)(i == s0);
+      en[j] = valid[j] ? i + (ml[j] ? ml[j] : 1u) : 256u;
     }
+    const bool anycap = __ballot(cap[0] || cap[1] || cap[2] || cap[3]) != 0;  // (else every length is exact)
+    if (anycap) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = 64 * j + lane;
-      const bool same = i < 255 && capl[i + 1] && offl[i + 1] == offl[i];
-      en[j] = !valid[j] ? 256u : !cap[j] ? i + (ml[j] ? ml[j] : 1u) : same ? kEndNext : 0u;
-      if (cap[j] && !same) {  // a run's last position: kRunExt bytes after its kMlCap
-        const uint32_t q = wb + i + kMlCap, off = offl[i];
-        uint4 x[kRunExt / 16], y[kRunExt / 16];
+      for (int j = 0; j < 4; ++j) capl[64 * j + lane] = (uint8_t)cap[j];
 #pragma unroll
-        for (int u = 0; u < (int)(kRunExt / 16); ++u) {
-          const uint64_t g = B.src + q + 16 * u;
-          x[u] = ld16c(base, g, nbytes);
-          y[u] = ld16c(base, g - off, nbytes);
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        const bool same = i < 255 && capl[i + 1] && offl[i + 1] == offl[i];
+        en[j] = !valid[j] ? 256u : !cap[j] ? i + (ml[j] ? ml[j] : 1u) : same ? kEndNext : 0u;
+        if (cap[j] && !same) {  // a run's last position: kRunExt bytes after its kMlCap
+          const uint32_t q = wb + i + kMlCap, off = offl[i];
+          uint4 x[kRunExt / 16], y[kRunExt / 16];
+#pragma unroll
+          for (int u = 0; u < (int)(kRunExt / 16); ++u) {
+            const uint64_t g = B.src + q + 16 * u;
+            x[u] = ld16c(base, g, nbytes);
+            y[u] = ld16c(base, g - off, nbytes);
+          }
+          uint32_t m = 0;
+#pragma unroll
+          for (int u = 0; u < (int)(kRunExt / 16); ++u) {
+            const uint32_t qu = q + 16 * u;
+            const uint64_t g = B.src + qu;
+            const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
+            m += m == 16 * (uint32_t)u ? mu : 0u;
+          }
+          en[j] = m == kRunExt ? kEndLong : i + kMlCap + m;
         }
-        uint32_t m = 0;
-#pragma unroll
-        for (int u = 0; u < (int)(kRunExt / 16); ++u) {
-          const uint32_t qu = q + 16 * u;
-          const uint64_t g = B.src + qu;
-          const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
-          m += m == 16 * (uint32_t)u ? mu : 0u;
-        }
-        en[j] = m == kRunExt ? kEndLong : i + kMlCap + m;
+        ends[i] = (uint16_t)en[j];
+        jp[i] = (uint16_t)(i + 1);
       }
-      ends[i] = (uint16_t)en[j];
-      jp[i] = (uint16_t)(i + 1);
     }
     // the next window's words and bytes, in flight meanwhile (requested after
     // the run ends' loads: the compiler's wait for those counts every older
@@ -884,8 +894,8 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     nwb = wb + 256;
     issue(nwb, nwd, nby);
     // the run's end to every position of the run (pointer jumping)
-    for (int r = 0; r < 8 && __ballot(en[0] == kEndNext || en[1] == kEndNext || en[2] == kEndNext ||
-                                     en[3] == kEndNext); ++r)
+    for (int r = 0; r < 8 && anycap && __ballot(en[0] == kEndNext || en[1] == kEndNext || en[2] == kEndNext ||
+                                                en[3] == kEndNext); ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t i = 64 * j + lane;
