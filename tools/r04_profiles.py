@@ -1,5 +1,5 @@
-"""Copy a round-4 GPU pass (tools/gpu_round4.sh <tag> suite bench prof zcprof,
-merged back as gpurun_out/<tag>/) into profiles/r04/:
+"""Copy a GPU pass (tools/gpu_round4.sh <tag> suite bench prof zcprof, merged
+back as gpurun_out/<tag>/) into profiles/rNN/ (round 4 by default):
 
   bench_default.json          the default bench line
   gpu_suite.txt               the GPU suite's summary lines
@@ -11,7 +11,7 @@ merged back as gpurun_out/<tag>/) into profiles/r04/:
   zstd/zc_kernel_stats.csv    rocprofv3 --stats of tools/zc_bench.py 1 2 text,binary
   zstd/pmc_text.json          the compressor's counter groups (tools/zc_pmc_summary.py)
 
-usage: python tools/r04_profiles.py <tag>"""
+usage: python tools/r04_profiles.py <tag> [round]"""
 import csv
 import json
 import os
@@ -32,9 +32,9 @@ def fetch(path, match):
     return v
 
 
-def main(tag):
+def main(tag, rnd=4):
     src = os.path.join(ROOT, "gpurun_out", tag)
-    dst = os.path.join(ROOT, "profiles", "r04")
+    dst = os.path.join(ROOT, "profiles", f"r{rnd:02d}")
     os.makedirs(os.path.join(dst, "zstd"), exist_ok=True)
     bench = line(os.path.join(src, "bench.json"))
     open(os.path.join(dst, "bench_default.json"), "w").write(bench)
@@ -78,13 +78,13 @@ def main(tag):
                "fetch_size_kib_scan": fs, "scan_launches": len(s),
                "scan_read_bytes_corrected": int(fs * 1024 * factor),
                "traffic_per_input_byte": round(fs * 1024 * factor / nbytes, 4),
-               "measured": f"gpurun_out/{tag}/calib (tools/scanbench 8 prod vs quadread, 8 GiB), round 4"},
+               "measured": f"gpurun_out/{tag}/calib (tools/scanbench 8 prod vs quadread, 8 GiB), round {rnd}"},
               open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     shutil.copy(os.path.join(src, "zc_stats", "zc_kernel_stats.csv"), os.path.join(dst, "zstd", "zc_kernel_stats.csv"))
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "zc_pmc_summary.py"), tag,
-                    os.path.join("profiles", "r04", "zstd", "pmc_text.json")], check=True, cwd=ROOT)
+                    os.path.join("profiles", f"r{rnd:02d}", "zstd", "pmc_text.json")], check=True, cwd=ROOT)
     print(bench.strip()[:300])
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 4)
