@@ -935,7 +935,8 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
   if (hipMemcpy(ctx->d_gear, kGear, 2048, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(ctx->d_gear16, g16, 2048, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(MCDC_E_DEVICE, "table upload failed"));
-  if (hipHostMalloc((void **)&ctx->h_res, 64, hipHostMallocDefault) != hipSuccess ||
+  // (words 0-4: the chunker's call summary; 8-11: the compressor's per-batch counts)
+  if (hipHostMalloc((void **)&ctx->h_res, 128, hipHostMallocDefault) != hipSuccess ||
       hipHostGetDevicePointer((void **)&ctx->d_res, ctx->h_res, 0) != hipSuccess)
     return bail(fail(MCDC_E_NOMEM, "pinned result word allocation failed"));
   *out = ctx;
@@ -1933,9 +1934,9 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   size_t tmpb = zc_tmp_bytes(nchunks);
   if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, nchunks * sizeof(mcdc_chunk))) ||
       (rc = ensure(ctx, ctx->zc_cnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->zc_first, (nchunks + 1) * 8)) ||
-      (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)))
+      (rc = ensure(ctx, ctx->zc_misc, 64)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)))
     return rc;
-  uint64_t *misc = (uint64_t *)ctx->zc_misc.p;  // [0] err, [1] raw bound, [2] output base
+  uint64_t *misc = (uint64_t *)ctx->zc_misc.p;  // [0] err, [1] raw bound, [2] output base, [4 + 2 k] set k's counts
   HIP_TRY(hipMemsetAsync(misc, 0, 32, st));
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
   const DevChunk *dch = (const DevChunk *)ctx->b3_chunks.p;
@@ -1983,7 +1984,8 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
         (rc = ensure(ctx, *z.words, (mb * kZcBlock + 1024) * 4)) || (rc = ensure(ctx, *z.recs, mb * kZcSeqCap * 8)))
       return rc;
   }
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // [0] setup done on st; [1 + k] set k's last final copy
+  // [0] setup done on st; [1 + k] set k's last final copy; [3 + k] set k's counts copied to the host
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   auto destroy = [&]() {
     for (auto &e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -2010,7 +2012,8 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
                     (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
                     (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
                     ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
-                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks, nseg);
+                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks, nseg, misc + 4 + 2 * k, ctx->h_res + 8 + 2 * k,
+                    ev[3 + k]);
     if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
     prev = k;
     c0 = c1;

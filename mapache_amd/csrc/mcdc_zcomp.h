@@ -27,6 +27,7 @@ struct ZcBlock {
   uint32_t flags;               // kZcRaw: k_zc_probe found the block hopeless (stored raw, no finder / parse)
 };
 constexpr uint32_t kZcRaw = 1u;
+constexpr uint32_t kZcSegRaw = 2u;  // (on a segment's first record) every block of the segment is kZcRaw
 // Far matches (k_zc_probe / k_zc_far): per block record kZcFarSlots table
 // entries (a segment of kZcSegBlocks records owns kZcSegBlocks x kZcFarSlots
 // slots) and kZcBlock / 1024 anchor ballots, carved from the batch's `recs`
@@ -53,11 +54,17 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true,
                      hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr, bool far = true,
-                     uint64_t nseg = 0);
+                     uint64_t nseg = 0, uint64_t *d_cnt = nullptr, uint64_t *h_cnt = nullptr,
+                     hipEvent_t ev_cnt = nullptr);
 // (final_after: the output offsets' previous update, on another stream, is
 // waited for before this batch's final copy; final_done: recorded after it;
 // far: some chunk is longer than one finder segment, k_zc_far runs; nseg:
 // the batch's finder segments, sum of ceil(blocks / kZcSegBlocks) over its
-// chunks -- the probe's and the finder's grids; 0 = one workgroup per block)
+// chunks -- the probe's grid; 0 = one workgroup per block.  d_cnt (device,
+// 2 words), h_cnt (pinned host, 2 words), ev_cnt: after the probe the
+// segments and blocks with work are moved to the front of the orders and
+// counted, the host waits for the two counts and sizes the finder's and the
+// parse's grids by them (a batch of hopeless blocks launches neither); all
+// null = the full grids)
 
 }  // namespace mcdc

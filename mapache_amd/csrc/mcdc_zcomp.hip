@@ -473,7 +473,8 @@ __device__ __forceinline__ uint32_t suffix16(uint4 x, uint4 y) {
 // The probe: one workgroup per finder segment (the segments longest first,
 // as k_zc_find).  Pass 1 over the segment: a byte histogram of each of its
 // blocks (4 of every 16 bytes: an 8 KiB sample, whose plug-in entropy of
-// uniform bytes is 7.98 bits); in a chunk of more than one segment, its far
+// uniform bytes is 7.98 bits; a chunk's last block under 16 KiB whole, the
+// threshold lowered by the smaller sample's bias); in a chunk of more than one segment, its far
 // anchors into its far table (latest per slot, built in LDS -- repeated keys
 // would serialise on one L2 address -- and stored to HBM; not for a chunk's
 // last segment: no later segment reads it) and their ballots (a bit per 16
@@ -531,9 +532,16 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
         w[0] = a.x;
       }
       const uint32_t hb = (p - seg0) >> 15;
+      // (a chunk's last block shorter than 16 KiB is counted whole: its
+      // sample would be too small to tell random bytes from others)
+      const bool whole = seg1 - (seg0 + (hb << 15)) < 16384u;
+      if (whole && !hash1) {
+        const uint4 a = fix16(ld16c(cb, p, cbytes), p, cbytes);
+        w[1] = a.y, w[2] = a.z, w[3] = a.w;
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (p + j < seg1) atomicAdd(&hist[hb][(w[0] >> (8 * j)) & 0xFFu], 1u);
+      for (int j = 0; j < 16; ++j)
+        if ((j < 4 || whole) && p + j < seg1) atomicAdd(&hist[hb][(w[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
       if (hash1) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -570,7 +578,11 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
       sc += __shfl_xor(sc, o);
       n += __shfl_xor(n, o);
     }
-    if (lane == 0) high[wv] = n >= 1024 && (float)n * __log2f((float)n) - sc >= kRawEntropy * (float)n ? 1u : 0u;
+    // (the threshold less the plug-in estimate's bias for n samples beyond an
+    // 8 KiB sample's, (K - 1) / (2 n ln 2) with K = 256 values: the same
+    // margin below uniform bytes at every sample size)
+    const float thr = kRawEntropy - 183.9f / (float)max(n, 1u) + 183.9f / 8192.f;
+    if (lane == 0) high[wv] = n >= 512 && (float)n * __log2f((float)n) - sc >= thr * (float)n ? 1u : 0u;
   }
   __syncthreads();
   uint32_t hend = 0;  // the end of the last high-entropy block
@@ -616,7 +628,9 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
     }
   }
   __syncthreads();
-  if (tid < nsb && high[tid] && !rep[tid]) blocks[bi0 + tid].flags = kZcRaw;
+  bool all = true;
+  for (uint32_t k = 0; k < nsb; ++k) all &= high[k] && !rep[k];
+  if (tid < nsb && high[tid] && !rep[tid]) blocks[bi0 + tid].flags = kZcRaw | (tid == 0 && all ? kZcSegRaw : 0u);
 }
 
 // Far matches: the 2^20 window of SecureStorage::compress (storage.rs:74-84)
@@ -685,6 +699,7 @@ __global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nb
     if (prefix16(x, fix16(ld16c(cb, c, cbytes), c, cbytes)) < kMlCap) continue;
     if (rescue) {
       atomicAnd(&blocks[bi].flags, ~kZcRaw);
+      atomicAnd(&blocks[bi - B.b % kZcSegBlocks].flags, ~kZcSegRaw);  // (the segment's first record)
       return;
     }
     uint32_t bk = 0;
@@ -2008,6 +2023,63 @@ __global__ __launch_bounds__(64) void k_zc_final(const uint8_t *base, const ZcBl
   }
 }
 
+// After the probe (and k_zc_far's rescue): the segments and blocks with work
+// to the front of the finder's and the parse's orders, stably (one
+// workgroup; tmp: 2 nblk words of scratch), and their counts to cnt[0],
+// cnt[1] -- the host sizes the finder's and the parse's grids by them.
+__global__ __launch_bounds__(1024) void k_zc_compact(const ZcBlock *blocks, uint64_t nblk, uint64_t nseg,
+                                                     uint32_t *order, uint32_t *porder, uint32_t *tmp,
+                                                     uint64_t *cnt) {
+  __shared__ uint32_t wtot[16], wpre[17];
+  MCDC_VGPR_PAD(32);  // (not an exact fill)
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / 64;
+  auto partition = [&](uint32_t *a, uint32_t *t, uint64_t n, uint32_t flag) -> uint32_t {
+    for (uint64_t i = tid; i < n; i += 1024) t[i] = a[i];
+    __syncthreads();
+    uint32_t kept = 0;  // (pass 1: how many stay in front)
+    for (uint64_t i = tid; i < n; i += 1024) kept += (blocks[t[i]].flags & flag) ? 0u : 1u;
+    kept = wave_sum(kept);
+    if (lane == 0) wtot[wv] = kept;
+    __syncthreads();
+    uint32_t total = 0;
+    for (int w = 0; w < 16; ++w) total += wtot[w];
+    __syncthreads();
+    uint32_t nk = 0, nd = 0;  // kept / dropped before this round
+    for (uint64_t i0 = 0; i0 < n; i0 += 1024) {
+      const uint64_t i = i0 + tid;
+      const bool in = i < n, keep = in && !(blocks[t[i]].flags & flag), drop = in && !keep;
+      const uint64_t bk = __ballot(keep), bd = __ballot(drop);
+      if (lane == 0) {
+        wtot[wv] = (uint32_t)__builtin_popcountll(bk) | (uint32_t)__builtin_popcountll(bd) << 16;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t a = 0;
+        for (int w = 0; w < 16; ++w) {
+          wpre[w] = a;
+          a += wtot[w];
+        }
+        wpre[16] = a;
+      }
+      __syncthreads();
+      const uint32_t rk = (wpre[wv] & 0xFFFF) + __builtin_amdgcn_mbcnt_hi((uint32_t)(bk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bk, 0u));
+      const uint32_t rd = (wpre[wv] >> 16) + __builtin_amdgcn_mbcnt_hi((uint32_t)(bd >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bd, 0u));
+      if (keep) a[nk + rk] = t[i];
+      if (drop) a[total + nd + rd] = t[i];
+      nk += wpre[16] & 0xFFFF;
+      nd += wpre[16] >> 16;
+      __syncthreads();
+    }
+    return total;
+  };
+  const uint32_t ns = partition(order, tmp, nseg, kZcSegRaw);
+  const uint32_t nb = partition(porder, tmp + nblk, nblk, kZcRaw);
+  if (tid == 0) {
+    cnt[0] = ns;
+    cnt[1] = nb;
+  }
+}
+
 __global__ void k_zc_advance(uint64_t *obase, const uint64_t *poff, uint64_t nblk) {
   MCDC_VGPR_PAD(8);  // (not an exact fill)
   if (threadIdx.x == 0 && blockIdx.x == 0) *obase += poff[nblk];
@@ -2034,7 +2106,8 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
-                     hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg) {
+                     hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg, uint64_t *d_cnt,
+                     uint64_t *h_cnt, hipEvent_t ev_cnt) {
   if (nblk == 0) return;
   if (nseg == 0 || nseg > nblk) nseg = nblk;  // (every segment's first record is in order[0, nseg))
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
@@ -2051,15 +2124,30 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   const dim3 gfar((unsigned)((nblk * kZcFarBallots + 3) / 4));
   if (far)
     hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, true);
-  hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nseg), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
-                     order);
-  if (far) hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, false);
-  hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
-                     seqs, porder);
-  if (huf)
-    hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nblk), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words,
-                       porder);
-  hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, seqs, words, T, porder);
+  uint64_t nfind = nseg, nwork = nblk;
+  if (d_cnt && h_cnt && ev_cnt) {  // (the orders' hopeless entries to the back; the host waits for the counts)
+    uint32_t *tmpo = reinterpret_cast<uint32_t *>(poff);  // (2 nblk + 2 words, free until the piece scan)
+    hipLaunchKernelGGL(k_zc_compact, dim3(1), dim3(1024), 0, st, blocks, nblk, nseg, order, porder, tmpo, d_cnt);
+    if (hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        hipEventRecord(ev_cnt, st) == hipSuccess && hipEventSynchronize(ev_cnt) == hipSuccess) {
+      const uint64_t c0v = ((volatile uint64_t *)h_cnt)[0], c1v = ((volatile uint64_t *)h_cnt)[1];
+      nfind = c0v < nseg ? c0v : nseg;
+      nwork = c1v < nblk ? c1v : nblk;
+    }
+  }
+  if (nfind)
+    hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nfind), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
+                       order);
+  if (far && nwork)
+    hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, false);
+  if (nwork) {
+    hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nwork), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
+                       seqs, porder);
+    if (huf)
+      hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nwork), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words,
+                         porder);
+    hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nwork), dim3(64), 0, st, blocks, nblk, seqs, words, T, porder);
+  }
   hipLaunchKernelGGL(k_zc_chain, dim3((unsigned)((nblk + kChainBlocks - 1) / kChainBlocks)), dim3(64), 0, st, blocks,
                      nblk, recs, words);
   hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, words, piece);
