@@ -376,13 +376,13 @@ def kernel_tree(ctx, nfiles: int, steps: int) -> dict:
         finally:
             ctx.device_free(d_out)
         for mode in ("host_zstd", "gpu_compress"):
-            def call():
+            def call():  # (the IDs as one array: the per-file split is Python work, not the call's)
                 with ctx.index_create() as ix:
                     return ctx.save_files(p512, ix, dp, offs, lens, key, nonces, hn, pad, n=n,
-                                          gpu_compress=mode == "gpu_compress", out_buf=ob)
-            dt, (ids, new, packed, packs) = _timed(call, steps, 1)
+                                          gpu_compress=mode == "gpu_compress", out_buf=ob, split=False)
+            dt, (ids, fb, new, packed, packs) = _timed(call, steps, 1)
             t = ctx.timing()
-            distinct = len({x.tobytes() for f in ids for x in f})
+            distinct = len({x.tobytes() for x in ids})
             body = packed[int(packs[0]["offset"]):int(packs[0]["offset"] + packs[0]["length"])].tobytes()
             hdr = O.parse_header(body, key)
             okd = all(O.blake3(np.frombuffer(O.storage_decode(body[o:o + ln], key, 16 << 20), np.uint8)) == b

@@ -470,7 +470,8 @@ class Context:
     @_locked
     def save_files(self, p: "McdcParams", index: "Index", data, offsets, lengths, key=None, nonces=None,
                    header_nonces=None, padding=None, max_pack_size: int = 16 << 20, n: int | None = None,
-                   gpu_compress: bool = False, gate_bytes: int = 0, out_buf: np.ndarray | None = None):
+                   gpu_compress: bool = False, gate_bytes: int = 0, out_buf: np.ndarray | None = None,
+                   split: bool = True):
         """The Archiver's save path for a run of files (mcdc_save_files): data is
         a host array (or a device pointer with n bytes); file f = data[offsets[f],
         + lengths[f]); gpu_compress: compress with the GPU zstd kernels in HBM
@@ -479,7 +480,11 @@ class Context:
         host array (e.g. pinned_bytes) the packs are written into when it is
         large enough (the returned packed bytes are then a view of it).  Returns
         (ids_per_file: list of (k, 32) uint8 arrays,
-        is_new per blob, packed bytes, PACK_DTYPE records)."""
+        is_new per blob, packed bytes, PACK_DTYPE records); split=False returns
+        the IDs as one (blobs, 32) array and file_blobs (file f's IDs are rows
+        file_blobs[f] .. file_blobs[f + 1]) instead of the per-file list
+        (80 000 files: ~40 ms of Python slicing, more than the call itself):
+        (ids, file_blobs, is_new, packed bytes, PACK_DTYPE records)."""
         if isinstance(data, int):
             dptr, nbytes, keep = data, int(n), None
         else:
@@ -496,7 +501,7 @@ class Context:
                        arrs[1].size // NONCE_BYTES, arrs[2].ctypes.data, arrs[2].size // 36, int(bool(gpu_compress)),
                        int(gate_bytes))
         fb = np.zeros(nf + 1, np.uint64)
-        bcap = int(sum(int(x) // max(p.min_size - 1, 1) + 2 for x in ext[:, 1])) if nf else 1
+        bcap = int((ext[:, 1] // np.uint64(max(p.min_size - 1, 1)) + np.uint64(2)).sum()) if nf else 1
         ids = np.zeros((max(bcap, 1), 32), np.uint8)
         nw = np.zeros(max(bcap, 1), np.uint8)
         ocap = int(ext[:, 1].sum() * 1.01) + 4096 * nf + (1 << 16) if nf else 1
@@ -520,6 +525,8 @@ class Context:
                 packs = np.zeros(np_.value, PACK_DTYPE)
         check(rc)
         del keep, kbuf
+        if not split:
+            return ids[:nb.value], fb, nw[:nb.value].astype(bool), out[:pb.value], packs[:np_.value]
         per_file = [ids[int(fb[f]):int(fb[f + 1])].copy() for f in range(nf)]
         return per_file, nw[:nb.value].astype(bool), out[:pb.value], packs[:np_.value]
 

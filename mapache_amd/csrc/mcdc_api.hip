@@ -256,6 +256,8 @@ struct mcdc_ctx {
   std::vector<uint64_t> plan_key;
   bool plan_valid = false;
   std::vector<uint64_t> bx_fs, bx_fe;
+  DevBuf bits_zero;          // run_bits words [bits_zero_at * 2, + cap bytes) zeroed after the last call
+  uint64_t bits_zero_at = 0;
   double call_t0 = 0;  // host entry time of the running call (host_pre_ms)  // mcdc_chunk_batch_device's file ranges (reused: no page faults per call)
   uint64_t *h_res = nullptr;  // pinned call summary written by k_finish
   uint64_t *h_fcnt = nullptr;  // pinned chunks-per-file, written by k_file_counts
@@ -421,7 +423,9 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // the bitmap words of the partial last tile (set with atomics) and the
   // counter are zeroed by one memset before the scan
   const uint64_t nbitw = nruns / 64 + 4;
+  const size_t rb_cap = ctx->run_bits.cap;
   if ((rc = ensure(ctx, ctx->run_bits, nbitw * 16 + 64))) return rc;
+  if (ctx->run_bits.cap != rb_cap) ctx->bits_zero = DevBuf{};  // (reallocated: the zeroed words are gone)
   if ((rc = ensure(ctx, ctx->err, 32))) return rc;  // (zeroed by the first scan launch)
   Work W{};
   W.base = base;
@@ -443,14 +447,26 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const uint64_t bw0 = nruns / 64 >= 2 ? nruns / 64 - 2 : 0;
   const size_t zero_bytes = (nbitw - bw0) * 16 + 8;
   const double t_pre = now_ms();
+  // The bitmap words of the partial last tile and the tile counter were zeroed
+  // at the end of the previous call if it had this layout (off the next
+  // call's path: two fill kernels of ~4 us each before the scan otherwise)
+  const bool zeroed = ctx->bits_zero.p == ctx->run_bits.p && ctx->bits_zero_at == bw0 &&
+                      ctx->bits_zero.cap == zero_bytes;
+  ctx->bits_zero = DevBuf{};
+  const bool lane_early = early && use_lane_walk(params, kn);
   if (early) {
-    HIP_TRY(hipEventRecord(ctx->ev_start, st));
-    HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
+    // (the scan's start and end events are recorded by its dispatch: an event
+    // record between two kernels delays the second by ~5 us, kernel traces
+    // of tools/small_probe.py)
+    if (!zeroed) {
+      HIP_TRY(hipEventRecord(ctx->ev_start, st));
+      HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
+    }
     const int pc = kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus);
-    if (n_al > 0) launch_scan(W, P, ctx->num_cus, st, 0, (n_al / kRun) / (64 / pc), true, pc, kn.scan_cold);
+    launch_scan(W, P, ctx->num_cus, st, 0, n_al > 0 ? (n_al / kRun) / (64 / pc) : 0, n_al > 0, pc, kn.scan_cold,
+                zeroed ? ctx->ev_start : nullptr, ctx->ev_scan);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev_part[0], st));
-    HIP_TRY(hipEventRecord(ctx->ev_scan, st));
+    if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));  // (the group walk's stream waits for it)
   }
   if (after_scan && (rc = after_scan())) return rc;
 
@@ -688,12 +704,18 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(ctx->ev_end, rs));
   if (want_counts) launch_file_counts(W, ctx->d_fcnt, rs);
-  launch_finish(W, ctx->d_res, rs);
+  // (a whole-call scan: its bitmap words zeroed for the next call by k_finish)
+  const bool rezero = early && n_al > 0;
+  launch_finish(W, ctx->d_res, rs, ctx->ev_end, rezero ? W.run_bits + 2 * bw0 : nullptr, (uint32_t)(zero_bytes / 8));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(rs));
   const double t_dev = now_ms();
+  if (rezero && !((volatile uint64_t *)ctx->h_res)[3]) {
+    ctx->bits_zero.p = ctx->run_bits.p;
+    ctx->bits_zero.cap = zero_bytes;
+    ctx->bits_zero_at = bw0;
+  }
   if (((volatile uint64_t *)ctx->h_res)[3]) {
     // some continuation did not merge into the next segment: resolve the whole
     // call with the general path (serial fallback / serial walk), which
@@ -701,9 +723,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 4, rs));  // incremental capacity bits are void
     launch_resolve_general(W, P, ctx->scan_tmp.p, tmpb, rs);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev_end, rs));
     if (want_counts) launch_file_counts(W, ctx->d_fcnt, rs);
-    launch_finish(W, ctx->d_res, rs);
+    launch_finish(W, ctx->d_res, rs, ctx->ev_end);
     HIP_TRY(hipGetLastError());
   }
 
@@ -1019,30 +1040,22 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
   const uintptr_t addr = (uintptr_t)d_arena;
   const uint8_t *base = (const uint8_t *)(addr & ~(uintptr_t)15);
   const uint64_t delta = addr & 15;
-  // The scan needs only the arena span: one branch-free pass for it (and the
-  // overflow test), the scan enqueued, then the per-file ranges and their
-  // overlap check built while it runs (the host loop over 80 000 files took
-  // ~0.1 ms before the first launch, tools/small_probe.py)
-  // (four independent maxima, branch-free: 4x faster than one max chain;
-  // an extent whose end wraps is rejected by ranges() below, and the span
-  // computed here only ever bounds what the scan reads)
-  uint64_t sm[4] = {0, 0, 0, 0};
-  size_t i4 = 0;
-  for (; i4 + 4 <= nbufs; i4 += 4)
-    for (int k = 0; k < 4; ++k) {
-      const uint64_t l = lens[i4 + k];
-      sm[k] = std::max(sm[k], (offsets[i4 + k] + l) & (0 - (uint64_t)(l != 0)));
-    }
-  for (; i4 < nbufs; ++i4) sm[0] = std::max(sm[0], (offsets[i4] + lens[i4]) & (0 - (uint64_t)(lens[i4] != 0)));
-  const uint64_t span = std::max(std::max(sm[0], sm[1]), std::max(sm[2], sm[3]));
-  // the workspace is sized from the arena span (gaps included), so the span is
-  // what the context bound limits
-  if (span > ctx->max_bytes)
-    return fail(MCDC_E_TOOBIG, "arena span %llu > max_bytes=%zu", (unsigned long long)span, ctx->max_bytes);
-  const uint64_t n_al = span ? (span + delta + 15) / 16 * 16 : 0;
+  // The scan needs only the arena span.  It is taken from the last non-empty
+  // buffer (files laid out in arena order, the usual case) and the scan
+  // enqueued at once; the per-file ranges, their overlap check and the true
+  // span are built while it runs.  A layout whose last buffer does not end
+  // furthest is found there and the call restarts with the true span (the
+  // speculative scan read a prefix of it).  Before, a pass over all extents
+  // for the span (~0.02 ms for 80 000 files) and the whole range loop
+  // (~0.1 ms) preceded the first launch (tools/small_probe.py).
+  size_t last = nbufs;
+  while (last > 0 && lens[last - 1] == 0) --last;
+  uint64_t span = last ? offsets[last - 1] + lens[last - 1] : 0;
+  if (last && span < offsets[last - 1]) span = 0;  // (wraps: rejected by ranges() below)
   std::vector<uint64_t> &fs = ctx->bx_fs, &fe = ctx->bx_fe;
   fs.resize(nbufs);
   fe.resize(nbufs);
+  bool respan = false;
   auto ranges = [&]() -> int {
     uint64_t hi = 0;
     bool sorted = true;
@@ -1054,6 +1067,11 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
       if (lens[i] == 0) continue;
       sorted = sorted && fs[i] >= hi;  // non-empty ranges in increasing order, disjoint
       hi = std::max(hi, fe[i]);
+    }
+    if (hi > delta + span) {  // (the span was not the last buffer's end)
+      respan = true;
+      span = hi - delta;
+      return MCDC_E_INTERNAL;
     }
     if (!sorted) {  // any order is allowed, overlaps are not (one chunk chain per byte range)
       std::vector<size_t> idx;
@@ -1067,7 +1085,16 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
     }
     return MCDC_OK;
   };
-  rc = run_pipeline(ctx, params, base, n_al, fs.data(), fe.data(), nbufs, out, cap, counts, n_out, ranges);
+  for (int attempt = 0;; ++attempt) {
+    // the workspace is sized from the arena span (gaps included), so the span
+    // is what the context bound limits
+    if (span > ctx->max_bytes)
+      return fail(MCDC_E_TOOBIG, "arena span %llu > max_bytes=%zu", (unsigned long long)span, ctx->max_bytes);
+    const uint64_t n_al = span ? (span + delta + 15) / 16 * 16 : 0;
+    rc = run_pipeline(ctx, params, base, n_al, fs.data(), fe.data(), nbufs, out, cap, counts, n_out, ranges);
+    if (!(respan && attempt == 0)) break;
+    respan = false;  // (once: ranges() now sees the true span)
+  }
   ctx->timing.h2d_ms = 0;
   ctx->timing.total_ms = now_ms() - t0;
   return rc;

@@ -176,9 +176,12 @@ Knobs read_knobs();
 
 // launch wrappers (mcdc_kernels.hip); all enqueue on `stream`.
 void launch_fill_random(void *dst, uint64_t pos, uint64_t n, uint64_t seed, hipStream_t stream);
-// scan of full tiles [tile0, tile1) (+ the partial last tile when `tail`)
+// scan of full tiles [tile0, tile1) (+ the partial last tile when `tail`);
+// ev0 / ev1 (optional) are recorded at the launch's start and end by the
+// dispatch itself (hipExtLaunchKernelGGL: no marker packets between kernels)
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
-                 uint64_t tile1, bool tail, int pieces, bool cold);
+                 uint64_t tile1, bool tail, int pieces, bool cold, hipEvent_t ev0 = nullptr,
+                 hipEvent_t ev1 = nullptr);
 int scan_pieces(uint64_t nruns_full, int num_cus);  // lane pieces per run for a whole-call scan
 uint64_t scan_waves(uint64_t ntiles, int num_cus);  // waves of a scan launch over ntiles
 void launch_spec(const Work &w, const DevParams &p, const Knobs &k, uint32_t s0, uint32_t s1, hipStream_t stream);
@@ -194,7 +197,10 @@ void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void
 void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
                             hipStream_t stream);
 size_t scan_tmp_bytes(uint32_t nsegs);
-void launch_finish(const Work &w, uint64_t *res, hipStream_t stream);
+// ev_done (optional): recorded by the dispatch; zero[0, zwords) (optional)
+// cleared when the call needs no general resolution (err[2] == 0)
+void launch_finish(const Work &w, uint64_t *res, hipStream_t stream, hipEvent_t ev_done = nullptr,
+                   uint64_t *zero = nullptr, uint32_t zwords = 0);
 void launch_file_counts(const Work &w, uint64_t *dst, hipStream_t stream);  // chunks per file -> dst
 
 }  // namespace mcdc

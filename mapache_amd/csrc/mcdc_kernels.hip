@@ -17,6 +17,7 @@
 //    merge (k_spec / k_link / k_walk); a file whose chains never merge falls
 //    back to one serial wave (k_fallback).  No CPU in the loop.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
@@ -664,22 +665,26 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
 // for comparison.
 // Tiles are in units of 64 / pieces runs (pieces = lane pieces per run).
 void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t stream, uint64_t tile0,
-                 uint64_t tile1, bool tail, int pieces, bool cold) {
+                 uint64_t tile1, bool tail, int pieces, bool cold, hipEvent_t ev0, hipEvent_t ev1) {
   const uint64_t rpt = 64 / (uint64_t)pieces;
   const uint64_t ntiles = tail ? (w.nruns + rpt - 1) / rpt - tile0 : tile1 - tile0;
   uint64_t blocks = ntiles;  // one block per CU up to the CU count (156 KiB LDS -> 1 block/CU)
   const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256);
   if (blocks > cap) blocks = cap;
-  if (blocks == 0) return;
+  if (blocks == 0) {  // (no launch: the events still mark this point of the stream)
+    if (ev0) (void)hipEventRecord(ev0, stream);
+    if (ev1) (void)hipEventRecord(ev1, stream);
+    return;
+  }
   const int t = tail ? 1 : 0;
   const dim3 gr((unsigned)blocks), bl(1024);
   if (cold && pieces != 1) {  // (one piece: the saved bytes would spill, 128 VGPRs)
-    if (pieces == 4) hipLaunchKernelGGL((k_scan_q<kRun, 4, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
-    else hipLaunchKernelGGL((k_scan_q<kRun, 2, true>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    if (pieces == 4) hipExtLaunchKernelGGL((k_scan_q<kRun, 4, true>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
+    else hipExtLaunchKernelGGL((k_scan_q<kRun, 2, true>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
   } else {
-    if (pieces == 4) hipLaunchKernelGGL((k_scan_q<kRun, 4, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
-    else if (pieces == 2) hipLaunchKernelGGL((k_scan_q<kRun, 2, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
-    else hipLaunchKernelGGL((k_scan_q<kRun, 1, false>), gr, bl, 0, stream, w, p, tile0, tile1, t);
+    if (pieces == 4) hipExtLaunchKernelGGL((k_scan_q<kRun, 4, false>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
+    else if (pieces == 2) hipExtLaunchKernelGGL((k_scan_q<kRun, 2, false>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
+    else hipExtLaunchKernelGGL((k_scan_q<kRun, 1, false>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
   }
 }
 
@@ -1827,7 +1832,13 @@ __global__ __launch_bounds__(256) void k_emit_long(Work W, DevParams P) {
 
 // Call summary for the host in one small write (pinned host memory): chunk
 // total, error bits, fallback file count.
-__global__ void k_finish(Work W, uint64_t *res) {
+// (zero: the scan's partial-tile bitmap words and tile counter, cleared for
+// the next call once every reader of them has run -- unless the call needs
+// the general resolution, which reads them again)
+__global__ void k_finish(Work W, uint64_t *res, uint64_t *zero, uint32_t zwords) {
+  MCDC_VGPR_PAD(12);  // (not an exact fill)
+  if (zero && W.err[2] == 0)
+    for (uint32_t i = threadIdx.x; i < zwords; i += blockDim.x) zero[i] = 0;
   if (threadIdx.x == 0) {
     res[0] = W.nsegs ? W.seg_off[W.nsegs] : 0;
     res[1] = W.err[0];
@@ -1837,8 +1848,9 @@ __global__ void k_finish(Work W, uint64_t *res) {
   }
 }
 
-void launch_finish(const Work &w, uint64_t *res, hipStream_t stream) {
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, stream, w, res);
+void launch_finish(const Work &w, uint64_t *res, hipStream_t stream, hipEvent_t ev_done, uint64_t *zero,
+                   uint32_t zwords) {
+  hipExtLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, stream, nullptr, ev_done, 0, w, res, zero, zwords);
 }
 
 // Chunks per file from the final segment offsets, written straight into

@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
                                                             uint64_t *fbits) {
   __shared__ uint32_t tab[1u << kNearLog];  // pass 1: the far table (its first slots); passes 2, 3: the near table
   __shared__ uint32_t hist[kZcSegBlocks][256];
-  __shared__ uint32_t rep[kZcSegBlocks], high[kZcSegBlocks];
+  __shared__ uint32_t rep[kZcSegBlocks], high[kZcSegBlocks], nsmp[kZcSegBlocks];
   static_assert(kZcSegBlocks * kZcFarSlots <= (1u << kNearLog), "the far table fits the near table's place");
   MCDC_VGPR_PAD(32);  // (not an exact fill)
   const uint64_t bi0 = order[blockIdx.x];
@@ -582,8 +582,15 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
     // 8 KiB sample's, (K - 1) / (2 n ln 2) with K = 256 values: the same
     // margin below uniform bytes at every sample size)
     const float thr = kRawEntropy - 183.9f / (float)max(n, 1u) + 183.9f / 8192.f;
-    if (lane == 0) high[wv] = n >= 512 && (float)n * __log2f((float)n) - sc >= thr * (float)n ? 1u : 0u;
+    if (lane == 0) {
+      high[wv] = n >= 512 && (float)n * __log2f((float)n) - sc >= thr * (float)n ? 1u : 0u;
+      nsmp[wv] = n;
+    }
   }
+  __syncthreads();
+  // (a chunk's last block too short to judge, under 512 bytes, follows the
+  // block before it: it would otherwise keep a random segment alive alone)
+  if (tid == 0 && nsb > 1 && nsmp[nsb - 1] < 512 && high[nsb - 2]) high[nsb - 1] = 1;
   __syncthreads();
   uint32_t hend = 0;  // the end of the last high-entropy block
   for (uint32_t k = 0; k < nsb; ++k)

@@ -523,9 +523,12 @@ def test_long_stretch_hashes_repeated(ctx):
 
 
 def test_batch_device_ranges_validated(ctx):
-    """mcdc_chunk_batch_device: files in any order are fine; overlapping
-    ranges, offset + length overflow and an arena span beyond the context's
-    max_bytes are rejected (MCDC_E_INVALID / MCDC_E_TOOBIG) before any launch."""
+    """mcdc_chunk_batch_device: files in any order are fine, including a last
+    file that does not end furthest (the scan is enqueued on the last file's
+    end before the ranges are read; the call then restarts with the true
+    span); overlapping ranges, offset + length overflow and an arena span
+    beyond the context's max_bytes are rejected (MCDC_E_INVALID /
+    MCDC_E_TOOBIG)."""
     n = 8 << 20
     dp = ctx.device_alloc(n)
     p = _lib.params(*PARAMS[0])
@@ -537,6 +540,13 @@ def test_batch_device_ranges_validated(ctx):
         r, rc = O.chunk_files(O.Params(*PARAMS[0]), [host[o:o + ln] for o, ln in zip(offs, lens)])
         assert (gc == rc).all()
         _same(g, r)
+        for offs, lens in (([6 << 20, 0, 2 << 20], [2 << 20, 1 << 20, (1 << 20) + 3]),  # the last ends at 3 MiB
+                           ([(7 << 20) + 5, 11, 3 << 20, 0], [(1 << 20) - 5, 2 << 20, 1 << 20, 0])):
+            for _ in range(2):  # (twice: the second call repeats the layout)
+                g, gc = ctx.chunk_batch_device(p, dp, offs, lens)
+                r, rc = O.chunk_files(O.Params(*PARAMS[0]), [host[o:o + ln] for o, ln in zip(offs, lens)])
+                assert (gc == rc).all()
+                _same(g, r)
         for offs, lens in (([0, 1 << 20], [(1 << 20) + 1, 5]), ([100, 50], [100, 100])):
             with pytest.raises(_lib.McdcError) as ei:
                 ctx.chunk_batch_device(p, dp, offs, lens)
@@ -553,6 +563,11 @@ def test_batch_device_ranges_validated(ctx):
             with pytest.raises(_lib.McdcError) as ei:
                 small.chunk_batch_device(p, dq, [0, 4 << 20], [256 << 10, 256 << 10])
             assert ei.value.code == _lib.MCDC_E_TOOBIG
+            with pytest.raises(_lib.McdcError) as ei:  # (the last file ends first: found after the scan's launch)
+                small.chunk_batch_device(p, dq, [4 << 20, 0], [256 << 10, 256 << 10])
+            assert ei.value.code == _lib.MCDC_E_TOOBIG
+            g, gc = small.chunk_batch_device(p, dq, [0], [256 << 10])  # (the context still works)
+            assert gc.sum() == len(g) > 0
         finally:
             small.device_free(dq)
     finally:

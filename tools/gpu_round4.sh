@@ -94,6 +94,18 @@ for stage in "$@"; do
     done
     cd $R
     echo zcprof done ;;
+  c3trace)  # kernel traces of the configs[3] paths: 80 000 small files chunked (tools/small_probe.py)
+             # and the kernel-tree save path with GPU compression (tools/tree_probe.py, 3 calls)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/small_trace -o small --output-format csv -- \
+      python3 $R/tools/small_probe.py > $OUT/small_probe.log 2> $OUT/small_trace.err \
+      || { echo "small trace rc=$?"; tail -5 $OUT/small_trace.err; exit 1; }
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/tree_trace -o tree --output-format csv -- \
+      python3 $R/tools/tree_probe.py 80000 3 > $OUT/tree_probe.log 2> $OUT/tree_trace.err \
+      || { echo "tree trace rc=$?"; tail -5 $OUT/tree_trace.err; exit 1; }
+    cd $R
+    cat $OUT/small_probe.log $OUT/tree_probe.log
+    echo c3trace done ;;
   b3pmc)  # chunk-ID kernel counters (tools/b3bench.py 16 GiB): instruction mix, VALUBusy, the held clock
     cd /tmp && export TMPDIR=/tmp
     i=0

@@ -27,8 +27,8 @@ with _lib.Context(0, 2 << 30) as ctx:
     for c in range(calls):
         t0 = time.perf_counter()
         with ctx.index_create() as ix:
-            ids, new, packed, packs = ctx.save_files(p, ix, dp, offs, lens, bytes(range(32)), nonces, hn, pad, n=n,
-                                                     gpu_compress=gpu, out_buf=ob)
+            ids, fb, new, packed, packs = ctx.save_files(p, ix, dp, offs, lens, bytes(range(32)), nonces, hn, pad, n=n,
+                                                     gpu_compress=gpu, out_buf=ob, split=False)
         dt = time.perf_counter() - t0
         print(f"call {c}: {dt * 1e3:.1f} ms  {n / dt / 2**30:.2f} GiB/s  stored {int(new.sum())}  packed {packed.size}",
               flush=True)
