@@ -692,7 +692,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
       HIP_TRY(hipEventRecord(ctx->ev_prep, st2));
       HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prep, 0));
     }
-    launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st);
+    launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st,
+                        want_counts ? ctx->d_fcnt : nullptr);
     HIP_TRY(hipGetLastError());
   }
   for (int i = 0; i < (lane_all ? 0 : K); ++i) {
@@ -704,7 +705,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
     HIP_TRY(hipGetLastError());
   }
-  if (want_counts) launch_file_counts(W, ctx->d_fcnt, rs);
+  if (want_counts && !(lane_all && nsegs)) launch_file_counts(W, ctx->d_fcnt, rs);  // (else by the emit)
   // (a whole-call scan: its bitmap words zeroed for the next call by k_finish)
   const bool rezero = early && n_al > 0;
   launch_finish(W, ctx->d_res, rs, ctx->ev_end, rezero ? W.run_bits + 2 * bw0 : nullptr, (uint32_t)(zero_bytes / 8));

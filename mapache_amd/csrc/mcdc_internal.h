@@ -192,8 +192,9 @@ void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uin
                              void *scan_tmp, size_t scan_tmp_bytes, hipStream_t stream, int gs = 16);
 // whole-call resolution with the lane walk (single part): spec, link, counts,
 // offsets and boundaries of every segment, the group walk for handed-back ones
+// fcnt (optional): chunks per file into pinned host memory, by the emit kernel
 void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void *scan_tmp, size_t scan_tmp_bytes,
-                         hipStream_t stream);
+                         hipStream_t stream, uint64_t *fcnt = nullptr);
 void launch_resolve_general(const Work &w, const DevParams &p, void *scan_tmp, size_t scan_tmp_bytes,
                             hipStream_t stream);
 size_t scan_tmp_bytes(uint32_t nsegs);

@@ -1767,8 +1767,11 @@ __device__ __forceinline__ void emit_one(const Work &W, const DevParams &P, cons
 // VGPR allocations are audited at build time: filling one
 // exactly lost the memory returns of whole waves (k_emit at 184/184 in round
 // 2), and a wrong ChunkData.hash is the one output no later stage re-checks.
+// fcnt (optional): chunks per file into pinned host memory (k_file_counts'
+// work, done by the threads whose segments are emitted: it overlaps the
+// emit's latency instead of following it, ~14 us for 80 000 files)
 template <int GS>
-__global__ __launch_bounds__(1024) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1) {
+__global__ __launch_bounds__(1024) void k_emit(Work W, DevParams P, uint32_t s0, uint32_t s1, uint64_t *fcnt) {
   __shared__ __attribute__((aligned(16))) uint64_t tab[256 * 32];
   __builtin_amdgcn_s_setprio(3);
   load_gear_rep(tab, W);
@@ -1802,6 +1805,11 @@ __global__ __launch_bounds__(1024) void k_emit(Work W, DevParams P, uint32_t s0,
       }
     }
   }
+  if (fcnt)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W.nfiles; i += gridDim.x * blockDim.x) {
+      const File F = W.files[i];
+      fcnt[i] = F.nsegs ? W.seg_off[F.first_seg + F.nsegs] - W.seg_off[F.first_seg] : 0;
+    }
 }
 
 // Continuation stretches longer than kEmitInline nodes (k_link appended their
@@ -2217,13 +2225,15 @@ static unsigned lane_grid(const Work &w, uint64_t items_per_block_round, uint64_
 // 16 on the group walk's ~16): a lane per chunk.  (Measured at 64 GiB: a
 // quad of lanes per chunk sharing one 80-byte load was slower, 87-110 us vs
 // 62 us: the emit is bound by outstanding L1 misses, not by requests.)
-static void launch_emit(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, int gs, hipStream_t stream) {
+static void launch_emit(const Work &w, const DevParams &p, uint32_t s0, uint32_t s1, int gs, hipStream_t stream,
+                        uint64_t *fcnt = nullptr) {
   if (s1 <= s0) return;
   const unsigned n = s1 - s0;
   if (gs == 8)
-    hipLaunchKernelGGL(k_emit<8>, dim3(lane_grid(w, 1024 / 8, n, 1)), dim3(1024), 0, stream, w, p, s0, s1);
+    hipLaunchKernelGGL(k_emit<8>, dim3(lane_grid(w, 1024 / 8, n, 1)), dim3(1024), 0, stream, w, p, s0, s1, fcnt);
   else
-    hipLaunchKernelGGL(k_emit<kGroup>, dim3(lane_grid(w, 1024 / kGroup, n, 1)), dim3(1024), 0, stream, w, p, s0, s1);
+    hipLaunchKernelGGL(k_emit<kGroup>, dim3(lane_grid(w, 1024 / kGroup, n, 1)), dim3(1024), 0, stream, w, p, s0, s1,
+                       fcnt);
 }
 
 // counts and offsets of segments [s0, s1) assuming the clean case
@@ -2258,7 +2268,7 @@ void launch_emit_incremental(const Work &w, const DevParams &p, uint32_t s0, uin
 // list kernels read their counts on the device (no host round trip): a fixed
 // grid that exits at once when nothing was handed back.
 void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void *scan_tmp, size_t scan_tmp_bytes_,
-                         hipStream_t stream) {
+                         hipStream_t stream, uint64_t *fcnt) {
   if (w.nsegs == 0) return;
   const unsigned lg = lane_grid(w, 256, w.nsegs);
   const unsigned listg = w.ncu ? w.ncu : 256;
@@ -2271,7 +2281,7 @@ void launch_resolve_lane(const Work &w, const DevParams &p, uint64_t *incl, void
   hipLaunchKernelGGL(k_link_list<kGroup>, dim3(listg), dim3(256), 0, stream, w, p, (const uint32_t *)w.punt_link,
                      (const uint32_t *)(w.err + 5));
   launch_counts_incremental(w, 0u, w.nsegs, incl, scan_tmp, scan_tmp_bytes_, stream);
-  launch_emit(w, p, 0u, w.nsegs, 8, stream);
+  launch_emit(w, p, 0u, w.nsegs, 8, stream, fcnt);
 }
 
 // General resolution after k_spec / k_link of every segment: serial fallback

@@ -776,10 +776,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane
 // window (position i of the window in lane i % 64, slot i / 64), without a
 // serial walk: every position's successor (+ its match length, or + 1 for a
 // literal) is known from its word, so the chain from the cursor is found by
-// pointer doubling in LDS (J_k = the 2^k-th successor, 8 levels; marking
-// S_{k+1} = S_k + J_k(S_k) from the cursor), and the chain's matches,
-// literals, literal lengths (an exclusive max-scan of match ends) and
-// sequence / literal indices (prefix counts of ballots) follow by wave scans.
+// pointer doubling in LDS (J_k = the 2^k-th successor, k <= 5; lane m finds
+// the chain's node m of each 64 from the cursor by composing J over the bits
+// of m), and the chain's matches and literals get their indices from prefix
+// counts of ballots, each match its literal length and previous offset from
+// the match ranked before it (LDS).
 // Capped matches (16 verified bytes) get their true lengths before the walk
 // (see the window loop); the first long one on the chain (more than kRunExt
 // bytes past the 16) is extended by the wave (2 KiB per step) and ends the
@@ -789,10 +790,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane
 __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
                                                  const uint32_t *words, uint8_t *stage, uint64_t *seqs,
                                                  const uint32_t *porder) {
-  __shared__ uint16_t J[8][257];
+  __shared__ uint16_t J[6][257];
   __shared__ uint16_t ends[257], jp[256];
   __shared__ uint8_t mk[260], capl[256];
-  __shared__ uint32_t offl[256], wbyt[64];
+  __shared__ uint32_t offl[256], wbyt[64], mend[256], moff[256];
   if (blockIdx.x >= nblk) return;
   const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   uint64_t *sq = seqs + bi * kZcSeqCap;
   uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0, last_off = 0;  // (last_off 0: no sequence yet)
   if (lane == 0) {
-    for (int k = 0; k < 8; ++k) J[k][256] = 256;
+    for (int k = 0; k < 6; ++k) J[k][256] = 256;
     ends[256] = 256;
   }
   // A window's words and source bytes (lane l: bytes [wb + 4 l, + 4)) are
@@ -937,27 +938,29 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       cj[j] = en[j] == kEndLong ? 256u : min(en[j], 256u);  // (a long run stops the chain)
       J[0][i] = (uint16_t)cj[j];
     }
-    // J_k of the lane's own positions stay in registers (16 bits each): a
-    // doubling round reads only J_k(J_k(i)), marking reads only mk
-    uint32_t jr[8][2];
-    jr[0][0] = cj[0] | cj[1] << 16;
-    jr[0][1] = cj[2] | cj[3] << 16;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
+    for (int k = 0; k < 5; ++k) {  // J_{k+1} = J_k(J_k), up to J_5 (32 nodes)
 #pragma unroll
       for (int j = 0; j < 4; ++j) cj[j] = J[k][cj[j]];
 #pragma unroll
       for (int j = 0; j < 4; ++j) J[k + 1][64 * j + lane] = (uint16_t)cj[j];
-      jr[k + 1][0] = cj[0] | cj[1] << 16;
-      jr[k + 1][1] = cj[2] | cj[3] << 16;
     }
+    // The chain's nodes 64 at a time: node m of a quarter is J_0..J_5
+    // composed over the set bits of m from the quarter's first node (lane m
+    // finds it: 6 LDS reads) and is marked (256: past the window or a long
+    // match); the next quarter starts one step after node 63.  Most windows
+    // of compressible data hold fewer than 64 nodes: one quarter, and the
+    // doubling stops at J_5 (it ran to J_7 and marked in 8 rounds before)
+    for (uint32_t st = s0, qq = 0; qq < 4 && st < 256; ++qq) {
+      uint32_t x = st;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 64 * j + lane;
-        if (mk[i]) mk[(jr[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu] = 1;
+      for (int b = 0; b < 6; ++b) {
+        const uint32_t y = J[b][x];
+        x = (lane >> b) & 1u ? y : x;
       }
+      mk[x] = 1;
+      st = (uint32_t)__builtin_amdgcn_readfirstlane((int)J[0][__builtin_amdgcn_readlane((int)x, 63)]);
+    }
     ZT(1);
     bool node[4], mt[4];
     int32_t long_first = 0x7FFFFFFF;
@@ -1001,10 +1004,15 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       }
     }
     ZT(2);
-    // this window's matches and literals, in position order (slot-major)
-    uint32_t mcount = 0, lcount = 0;
-    int32_t pend = -1, pidx = -1;  // running exclusive max-scans: end / index of the previous match
-    uint32_t exit_pos = 0;
+    // this window's matches and literals, in position order (slot-major).
+    // Pass 1: window ranks from ballots; each match's end and offset into LDS
+    // at its rank, each literal's byte out.  Pass 2: a match's literal length
+    // and the offset it may repeat from the match ranked before it (the
+    // block's carried lit0 / last_off for the window's first) -- two LDS reads
+    // where a wave max-scan carried them (13 DPP steps per slot before).
+    uint32_t mcount = 0, lcount = 0, exit_pos = 0;
+    uint32_t mrk[4], mln[4];
+    bool mm[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane, q = wb + i;
@@ -1013,34 +1021,34 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
       const uint64_t bm = __ballot(m), bl = __ballot(l);
       const uint32_t mr = mcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       const uint32_t lr = lcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-      // exclusive scans over this slot's lanes, carried from the earlier slots
-      // (one scan: the match index in the high half, its end - wb in the low;
-      // the last match at or before a lane has both the largest index and end)
-      const int32_t key = wave_incl_max(m ? (int32_t)(i << 16 | (i + mlen)) : -1, lane);
-      const int32_t pk = wave_shr1(key, -1);
-      const int32_t ie = key >= 0 ? (int32_t)(wb + (key & 0xFFFF)) : -1, ii = key >= 0 ? key >> 16 : -1;
-      int32_t pe = pk >= 0 ? (int32_t)(wb + (pk & 0xFFFF)) : -1, pi = pk >= 0 ? pk >> 16 : -1;
-      pe = max(pe, pend);
-      pi = max(pi, pidx);
       if (m) {
-        const uint32_t start = pe >= 0 ? (uint32_t)pe : lit0;
-        const uint32_t ll = q - start, off = offl[i];
-        const uint32_t poff = pi >= 0 ? offl[pi] : last_off;
-        const uint32_t ov = (ll && off == poff) ? 1u : off + 3;
-        sq[nseq + mr] = zs::seq_pack_ov(ll, mlen, ov);
+        mend[mr] = q + mlen;
+        moff[mr] = offl[i];
       }
       if (l) lit[nlit + lr] = reinterpret_cast<const uint8_t *>(wbyt)[i];
-      pend = max(pend, lane63(ie));
-      pidx = max(pidx, lane63(ii));
       mcount += (uint32_t)__builtin_popcountll(bm);
       lcount += (uint32_t)__builtin_popcountll(bl);
       if (in) exit_pos = max(exit_pos, q + (m ? mlen : 1u));
+      mm[j] = m;
+      mrk[j] = mr;
+      mln[j] = mlen;
+    }
+    lds_sync();  // (the ranks' ends and offsets written by other lanes)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (mm[j]) {
+        const uint32_t i = 64 * j + lane, q = wb + i, mr = mrk[j];
+        const uint32_t start = mr ? mend[mr - 1] : lit0, poff = mr ? moff[mr - 1] : last_off;
+        const uint32_t ll = q - start, off = offl[i];
+        const uint32_t ov = (ll && off == poff) ? 1u : off + 3;
+        sq[nseq + mr] = zs::seq_pack_ov(ll, mln[j], ov);
+      }
     }
     nseq += mcount;
     nlit += lcount;
-    if (pidx >= 0) {
-      lit0 = (uint32_t)pend;
-      last_off = offl[pidx];
+    if (mcount) {
+      lit0 = mend[mcount - 1];
+      last_off = moff[mcount - 1];
     }
     cur = (uint32_t)wave_max((int32_t)exit_pos);
     ZT(3);
