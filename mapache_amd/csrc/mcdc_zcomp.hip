@@ -793,7 +793,8 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   __shared__ uint16_t J[6][257];
   __shared__ uint16_t ends[257], jp[256];
   __shared__ uint8_t mk[260], capl[256];
-  __shared__ uint32_t offl[256], wbyt[64], mend[256], moff[256];
+  __shared__ uint32_t offl[256], wbyt[64], mend[256], moff[256], llen[256];
+  __shared__ uint16_t xlist[256];
   if (blockIdx.x >= nblk) return;
   const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
@@ -883,33 +884,49 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     if (anycap) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) capl[64 * j + lane] = (uint8_t)cap[j];
+      // the runs' last positions, listed (ballot ranks) and extended one per
+      // lane: one round of loads for the window (they were per slot: four
+      // dependent memory round trips in a window of source code)
+      uint32_t nx = 0;
+      bool ext[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t i = 64 * j + lane;
         const bool same = i < 255 && capl[i + 1] && offl[i + 1] == offl[i];
+        ext[j] = cap[j] && !same;
         en[j] = !valid[j] ? 256u : !cap[j] ? i + (ml[j] ? ml[j] : 1u) : same ? kEndNext : 0u;
-        if (cap[j] && !same) {  // a run's last position: kRunExt bytes after its kMlCap
-          const uint32_t q = wb + i + kMlCap, off = offl[i];
-          uint4 x[kRunExt / 16], y[kRunExt / 16];
-#pragma unroll
-          for (int u = 0; u < (int)(kRunExt / 16); ++u) {
-            const uint64_t g = B.src + q + 16 * u;
-            x[u] = ld16c(base, g, nbytes);
-            y[u] = ld16c(base, g - off, nbytes);
-          }
-          uint32_t m = 0;
-#pragma unroll
-          for (int u = 0; u < (int)(kRunExt / 16); ++u) {
-            const uint32_t qu = q + 16 * u;
-            const uint64_t g = B.src + qu;
-            const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
-            m += m == 16 * (uint32_t)u ? mu : 0u;
-          }
-          en[j] = m == kRunExt ? kEndLong : i + kMlCap + m;
-        }
+        const uint64_t bx = __ballot(ext[j]);
+        if (ext[j])
+          xlist[nx + __builtin_amdgcn_mbcnt_hi((uint32_t)(bx >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bx, 0u))] =
+              (uint16_t)i;
+        nx += (uint32_t)__builtin_popcountll(bx);
         ends[i] = (uint16_t)en[j];
         jp[i] = (uint16_t)(i + 1);
       }
+      lds_sync();  // (the list, written by other lanes)
+      for (uint32_t r = lane; r < nx; r += 64) {  // kRunExt bytes after the run's kMlCap
+        const uint32_t i = xlist[r], q = wb + i + kMlCap, off = offl[i];
+        uint4 x[kRunExt / 16], y[kRunExt / 16];
+#pragma unroll
+        for (int u = 0; u < (int)(kRunExt / 16); ++u) {
+          const uint64_t g = B.src + q + 16 * u;
+          x[u] = ld16c(base, g, nbytes);
+          y[u] = ld16c(base, g - off, nbytes);
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int u = 0; u < (int)(kRunExt / 16); ++u) {
+          const uint32_t qu = q + 16 * u;
+          const uint64_t g = B.src + qu;
+          const uint32_t mu = qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
+          m += m == 16 * (uint32_t)u ? mu : 0u;
+        }
+        ends[i] = (uint16_t)(m == kRunExt ? kEndLong : i + kMlCap + m);
+      }
+      lds_sync();
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ext[j]) en[j] = ends[64 * j + lane];
     }
     // the next window's words and bytes, in flight meanwhile (requested after
     // the run ends' loads: the compiler's wait for those counts every older
@@ -950,33 +967,34 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
     // finds it: 6 LDS reads) and is marked (256: past the window or a long
     // match); the next quarter starts one step after node 63.  Most windows
     // of compressible data hold fewer than 64 nodes: one quarter, and the
-    // doubling stops at J_5 (it ran to J_7 and marked in 8 rounds before)
-    for (uint32_t st = s0, qq = 0; qq < 4 && st < 256; ++qq) {
-      uint32_t x = st;
-#pragma unroll
-      for (int b = 0; b < 6; ++b) {
-        const uint32_t y = J[b][x];
-        x = (lane >> b) & 1u ? y : x;
-      }
-      mk[x] = 1;
-      st = (uint32_t)__builtin_amdgcn_readfirstlane((int)J[0][__builtin_amdgcn_readlane((int)x, 63)]);
-    }
+    // doubling stops at J_5 (it ran to J_7 and marked in 8 rounds before).
+    // The chain stops at a long match: the wave extends it (2 KiB per step:
+    // lane k compares bytes [.. + 32 k, + 32)) and, if it ends inside the
+    // window, marks on from its end (J holds for every position) -- a long
+    // match ended the window before, a window reload and recomputation each
+    // (source code and binary data: many 48-byte-plus repeats per window).
     ZT(1);
-    bool node[4], mt[4];
-    int32_t long_first = 0x7FFFFFFF;
+    for (uint32_t st0 = s0;;) {
+      for (uint32_t st = st0, qq = 0; qq < 4 && st < 256; ++qq) {
+        uint32_t x = st;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = 64 * j + lane;
-      node[j] = valid[j] && mk[i];
-      mt[j] = node[j] && ml[j] != 0;
-      const uint64_t bl = __ballot(mt[j] && en[j] == kEndLong);
-      if (long_first == 0x7FFFFFFF && bl) long_first = 64 * j + (int32_t)__builtin_ctzll(bl);
-    }
-    uint32_t L = 255, mlt = 0;  // nodes <= L are this window's; the long match at L (if any) is mlt long
-    if (long_first != 0x7FFFFFFF) {  // extend it (2 KiB per step: lane k compares bytes [.. + 32 k, + 32))
-      L = (uint32_t)long_first;
-      const uint32_t pos = wb + L, off = offl[L];
-      mlt = kMlCap;
+        for (int b = 0; b < 6; ++b) {
+          const uint32_t y = J[b][x];
+          x = (lane >> b) & 1u ? y : x;
+        }
+        mk[x] = 1;
+        st = (uint32_t)__builtin_amdgcn_readfirstlane((int)J[0][__builtin_amdgcn_readlane((int)x, 63)]);
+      }
+      int32_t lf = 0x7FFFFFFF;  // the first long match on the chain from st0
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = 64 * j + lane;
+        const uint64_t bl = __ballot(i >= st0 && en[j] == kEndLong && mk[i]);
+        if (lf == 0x7FFFFFFF && bl) lf = 64 * j + (int32_t)__builtin_ctzll(bl);
+      }
+      if (lf == 0x7FFFFFFF) break;
+      const uint32_t L = (uint32_t)lf, pos = wb + L, off = offl[L];
+      uint32_t mlt = kMlCap;
       for (;;) {
         const uint32_t q = pos + mlt + 32 * lane;
         uint32_t m = 0;
@@ -1002,6 +1020,16 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         }
         mlt += 2048;
       }
+      if (lane == 0) llen[L] = mlt;
+      if (L + mlt >= 256) break;  // (the window ends with it)
+      st0 = L + mlt;
+    }
+    bool node[4], mt[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = 64 * j + lane;
+      node[j] = valid[j] && mk[i];
+      mt[j] = node[j] && ml[j] != 0;
     }
     ZT(2);
     // this window's matches and literals, in position order (slot-major).
@@ -1016,8 +1044,8 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = 64 * j + lane, q = wb + i;
-      const bool in = node[j] && i <= L, m = in && mt[j], l = in && !mt[j];
-      const uint32_t mlen = (i == L && mlt) ? mlt : cap[j] ? en[j] - i : ml[j];
+      const bool in = node[j], m = in && mt[j], l = in && !mt[j];
+      const uint32_t mlen = en[j] == kEndLong ? llen[i] : cap[j] ? en[j] - i : ml[j];
       const uint64_t bm = __ballot(m), bl = __ballot(l);
       const uint32_t mr = mcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       const uint32_t lr = lcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));

@@ -1,6 +1,9 @@
 """GPU zstd compression throughput and ratio (mcdc_zstd_compress_device) on a
 random stream and on the bench's synthetic corpora, chunked at 16/64/256 KiB
 (or mapache's 512K/1M/8M: P512); device-resident in and out.
+Kind "tree": the configs[3] kernel-tree stand-in (tests/corpora.kernel_tree,
+1.33 GB), one chunk per file as the save path's whole-file branch stores them
+(GiB ignored).
 Usage: python tools/zc_bench.py [GiB] [steps] [kinds,...] [P16|P512]"""
 import json
 import os
@@ -19,11 +22,25 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 n = int(gib * (1 << 30))
 p = _lib.params(524288, 1048576, 8388608, 1) if len(sys.argv) > 4 and sys.argv[4] == "P512" else \
     _lib.params(16384, 65536, 262144, 1)
-ctx = _lib.Context(0, n + (1 << 20))
+ctx_cap = n + (1 << 20)
+ctx = _lib.Context(0, ctx_cap)
 res = {}
+n_arg = n
 for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records", "binary", "far")):
+    n = n_arg
+    tree = None
+    if kind == "tree":
+        from tests import corpora
+        tree = corpora.kernel_tree(80000)
+        n = int(tree[0].size)
+        if n + (1 << 20) > ctx_cap:
+            ctx.close()
+            ctx_cap = n + (1 << 20)
+            ctx = _lib.Context(0, ctx_cap)
     dp = ctx.device_alloc(n)
-    if kind == "random":
+    if tree is not None:
+        ctx.h2d(dp, tree[0])
+    elif kind == "random":
         ctx.fill_random(dp, n, 0x6d61706163686521)
     else:  # the shared synthetic corpora (tests/corpora.py), a 64 MiB pattern repeated
         sys.path.insert(0, ROOT)
@@ -31,10 +48,17 @@ for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text",
         base = corpora.by_name(kind, 64 << 20).tobytes()
         for o in range(0, n, len(base)):
             ctx.h2d(dp + o, np.frombuffer(base[:min(len(base), n - o)], np.uint8))
-    cap_c = n // 16383 + 2
-    d_ch = ctx.device_alloc(24 * cap_c)
-    k = ctx.chunk_device_to_device(p, dp, n, d_ch, cap_c)
-    ch = ctx.d2h_chunks(d_ch, k)
+    if tree is not None:  # one chunk per file
+        ch = np.zeros(tree[1].size, _lib.CHUNK_DTYPE)
+        ch["offset"], ch["length"] = tree[1], tree[2]
+        k = int(ch.size)
+        d_ch = ctx.device_alloc(24 * k)
+        ctx.h2d(d_ch, ch.view(np.uint8))
+    else:
+        cap_c = n // 16383 + 2
+        d_ch = ctx.device_alloc(24 * cap_c)
+        k = ctx.chunk_device_to_device(p, dp, n, d_ch, cap_c)
+        ch = ctx.d2h_chunks(d_ch, k)
     cap = _lib.Context.zstd_compress_bound(ch["length"])
     d_out, d_fr = ctx.device_alloc(cap), ctx.device_alloc(16 * k)
     ctx.zstd_compress(dp, n, (d_ch, k), d_out, cap, frames_out=d_fr)
