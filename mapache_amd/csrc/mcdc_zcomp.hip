@@ -1772,6 +1772,7 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
 // CUs.  The machines are VALU-bound (one wave per SIMD): k_zc_plan hands
 // them their codes, one byte per sequence, in walking order.
 constexpr uint32_t kChainBlocks = 9;
+constexpr uint32_t kChainSplit = 64;  // blocks with at least this many sequences: two lanes per state machine
 __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t nblk, uint64_t *recs,
                                                  uint32_t *words) {
   __shared__ FseCTL tb[3 * kChainBlocks];
@@ -1796,29 +1797,45 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   }
   __syncthreads();
   ZT(0);
-  const uint32_t j = min(lane / 3, kChainBlocks - 1), k = lane % 3;
+  // Two lanes per state machine: lane jk (< 27) walks the first half of its
+  // block's sequences from the true initial state, lane 27 + jk the second
+  // half from a guessed one (the initial state of the half's first code, as
+  // if the stream began there), so the wave's dependent LDS chain is half as
+  // long.  The second lane then re-walks its half from the true state beside
+  // the guessed walk until the two states agree (an encoder's state map is
+  // many-to-one: they agree within a few codes), rewriting those records.
+  const uint32_t half = lane >= 3 * kChainBlocks ? 1u : 0u, jk = lane - half * 3 * kChainBlocks;
+  const uint32_t j = min(jk / 3, kChainBlocks - 1), k = jk % 3;
   const uint64_t b = g0 + j;
-  const bool act = lane < 3 * kChainBlocks && b < nblk;
+  const bool act = lane < 6 * kChainBlocks && b < nblk;
   const uint32_t ns = act ? blocks[b].nseq : 0u;
+  const bool split = ns >= kChainSplit;
+  const uint32_t h = split ? ns / 2 : ns;                       // half 0: codes [1, h), half 1: [h, ns)
+  const uint32_t m_lo = half ? h : 1u, m_hi = half ? (split ? ns : h) : h;
+  const uint32_t nsl = m_hi > m_lo ? m_hi - m_lo : 0u;
   const FseCTL &ct = tb[3 * j + k];
   uint16_t *rec = reinterpret_cast<uint16_t *>(recs + (act ? b : 0) * kZcSeqCap);
   const uint8_t *cd = seq_codes(words, act ? b : 0, k);  // codes in walking order: cd[m] = sequence ns - 1 - m
+  const uint8_t *cdl = cd + m_lo;
   // 16 sequences per batch: codes of batch t in a register quad, of batch
   // t + 1 in flight (a load outside the compiler's wait counting, waited
   // for after the batch's steps, before its records are stored; 16 steps of
   // the chain cover the load's latency, 8 did not)
   auto issue = [&](uint32_t m0) {
     u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(cd + m0) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(cdl + m0) : "memory");
     return v;
   };
-  const int32_t top = wave_max((int32_t)ns);  // (the wave's longest block sets the batch count)
-  uint32_t state = 0;
-  if (ns) {  // the last sequence: the initial state (no bits)
-    const uint32_t c = cd[0], dnb = ct.dnb[c];
-    const uint32_t nb = (dnb + (1u << 15)) >> 16;
-    state = ct.state[((((nb << 16) - dnb)) >> nb) + ct.dfs[c]];
-    rec[4 * (ns - 1) + k] = 0;
+  auto init_state = [&](uint32_t c) {  // the state after a stream's first code (no bits)
+    const uint32_t dnb = ct.dnb[c], nb = (dnb + (1u << 15)) >> 16;
+    return (uint32_t)ct.state[((((nb << 16) - dnb)) >> nb) + ct.dfs[c]];
+  };
+  const int32_t top = wave_max((int32_t)nsl);  // (the wave's longest half sets the batch count)
+  uint32_t state = 0, guess = 0;
+  if (ns && (half == 0 || split)) {
+    state = init_state(cd[half ? h - 1 : 0]);
+    guess = state;
+    if (half == 0) rec[4 * (ns - 1) + k] = 0;  // the last sequence: the initial state (no bits)
   }
   // one batch: the codes in cq (waited for), the next batch's requested into
   // nq; the loop alternates two register quads, so that no register with a
@@ -1840,24 +1857,44 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
       const uint32_t nb = (state + dn[u]) >> 16;
       r[u] = nb | (state & ((1u << nb) - 1u)) << 4;
       const uint32_t nxt = ct.state[((state >> nb) + (uint32_t)df[u]) & 511u];
-      const bool in = m0 + u < (int32_t)ns;
+      const bool in = m0 + u < (int32_t)nsl;
       state = in ? nxt : state;
       sbits += in ? nb : 0u;
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(nq)::"memory");
 #pragma unroll
     for (int u = 0; u < 16; ++u)
-      if (m0 + u < (int32_t)ns) rec[4 * (ns - 1 - (uint32_t)(m0 + u)) + k] = (uint16_t)r[u];
+      if (m0 + u < (int32_t)nsl) rec[4 * (ns - 1 - (m_lo + (uint32_t)(m0 + u))) + k] = (uint16_t)r[u];
   };
-  u32x4 qa = issue(1), qb;
+  u32x4 qa = issue(0), qb;
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa)::"memory");
-  for (int32_t m0 = 1; m0 < top; m0 += 32) {  // m: sequence ns - 1 - m
+  for (int32_t m0 = 0; m0 < top; m0 += 32) {
     batch(m0, qa, qb);
     batch(m0 + 16, qb, qa);
   }
-  if (act && ns) {
+  // the first half's final state and bits to the second half's lane
+  const uint32_t src = (half ? jk : lane) * 4;
+  const uint32_t s_true = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)state);
+  const uint32_t bits0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)sbits);
+  if (act && half && split) {
+    // re-walk from the true state beside the guessed walk until they agree
+    uint32_t st = s_true, sg = guess;
+    for (uint32_t m = h; m < ns && st != sg;) {
+      const u32x4 q = *reinterpret_cast<const u32x4 *>(cd + m);  // (16 codes; the slack covers the end)
+      for (int u = 0; u < 16 && m < ns && st != sg; ++u, ++m) {
+        const uint32_t c = (q[u >> 2] >> (8 * (u & 3))) & 63u, dn = ct.dnb[c], df = (uint32_t)ct.dfs[c];
+        const uint32_t nt = (st + dn) >> 16, ng = (sg + dn) >> 16;
+        rec[4 * (ns - 1 - m) + k] = (uint16_t)(nt | (st & ((1u << nt) - 1u)) << 4);
+        sbits += nt - ng;
+        st = ct.state[((st >> nt) + df) & 511u];
+        sg = ct.state[((sg >> ng) + df) & 511u];
+      }
+    }
+    if (st != sg) state = st;  // (never agreed: the true walk ran to the end)
+  }
+  if (act && ns && (half ? split : !split)) {  // the walk that ends at the block's last code
     seq_tab(words, b)->fin[k] = state;
-    seq_tab(words, b)->sbits[k] = sbits;
+    seq_tab(words, b)->sbits[k] = sbits + (half ? bits0 : 0u);
   }
   ZT(1);
   ZT_PRINT("chain", blockIdx.x % 97 == 0);
