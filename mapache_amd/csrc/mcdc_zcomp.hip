@@ -38,13 +38,15 @@
 //   k_zc_parse   ONE WAVE PER BLOCK: the greedy parse over the words, 256
 //                positions per window without a serial walk: capped matches
 //                (16 verified bytes) get their true lengths per run of one
-//                repeat (its last position extended, the end handed back by
-//                pointer jumping); the chain from the cursor by pointer
-//                doubling, its matches, literal lengths and indices by wave
-//                scans; a match longer than 48 bytes on the chain extended
-//                2 KiB per wave step, ending the window; repeat code 1
-//                for an offset equal to the previous sequence's; literals to
-//                the block's staging slot, sequences to scratch
+//                repeat (its last position extended, one per lane from a
+//                ranked list, the end handed back by pointer jumping); the
+//                chain from the cursor by pointer doubling (lane m composes
+//                J over the bits of m); a match longer than 48 bytes on the
+//                chain extended 2 KiB per wave step and the chain continued
+//                from its end; match and literal indices by ballot ranks,
+//                literal lengths and repeat code 1 from the match ranked
+//                before; literals to the block's staging slot, sequences to
+//                scratch
 //   k_zc_huff    ONE WAVE PER BLOCK: the block's literals (all of a block
 //                without matches) as a Huffman-coded (or RLE) literals
 //                section when smaller than raw: histogram of the 256 byte
@@ -54,7 +56,7 @@
 //                (four above 1023 literals) by the whole wave in lane pieces
 //   k_zc_plan    ONE WAVE PER BLOCK: per symbol type the block's own FSE
 //   k_zc_chain   table or the predefined one (seq_plan); the three state
-//   k_zc_encode  machines of 9 blocks per wave, one per lane (their bits to
+//   k_zc_encode  machines of 9 blocks per wave, two lanes each (their bits to
 //                scratch); then every sequence's bits placed by the block's
 //                wave; the block kept compressed only if smaller than raw
 //   scan         piece sizes (frame header on a chunk's first block, block
