@@ -383,8 +383,10 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     const bool okl = el != 0 && (el & 0x1FFFu) == gl && cl < p && p - cl <= zs::kWindow;
     const bool oks = es != 0 && (es & 0x1FFFu) == gs && cs < p && p - cs <= zs::kWindow;
 #else
-    const bool okl = el != 0 && (el & 0x1FFFu) == gl && p - cl <= zs::kWindow;
-    const bool oks = es != 0 && (es & 0x1FFFu) == gs && p - cs <= zs::kWindow;
+    // (an entry is an earlier tile's position of this segment or the
+    // re-inserted bytes: less than 2^20 back, no window test needed)
+    const bool okl = el != 0 && (el & 0x1FFFu) == gl;
+    const bool oks = es != 0 && (es & 0x1FFFu) == gs;
 #endif
     const uint32_t q = okl ? cl : oks ? cs : p;
     S.v = find;
@@ -1349,14 +1351,25 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   }
   __syncthreads();
   uint32_t r[4] = {0, 0, 0, 0};
-  for (uint32_t t = 0; t < 256; t += 4) {
-    const uint4 q = *reinterpret_cast<const uint4 *>(&hist[0][t]);  // (broadcast)
-    const uint32_t qs[4] = {q.x, q.y, q.z, q.w};
+  if (distinct <= 96) {  // (text: a few dozen symbols -- compare against the present ones only)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int g = 0; g < 4; ++g)
+      for (uint64_t m = pm[g]; m; m &= m - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m), t = 64 * g + l;
+        const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)c[g], (int)l);
 #pragma unroll
-      for (int h = 0; h < 4; ++h)
-        r[h] += (qs[j] && (qs[j] < c[h] || (qs[j] == c[h] && t + j < lane + 64 * h))) ? 1u : 0u;
+        for (int h = 0; h < 4; ++h) r[h] += (q < c[h] || (q == c[h] && t < lane + 64 * h)) ? 1u : 0u;
+      }
+  } else {
+    for (uint32_t t = 0; t < 256; t += 4) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(&hist[0][t]);  // (broadcast)
+      const uint32_t qs[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          r[h] += (qs[j] && (qs[j] < c[h] || (qs[j] == c[h] && t + j < lane + 64 * h))) ? 1u : 0u;
+    }
   }
   ZT(0);
 #if MCDC_ZC_HCUT == 1  // (A/B timing: stop after the counts)
