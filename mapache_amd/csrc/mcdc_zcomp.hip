@@ -260,10 +260,21 @@ __device__ __forceinline__ void ast32s(uint32_t *sbase, uint32_t off, uint32_t v
   asm volatile("global_store_dword %0, %1, %2" ::"v"(off), "v"(v), "s"(sbase) : "memory");
 }
 
-// Common prefix of two 16-byte strings.
+// Common prefix of two 16-byte strings, branch-free: the first differing bit
+// of each dword (v_ffbl: ~0 for none), offset by the dword's position with
+// clamping adds (~0 stays ~0), the minimum / 8 (the ctz-per-half form was
+// compiled to divergent branches, both sides run in a mixed wave).
+__device__ __forceinline__ uint32_t ffbl32(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
-  const uint64_t d0 = (uint64_t)(x.y ^ y.y) << 32 | (x.x ^ y.x), d1 = (uint64_t)(x.w ^ y.w) << 32 | (x.z ^ y.z);
-  return d0 ? (uint32_t)__builtin_ctzll(d0) >> 3 : d1 ? 8u + ((uint32_t)__builtin_ctzll(d1) >> 3) : 16u;
+  const uint32_t b0 = ffbl32(x.x ^ y.x);
+  const uint32_t b1 = __builtin_elementwise_add_sat(ffbl32(x.y ^ y.y), 32u);
+  const uint32_t b2 = __builtin_elementwise_add_sat(ffbl32(x.z ^ y.z), 64u);
+  const uint32_t b3 = __builtin_elementwise_add_sat(ffbl32(x.w ^ y.w), 96u);
+  return min(min(min(b0, b1), min(b2, b3)), 128u) >> 3;
 }
 
 // The match finder: one workgroup of kFindThreads threads per segment (up to
