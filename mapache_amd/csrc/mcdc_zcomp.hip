@@ -332,7 +332,8 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
   // 16-byte loads at chunk offsets clamped to the last 16 readable bytes; a
   // tile within 16 bytes of the end realigns them (fix16), others use them as loaded
   const uint32_t last16 = (uint32_t)min<uint64_t>(cbytes - 16, 0xFFFFFFF0ull);
-  const uint64_t tail0 = cbytes >= kFindTile + 16 ? cbytes - (kFindTile + 16) : 0;  // tiles from here: the tail
+  // tiles from here: the tail (32-bit: a uniform compare stays on the scalar unit; positions are < 2^31)
+  const uint32_t tail0 = (uint32_t)min<uint64_t>(cbytes >= kFindTile + 16 ? cbytes - (kFindTile + 16) : 0, 0xFFFFFFFFull);
   // Two tiles in flight: a tile's own bytes are requested two tiles ahead,
   // and its candidate's bytes are verified two tiles later (the counter
   // retires in order, so waiting for a tile's own bytes leaves the newer
