@@ -1733,9 +1733,12 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   std::vector<mcdc_chunk> sch(m);
   for (size_t k = 0; k < m; ++k) sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
   std::vector<mcdc_blob> fr(m);
-  size_t bound = 0, cbytes = 0;
-  int rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, nullptr, 0, &bound, fr.data());
-  if (rc != MCDC_E_CAPACITY) return rc ? rc : fail(MCDC_E_INTERNAL, "compress bound query did not report a bound");
+  size_t bound = 0, cbytes = 0;  // the raw-frame bound k_zc_nblocks reports, from the lengths
+  for (size_t k = 0; k < m; ++k) {
+    const uint64_t len = sext[k].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
+    bound += zs::kFrameHdr + zs::kBlockHdr * nb + len;
+  }
+  int rc = MCDC_OK;
   // (buffers of their own: plan_packs' header encode reuses enc_in / enc_out)
   if ((rc = ensure(ctx, ctx->sv_comp, std::max<size_t>(bound, 1))) ||
       (rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->sv_comp.p, bound, &cbytes, fr.data())))
@@ -1775,9 +1778,15 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     HIP_TRY(hipMemcpyAsync(D + P.pk[k].offset + P.body[k], P.meta.data() + P.moff[k], P.moff[k + 1] - P.moff[k],
                            hipMemcpyHostToDevice, ctx->stream));
   }
+  // the packs cross PCIe on the second stream while their IDs are computed
+  // (both only read D; ~7 ms of D2H for the kernel-tree stand-in's packs)
+  HIP_TRY(hipEventRecord(ctx->ev_prep, ctx->stream));
+  HIP_TRY(hipStreamWaitEvent(ctx->stream2, ctx->ev_prep, 0));
+  HIP_TRY(hipMemcpyAsync(packs_out, D, P.total, hipMemcpyDeviceToHost, ctx->stream2));
   std::vector<uint8_t> pid(32 * np);
-  if ((rc = mcdc_chunk_ids_device(ctx, D, P.total, P.pk.data(), np, pid.data()))) return rc;
-  HIP_TRY(hipMemcpyAsync(packs_out, D, P.total, hipMemcpyDeviceToHost, ctx->stream));
+  rc = mcdc_chunk_ids_device(ctx, D, P.total, P.pk.data(), np, pid.data());
+  HIP_TRY(hipStreamSynchronize(ctx->stream2));
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   fill_pack_records(P, pid.data(), packs);
   return MCDC_OK;
