@@ -801,7 +801,10 @@ int give_back(mcdc_ctx *ctx, void *dst, const void *d_src, size_t bytes) {
 // the extents come from a boundary list instead (mcdc_seal_chunks_device).
 int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size_t n_in, const mcdc_blob *blobs,
              size_t nblobs, const uint8_t *nonces, void *d_out, size_t out_cap, uint64_t *out_offsets,
-             int32_t *status, const mcdc_chunk *chunks = nullptr) {
+             int32_t *status, const mcdc_chunk *chunks = nullptr, bool wait_done = true) {
+  // (wait_done false, seal only: returns once the kernels are enqueued and
+  // out_offsets is written; the caller orders later work on the context's
+  // stream and synchronises it)
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!key || (!d_in && n_in) || (nblobs && !blobs && !chunks) || (!open && nblobs && !nonces))
@@ -853,6 +856,7 @@ int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size
   HIP_TRY(hipStreamSynchronize(st));
   if (herr) return fail(MCDC_E_INVALID, "a blob extent lies outside the %zu-byte input", n_in);
   if ((rc = give_back(ctx, out_offsets, ooff, (n + 1) * 8))) return rc;
+  if (!wait_done && !open) HIP_TRY(hipStreamSynchronize(st));  // (the offsets before the seal is enqueued)
   if (total > out_cap || (total && !d_out)) {
     HIP_TRY(hipStreamSynchronize(st));
     return fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", out_cap, (unsigned long long)total);
@@ -878,6 +882,10 @@ int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
   std::memset(mk.rk, 0, sizeof mk.rk);
+  if (!wait_done && !open) {
+    ctx->timing.total_ms = now_ms() - t0;
+    return MCDC_OK;
+  }
   std::vector<int32_t> hstat;
   if (open) {
     hstat.resize(n);
@@ -1749,7 +1757,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     const size_t scap = cbytes + (size_t)kAeadOverhead * m;
     if ((rc = ensure(ctx, ctx->sv_seal, scap)) ||
         (rc = aead_run(ctx, 0, store->key, ctx->sv_comp.p, cbytes, fr.data(), m, store->nonces, ctx->sv_seal.p, scap,
-                       eo.data(), nullptr)))
+                       eo.data(), nullptr, nullptr, false)))  // (the pack plan's host work overlaps the seal)
       return rc;
     E = (const uint8_t *)ctx->sv_seal.p;
   } else {  // frames are back to back from sv_comp
