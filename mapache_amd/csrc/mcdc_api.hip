@@ -236,7 +236,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, sv_comp, sv_seal, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs,
+      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs,
       zc_blocks2, zc_stage2, zc_seqs2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_recs2;  // (the second batch set)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
@@ -263,6 +263,8 @@ struct mcdc_ctx {
   uint64_t *h_fcnt = nullptr;  // pinned chunks-per-file, written by k_file_counts
   uint64_t *d_fcnt = nullptr;  // its device alias
   size_t h_fcnt_cap = 0;       // entries
+  void *h_save = nullptr;      // pinned staging of the save path's new blobs (host zstd mode, device input)
+  size_t h_save_cap = 0;       // bytes
   uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
@@ -344,6 +346,24 @@ int ensure_fcnt(mcdc_ctx *ctx, size_t n) {
   }
   HIP_TRY(hipHostGetDevicePointer((void **)&ctx->d_fcnt, ctx->h_fcnt, 0));
   ctx->h_fcnt_cap = alloc;
+  return MCDC_OK;
+}
+
+int ensure_hsave(mcdc_ctx *ctx, size_t bytes) {
+  if (ctx->h_save_cap >= bytes) return MCDC_OK;
+  if (ctx->h_save) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipHostFree(ctx->h_save));
+    ctx->h_save = nullptr;
+    ctx->h_save_cap = 0;
+  }
+  const size_t alloc = (bytes + bytes / 8 + 4095) / 4096 * 4096;
+  if (hipHostMalloc(&ctx->h_save, alloc, hipHostMallocDefault) != hipSuccess) {
+    ctx->h_save = nullptr;
+    (void)hipGetLastError();
+    return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", alloc);
+  }
+  ctx->h_save_cap = alloc;
   return MCDC_OK;
 }
 
@@ -981,6 +1001,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
+  if (ctx->h_save) (void)hipHostFree(ctx->h_save);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
@@ -991,7 +1012,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
+                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_recs,
                     &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_seqs2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
                     &ctx->zc_words2, &ctx->zc_recs2};
@@ -1807,23 +1828,34 @@ static int save_encode_host(mcdc_ctx *ctx, const mcdc_store *store, const void *
                             const std::vector<uint8_t> &types, void *packs_out, size_t packs_out_cap,
                             size_t *packs_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks) {
   const size_t m = sext.size();
-  std::vector<uint8_t> staged;
   const uint8_t *src = (const uint8_t *)data;
-  if (!host_in && m) {  // device input: bring the new blobs over (the zstd stage runs on the host)
+  size_t src_n = n;
+  if (!host_in && m) {
+    // device input: the new blobs gathered in HBM (one kernel), then one D2H
+    // into the context's pinned staging (the zstd stage runs on the host).
+    // One copy per blob cost ~15 us each: 1.1 s of the kernel-tree
+    // stand-in's 72 167 blobs.
+    std::vector<uint64_t> gx(3 * m);
     size_t tot = 0;
-    for (auto &e : sext) tot += e.length;
-    staged.resize(std::max<size_t>(tot, 1));
-    size_t o = 0;
-    for (auto &e : sext) {
-      if (e.length)
-        HIP_TRY(hipMemcpyAsync(staged.data() + o, d + e.offset, e.length, hipMemcpyDeviceToHost, ctx->stream));
-      e.offset = o;
-      o += e.length;
+    for (size_t k = 0; k < m; ++k) {
+      tot += ((uintptr_t)d + sext[k].offset - tot) & 15;  // (congruent to the source modulo 16; HBM buffers 256-aligned)
+      gx[3 * k] = sext[k].offset;
+      gx[3 * k + 1] = tot;
+      gx[3 * k + 2] = sext[k].length;
+      sext[k].offset = tot;
+      tot += sext[k].length;
     }
+    int rc0 = MCDC_OK;
+    if ((rc0 = ensure(ctx, ctx->sv_comp, std::max<size_t>(tot, 1))) ||
+        (rc0 = stage_arg(ctx, ctx->sv_ext, gx.data(), gx.size() * 8)) || (rc0 = ensure_hsave(ctx, tot)))
+      return rc0;
+    launch_gather(d, (const uint64_t *)ctx->sv_ext.p, m, (uint8_t *)ctx->sv_comp.p, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    if (tot) HIP_TRY(hipMemcpyAsync(ctx->h_save, ctx->sv_comp.p, tot, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    src = staged.data();
+    src = (const uint8_t *)ctx->h_save;
+    src_n = tot;
   }
-  const size_t src_n = host_in ? n : staged.size();
   size_t ecap = 0;
   for (auto &e : sext) ecap += e.length + e.length / 64 + 64;
   std::vector<uint8_t> enc(std::max<size_t>(ecap, 1));

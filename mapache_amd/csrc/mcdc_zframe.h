@@ -17,4 +17,9 @@ void launch_zframe_sizes(const DevChunk *chunks, uint64_t n, uint64_t nbytes, ui
 void launch_zframe_write(const uint8_t *base, const DevChunk *chunks, uint64_t n, const uint64_t *off, uint8_t *out,
                          uint64_t *ext, hipStream_t st);
 
+// Gather: segment i = src[ext[3 i], + ext[3 i + 2]) to dst + ext[3 i + 1]
+// (dst + ext[3 i + 1] congruent to src + ext[3 i] modulo 16: whole 16-byte
+// loads and stores between a byte head and tail).  One workgroup per segment.
+void launch_gather(const uint8_t *src, const uint64_t *ext, uint64_t n, uint8_t *dst, hipStream_t st);
+
 }  // namespace mcdc

@@ -154,4 +154,29 @@ void launch_zframe_write(const uint8_t *base, const DevChunk *chunks, uint64_t n
                        ext);
 }
 
+// One workgroup per segment (grid-stride over segments): the bytes before the
+// first 16-byte boundary of the source and after the last one byte by byte,
+// the middle in aligned 16-byte loads and stores (the destination offset is
+// congruent to the source's modulo 16, launch_gather's contract).
+__global__ __launch_bounds__(256) void k_gather(const uint8_t *__restrict__ src, const uint64_t *__restrict__ ext,
+                                                uint64_t n, uint8_t *__restrict__ dst) {
+  MCDC_VGPR_PAD(16);  // (not an exact fill)
+  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint64_t so = ext[3 * i], dof = ext[3 * i + 1], len = ext[3 * i + 2];
+    const uint64_t head = min<uint64_t>(len, (16 - ((uintptr_t)(src + so) & 15)) & 15), nq = (len - head) / 16,
+                   body = 16 * nq;
+    for (uint64_t k = threadIdx.x; k < head; k += blockDim.x) dst[dof + k] = src[so + k];
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src + so + head);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst + dof + head);
+    for (uint64_t k = threadIdx.x; k < nq; k += blockDim.x) d4[k] = s4[k];
+    for (uint64_t k = head + body + threadIdx.x; k < len; k += blockDim.x) dst[dof + k] = src[so + k];
+  }
+}
+
+void launch_gather(const uint8_t *src, const uint64_t *ext, uint64_t n, uint8_t *dst, hipStream_t st) {
+  if (n == 0) return;
+  const unsigned g = (unsigned)(n < 65536 ? n : 65536);
+  hipLaunchKernelGGL(k_gather, dim3(g), dim3(256), 0, st, src, ext, n, dst);
+}
+
 }  // namespace mcdc
