@@ -265,6 +265,10 @@ struct mcdc_ctx {
   size_t h_fcnt_cap = 0;       // entries
   void *h_save = nullptr;      // pinned staging of the save path's new blobs (host zstd mode, device input)
   size_t h_save_cap = 0;       // bytes
+  void *h_zarena = nullptr;    // pinned: mcdc_encode_blobs' frames back to back (its H2D source)
+  size_t h_zarena_cap = 0;
+  std::unique_ptr<uint8_t[]> h_zbuf;  // mcdc_encode_blobs' per-frame bound regions (kept: no page faults per call)
+  size_t h_zbuf_cap = 0;
   uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
@@ -349,23 +353,26 @@ int ensure_fcnt(mcdc_ctx *ctx, size_t n) {
   return MCDC_OK;
 }
 
-int ensure_hsave(mcdc_ctx *ctx, size_t bytes) {
-  if (ctx->h_save_cap >= bytes) return MCDC_OK;
-  if (ctx->h_save) {
+// A pinned host buffer of the context, grown (never shrunk) and kept.
+int ensure_pinned(mcdc_ctx *ctx, void *&p, size_t &cap, size_t bytes) {
+  if (cap >= bytes) return MCDC_OK;
+  if (p) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipHostFree(ctx->h_save));
-    ctx->h_save = nullptr;
-    ctx->h_save_cap = 0;
+    HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipHostFree(p));
+    p = nullptr;
+    cap = 0;
   }
   const size_t alloc = (bytes + bytes / 8 + 4095) / 4096 * 4096;
-  if (hipHostMalloc(&ctx->h_save, alloc, hipHostMallocDefault) != hipSuccess) {
-    ctx->h_save = nullptr;
+  if (hipHostMalloc(&p, alloc, hipHostMallocDefault) != hipSuccess) {
+    p = nullptr;
     (void)hipGetLastError();
     return fail(MCDC_E_NOMEM, "hipHostMalloc(%zu) failed", alloc);
   }
-  ctx->h_save_cap = alloc;
+  cap = alloc;
   return MCDC_OK;
 }
+int ensure_hsave(mcdc_ctx *ctx, size_t bytes) { return ensure_pinned(ctx, ctx->h_save, ctx->h_save_cap, bytes); }
 
 // Where k_emit can write the caller's output array directly: a device
 // pointer on the context's device (the boundary list stays in HBM for a
@@ -1002,6 +1009,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
   if (ctx->h_save) (void)hipHostFree(ctx->h_save);
+  if (ctx->h_zarena) (void)hipHostFree(ctx->h_zarena);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
@@ -1536,18 +1544,30 @@ int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   const double t0 = now_ms();
   std::vector<uint64_t> off(nblobs), len(nblobs);
   for (size_t i = 0; i < nblobs; ++i) off[i] = blobs[i].offset, len[i] = blobs[i].length;
-  std::vector<std::vector<uint8_t>> comp;
-  const std::string zerr =
-      mcdc::host::zstd_compress_all((const uint8_t *)h_in, off.data(), len.data(), nblobs, zstd_threads(), comp);
+  // every frame into its own bound-sized region of one buffer (no per-blob
+  // allocation or zero fill), then packed back to back
+  const mcdc::host::ZstdApi &za = mcdc::host::zstd_api();
+  if (!za.ok) return fail(MCDC_E_INTERNAL, "%s", za.why.c_str());
+  std::vector<uint64_t> bo(nblobs + 1, 0), clen(nblobs, 0);
+  for (size_t i = 0; i < nblobs; ++i) bo[i + 1] = bo[i] + za.compressBound(len[i]) + 64;
+  if (ctx->h_zbuf_cap < bo[nblobs]) {  // (kept by the context: a fresh multi-GB buffer per call page-faults)
+    const size_t alloc = (size_t)(bo[nblobs] + bo[nblobs] / 8 + 4096);
+    ctx->h_zbuf.reset(new (std::nothrow) uint8_t[alloc]);
+    ctx->h_zbuf_cap = ctx->h_zbuf ? alloc : 0;
+    if (!ctx->h_zbuf) return fail(MCDC_E_NOMEM, "host allocation of %zu bytes failed", alloc);
+  }
+  uint8_t *const cbuf = ctx->h_zbuf.get();
+  const std::string zerr = mcdc::host::zstd_compress_into((const uint8_t *)h_in, off.data(), len.data(), nblobs,
+                                                          zstd_threads(), cbuf, bo.data(), clen.data());
   if (!zerr.empty()) return fail(MCDC_E_INTERNAL, "%s", zerr.c_str());
   std::vector<mcdc_blob> ext(nblobs);
   size_t total = 0;
-  for (size_t i = 0; i < nblobs; ++i) ext[i] = mcdc_blob{total, comp[i].size()}, total += comp[i].size();
-  std::vector<uint8_t> arena(std::max<size_t>(total, 1));
+  for (size_t i = 0; i < nblobs; ++i) ext[i] = mcdc_blob{total, clen[i]}, total += clen[i];
+  if ((rc = ensure_pinned(ctx, ctx->h_zarena, ctx->h_zarena_cap, std::max<size_t>(total, 1)))) return rc;
+  uint8_t *const arena = (uint8_t *)ctx->h_zarena;  // (pinned: the H2D below runs at the DMA rate)
   mcdc::host::parallel_items(nblobs, zstd_threads(), [&](size_t i, int) {
-    if (!comp[i].empty()) std::memcpy(arena.data() + ext[i].offset, comp[i].data(), comp[i].size());
+    if (clen[i]) std::memcpy(arena + ext[i].offset, cbuf + bo[i], clen[i]);
   });
-  comp.clear();
   if (!key) {  // SecureStorage::build(): no key, encrypt() returns the compressed bytes (storage.rs:120-125)
     if (out_offsets) {
       for (size_t i = 0; i < nblobs; ++i) out_offsets[i] = ext[i].offset;
@@ -1555,7 +1575,7 @@ int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
     }
     if (total > out_cap || (total && !h_out))
       return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", out_cap, total);
-    if (total) std::memcpy(h_out, arena.data(), total);
+    if (total) std::memcpy(h_out, arena, total);
     ctx->timing = mcdc_timing{};
     ctx->timing.bytes = n_in;
     ctx->timing.total_ms = now_ms() - t0;
@@ -1563,7 +1583,7 @@ int mcdc_encode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   }
   const size_t cap = total + (size_t)kAeadOverhead * nblobs;
   if ((rc = ensure(ctx, ctx->enc_in, total)) || (rc = ensure(ctx, ctx->enc_out, cap))) return rc;
-  if (total) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, arena.data(), total, hipMemcpyHostToDevice, ctx->stream));
+  if (total) HIP_TRY(hipMemcpyAsync(ctx->enc_in.p, arena, total, hipMemcpyHostToDevice, ctx->stream));
   std::vector<uint64_t> oo(nblobs + 1);
   if ((rc = aead_run(ctx, 0, key, ctx->enc_in.p, total, ext.data(), nblobs, nonces, ctx->enc_out.p, cap, oo.data(),
                      nullptr)))

@@ -105,6 +105,54 @@ void parallel_items(size_t n, int threads, F fn) {
   for (auto &t : pool) t.join();
 }
 
+// compress blob i = in[off[i], + len[i]) into out_base[out_off[i], + its
+// compressBound + 64), its size to out_len[i]; returns "" or an error
+// (one output region per blob, no per-blob allocation)
+inline std::string zstd_compress_into(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
+                                      int threads, uint8_t *out_base, const uint64_t *out_off, uint64_t *out_len) {
+  const ZstdApi &z = zstd_api();
+  if (!z.ok) return z.why;
+  std::vector<void *> cctx((size_t)std::max(1, threads), nullptr);
+  std::mutex emu;
+  std::string err;
+  parallel_items(n, threads, [&](size_t i, int w) {
+    out_len[i] = 0;
+    if (!cctx[w]) {
+      cctx[w] = z.createCCtx();
+      const bool ok = cctx[w] && !z.isError(z.cctxSetParameter(cctx[w], kZstdCLevel, kZstdLevel)) &&
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCWindowLog, kZstdWindowLog)) &&
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCChecksum, 0)) &&
+                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCContentSize, 0));  // (as zstd_compress_all)
+      if (!ok) {
+        std::lock_guard<std::mutex> lk(emu);
+        err = "zstd rejected level 3 / window log 20 / no checksum / no content size";
+        if (cctx[w]) z.freeCCtx(cctx[w]);
+        cctx[w] = nullptr;
+        return;
+      }
+    }
+    ZInBuf ib{in + off[i], (size_t)len[i], 0};
+    ZOutBuf ob{out_base + out_off[i], z.compressBound(len[i]) + 64, 0};
+    size_t r = z.compressStream2(cctx[w], &ob, &ib, kZstdEContinue);
+    if (!z.isError(r)) {
+      do {
+        r = z.compressStream2(cctx[w], &ob, &ib, kZstdEEnd);
+      } while (!z.isError(r) && r != 0 && ob.pos < ob.size);
+    }
+    if (z.isError(r) || r != 0) {  // (the context is mid-frame: drop it)
+      std::lock_guard<std::mutex> lk(emu);
+      err = std::string("zstd compression failed: ") + (z.isError(r) ? z.getErrorName(r) : "output bound");
+      z.freeCCtx(cctx[w]);
+      cctx[w] = nullptr;
+      return;
+    }
+    out_len[i] = ob.pos;
+  });
+  for (void *c : cctx)
+    if (c) z.freeCCtx(c);
+  return err;
+}
+
 // compress blob i = in[off[i], + len[i]) into out[i]; returns "" or an error
 inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
                                      int threads, std::vector<std::vector<uint8_t>> &out) {
