@@ -269,6 +269,8 @@ struct mcdc_ctx {
   size_t h_zarena_cap = 0;
   std::unique_ptr<uint8_t[]> h_zbuf;  // mcdc_encode_blobs' per-frame bound regions (kept: no page faults per call)
   size_t h_zbuf_cap = 0;
+  void *h_encb = nullptr;      // pinned: mcdc_save_files' encoded blobs (host zstd mode)
+  size_t h_encb_cap = 0;
   uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
@@ -1010,6 +1012,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
   if (ctx->h_save) (void)hipHostFree(ctx->h_save);
   if (ctx->h_zarena) (void)hipHostFree(ctx->h_zarena);
+  if (ctx->h_encb) (void)hipHostFree(ctx->h_encb);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
@@ -1878,22 +1881,28 @@ static int save_encode_host(mcdc_ctx *ctx, const mcdc_store *store, const void *
   }
   size_t ecap = 0;
   for (auto &e : sext) ecap += e.length + e.length / 64 + 64;
-  std::vector<uint8_t> enc(std::max<size_t>(ecap, 1));
+  // (the encoded blobs in a buffer the context keeps: a fresh multi-GB vector
+  // per call was zero-filled and page-faulted)
+  auto enc_buf = [&](size_t bytes) -> uint8_t * {  // (pinned: the sealed blobs' D2H runs at the DMA rate)
+    return ensure_pinned(ctx, ctx->h_encb, ctx->h_encb_cap, bytes) == MCDC_OK ? (uint8_t *)ctx->h_encb : nullptr;
+  };
+  uint8_t *enc = enc_buf(std::max<size_t>(ecap, 1));
+  if (!enc) return fail(MCDC_E_NOMEM, "host allocation of %zu bytes failed", ecap);
   std::vector<uint64_t> eo(m + 1, 0);
   int rc = MCDC_OK;
   if (m) {
-    rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), ecap, eo.data());
+    rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc, ecap, eo.data());
     if (rc == MCDC_E_CAPACITY) {
-      enc.resize(std::max<uint64_t>(eo[m], 1));
-      rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc.data(), enc.size(),
-                             eo.data());
+      ecap = std::max<uint64_t>(eo[m], 1);
+      if (!(enc = enc_buf(ecap))) return fail(MCDC_E_NOMEM, "host allocation of %zu bytes failed", ecap);
+      rc = mcdc_encode_blobs(ctx, store->key, src, src_n, sext.data(), m, store->nonces, enc, ecap, eo.data());
     }
     if (rc) return rc;
   }
   std::vector<mcdc_blob> eext(m);
   for (size_t k = 0; k < m; ++k) eext[k] = mcdc_blob{eo[k], eo[k + 1] - eo[k]};
   size_t pb = 0;
-  rc = mcdc_pack_blobs(ctx, store->key, enc.data(), eo[m], eext.data(), sids.data(), types.data(), m,
+  rc = mcdc_pack_blobs(ctx, store->key, enc, eo[m], eext.data(), sids.data(), types.data(), m,
                        store->max_pack_size, store->header_nonces, store->nheader_nonces, store->padding,
                        store->npadding, packs_out, packs_out_cap, &pb, packs, packs_cap, npacks);
   if (packs_bytes) *packs_bytes = pb;
