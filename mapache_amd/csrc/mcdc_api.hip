@@ -1616,7 +1616,6 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   const double t0 = now_ms();
   std::vector<uint64_t> poff(nblobs), plen(nblobs);
   std::vector<int32_t> st(std::max<size_t>(nblobs, 1), 0);
-  std::vector<uint8_t> plain;
   const uint8_t *zin = (const uint8_t *)h_in;
   mcdc_timing tm{};
   if (key) {
@@ -1627,13 +1626,16 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
                   st.data());
     if (rc && rc != MCDC_E_AUTH) return rc;
     tm = ctx->timing;
-    plain.resize(std::max<uint64_t>(oo[nblobs], 1));
+    // (the opened frames into a pinned buffer the context keeps: DMA rate, no
+    // zero fill or page faults per call)
+    if ((rc = ensure_pinned(ctx, ctx->h_zarena, ctx->h_zarena_cap, std::max<uint64_t>(oo[nblobs], 1)))) return rc;
+    uint8_t *const plain = (uint8_t *)ctx->h_zarena;
     if (oo[nblobs]) {
-      HIP_TRY(hipMemcpyAsync(plain.data(), ctx->enc_out.p, oo[nblobs], hipMemcpyDeviceToHost, ctx->stream));
+      HIP_TRY(hipMemcpyAsync(plain, ctx->enc_out.p, oo[nblobs], hipMemcpyDeviceToHost, ctx->stream));
       HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     for (size_t i = 0; i < nblobs; ++i) poff[i] = oo[i], plen[i] = oo[i + 1] - oo[i];
-    zin = plain.data();
+    zin = plain;
   } else {  // SecureStorage::build(): decrypt() is the identity, only decompress (storage.rs:67-69)
     for (size_t i = 0; i < nblobs; ++i) poff[i] = sealed[i].offset, plen[i] = sealed[i].length;
   }
