@@ -1,7 +1,8 @@
 // CPU test of mapache_amd/host/zstd_stage.hpp (the zstd half of
 // SecureStorage::encode / decode, storage.rs:74-94) under plain, ASan+UBSan
 // and TSan builds: many blobs compressed and decompressed on a thread pool,
-// round trips, empty blobs, a corrupt frame and a skipped (failed-tag) blob.
+// round trips, empty blobs, a corrupt frame and a skipped (failed-tag) blob;
+// zstd_compress_into's frames equal zstd_compress_all's.
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -43,6 +44,21 @@ int main(int argc, char **argv) {
   std::string err = mcdc::host::zstd_compress_all(data.data(), off.data(), len.data(), off.size(), threads, comp);
   CHECK(err.empty());
   if (!err.empty()) std::printf("%s\n", err.c_str());
+  // zstd_compress_into (one buffer of bound-sized regions, what
+  // mcdc_encode_blobs uses): the same frames, byte for byte
+  {
+    const mcdc::host::ZstdApi &z = mcdc::host::zstd_api();
+    std::vector<uint64_t> bo(off.size() + 1, 0), cl(off.size(), 0);
+    for (size_t i = 0; i < off.size(); ++i) bo[i + 1] = bo[i] + z.compressBound(len[i]) + 64;
+    std::vector<uint8_t> buf(bo.back());
+    err = mcdc::host::zstd_compress_into(data.data(), off.data(), len.data(), off.size(), threads, buf.data(),
+                                         bo.data(), cl.data());
+    CHECK(err.empty());
+    for (size_t i = 0; i < off.size(); ++i) {
+      CHECK(cl[i] == comp[i].size());
+      if (cl[i] == comp[i].size()) CHECK(std::memcmp(buf.data() + bo[i], comp[i].data(), cl[i]) == 0);
+    }
+  }
   // frames back to back, one of them corrupted, one skipped
   std::vector<uint8_t> packed;
   std::vector<uint64_t> po, pl;
