@@ -24,6 +24,9 @@ p = _lib.params(524288, 1048576, 8388608, 1) if len(sys.argv) > 4 and sys.argv[4
     _lib.params(16384, 65536, 262144, 1)
 ctx_cap = n + (1 << 20)
 ctx = _lib.Context(0, ctx_cap)
+ZC_BATCH = int(os.environ.get("ZC_BATCH", "0"))  # (A/B: the compressor's batch, "zc_batch_blocks")
+if ZC_BATCH:
+    ctx.set_option("zc_batch_blocks", ZC_BATCH)
 res = {}
 n_arg = n
 for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records", "binary", "far")):
@@ -37,6 +40,8 @@ for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text",
             ctx.close()
             ctx_cap = n + (1 << 20)
             ctx = _lib.Context(0, ctx_cap)
+            if ZC_BATCH:
+                ctx.set_option("zc_batch_blocks", ZC_BATCH)
     dp = ctx.device_alloc(n)
     if tree is not None:
         ctx.h2d(dp, tree[0])
