@@ -235,9 +235,10 @@ int mcdc_open_device(struct mcdc_ctx *ctx, const uint8_t key[32], const void *d_
  * (encrypt / decrypt are the identity, :120-125, :146-151) and nonces may be
  * NULL.  Host memory: encode keeps, per context, a buffer of the blobs'
  * zstd bounds and a pinned one of the frames (about 1.1 and 0.4 x the
- * input for text), grown and reused by later calls; mcdc_save_files in
- * host-zstd mode from device input also keeps a pinned copy of the new
- * blobs. */
+ * input for text), grown and reused by later calls (decode reuses the
+ * pinned one for the opened frames); mcdc_save_files in host-zstd mode from
+ * device input also keeps a pinned copy of the new blobs and of their
+ * encoded form.  All are freed by mcdc_ctx_destroy. */
 int mcdc_encode_blobs(struct mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, size_t n_in,
                       const mcdc_blob *blobs, size_t nblobs, const uint8_t *nonces, void *h_out,
                       size_t out_cap, uint64_t *out_offsets);
