@@ -275,8 +275,8 @@ int mcdc_zstd_frames_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, 
  * a chunk outside [0, n) or of 2 GiB or more -> MCDC_E_INVALID.
  * Scratch: device memory of the context, grown on first use and kept (not
  * counted against max_bytes): about 9 bytes per byte of a batch of whole
- * chunks, a batch holding up to 8192 blocks of 32 KiB (2.3 GiB), two batch
- * sets once the input exceeds one (4.5 GiB); a chunk longer than a batch
+ * chunks, a batch holding up to 16384 blocks of 32 KiB (4.5 GiB), two batch
+ * sets once the input exceeds one (9 GiB); a chunk longer than a batch
  * takes a batch of its own size.  mcdc_zstd_compress_scratch reports the
  * exact amount for a chunk list before the call. */
 int mcdc_zstd_compress_device(struct mcdc_ctx *ctx, const void *d_data, size_t n, const mcdc_chunk *chunks,
@@ -452,8 +452,8 @@ int mcdc_device_free(struct mcdc_ctx *ctx, void *d_ptr);
  * second HIP runtime, e.g. torch's, in the libmcdc process). */
 int mcdc_ctx_synchronize(struct mcdc_ctx *ctx);
 /* Per-context settings for tests and tuning (not reference interface):
- *   "zc_batch_blocks"        blocks per GPU compressor batch (default 16384,
- *                            512 MiB; two streams take half each), >= 8
+ *   "zc_batch_blocks"        blocks per GPU compressor batch (default 32768,
+ *                            1 GiB; two streams take half each), >= 8
  *   "zc_two"                 0: compressor batches on one stream
  *   "test_fail_after_index"  1: mcdc_save_files fails after its index add
  *                            (exercises the rollback)

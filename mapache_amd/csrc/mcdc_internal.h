@@ -162,7 +162,7 @@ struct Knobs {
   bool zc_huf = true;      // MCDC_ZC_HUF: Huffman / RLE literals in the GPU zstd compressor
   bool zc_two = true;      // MCDC_ZC_TWO: compressor batches alternate between two streams
   // set by mcdc_ctx_set_option only (no environment variable):
-  uint64_t zc_batch = 16384;           // "zc_batch_blocks": blocks per compressor batch (two streams: half each)
+  uint64_t zc_batch = 32768;           // "zc_batch_blocks": blocks per compressor batch (two streams: half each)
   bool test_fail_after_index = false;  // "test_fail_after_index": mcdc_save_files fails after its index
                                        // add (test hook: the rollback path, tests/test_gpu_save.py)
   // A/B builds only

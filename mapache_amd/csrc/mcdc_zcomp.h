@@ -14,10 +14,6 @@ constexpr uint32_t kZcSeqCap = kZcBlock / 4;       // sequences per block: every
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
 constexpr uint32_t kZcSegBlocks = 8;               // blocks of a chunk one match-finder workgroup covers
 constexpr uint32_t kZcPrime = 65536;               // bytes before a segment the finder re-inserts
-#ifndef MCDC_ZC_BATCH
-#define MCDC_ZC_BATCH 16384  // (compile-time A/B knob)
-#endif
-constexpr uint64_t kZcBatchBlocks = MCDC_ZC_BATCH;  // blocks per batch (512 MiB; more for a longer chunk)
 
 struct ZcBlock {
   uint64_t src;                 // chunk bytes [src, src + len) of the input
@@ -44,9 +40,10 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 // Scratch per batch of nblk blocks (bytes), all device memory of the context:
 //   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot, seqs nblk x kZcSeqCap
 //   x 8, state records nblk x kZcSeqCap x 8, match words (nblk x kZcBlock +
-//   1024) x 4 (9 x the batch's input in all: 4.5 GiB for a full batch),
-//   piece / poff (nblk + 1) x 8.  A batch holds whole chunks, at most
-//   kZcBatchBlocks blocks unless one chunk is longer (1 GiB: 7 x 2^18 words).
+//   1024) x 4 (9 x the batch's input in all: 4.5 GiB for a batch set of
+//   16384 blocks), piece / poff (nblk + 1) x 8.  A batch holds whole chunks,
+//   at most the context's "zc_batch_blocks" (32768: two sets of 16384 on two
+//   streams) unless one chunk is longer (1 GiB: 7 x 2^18 words).
 // one batch: the chunks [c0, c1), blocks [b0, b0 + nblk)
 void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
                      uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
