@@ -386,7 +386,10 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     const uint32_t m5 = mix5(x.x, x.y), m8 = mix8(x.x, x.y);
     const uint32_t hs = m5 >> (32 - kHsLog), hl = m8 >> (32 - kHlLog);
     const uint32_t gs = (m5 >> (32 - kHsLog - 13)) & 0x1FFFu, gl = (m8 >> (32 - kHlLog - 13)) & 0x1FFFu;
-    const uint32_t es = find && vs ? hts[hs] : 0u, el = find && vl ? htl[hl] : 0u;
+    // (both slots read by every lane, the result masked: no exec-mask branch
+    // around the LDS reads; a slot index is always in range)
+    const uint32_t rs = hts[hs], rl = htl[hl];
+    const uint32_t es = find && vs ? rs : 0u, el = find && vl ? rl : 0u;
     verify(S);
     ZC_TICK(1);
     // the candidate: the long key's if its tag matches, else the short key's
