@@ -284,27 +284,27 @@ class Context:
         n = len(arrs)
         ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
         lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
-        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        counts = np.empty(max(n, 1), dtype=np.uint64)  # (every entry written by the call)
         cap = sum(self._bound(a.size, p) for a in arrs) + 1
         out = np.zeros(cap, dtype=CHUNK_DTYPE)
         n_out = ctypes.c_size_t()
         check(load().mcdc_chunk_batch(self._h, ctypes.byref(p), ptrs, lens, n, out.ctypes.data, cap,
                                       counts.ctypes.data, ctypes.byref(n_out)))
-        return out[: n_out.value].copy(), counts[:n].astype(np.int64)
+        return out[: n_out.value].copy(), counts[:n].view(np.int64)  # (counts < 2^63: a view, no copy)
 
     @_locked
     def chunk_batch_device(self, p: McdcParams, d_arena: int, offsets, lens):
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
         ls = np.ascontiguousarray(lens, dtype=np.uint64)
         n = offs.size
-        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        counts = np.empty(max(n, 1), dtype=np.uint64)  # (every entry written by the call)
         cap = int(sum(self._bound(int(x), p) for x in ls)) + 1
         out = np.zeros(cap, dtype=CHUNK_DTYPE)
         n_out = ctypes.c_size_t()
         check(load().mcdc_chunk_batch_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_arena),
                                              offs.ctypes.data, ls.ctypes.data, n, out.ctypes.data, cap,
                                              counts.ctypes.data, ctypes.byref(n_out)))
-        return out[: n_out.value].copy(), counts[:n].astype(np.int64)
+        return out[: n_out.value].copy(), counts[:n].view(np.int64)  # (counts < 2^63: a view, no copy)
 
     @_locked
     def chunk_device_to_device(self, p: McdcParams, d_ptr: int, n: int, d_out: int, cap: int) -> int:
@@ -322,12 +322,12 @@ class Context:
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
         ls = np.ascontiguousarray(lens, dtype=np.uint64)
         n = offs.size
-        counts = np.zeros(max(n, 1), dtype=np.uint64)
+        counts = np.empty(max(n, 1), dtype=np.uint64)  # (every entry written by the call)
         n_out = ctypes.c_size_t()
         check(load().mcdc_chunk_batch_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_arena),
                                              offs.ctypes.data, ls.ctypes.data, n, ctypes.c_void_p(d_out), cap,
                                              counts.ctypes.data, ctypes.byref(n_out)))
-        return n_out.value, counts[:n].astype(np.int64)
+        return n_out.value, counts[:n].view(np.int64)  # (counts < 2^63: a view, no copy)
 
     @_locked
     def chunk_ids(self, d_data: int, n: int, chunks, ids=None) -> np.ndarray:
