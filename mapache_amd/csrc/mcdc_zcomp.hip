@@ -1844,7 +1844,8 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   const uint32_t m_lo = half ? h : 1u, m_hi = half ? (split ? ns : h) : h;
   const uint32_t nsl = m_hi > m_lo ? m_hi - m_lo : 0u;
   const FseCTL &ct = tb[3 * j + k];
-  uint16_t *rec = reinterpret_cast<uint16_t *>(recs + (act ? b : 0) * kZcSeqCap);
+  // type k's state records, one 16-bit word per sequence (sequence order)
+  uint16_t *rec = reinterpret_cast<uint16_t *>(recs + (act ? b : 0) * kZcSeqCap) + k * kZcSeqCap;
   const uint8_t *cd = seq_codes(words, act ? b : 0, k);  // codes in walking order: cd[m] = sequence ns - 1 - m
   const uint8_t *cdl = cd + m_lo;
   // 16 sequences per batch: codes of batch t in a register quad, of batch
@@ -1865,7 +1866,7 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   if (ns && (half == 0 || split)) {
     state = init_state(cd[half ? h - 1 : 0]);
     guess = state;
-    if (half == 0) rec[4 * (ns - 1) + k] = 0;  // the last sequence: the initial state (no bits)
+    if (half == 0) rec[ns - 1] = 0;  // the last sequence: the initial state (no bits)
   }
   // one batch: the codes in cq (waited for), the next batch's requested into
   // nq; the loop alternates two register quads, so that no register with a
@@ -1892,9 +1893,17 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
       sbits += in ? nb : 0u;
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(nq)::"memory");
+    if (m0 + 16 <= (int32_t)nsl) {  // a whole batch: its 16 records are 32 contiguous bytes (r[15] first)
+      const u32x4 v0 = {r[15] | r[14] << 16, r[13] | r[12] << 16, r[11] | r[10] << 16, r[9] | r[8] << 16};
+      const u32x4 v1 = {r[7] | r[6] << 16, r[5] | r[4] << 16, r[3] | r[2] << 16, r[1] | r[0] << 16};
+      uint16_t *d = rec + (ns - 1 - (m_lo + (uint32_t)m0 + 15));  // (2-byte aligned: gfx950 stores a
+      asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(d), "v"(v0) : "memory");  // misaligned
+      asm volatile("global_store_dwordx4 %0, %1, off offset:16" ::"v"(d), "v"(v1) : "memory");  // quad as is)
+    } else {
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (m0 + u < (int32_t)nsl) rec[4 * (ns - 1 - (m_lo + (uint32_t)(m0 + u))) + k] = (uint16_t)r[u];
+      for (int u = 0; u < 16; ++u)
+        if (m0 + u < (int32_t)nsl) rec[ns - 1 - (m_lo + (uint32_t)(m0 + u))] = (uint16_t)r[u];
+    }
   };
   u32x4 qa = issue(0), qb;
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa)::"memory");
@@ -1914,7 +1923,7 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
       for (int u = 0; u < 16 && m < ns && st != sg; ++u, ++m) {
         const uint32_t c = (q[u >> 2] >> (8 * (u & 3))) & 63u, dn = ct.dnb[c], df = (uint32_t)ct.dfs[c];
         const uint32_t nt = (st + dn) >> 16, ng = (sg + dn) >> 16;
-        rec[4 * (ns - 1 - m) + k] = (uint16_t)(nt | (st & ((1u << nt) - 1u)) << 4);
+        rec[ns - 1 - m] = (uint16_t)(nt | (st & ((1u << nt) - 1u)) << 4);
         sbits += nt - ng;
         st = ct.state[((st >> nt) + df) & 511u];
         sg = ct.state[((sg >> ng) + df) & 511u];
@@ -1957,7 +1966,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   const uint64_t *sq = seqs + bi * kZcSeqCap;
-  const uint16_t *rec = reinterpret_cast<const uint16_t *>(recs + bi * kZcSeqCap);
+  const uint16_t *rec = reinterpret_cast<const uint16_t *>(recs + bi * kZcSeqCap);  // LL, OF, ML records
   uint8_t *st = stage + bi * kZcSlot;
   uint32_t csize = 0;
   if (ns || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
@@ -2011,16 +2020,18 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
           wi += nwords;
         };
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-        auto issue = [&](int32_t b1, u32x2 &q, u32x2 &r) {
+        auto issue = [&](int32_t b1, u32x2 &q, uint32_t &r0, uint32_t &r1, uint32_t &r2) {
           const int32_t i = b1 - 1 - (int32_t)lane, ic = i >= 0 ? i : 0;
           asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(q) : "v"(sq + ic) : "memory");
-          asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(rec + 4 * ic) : "memory");
+          asm volatile("global_load_ushort %0, %1, off" : "=v"(r0) : "v"(rec + ic) : "memory");
+          asm volatile("global_load_ushort %0, %1, off" : "=v"(r1) : "v"(rec + kZcSeqCap + ic) : "memory");
+          asm volatile("global_load_ushort %0, %1, off" : "=v"(r2) : "v"(rec + 2 * kZcSeqCap + ic) : "memory");
         };
-        auto batch = [&](int32_t b1, u32x2 &qv, u32x2 &rv) {
+        auto batch = [&](int32_t b1, u32x2 &qv, uint32_t &r0, uint32_t &r1, uint32_t &r2) {
           const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
           const int32_t i = b1 - 1 - (int32_t)lane;  // lane 0 the batch's last sequence (written first)
-          const uint64_t q = (uint64_t)qv.y << 32 | qv.x, rr = (uint64_t)rv.y << 32 | rv.x;
-          issue(b1 - 64, qv, rv);  // the next batch's, waited for at this one's end
+          const uint64_t q = (uint64_t)qv.y << 32 | qv.x, rr = (uint64_t)r2 << 32 | r1 << 16 | r0;
+          issue(b1 - 64, qv, r0, r1, r2);  // the next batch's, waited for at this one's end
           uint64_t lo = 0, hi = 0;
           uint32_t nb = 0;
           if (i >= b0) {
@@ -2048,12 +2059,13 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
           if (nb) or_bits(wb, cb + incl - nb, lo, hi, nb);
           cb += (uint32_t)lane63((int32_t)incl);
           if (cb >= 512 * 32) flush(false);
-          asm volatile("s_waitcnt vmcnt(0)" : "+v"(qv), "+v"(rv)::"memory");
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(qv), "+v"(r0), "+v"(r1), "+v"(r2)::"memory");
         };
-        u32x2 qa, ra;
-        issue((int32_t)ns, qa, ra);
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa), "+v"(ra)::"memory");
-        for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) batch(b1, qa, ra);
+        u32x2 qa;
+        uint32_t ra0, ra1, ra2;
+        issue((int32_t)ns, qa, ra0, ra1, ra2);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qa), "+v"(ra0), "+v"(ra1), "+v"(ra2)::"memory");
+        for (int32_t b1 = (int32_t)ns; b1 > 0; b1 -= 64) batch(b1, qa, ra0, ra1, ra2);
         // final states (ML, OF, LL: log bits each), the end mark, the last words
         const uint32_t f0 = tab->fin[0], f1 = tab->fin[1], f2 = tab->fin[2];  // final states of LL, OF, ML
         {
