@@ -1618,7 +1618,8 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
 //   k_zc_chain   ONE LANE PER STATE MACHINE, 9 blocks x 3 types per wave:
 //                the wave's 27 tables in LDS, each lane walks its block's
 //                sequences from the last to the first, per sequence the state
-//                bits (count | value << 4, 16 bits) to scratch, then the final
+//                bits (count | value << 4, 16 bits; one array per symbol type,
+//                a batch of 16 stored as 32 contiguous bytes), then the final
 //                state; codes prefetched 8 sequences ahead
 //   k_zc_encode  ONE WAVE PER BLOCK: per sequence its bits (state bits + extra
 //                bits), 64 sequences at a time OR-ed into an LDS buffer at
@@ -1966,7 +1967,8 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   const uint64_t *sq = seqs + bi * kZcSeqCap;
-  const uint16_t *rec = reinterpret_cast<const uint16_t *>(recs + bi * kZcSeqCap);  // LL, OF, ML records
+  // the state records: three arrays of kZcSeqCap 16-bit words (LL, OF, ML), by sequence
+  const uint16_t *rec = reinterpret_cast<const uint16_t *>(recs + bi * kZcSeqCap);
   uint8_t *st = stage + bi * kZcSlot;
   uint32_t csize = 0;
   if (ns || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
