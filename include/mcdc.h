@@ -455,6 +455,9 @@ int mcdc_ctx_synchronize(struct mcdc_ctx *ctx);
  *   "zc_batch_blocks"        blocks per GPU compressor batch (default 32768,
  *                            1 GiB; two streams take half each), >= 8
  *   "zc_two"                 0: compressor batches on one stream
+ *   "zc_small"               0: chunks of one block (<= 32 KiB) through the
+ *                            long chunks' probe and match finder instead of
+ *                            the small-chunk kernel (A/B and tests)
  *   "test_fail_after_index"  1: mcdc_save_files fails after its index add
  *                            (exercises the rollback)
  * Unknown name -> MCDC_E_INVALID. */

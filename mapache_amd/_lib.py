@@ -646,7 +646,7 @@ class Context:
 
     @_locked
     def set_option(self, name: str, value: int) -> None:
-        """mcdc_ctx_set_option: "zc_batch_blocks", "zc_two",
+        """mcdc_ctx_set_option: "zc_batch_blocks", "zc_two", "zc_small",
         "test_fail_after_index" (test and tuning settings of this context)."""
         check(load().mcdc_ctx_set_option(self._h, name.encode(), int(value)))
 

@@ -236,7 +236,7 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs,
+      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs,
       zc_blocks2, zc_stage2, zc_seqs2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_recs2;  // (the second batch set)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
@@ -277,6 +277,13 @@ struct mcdc_ctx {
 
 namespace {
 
+// The bytes ensure() allocates for a request (headroom against regrowth):
+// mcdc_zstd_compress_scratch reports the same.
+size_t ensure_bytes(size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  return (bytes + bytes / 8 + 255) / 256 * 256;
+}
+
 int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return MCDC_OK;
@@ -287,7 +294,7 @@ int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
     b.p = nullptr;
     b.cap = 0;
   }
-  size_t alloc = (bytes + bytes / 8 + 255) / 256 * 256;  // headroom against regrowth
+  const size_t alloc = ensure_bytes(bytes);
   if (hipMalloc(&b.p, alloc) != hipSuccess) {
     b.p = nullptr;
     (void)hipGetLastError();
@@ -1023,7 +1030,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
+                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_cls, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_recs,
                     &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_seqs2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
                     &ctx->zc_words2, &ctx->zc_recs2};
@@ -1078,6 +1085,10 @@ int mcdc_chunk_batch_device(mcdc_ctx *ctx, const mcdc_params *params, const void
   if (nbufs && (!d_arena || !offsets || !lens)) return fail(MCDC_E_INVALID, "NULL argument");
   const double t0 = now_ms();
   ctx->call_t0 = t0;
+  struct ClearT0 {  // (every exit, failures included: a later call never reads a stale start)
+    mcdc_ctx *c;
+    ~ClearT0() { c->call_t0 = 0; }
+  } clear_t0{ctx};
   const uintptr_t addr = (uintptr_t)d_arena;
   const uint8_t *base = (const uint8_t *)(addr & ~(uintptr_t)15);
   const uint64_t delta = addr & 15;
@@ -1290,6 +1301,8 @@ int mcdc_ctx_set_option(mcdc_ctx *ctx, const char *name, long long value) {
     ctx->knobs.zc_batch = (uint64_t)value;
   } else if (n == "zc_two") {
     ctx->knobs.zc_two = value != 0;
+  } else if (n == "zc_small") {
+    ctx->knobs.zc_small = value != 0;
   } else if (n == "test_fail_after_index") {
     ctx->knobs.test_fail_after_index = value != 0;
   } else {
@@ -2042,20 +2055,23 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   size_t tmpb = zc_tmp_bytes(nchunks);
   if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, nchunks * sizeof(mcdc_chunk))) ||
       (rc = ensure(ctx, ctx->zc_cnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->zc_first, (nchunks + 1) * 8)) ||
-      (rc = ensure(ctx, ctx->zc_misc, 64)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)))
+      (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)) ||
+      (rc = ensure(ctx, ctx->zc_cls, nchunks + 1)))
     return rc;
-  uint64_t *misc = (uint64_t *)ctx->zc_misc.p;  // [0] err, [1] raw bound, [2] output base, [4 + 2 k] set k's counts
+  uint64_t *misc = (uint64_t *)ctx->zc_misc.p;  // [0] err, [1] raw bound, [2] output base
   HIP_TRY(hipMemsetAsync(misc, 0, 32, st));
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
   const DevChunk *dch = (const DevChunk *)ctx->b3_chunks.p;
   uint64_t *first = (uint64_t *)ctx->zc_first.p;
-  launch_zc_nblocks(dch, nchunks, n, (uint64_t *)ctx->zc_cnt.p, first, (uint32_t *)misc, misc + 1, ctx->zc_tmp.p,
-                    tmpb, st);
+  launch_zc_nblocks(dch, nchunks, n, (uint64_t *)ctx->zc_cnt.p, first, (uint32_t *)misc, misc + 1,
+                    (uint8_t *)ctx->zc_cls.p, ctx->zc_tmp.p, tmpb, st);
   HIP_TRY(hipGetLastError());
   std::vector<uint64_t> hfirst(nchunks + 1);
+  std::vector<uint8_t> hcls(nchunks);  // (the k_zc_small class of each chunk: the list may be device memory)
   uint64_t hm[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(hm, misc, 16, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hfirst.data(), first, (nchunks + 1) * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hcls.data(), ctx->zc_cls.p, nchunks, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (hm[0]) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer or is 2 GiB or longer", n);
   if (out_bytes) *out_bytes = hm[1];  // the capacity that always suffices (raw frames of 32 KiB blocks)
@@ -2092,8 +2108,8 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
         (rc = ensure(ctx, *z.words, (mb * kZcBlock + 1024) * 4)) || (rc = ensure(ctx, *z.recs, mb * kZcSeqCap * 8)))
       return rc;
   }
-  // [0] setup done on st; [1 + k] set k's last final copy; [3 + k] set k's counts copied to the host
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  // [0] setup done on st; [1 + k] set k's last final copy
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   auto destroy = [&]() {
     for (auto &e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -2110,18 +2126,19 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   }
   int k = 0, prev = -1;  // set of the batch, set of the batch before
   for (uint64_t c0 = 0; c0 < nchunks; k ^= two ? 1 : 0) {  // batches of whole chunks, <= mb blocks each
-    uint64_t c1 = c0 + 1, nseg = (hfirst[c0 + 1] - hfirst[c0] + kZcSegBlocks - 1) / kZcSegBlocks;
-    while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb) {
-      nseg += (hfirst[c1 + 1] - hfirst[c1] + kZcSegBlocks - 1) / kZcSegBlocks;
+    uint64_t c1 = c0, nseg = 0, nsmall[4] = {0, 0, 0, 0};  // (chunks of one block per k_zc_small class)
+    do {
+      const uint64_t nbk = hfirst[c1 + 1] - hfirst[c1];
+      nseg += (nbk + kZcSegBlocks - 1) / kZcSegBlocks;
+      if (hcls[c1] < 4) ++nsmall[hcls[c1]];
       ++c1;
-    }
+    } while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb);
     const Set &z = sets[k];
     launch_zc_batch((const uint8_t *)d_data, n, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
                     (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
                     (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
                     ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
-                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks, nseg, misc + 4 + 2 * k, ctx->h_res + 8 + 2 * k,
-                    ev[3 + k]);
+                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks, nseg, ctx->knobs.zc_small ? nsmall : nullptr);
     if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
     prev = k;
     c0 = c1;
@@ -2146,7 +2163,9 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
 }
 
 int mcdc_zstd_compress_scratch(mcdc_ctx *ctx, const mcdc_chunk *chunks, size_t nchunks, size_t *bytes) {
-  if (!ctx || !bytes || (nchunks && !chunks)) return fail(MCDC_E_INVALID, "NULL argument");
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!bytes || (nchunks && !chunks)) return fail(MCDC_E_INVALID, "NULL argument");
   if (is_device_ptr(chunks)) return fail(MCDC_E_INVALID, "chunks must be host memory");
   *bytes = 0;
   if (nchunks == 0) return MCDC_OK;
@@ -2160,10 +2179,15 @@ int mcdc_zstd_compress_scratch(mcdc_ctx *ctx, const mcdc_chunk *chunks, size_t n
   const uint64_t zb = ctx->knobs.zc_batch;
   const bool two = ctx->knobs.zc_two && total_blocks > zb / 2 && longest <= zb / 2;
   const uint64_t mb = two ? zb / 2 : std::max(std::min<uint64_t>(total_blocks, zb), longest);
+  // (every buffer as ensure() allocates it, headroom included; the call's
+  // own buffers as mcdc_zstd_compress_device requests them)
   const uint64_t tmpb = std::max(zc_tmp_bytes(nchunks), zc_tmp_bytes(mb));
-  const uint64_t set = tmpb + mb * sizeof(ZcBlock) + mb * kZcSlot + 2 * mb * kZcSeqCap * 8 + 2 * (mb + 1) * 8 +
-                       (mb * kZcBlock + 1024) * 4;
-  const uint64_t call = nchunks * sizeof(mcdc_chunk) + 2 * (nchunks + 1) * 8 + 32 + nchunks * 16;
+  const uint64_t set = ensure_bytes(tmpb) + ensure_bytes(mb * sizeof(ZcBlock)) + ensure_bytes(mb * kZcSlot) +
+                       2 * ensure_bytes(mb * kZcSeqCap * 8) + 2 * ensure_bytes((mb + 1) * 8) +
+                       ensure_bytes((mb * kZcBlock + 1024) * 4);
+  const uint64_t call = ensure_bytes(nchunks * sizeof(mcdc_chunk)) + 2 * ensure_bytes((nchunks + 1) * 8) +
+                        ensure_bytes(nchunks + 1) +
+                        ensure_bytes(32) + ensure_bytes(nchunks * 16);
   *bytes = (size_t)(set * (two ? 2 : 1) + call);
   return MCDC_OK;
 }

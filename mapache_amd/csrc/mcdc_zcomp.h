@@ -34,9 +34,10 @@ constexpr uint32_t kZcFarBallots = (uint32_t)(kZcBlock / 1024);
 size_t zc_tmp_bytes(uint64_t n);
 // cnt[i] = blocks of chunk i (n + 1 entries), first = exclusive prefix; chunks
 // outside [0, nbytes) or of 2 GiB or more set *err; bound[0] += sum of the raw
-// frame sizes (the output capacity that always suffices).
+// frame sizes (the output capacity that always suffices); cls[i] = the
+// k_zc_small class of a chunk of one block (zc_small_class), 4 for longer.
 void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint64_t *first,
-                       uint32_t *err, uint64_t *bound, void *tmp, size_t tmp_bytes, hipStream_t st);
+                       uint32_t *err, uint64_t *bound, uint8_t *cls, void *tmp, size_t tmp_bytes, hipStream_t st);
 // Scratch per batch of nblk blocks (bytes), all device memory of the context:
 //   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot, seqs nblk x kZcSeqCap
 //   x 8, state records nblk x kZcSeqCap x 8, match words (nblk x kZcBlock +
@@ -51,17 +52,24 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true,
                      hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr, bool far = true,
-                     uint64_t nseg = 0, uint64_t *d_cnt = nullptr, uint64_t *h_cnt = nullptr,
-                     hipEvent_t ev_cnt = nullptr);
+                     uint64_t nseg = 0, const uint64_t *nsmall = nullptr);
+// Chunks of one block (<= 32 KiB) are probed and matched by k_zc_small, one
+// workgroup per chunk with the chunk's bytes and its tables in LDS, in four
+// size classes: chunks of up to kZcSmallClass[k] bytes and more than
+// kZcSmallClass[k + 1] (k = 0 the longest).  nsmall[k]: the batch's chunks
+// of class k (the host counts them from the chunk lengths).
+constexpr uint32_t kZcSmallClass[5] = {32768, 16384, 8192, 4096, 0};
+__host__ __device__ inline int zc_small_class(uint64_t len) {
+  return len > 16384 ? 0 : len > 8192 ? 1 : len > 4096 ? 2 : 3;
+}
 // (final_after: the output offsets' previous update, on another stream, is
 // waited for before this batch's final copy; final_done: recorded after it;
 // far: some chunk is longer than one finder segment, k_zc_far runs; nseg:
 // the batch's finder segments, sum of ceil(blocks / kZcSegBlocks) over its
-// chunks -- the probe's grid; 0 = one workgroup per block.  d_cnt (device,
-// 2 words), h_cnt (pinned host, 2 words), ev_cnt: after the probe the
-// segments and blocks with work are moved to the front of the orders and
-// counted, the host waits for the two counts and sizes the finder's and the
-// parse's grids by them (a batch of hopeless blocks launches neither); all
-// null = the full grids)
+// chunks -- the probe's and the finder's grids; 0 = one workgroup per block.
+// nsmall: the batch's chunks of one block per k_zc_small class
+// (kZcSmallClass), or null = every chunk through k_zc_probe and k_zc_find.
+// Nothing is read back: segments and blocks found hopeless return at once in
+// every later kernel, so the host never waits inside a batch)
 
 }  // namespace mcdc

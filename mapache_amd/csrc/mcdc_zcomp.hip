@@ -94,8 +94,10 @@ constexpr uint32_t kHsLog = MCDC_ZC_HS, kHlLog = MCDC_ZC_HL;
 #ifndef MCDC_ZC_FT
 #define MCDC_ZC_FT 1024  // (compile-time A/B knob)
 #endif
+#ifndef MCDC_ZC_DEPTH
+#define MCDC_ZC_DEPTH 2  // (compile-time A/B knob: tiles of loads in flight in k_zc_find; 4 measured no faster)
+#endif
 constexpr uint32_t kFindThreads = MCDC_ZC_FT;  // threads per workgroup (16 waves)
-constexpr uint32_t kFindTile = kFindThreads;  // positions per step
 constexpr uint32_t kMlCap = 16;               // match bytes verified per candidate (longer: k_zc_parse extends)
 constexpr uint32_t kPrime = kZcPrime;         // bytes before a segment re-inserted (farther: k_zc_far)
 // Match words: length (<= kMlCap) << 24 | offset; bit 31 marks a verified
@@ -131,8 +133,22 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Within one wave LDS operations complete in issue order: a wave-sized tile
+// only has to keep the compiler from moving its table reads and inserts across
+// each other.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+template <uint32_t NT>
+__device__ __forceinline__ void tile_sync() {
+  if constexpr (NT > 64) lds_sync();
+  else wave_lds_order();
+}
+
 __global__ void k_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint32_t *err,
-                             uint64_t *bound) {
+                             uint64_t *bound, uint8_t *cls) {
   MCDC_VGPR_PAD(12);  // (not an exact fill)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t raw = 0;
@@ -142,6 +158,7 @@ __global__ void k_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes
     if (!ok) atomicOr(err, 1u);
     const uint64_t nb = c.length ? (c.length + kZcBlock - 1) / kZcBlock : 1;
     cnt[i] = nb;
+    cls[i] = nb == 1 ? (uint8_t)zc_small_class(c.length) : (uint8_t)4;
     raw = kFrameHdr + kBlockHdr * nb + c.length;
   } else if (i == n) {
     cnt[i] = 0;
@@ -169,6 +186,18 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
   }
 }
 
+// A finder segment's cost in 4 KiB steps (its blocks plus the re-inserted
+// bytes), with the chunks of one block (<= 32 KiB, no re-inserted bytes) at
+// (len - 1) / 4096 = 0 .. 7 and every other segment at 8 or more, so that a
+// descending sort puts the small chunks (k_zc_small) after the others, their
+// size classes (kZcSmallClass) in contiguous ranges.
+__device__ __forceinline__ uint32_t seg_cost(const ZcBlock *blocks, const ZcBlock &B, uint64_t r) {
+  if (B.nb == 1) return B.len ? (B.len - 1) / 4096 : 0u;
+  const uint32_t nsb = min<uint32_t>(kZcSegBlocks, B.nb - B.b);
+  const uint32_t bytes = (nsb - 1) * kZcBlock + blocks[r + nsb - 1].len + (B.b ? kPrime : 0u);
+  return max(bytes / 4096, 8u);
+}
+
 // The finder's segments by cost, longest first: a segment's blocks (<=
 // kZcSegBlocks) plus, after a chunk's first segment, the kPrime bytes it
 // re-inserts, by 4 KiB; order[i] = the record starting the i-th
@@ -187,9 +216,7 @@ __global__ __launch_bounds__(1024) void k_zc_segorder(const ZcBlock *blocks, uin
   if (tid < kPKeys) pcnt[tid] = 0;
   __syncthreads();
   auto key = [&](const ZcBlock &B, uint64_t r) {  // (descending cost by 4 KiB: bucket 0 = the costliest)
-    const uint32_t nsb = min<uint32_t>(kZcSegBlocks, B.nb - B.b);
-    const uint32_t bytes = (nsb - 1) * kZcBlock + blocks[r + nsb - 1].len + (B.b ? kPrime : 0u);
-    return kKeys - 1 - min(kKeys - 1, bytes / 4096);
+    return kKeys - 1 - min(kKeys - 1, seg_cost(blocks, B, r));
   };
   auto pkey = [&](const ZcBlock &B) { return kPKeys - 1 - min<uint32_t>(kPKeys - 1, B.len / 4096); };
   for (uint64_t r = tid; r < nblk; r += 1024) {
@@ -277,7 +304,7 @@ __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
   return min(min(min(b0, b1), min(b2, b3)), 128u) >> 3;
 }
 
-// The match finder: one workgroup of kFindThreads threads per segment (up to
+// The match finder: one workgroup of NT threads per segment (up to
 // kZcSegBlocks blocks of one chunk, the first record of the segment's blocks:
 // other workgroups return).  Writes words[(block - batch start) * kZcBlock +
 // position in block] for every position of the segment: match length (<=
@@ -294,10 +321,14 @@ __device__ __forceinline__ uint32_t prefix16(uint4 x, uint4 y) {
 // Workgroups take the segments longest first (order[], k_zc_segorder): one
 // workgroup fills a CU (its tables are the whole LDS), and a segment of 8
 // blocks that started last would run on alone at the end of the launch.
-__global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, uint64_t nbytes,
-                                                          const ZcBlock *blocks, uint64_t nblk, uint32_t *words,
-                                                          const uint32_t *order) {
-  __shared__ __attribute__((aligned(16))) uint32_t hts[1u << kHsLog], htl[1u << kHlLog];
+template <uint32_t NT, uint32_t HS, uint32_t HL>
+__global__ __launch_bounds__(NT) void k_zc_find_t(const uint8_t *base, uint64_t nbytes, const ZcBlock *blocks,
+                                                  uint64_t nblk, uint32_t *words, const uint32_t *order) {
+  static_assert(NT % 64 == 0 && HS + 13 <= 32 && HL + 13 <= 32, "tile and tables");
+  constexpr uint32_t kFindTile = NT;  // positions per step
+  constexpr uint32_t kDepth = MCDC_ZC_DEPTH;  // tiles of loads in flight (2 or 4)
+  static_assert(kDepth == 2 || kDepth == 4, "finder pipeline depth");
+  __shared__ __attribute__((aligned(16))) uint32_t hts[1u << HS], htl[1u << HL];
   const uint64_t bi0 = order[blockIdx.x];
   if (bi0 >= nblk) return;
   const ZcBlock B0 = blocks[bi0];
@@ -324,11 +355,11 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     if (all_raw) return;
   }
   if (clen < 16 || cbytes < 16) {  // (too short to match: every position a literal)
-    for (uint32_t p = seg0 + tid; p < seg1; p += kFindThreads) wseg[p] = 0u;
+    for (uint32_t p = seg0 + tid; p < seg1; p += NT) wseg[p] = 0u;
     return;
   }
-  for (uint32_t k = tid; k < (1u << kHsLog) / 4; k += kFindThreads) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
-  for (uint32_t k = tid; k < (1u << kHlLog) / 4; k += kFindThreads) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = tid; k < (1u << HS) / 4; k += NT) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = tid; k < (1u << HL) / 4; k += NT) reinterpret_cast<uint4 *>(htl)[k] = make_uint4(0, 0, 0, 0);
   // 16-byte loads at chunk offsets clamped to the last 16 readable bytes; a
   // tile within 16 bytes of the end realigns them (fix16), others use them as loaded
   const uint32_t last16 = (uint32_t)min<uint64_t>(cbytes - 16, 0xFFFFFFF0ull);
@@ -344,9 +375,17 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     uint4 x;
     u32x4 y;
   };
-  Stage s0{}, s1{};  // tiles t - 2 (verified now) and t - 1
+  // (kDepth tiles in flight: stage k holds tile t - kDepth + k; a tile's own
+  // bytes are requested kDepth tiles ahead, its candidate's verified kDepth
+  // tiles later)
+  Stage s0{}, s1{}, s2{}, s3{};
   u32x4 n0 = ald16s(cb, min(prime0 + tid, last16)), n1 = ald16s(cb, min(prime0 + kFindTile + tid, last16));
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1)::"memory");
+  u32x4 n2 = {0, 0, 0, 0}, n3 = {0, 0, 0, 0};  // (unused at depth 2; never a copy of a pending load)
+  if constexpr (kDepth == 4) {
+    n2 = ald16s(cb, min(prime0 + 2 * kFindTile + tid, last16));
+    n3 = ald16s(cb, min(prime0 + 3 * kFindTile + tid, last16));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3)::"memory");
   auto verify = [&](const Stage &S) {
     const uint32_t bend = min(clen, (S.p / (uint32_t)kZcBlock + 1) * (uint32_t)kZcBlock);
     const uint32_t lim = S.p < bend ? min(kMlCap, bend - S.p) : 0u;
@@ -365,17 +404,18 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
 #else
 #define ZC_TICK(k) ((void)0)
 #endif
-  // one tile; n: its own bytes on entry, the bytes of the tile two ahead on
-  // exit; S: the tile two back on entry (verified here), this tile on exit.
-  // The loop below alternates two (n, S) sets, so no register with a pending
-  // load is ever copied.  Per step the memory operations are: the verified
-  // word's store (or none), then the loads y (every lane: a lane without a
-  // candidate reads its own position, so the count is fixed) and n; a
-  // step's loads are used two steps later, after the 2 loads of the step
-  // between.
+  // one tile; n: its own bytes on entry, the bytes of the tile kDepth ahead
+  // on exit; S: the tile kDepth back on entry (verified here), this tile on
+  // exit.  The loop below rotates kDepth (n, S) sets, so no register with a
+  // pending load is ever copied.  Per step the memory operations are: the
+  // verified word's store (or none), then the loads y (every lane: a lane
+  // without a candidate reads its own position, so the count is fixed) and
+  // n; a step's loads are used kDepth steps later, after the 2 (kDepth - 1)
+  // loads of the steps between (a pending store only makes the wait longer).
   auto step = [&](uint32_t t0, u32x4 &n, Stage &S) {
     ZC_TICK(4);
-    asm volatile("s_waitcnt vmcnt(2)" : "+v"(n), "+v"(S.y)::"memory");
+    if constexpr (kDepth == 4) asm volatile("s_waitcnt vmcnt(6)" : "+v"(n), "+v"(S.y)::"memory");
+    else asm volatile("s_waitcnt vmcnt(2)" : "+v"(n), "+v"(S.y)::"memory");
     ZC_TICK(0);
     const uint32_t p = t0 + tid;
     const bool tail = t0 >= tail0;
@@ -384,8 +424,8 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     const bool find = t0 >= seg0 && p < seg1;  // (prime tiles only insert; tiles past the segment: nothing kept)
     const bool vs = p + 5 <= clen, vl = p + 8 <= clen;
     const uint32_t m5 = mix5(x.x, x.y), m8 = mix8(x.x, x.y);
-    const uint32_t hs = m5 >> (32 - kHsLog), hl = m8 >> (32 - kHlLog);
-    const uint32_t gs = (m5 >> (32 - kHsLog - 13)) & 0x1FFFu, gl = (m8 >> (32 - kHlLog - 13)) & 0x1FFFu;
+    const uint32_t hs = m5 >> (32 - HS), hl = m8 >> (32 - HL);
+    const uint32_t gs = (m5 >> (32 - HS - 13)) & 0x1FFFu, gl = (m8 >> (32 - HL - 13)) & 0x1FFFu;
     // (both slots read by every lane, the result masked: no exec-mask branch
     // around the LDS reads; a slot index is always in range)
     const uint32_t rs = hts[hs], rl = htl[hl];
@@ -416,10 +456,10 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
 #else
     S.y = ald16s(cb, min(q, last16));
 #endif
-    n = ald16s(cb, min(p + 2 * kFindTile, last16));
+    n = ald16s(cb, min(p + kDepth * kFindTile, last16));
     const uint32_t r = (p - prime0 + 1) << 13;
 #ifndef MCDC_ZC_NOBAR  // (A/B timing only: no barriers, racy lookups)
-    lds_sync();  // every lookup of the tile before any insert
+    tile_sync<NT>();  // every lookup of the tile before any insert
 #endif
     ZC_TICK(2);
 #ifndef MCDC_ZC_NOINS  // (A/B timing only: no inserts, no candidates)
@@ -427,23 +467,33 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
     if (vl) atomicMax(htl + hl, r | gl);
 #endif
 #ifndef MCDC_ZC_NOBAR
-    lds_sync();  // every insert before the next tile's lookups
+    tile_sync<NT>();  // every insert before the next tile's lookups
 #endif
     ZC_TICK(3);
 #ifdef MCDC_ZC_TIMING
     ++nsteps;
 #endif
   };
-  __syncthreads();
+  if constexpr (NT > 64) __syncthreads();
+  else wave_lds_order();  // (the cleared tables before the first lookups)
   // (both steps unconditional: a tile past the segment keeps nothing, and a
   // join after a conditional step would cost the compiler's own waits)
-  for (uint32_t t0 = prime0; t0 < seg1; t0 += 2 * kFindTile) {
+  for (uint32_t t0 = prime0; t0 < seg1; t0 += kDepth * kFindTile) {
     step(t0, n0, s0);
     step(t0 + kFindTile, n1, s1);
+    if constexpr (kDepth == 4) {
+      step(t0 + 2 * kFindTile, n2, s2);
+      step(t0 + 3 * kFindTile, n3, s3);
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(s0.y), "+v"(s1.y)::"memory");
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3), "+v"(s0.y), "+v"(s1.y), "+v"(s2.y),
+               "+v"(s3.y)::"memory");
   verify(s0);
   verify(s1);
+  if constexpr (kDepth == 4) {
+    verify(s2);
+    verify(s3);
+  }
 #ifdef MCDC_ZC_TIMING
   if (tid == 0 && bi0 % 509 == 0)
     printf("ZCT wg %lu steps %u wait %lu calc %lu bar1 %lu bar2 %lu loop %lu\n", (unsigned long)bi0, nsteps,
@@ -452,6 +502,9 @@ __global__ __launch_bounds__(kFindThreads) void k_zc_find(const uint8_t *base, u
 }
 
 
+// The match finder over the segments of the batch (k_zc_find_t above): the
+// 1024-thread form with the full tables for chunks of more than one block.
+#define MCDC_ZC_FIND_BIG k_zc_find_t<kFindThreads, kHsLog, kHlLog>
 // ---- the probe and the far matches --------------------------------------
 // Anchors: positions whose 8-byte key mixes (mix8) to a value with its top
 // bits clear, so that a repeated stretch has anchors at the same places in
@@ -569,7 +622,8 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
           const uint32_t lo = byte_window(w, j), hi = byte_window(w, j + 4), m8 = mix8(lo, hi);
           if (!far_anchor(m8)) continue;
           fm |= 1u << j;
-          if (far_out) atomicMax(&tab[far_slot(m8)], (q - seg0 + 1) << 14 | anchor_tag(mix5(lo, hi)));
+          // (q - seg0 + 1 takes 18 bits: the segment's very last position, 2^18, is not inserted)
+          if (far_out && q - seg0 + 1 < (1u << 18)) atomicMax(&tab[far_slot(m8)], (q - seg0 + 1) << 14 | anchor_tag(mix5(lo, hi)));
         }
       }
     }
@@ -657,6 +711,134 @@ __global__ __launch_bounds__(kProbeThreads) void k_zc_probe(const uint8_t *base,
   bool all = true;
   for (uint32_t k = 0; k < nsb; ++k) all &= high[k] && !rep[k];
   if (tid < nsb && high[tid] && !rep[tid]) blocks[bi0 + tid].flags = kZcRaw | (tid == 0 && all ? kZcSegRaw : 0u);
+}
+
+// The small chunks: every chunk of one block (<= DMAX bytes, the size class
+// kZcSmallClass) probed and matched by one workgroup of W waves, with the
+// chunk's bytes and its tables in LDS -- k_zc_find's 1024-thread tiles over
+// global loads are latency-bound on a chunk of a few KiB (two tiles of loads
+// in flight, a CU per chunk), and lose the matches inside a tile.  Here:
+//   1. the chunk's bytes into LDS (every load issued at once) and their
+//      order-0 histogram (a chunk under 16 KiB whole, else 4 of every 16
+//      bytes), in the table space;
+//   2. its entropy as k_zc_probe's test (kRawEntropy, the same bias term);
+//   3. the match finder over LDS: tiles of 64 W positions (the tables as the
+//      earlier tiles left them, then the tile's inserts, LDS max atomics:
+//      the latest position per slot), tables of 2^HS / 2^HL 32-bit entries
+//      sized to the class (zstd too shrinks its tables to a small source;
+//      tools/zc_model4.cpp priced the classes: 97-98 % of level 3 on the
+//      kernel-tree files, 94.5 % with k_zc_find), each position's candidate
+//      verified on 16 bytes from LDS;
+//   4. a chunk of high entropy without a verified match of 8 bytes or more is
+//      hopeless (kZcRaw, as k_zc_probe's repeat test), stored raw.
+// LDS: the bytes (DMAX) then the tables: exactly 160 KiB / (the class's
+// workgroups per CU).
+template <uint32_t W, uint32_t HS, uint32_t HL, uint32_t DMAX>
+__global__ __launch_bounds__(64 * W) void k_zc_small(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks,
+                                                     uint64_t nblk, uint32_t *words, const uint32_t *order) {
+  constexpr uint32_t NT = 64 * W;
+  static_assert(DMAX % 16 == 0 && (1u << HS) >= 256 && HS + 13 <= 32 && HL + 13 <= 32, "class shape");
+  // (one array: the bytes first, so that the reads past a chunk's end land in the tables)
+  __shared__ __attribute__((aligned(16))) uint32_t lds[DMAX / 4 + (1u << HS) + (1u << HL)];
+  uint32_t *const dat = lds, *const hts = lds + DMAX / 4, *const htl = hts + (1u << HS);
+  MCDC_VGPR_PAD(40);  // (not an exact fill)
+  const uint64_t bi = order[blockIdx.x];
+  if (bi >= nblk) return;
+  const ZcBlock B = blocks[bi];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), L = B.len;
+  if (B.nb != 1 || L > DMAX) return;  // (not this class: the host's counts disagree)
+  const uint8_t *cb = base + B.src;
+  const uint64_t cbytes = nbytes - B.src;
+  uint32_t *const wc = words + bi * kZcBlock;
+  if (L < 16 || cbytes < 16) {  // (too short to match: every position a literal; flags stay 0)
+    for (uint32_t p = tid; p < L; p += NT) wc[p] = 0u;
+    return;
+  }
+  // 1. the bytes (16-byte loads at chunk offsets: misaligned global loads;
+  // the last 16 readable bytes realigned) and the histogram
+  uint32_t *const hist = hts;  // (256 words, cleared with the tables below)
+  for (uint32_t k = tid; k < 256; k += NT) hist[k] = 0u;
+  const uint32_t nq = (L + 15) / 16;
+  constexpr uint32_t kQ = DMAX / 16 / NT;  // quads per thread
+  static_assert(kQ * NT * 16 == DMAX, "quads per thread");
+  uint4 q[kQ];
+#pragma unroll
+  for (uint32_t j = 0; j < kQ; ++j) {
+    const uint32_t k = tid + j * NT;
+    q[j] = k < nq ? fix16(ld16c(cb, 16 * k, cbytes), 16 * k, cbytes) : make_uint4(0, 0, 0, 0);
+  }
+  tile_sync<NT>();  // (the histogram cleared)
+  const bool whole = L < 16384;
+#pragma unroll
+  for (uint32_t j = 0; j < kQ; ++j) {
+    const uint32_t k = tid + j * NT;
+    if (k < nq) {
+      reinterpret_cast<uint4 *>(dat)[k] = q[j];
+      const uint32_t w4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+      for (int b = 0; b < 16; ++b)
+        if ((b < 4 || whole) && 16 * k + b < L) atomicAdd(&hist[(w4[b >> 2] >> (8 * (b & 3))) & 0xFFu], 1u);
+    }
+  }
+  // 2. entropy (wave 0; thread 0 keeps the answer): n log2 n - sum c log2 c
+  // >= thr n, thr as k_zc_probe's
+  tile_sync<NT>();
+  bool high = false;
+  if (tid < 64) {
+    float sc = 0.f;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint32_t c = hist[lane + 64 * h];
+      sc += c ? (float)c * __log2f((float)c) : 0.f;
+    }
+    for (int o = 32; o > 0; o >>= 1) sc += __shfl_xor(sc, o);
+    const uint32_t n = whole ? L : 4 * (L / 16) + min(4u, L % 16);  // (the bytes counted)
+    const float thr = kRawEntropy - 183.9f / (float)max(n, 1u) + 183.9f / 8192.f;
+    high = n >= 512 && (float)n * __log2f((float)n) - sc >= thr * (float)n;
+  }
+  tile_sync<NT>();
+  for (uint32_t k = tid; k < ((1u << HS) + (1u << HL)) / 4; k += NT) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
+  tile_sync<NT>();
+  // 3. the finder, NT positions per tile
+  auto bytes16 = [&](uint32_t p) {  // chunk bytes p .. p + 15 from LDS (past L: anything)
+    const uint32_t i = p >> 2, sh = p & 3;
+    const uint32_t d0 = dat[i], d1 = dat[i + 1], d2 = dat[i + 2], d3 = dat[i + 3], d4 = dat[i + 4];
+    return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                      __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+  };
+  bool rep = false;
+  for (uint32_t t0 = 0; t0 < L; t0 += NT) {
+    const uint32_t p = t0 + tid;
+    const uint4 x = bytes16(min(p, L - 1));
+    const bool vs = p + 5 <= L, vl = p + 8 <= L;
+    const uint32_t m5 = mix5(x.x, x.y), m8 = mix8(x.x, x.y);
+    const uint32_t hs = m5 >> (32 - HS), hl = m8 >> (32 - HL);
+    const uint32_t gs = (m5 >> (32 - HS - 13)) & 0x1FFFu, gl = (m8 >> (32 - HL - 13)) & 0x1FFFu;
+    const uint32_t es = vs ? hts[hs] : 0u, el = vl ? htl[hl] : 0u;
+    const bool okl = el != 0 && (el & 0x1FFFu) == gl, oks = es != 0 && (es & 0x1FFFu) == gs;
+    const uint32_t c = okl ? (el >> 13) - 1 : oks ? (es >> 13) - 1 : p;
+    const uint4 y = bytes16(min(c, L - 1));
+    const uint32_t lim = p < L ? min(kMlCap, L - p) : 0u;
+    const uint32_t m = (okl || oks) ? min(prefix16(x, y), lim) : 0u;
+    rep |= m >= 8;
+    if (p < L) wc[p] = m >= zs::kMinMatch ? (m << 24 | (p - c) | (m == kMlCap ? kZcLocalCap : 0u)) : 0u;
+    tile_sync<NT>();  // every lookup of the tile before any insert
+    const uint32_t r = (p + 1) << 13;
+    if (vs) atomicMax(hts + hs, r | gs);
+    if (vl) atomicMax(htl + hl, r | gl);
+    tile_sync<NT>();  // every insert before the next tile's lookups
+  }
+  // 4. hopeless: high entropy, no repeat (the tables are free: hts[0] is the
+  // workgroup's "any repeat")
+  bool any = __ballot(rep) != 0;
+  if constexpr (W > 1) {
+    if (tid == 0) hts[0] = 0u;
+    __syncthreads();
+    if (any && lane == 0) hts[0] = 1u;  // (any writer)
+    __syncthreads();
+    any = hts[0] != 0u;
+  }
+  if (tid == 0 && high && !any) blocks[bi].flags = kZcRaw | kZcSegRaw;
 }
 
 // Far matches: the 2^20 window of SecureStorage::compress (storage.rs:74-84)
@@ -2147,63 +2329,6 @@ __global__ __launch_bounds__(64) void k_zc_final(const uint8_t *base, const ZcBl
   }
 }
 
-// After the probe (and k_zc_far's rescue): the segments and blocks with work
-// to the front of the finder's and the parse's orders, stably (one
-// workgroup; tmp: 2 nblk words of scratch), and their counts to cnt[0],
-// cnt[1] -- the host sizes the finder's and the parse's grids by them.
-__global__ __launch_bounds__(1024) void k_zc_compact(const ZcBlock *blocks, uint64_t nblk, uint64_t nseg,
-                                                     uint32_t *order, uint32_t *porder, uint32_t *tmp,
-                                                     uint64_t *cnt) {
-  __shared__ uint32_t wtot[16], wpre[17];
-  MCDC_VGPR_PAD(32);  // (not an exact fill)
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / 64;
-  auto partition = [&](uint32_t *a, uint32_t *t, uint64_t n, uint32_t flag) -> uint32_t {
-    for (uint64_t i = tid; i < n; i += 1024) t[i] = a[i];
-    __syncthreads();
-    uint32_t kept = 0;  // (pass 1: how many stay in front)
-    for (uint64_t i = tid; i < n; i += 1024) kept += (blocks[t[i]].flags & flag) ? 0u : 1u;
-    kept = wave_sum(kept);
-    if (lane == 0) wtot[wv] = kept;
-    __syncthreads();
-    uint32_t total = 0;
-    for (int w = 0; w < 16; ++w) total += wtot[w];
-    __syncthreads();
-    uint32_t nk = 0, nd = 0;  // kept / dropped before this round
-    for (uint64_t i0 = 0; i0 < n; i0 += 1024) {
-      const uint64_t i = i0 + tid;
-      const bool in = i < n, keep = in && !(blocks[t[i]].flags & flag), drop = in && !keep;
-      const uint64_t bk = __ballot(keep), bd = __ballot(drop);
-      if (lane == 0) {
-        wtot[wv] = (uint32_t)__builtin_popcountll(bk) | (uint32_t)__builtin_popcountll(bd) << 16;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        uint32_t a = 0;
-        for (int w = 0; w < 16; ++w) {
-          wpre[w] = a;
-          a += wtot[w];
-        }
-        wpre[16] = a;
-      }
-      __syncthreads();
-      const uint32_t rk = (wpre[wv] & 0xFFFF) + __builtin_amdgcn_mbcnt_hi((uint32_t)(bk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bk, 0u));
-      const uint32_t rd = (wpre[wv] >> 16) + __builtin_amdgcn_mbcnt_hi((uint32_t)(bd >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bd, 0u));
-      if (keep) a[nk + rk] = t[i];
-      if (drop) a[total + nd + rd] = t[i];
-      nk += wpre[16] & 0xFFFF;
-      nd += wpre[16] >> 16;
-      __syncthreads();
-    }
-    return total;
-  };
-  const uint32_t ns = partition(order, tmp, nseg, kZcSegRaw);
-  const uint32_t nb = partition(porder, tmp + nblk, nblk, kZcRaw);
-  if (tid == 0) {
-    cnt[0] = ns;
-    cnt[1] = nb;
-  }
-}
-
 __global__ void k_zc_advance(uint64_t *obase, const uint64_t *poff, uint64_t nblk) {
   MCDC_VGPR_PAD(8);  // (not an exact fill)
   if (threadIdx.x == 0 && blockIdx.x == 0) *obase += poff[nblk];
@@ -2218,9 +2343,9 @@ size_t zc_tmp_bytes(uint64_t n) {
 }
 
 void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint64_t *first,
-                       uint32_t *err, uint64_t *bound, void *tmp, size_t tmp_bytes, hipStream_t st) {
+                       uint32_t *err, uint64_t *bound, uint8_t *cls, void *tmp, size_t tmp_bytes, hipStream_t st) {
   hipLaunchKernelGGL(k_zc_nblocks, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, chunks, n, nbytes, cnt,
-                     err, bound);
+                     err, bound, cls);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, cnt, first, (int)n + 1, st);
 }
@@ -2230,10 +2355,9 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
                      uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
-                     hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg, uint64_t *d_cnt,
-                     uint64_t *h_cnt, hipEvent_t ev_cnt) {
+                     hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg, const uint64_t *nsmall) {
   if (nblk == 0) return;
-  if (nseg == 0 || nseg > nblk) nseg = nblk;  // (every segment's first record is in order[0, nseg))
+  if (nseg == 0 || nseg > nblk) nseg = nblk, nsmall = nullptr;  // (every segment's first record is in order[0, nseg))
   hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
                      b0, blocks);
   // (piece, nblk + 1 words of 8 bytes, is free until k_zc_encode: the
@@ -2243,25 +2367,40 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   // (the far tables and ballots live in recs, free until k_zc_chain)
   uint32_t *ftab = reinterpret_cast<uint32_t *>(recs);
   uint64_t *fbits = reinterpret_cast<uint64_t *>(ftab + nblk * kZcFarSlots);
-  hipLaunchKernelGGL(k_zc_probe, dim3((unsigned)nseg), dim3(kProbeThreads), 0, st, base, nbytes, blocks, nblk, order,
-                     ftab, fbits);
+  // the probe over the segments of longer chunks (the front of the order),
+  // the small chunks (one block) by k_zc_small per size class (then the
+  // order's back, longest first: kZcSmallClass)
+  const uint64_t *ns_ = nsmall;
+  const uint64_t nsmall_all = ns_ ? ns_[0] + ns_[1] + ns_[2] + ns_[3] : 0;
+  const uint64_t nprobe = nsmall_all <= nseg ? nseg - nsmall_all : nseg;
+  if (nprobe)
+    hipLaunchKernelGGL(k_zc_probe, dim3((unsigned)nprobe), dim3(kProbeThreads), 0, st, base, nbytes, blocks, nblk,
+                       order, ftab, fbits);
+  if (nsmall_all && nsmall_all <= nseg) {
+    const uint32_t *os = order + nprobe;
+    if (ns_[0])
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_zc_small<4, 13, 12, 32768>), dim3((unsigned)ns_[0]), dim3(256), 0, st, base,
+                         nbytes, blocks, nblk, words, os);
+    if (ns_[1])
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_zc_small<4, 12, 11, 16384>), dim3((unsigned)ns_[1]), dim3(256), 0, st, base,
+                         nbytes, blocks, nblk, words, os + ns_[0]);
+    if (ns_[2])
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_zc_small<2, 12, 11, 8192>), dim3((unsigned)ns_[2]), dim3(128), 0, st, base,
+                         nbytes, blocks, nblk, words, os + ns_[0] + ns_[1]);
+    if (ns_[3])
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_zc_small<1, 11, 10, 4096>), dim3((unsigned)ns_[3]), dim3(64), 0, st, base,
+                         nbytes, blocks, nblk, words, os + ns_[0] + ns_[1] + ns_[2]);
+  }
   const dim3 gfar((unsigned)((nblk * kZcFarBallots + 3) / 4));
   if (far)
     hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, true);
-  uint64_t nfind = nseg, nwork = nblk;
-  if (d_cnt && h_cnt && ev_cnt) {  // (the orders' hopeless entries to the back; the host waits for the counts)
-    uint32_t *tmpo = reinterpret_cast<uint32_t *>(poff);  // (2 nblk + 2 words, free until the piece scan)
-    hipLaunchKernelGGL(k_zc_compact, dim3(1), dim3(1024), 0, st, blocks, nblk, nseg, order, porder, tmpo, d_cnt);
-    if (hipMemcpyAsync(h_cnt, d_cnt, 16, hipMemcpyDeviceToHost, st) == hipSuccess &&
-        hipEventRecord(ev_cnt, st) == hipSuccess && hipEventSynchronize(ev_cnt) == hipSuccess) {
-      const uint64_t c0v = ((volatile uint64_t *)h_cnt)[0], c1v = ((volatile uint64_t *)h_cnt)[1];
-      nfind = c0v < nseg ? c0v : nseg;
-      nwork = c1v < nblk ? c1v : nblk;
-    }
-  }
-  if (nfind)
-    hipLaunchKernelGGL(k_zc_find, dim3((unsigned)nfind), dim3(kFindThreads), 0, st, base, nbytes, blocks, nblk, words,
-                       order);
+  // the finder over the segments of chunks of more than one block (the small
+  // chunks' words are k_zc_small's); segments and blocks k_zc_probe /
+  // k_zc_small found hopeless return at once, here and in every kernel after
+  const uint64_t nbig = nprobe, nwork = nblk;
+  if (nbig)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(MCDC_ZC_FIND_BIG), dim3((unsigned)nbig), dim3(kFindThreads), 0, st, base, nbytes,
+                       blocks, nblk, words, order);
   if (far && nwork)
     hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, false);
   if (nwork) {

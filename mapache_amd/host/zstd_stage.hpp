@@ -22,6 +22,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace mcdc {
@@ -105,60 +106,20 @@ void parallel_items(size_t n, int threads, F fn) {
   for (auto &t : pool) t.join();
 }
 
-// compress blob i = in[off[i], + len[i]) into out_base[out_off[i], + its
-// compressBound + 64), its size to out_len[i]; returns "" or an error
-// (one output region per blob, no per-blob allocation)
-inline std::string zstd_compress_into(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
-                                      int threads, uint8_t *out_base, const uint64_t *out_off, uint64_t *out_len) {
+// Compress blob i = in[off[i], + len[i]) for every i on up to `threads` host
+// threads, one compression context per thread, exactly as the crate's
+// ZstdEncoder writes a blob (storage.rs:74-84): level 3, window log 20, no
+// checksum; write_all (ZSTD_e_continue), then finish (ZSTD_e_end until
+// flushed), the size never pledged -- so the frames carry no content size and
+// keep the window descriptor.  dst(i) -> (pointer, capacity >= its
+// compressBound + 64) says where blob i goes, done(i, bytes) receives its size
+// (not called for a blob that failed).  Returns "" or an error.  The one
+// place the host encodes blobs: both entry points below are thin wrappers.
+template <class Dst, class Done>
+inline std::string zstd_compress_each(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
+                                      int threads, Dst dst, Done done) {
   const ZstdApi &z = zstd_api();
   if (!z.ok) return z.why;
-  std::vector<void *> cctx((size_t)std::max(1, threads), nullptr);
-  std::mutex emu;
-  std::string err;
-  parallel_items(n, threads, [&](size_t i, int w) {
-    out_len[i] = 0;
-    if (!cctx[w]) {
-      cctx[w] = z.createCCtx();
-      const bool ok = cctx[w] && !z.isError(z.cctxSetParameter(cctx[w], kZstdCLevel, kZstdLevel)) &&
-                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCWindowLog, kZstdWindowLog)) &&
-                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCChecksum, 0)) &&
-                      !z.isError(z.cctxSetParameter(cctx[w], kZstdCContentSize, 0));  // (as zstd_compress_all)
-      if (!ok) {
-        std::lock_guard<std::mutex> lk(emu);
-        err = "zstd rejected level 3 / window log 20 / no checksum / no content size";
-        if (cctx[w]) z.freeCCtx(cctx[w]);
-        cctx[w] = nullptr;
-        return;
-      }
-    }
-    ZInBuf ib{in + off[i], (size_t)len[i], 0};
-    ZOutBuf ob{out_base + out_off[i], z.compressBound(len[i]) + 64, 0};
-    size_t r = z.compressStream2(cctx[w], &ob, &ib, kZstdEContinue);
-    if (!z.isError(r)) {
-      do {
-        r = z.compressStream2(cctx[w], &ob, &ib, kZstdEEnd);
-      } while (!z.isError(r) && r != 0 && ob.pos < ob.size);
-    }
-    if (z.isError(r) || r != 0) {  // (the context is mid-frame: drop it)
-      std::lock_guard<std::mutex> lk(emu);
-      err = std::string("zstd compression failed: ") + (z.isError(r) ? z.getErrorName(r) : "output bound");
-      z.freeCCtx(cctx[w]);
-      cctx[w] = nullptr;
-      return;
-    }
-    out_len[i] = ob.pos;
-  });
-  for (void *c : cctx)
-    if (c) z.freeCCtx(c);
-  return err;
-}
-
-// compress blob i = in[off[i], + len[i]) into out[i]; returns "" or an error
-inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
-                                     int threads, std::vector<std::vector<uint8_t>> &out) {
-  const ZstdApi &z = zstd_api();
-  if (!z.ok) return z.why;
-  out.assign(n, {});
   std::vector<void *> cctx((size_t)std::max(1, threads), nullptr);
   std::mutex emu;
   std::string err;
@@ -168,9 +129,6 @@ inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, con
       const bool ok = cctx[w] && !z.isError(z.cctxSetParameter(cctx[w], kZstdCLevel, kZstdLevel)) &&
                       !z.isError(z.cctxSetParameter(cctx[w], kZstdCWindowLog, kZstdWindowLog)) &&
                       !z.isError(z.cctxSetParameter(cctx[w], kZstdCChecksum, 0)) &&
-                      // the crate's streaming encoder (write_all + finish) never pledges a
-                      // size, so its frames carry no content size and keep the window
-                      // descriptor: the same 6-byte frame header here
                       !z.isError(z.cctxSetParameter(cctx[w], kZstdCContentSize, 0));
       if (!ok) {  // never compress with other settings than the reference's
         std::lock_guard<std::mutex> lk(emu);
@@ -180,12 +138,9 @@ inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, con
         return;
       }
     }
-    // as the crate's ZstdEncoder: write_all (ZSTD_e_continue), then finish
-    // (ZSTD_e_end until flushed); the size is never pledged
-    std::vector<uint8_t> &o = out[i];
-    o.resize(z.compressBound(len[i]) + 64);
+    const std::pair<uint8_t *, size_t> d = dst(i, z.compressBound(len[i]) + 64);
     ZInBuf ib{in + off[i], (size_t)len[i], 0};
-    ZOutBuf ob{o.data(), o.size(), 0};
+    ZOutBuf ob{d.first, d.second, 0};
     size_t r = z.compressStream2(cctx[w], &ob, &ib, kZstdEContinue);
     if (!z.isError(r)) {
       do {
@@ -197,13 +152,43 @@ inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, con
       err = std::string("zstd compression failed: ") + (z.isError(r) ? z.getErrorName(r) : "output bound");
       z.freeCCtx(cctx[w]);
       cctx[w] = nullptr;
-      o.clear();
       return;
     }
-    o.resize(ob.pos);
+    done(i, ob.pos);
   });
   for (void *c : cctx)
     if (c) z.freeCCtx(c);
+  return err;
+}
+
+// compress blob i into out_base[out_off[i], + its compressBound + 64), its
+// size to out_len[i] (0 if it failed): one output region per blob, no
+// per-blob allocation
+inline std::string zstd_compress_into(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
+                                      int threads, uint8_t *out_base, const uint64_t *out_off, uint64_t *out_len) {
+  for (size_t i = 0; i < n; ++i) out_len[i] = 0;
+  return zstd_compress_each(
+      in, off, len, n, threads, [&](size_t i, size_t cap) { return std::make_pair(out_base + out_off[i], cap); },
+      [&](size_t i, size_t bytes) { out_len[i] = bytes; });
+}
+
+// compress blob i into out[i] (empty if it failed)
+inline std::string zstd_compress_all(const uint8_t *in, const uint64_t *off, const uint64_t *len, size_t n,
+                                     int threads, std::vector<std::vector<uint8_t>> &out) {
+  out.assign(n, {});
+  std::vector<uint8_t> ok(n, 0);
+  std::string err = zstd_compress_each(
+      in, off, len, n, threads,
+      [&](size_t i, size_t cap) {
+        out[i].resize(cap);
+        return std::make_pair(out[i].data(), cap);
+      },
+      [&](size_t i, size_t bytes) {
+        out[i].resize(bytes);
+        ok[i] = 1;
+      });
+  for (size_t i = 0; i < n; ++i)
+    if (!ok[i]) out[i].clear();
   return err;
 }
 

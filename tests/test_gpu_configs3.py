@@ -94,4 +94,4 @@ def test_kernel_tree_gpu_compress_decodes(ctx, tree):
     with ThreadPoolExecutor(8) as ex:
         assert all(ex.map(check, range(len(hdrs))))
     host_bytes = sum(len(p) for p, _ in r_packs)
-    assert out.size < 1.08 * host_bytes, (out.size, host_bytes)  # ratio beside the host level 3's
+    assert out.size <= host_bytes / 0.95, (out.size, host_bytes)  # ratio >= 0.95 x the host level 3's

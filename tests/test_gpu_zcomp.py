@@ -156,6 +156,68 @@ def test_hopeless_blocks_and_repeats(ctx, p):
     assert nb2 == allrand.size + 6 * len(ch2) + 3 * nblk  # every block raw
 
 
+def _small_chunks(n_chunks, seed):
+    """Chunks of one block (0 - 32 KiB, every k_zc_small class and its edges)
+    at unaligned offsets of a buffer of text, records, binary, random bytes,
+    zeros and a random stretch repeated within a chunk; the last chunk ends at
+    the buffer's last byte."""
+    rng = np.random.default_rng(seed)
+    kinds = ["text", "records", "binary", "random", "zeros", "reprand"]
+    edges = [0, 1, 15, 16, 17, 511, 512, 4095, 4096, 4097, 8191, 8192, 8193, 16383, 16384, 16385, 32767, 32768]
+    lens = np.concatenate([edges, np.exp(rng.normal(np.log(6000), 1.0, n_chunks - len(edges))).astype(np.int64)])
+    lens = np.minimum(lens, 32768)
+    parts, offs, at = [], [], 0
+    for i, ln in enumerate(lens):
+        gap = int(rng.integers(0, 17))
+        k = kinds[i % len(kinds)]
+        if k == "reprand":  # random bytes whose second half repeats the first: not hopeless
+            h = O.random_bytes(int(ln) // 2 + 1, seed + i)
+            b = np.concatenate([h, h])[:ln]
+        elif k == "random":
+            b = O.random_bytes(int(ln), seed + i)
+        elif k == "zeros":
+            b = np.zeros(int(ln), np.uint8)
+        else:
+            b = corpora.by_name(k, int(ln) + 1, seed + i)[:ln]
+        parts += [O.random_bytes(gap, i), b]
+        offs.append(at + gap)
+        at += gap + int(ln)
+    data = np.concatenate(parts)
+    ch = np.zeros(len(lens), dtype=_lib.CHUNK_DTYPE)
+    ch["offset"], ch["length"] = offs, lens
+    return data, ch, kinds
+
+
+def test_small_chunks(ctx):
+    """Chunks of one block go through k_zc_small (the chunk and its tables in
+    LDS, four size classes): every frame decodes; a random chunk of 512 bytes
+    or more is stored raw, a random stretch repeated inside a chunk is not;
+    the ratio on the text-like chunks is within 5 % of level 3's and no worse
+    than the long-chunk kernels' (option "zc_small" 0) on the same chunks;
+    the output is the same in one batch or in many."""
+    data, ch, kinds = _small_chunks(4000, 11)
+    fr, out, nbytes = _compress(ctx, data, ch)
+    _check_frames(data, ch, fr, out, nbytes)
+    kind = np.array([kinds[i % len(kinds)] for i in range(len(ch))])
+    ln = ch["length"].astype(np.int64)
+    raw = fr[:, 1].astype(np.int64) == ln + 6 + 3  # one raw block
+    assert raw[(kind == "random") & (ln >= 512)].all()
+    assert not raw[(kind == "reprand") & (ln >= 4096)].any()
+    textlike = np.isin(kind, ["text", "records", "binary"]) & (ln >= 64)
+    sel = ch[textlike]
+    lvl3 = _level3(data, sel)
+    mine = int(fr[textlike, 1].sum())
+    assert mine <= lvl3 / 0.95, (mine, lvl3)
+    with _lib.Context(0, 1 << 30) as c2:
+        c2.set_option("zc_small", 0)
+        fr0, out0, nb0 = _compress(c2, data, ch)
+    assert mine <= int(fr0[textlike, 1].sum()), (mine, int(fr0[textlike, 1].sum()))
+    with _lib.Context(0, 1 << 30) as c3:
+        c3.set_option("zc_batch_blocks", 64)
+        fr1, out1, nb1 = _compress(c3, data, ch)
+    assert nb1 == nbytes and (out1 == out).all() and (fr1 == fr).all()
+
+
 def test_edge_lengths_offsets_overlaps(ctx):
     data = _data("mixed", 3 << 20, 9)
     lens = [0, 1, 3, 4, 5, 63, 64, 65, 16383, 16384, 16385, 32767, 32768, 32769, 65535, 65536, 65537, 100001,
