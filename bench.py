@@ -153,6 +153,76 @@ def _same(a: np.ndarray, b: np.ndarray) -> bool:
                 and (a["hash"] == b["hash"]).all())
 
 
+class ClockSampler:
+    """The engine clock the GPU holds during a timed region: a thread reads
+    the amdgpu driver's current SCLK (the starred level of
+    /sys/class/drm/cardN/device/pp_dpm_sclk; the card whose PCI address is
+    this process's HIP device) every `period_s` while the region runs.  Read
+    only, no GPU context: a box whose clock sags under load is told apart from
+    a slow kernel by this number beside the roofline fraction."""
+
+    def __init__(self, device: int, period_s: float = 0.002):
+        import threading
+        self.period, self.samples, self.path, self.why = period_s, [], None, None
+        self._stop = threading.Event()
+        self._t = None
+        try:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            buf = ctypes.create_string_buffer(64)
+            if hip.hipDeviceGetPCIBusId(buf, 64, int(device)) != 0:
+                raise OSError("hipDeviceGetPCIBusId failed")
+            bus = buf.value.decode().lower()
+            for card in sorted(os.listdir("/sys/class/drm")):
+                dev = os.path.join("/sys/class/drm", card, "device")
+                f = os.path.join(dev, "pp_dpm_sclk")
+                if card.startswith("card") and os.path.exists(f) and \
+                        os.path.basename(os.path.realpath(dev)).lower().endswith(bus[-7:]):
+                    self.path = f
+                    break
+            if self.path is None:
+                self.why = f"no pp_dpm_sclk for PCI {bus}"
+        except Exception as ex:  # reported, never fatal
+            self.why = f"{type(ex).__name__}: {ex}"
+
+    def _read(self):
+        with open(self.path) as f:
+            for line in f:
+                if line.rstrip().endswith("*"):
+                    return int(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+        return None
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                v = self._read()
+                if v:
+                    self.samples.append(v)
+            except Exception:
+                pass
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        import threading
+        if self.path:
+            self._t = threading.Thread(target=self._run, daemon=True)
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t:
+            self._t.join()
+
+    def summary(self) -> dict:
+        if not self.samples:
+            return {"sclk_mhz": None, "why": self.why or "no samples"}
+        v = np.array(self.samples, np.float64)
+        return {"sclk_mhz_mean": round(float(v.mean()), 1), "sclk_mhz_min": int(v.min()), "sclk_mhz_max": int(v.max()),
+                "samples": int(v.size), "source": f"{self.path}, the starred level every "
+                                                  f"{self.period * 1e3:g} ms over the timed region"}
+
+
 def _cpus():
     try:
         return len(os.sched_getaffinity(0))
@@ -1017,18 +1087,20 @@ def main() -> int:
         step()
     split_stats.clear()
     scan_ms, dev_ms, total_ms = [], [], []
+    clock = ClockSampler(local)
     barrier()
-    t0 = time.perf_counter()
-    count = 0
-    for _ in range(a.steps):
-        count = step()
-        t = ctx.timing() if world == 1 else None
-        if t:
-            scan_ms.append(t["scan_ms"])
-            dev_ms.append(t["device_ms"])
-            total_ms.append(t["total_ms"])
-    barrier()
-    elapsed = allreduce_max(time.perf_counter() - t0)
+    with clock:
+        t0 = time.perf_counter()
+        count = 0
+        for _ in range(a.steps):
+            count = step()
+            t = ctx.timing() if world == 1 else None
+            if t:
+                scan_ms.append(t["scan_ms"])
+                dev_ms.append(t["device_ms"])
+                total_ms.append(t["total_ms"])
+        barrier()
+        elapsed = allreduce_max(time.perf_counter() - t0)
     if world > 1:  # the main call's device timings (outside the timed loop)
         ctx.chunk_device_to_device(p, dp, hi - s, d_out, cap)
         t = ctx.timing()
@@ -1058,7 +1130,8 @@ def main() -> int:
         "roofline": {"bound": "hbm", "kernel": "k_scan_q", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": int(round(tpb * (hi - s))) if tpb else None, "traffic_unit": "bytes per launch",
-                     "traffic_source": tsrc, "bytes_per_launch": hi - s, "avg_launch_ms": round(scan_avg, 3)},
+                     "traffic_source": tsrc, "bytes_per_launch": hi - s, "avg_launch_ms": round(scan_avg, 3),
+                     "clock": clock.summary()},
         "device_only": {"scan_ms": round(scan_avg, 3), "device_ms": round(float(np.mean(dev_ms)), 3),
                         "gib_s": round((hi - s) / (float(np.mean(dev_ms)) * 1e-3) / GIB, 2),
                         "call_ms": round(float(np.mean(total_ms)), 3)},

@@ -365,9 +365,12 @@ typedef struct {
   size_t npadding;
   uint32_t gpu_compress;        /* 0: zstd level 3 on host threads (the crate's bytes);
                                    1: mcdc_zstd_compress_device in HBM (frames mapache's
-                                   decoder reads, not byte-equal to level 3), then the
-                                   seal, pack assembly and pack IDs in HBM; one D2H of
-                                   the packs: the whole save path on the GPU */
+                                   decoder reads, not byte-equal to level 3), the seal
+                                   straight into the packs' layout and the pack IDs in
+                                   HBM, the packs copied out while later blobs compress:
+                                   the whole save path on the GPU.  The pack headers'
+                                   zstd frames hold raw blocks (decode-equal; so their
+                                   size, and the layout, are known before the seal) */
   uint64_t gate_bytes;          /* processor::save_file's size gate (:144): a file shorter
                                    than this is one blob, never chunked; 0 = the
                                    reference's MIN_CHUNK_SIZE (512 KiB, defaults.rs:35),
@@ -455,6 +458,10 @@ int mcdc_ctx_synchronize(struct mcdc_ctx *ctx);
  *   "zc_batch_blocks"        blocks per GPU compressor batch (default 32768,
  *                            1 GiB; two streams take half each), >= 8
  *   "zc_two"                 0: compressor batches on one stream
+ *   "save_group_blocks"      GPU save path: 32 KiB blocks per compression
+ *                            group (0, the default: "zc_batch_blocks"); the
+ *                            packs a group closes are copied out while the
+ *                            next group compresses
  *   "zc_small"               0: chunks of one block (<= 32 KiB) through the
  *                            long chunks' probe and match finder instead of
  *                            the small-chunk kernel (A/B and tests)

@@ -222,6 +222,7 @@ struct mcdc_ctx {
   size_t max_bytes = 0;
   hipStream_t stream = nullptr;   // scan (and input copies)
   hipStream_t stream2 = nullptr;  // chain resolution, overlapping the scan's later parts
+  hipStream_t stream3 = nullptr;  // the GPU save path's pack copies to the host, beside the compressor
   hipEvent_t ev_start = nullptr, ev_scan = nullptr, ev_end = nullptr, ev_h2d0 = nullptr,
              ev_h2d1 = nullptr;
   hipEvent_t ev_part[kMaxParts] = {};
@@ -271,6 +272,8 @@ struct mcdc_ctx {
   size_t h_zbuf_cap = 0;
   void *h_encb = nullptr;      // pinned: mcdc_save_files' encoded blobs (host zstd mode)
   size_t h_encb_cap = 0;
+  void *h_meta = nullptr;      // pinned: the GPU save path's encoded pack headers (their H2D source)
+  size_t h_meta_cap = 0;
   uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
@@ -290,6 +293,7 @@ int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
   if (b.p) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipStreamSynchronize(ctx->stream3));
     HIP_TRY(hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -309,6 +313,7 @@ int ensure_stage(mcdc_ctx *ctx, size_t bytes) {
   if (ctx->h_stage) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipStreamSynchronize(ctx->stream3));
     HIP_TRY(hipHostFree(ctx->h_stage));
     ctx->h_stage = nullptr;
     ctx->h_stage_cap = 0;
@@ -328,6 +333,7 @@ int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
   if (ctx->h_tab) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipStreamSynchronize(ctx->stream3));
     HIP_TRY(hipHostFree(ctx->h_tab));
     ctx->h_tab = nullptr;
     ctx->h_tab_cap = 0;
@@ -347,6 +353,7 @@ int ensure_fcnt(mcdc_ctx *ctx, size_t n) {
   if (ctx->h_fcnt) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipStreamSynchronize(ctx->stream3));
     HIP_TRY(hipHostFree(ctx->h_fcnt));
     ctx->h_fcnt = nullptr;
     ctx->h_fcnt_cap = 0;
@@ -368,6 +375,7 @@ int ensure_pinned(mcdc_ctx *ctx, void *&p, size_t &cap, size_t bytes) {
   if (p) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
+    HIP_TRY(hipStreamSynchronize(ctx->stream3));
     HIP_TRY(hipHostFree(p));
     p = nullptr;
     cap = 0;
@@ -837,10 +845,13 @@ int give_back(mcdc_ctx *ctx, void *dst, const void *d_src, size_t bytes) {
 // the extents come from a boundary list instead (mcdc_seal_chunks_device).
 int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size_t n_in, const mcdc_blob *blobs,
              size_t nblobs, const uint8_t *nonces, void *d_out, size_t out_cap, uint64_t *out_offsets,
-             int32_t *status, const mcdc_chunk *chunks = nullptr, bool wait_done = true) {
+             int32_t *status, const mcdc_chunk *chunks = nullptr, bool wait_done = true,
+             const uint64_t *place = nullptr) {
   // (wait_done false, seal only: returns once the kernels are enqueued and
   // out_offsets is written; the caller orders later work on the context's
-  // stream and synchronises it)
+  // stream and synchronises it.  place, seal only: host array of nblobs + 1,
+  // blob i's output at d_out + place[i] instead of back to back, place[n] the
+  // end of the furthest one -- the GPU save path seals into the pack layout)
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!key || (!d_in && n_in) || (nblobs && !blobs && !chunks) || (!open && nblobs && !nonces))
@@ -891,7 +902,12 @@ int aead_run(mcdc_ctx *ctx, int open, const uint8_t *key, const void *d_in, size
   HIP_TRY(hipMemcpyAsync(&ntiles, toff + n, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (herr) return fail(MCDC_E_INVALID, "a blob extent lies outside the %zu-byte input", n_in);
-  if ((rc = give_back(ctx, out_offsets, ooff, (n + 1) * 8))) return rc;
+  if (place && !open) {  // (the sizes' scan is kept for the tile offsets; the output offsets replaced)
+    HIP_TRY(hipMemcpyAsync(ooff, place, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    total = place[n];
+  } else if ((rc = give_back(ctx, out_offsets, ooff, (n + 1) * 8))) {
+    return rc;
+  }
   if (!wait_done && !open) HIP_TRY(hipStreamSynchronize(st));  // (the offsets before the seal is enqueued)
   if (total > out_cap || (total && !d_out)) {
     HIP_TRY(hipStreamSynchronize(st));
@@ -981,7 +997,8 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(MCDC_E_DEVICE, "hipStreamCreate failed"));
   hipEvent_t *evs[] = {&ctx->ev_start, &ctx->ev_scan, &ctx->ev_end, &ctx->ev_h2d0, &ctx->ev_h2d1};
   for (hipEvent_t *e : evs)
@@ -1014,12 +1031,14 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
   if (ctx->h_save) (void)hipHostFree(ctx->h_save);
   if (ctx->h_zarena) (void)hipHostFree(ctx->h_zarena);
   if (ctx->h_encb) (void)hipHostFree(ctx->h_encb);
+  if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
@@ -1050,6 +1069,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   ctx->pool.reset();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   delete ctx;
 }
 
@@ -1286,6 +1306,7 @@ int mcdc_ctx_synchronize(mcdc_ctx *ctx) {
   // contexts' work on the device is not waited for
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream2));
+  HIP_TRY(hipStreamSynchronize(ctx->stream3));
   HIP_TRY(hipStreamSynchronize(nullptr));
   return MCDC_OK;
 }
@@ -1303,6 +1324,9 @@ int mcdc_ctx_set_option(mcdc_ctx *ctx, const char *name, long long value) {
     ctx->knobs.zc_two = value != 0;
   } else if (n == "zc_small") {
     ctx->knobs.zc_small = value != 0;
+  } else if (n == "save_group_blocks") {
+    if (value < 0) return fail(MCDC_E_INVALID, "save_group_blocks %lld < 0", value);
+    ctx->knobs.save_group_blocks = (uint64_t)value;
   } else if (n == "test_fail_after_index") {
     ctx->knobs.test_fail_after_index = value != 0;
   } else {
@@ -1679,6 +1703,13 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   return MCDC_OK;
 }
 
+#ifdef MCDC_SAVE_TRACE  // (A/B builds only: host time of the save path's stages, to stderr)
+#define SAVE_T(name) fprintf(stderr, "SAVE %-14s %8.3f ms\n", name, now_ms() - t_trace0)
+#else
+#define SAVE_T(name) ((void)0)
+#endif
+static double t_trace0 = 0;
+
 // ------------------------------------------------------------ pack plan --
 // Packer::add_blob / flush over a run of encoded blob lengths
 // (packer.rs:101-186, flush rule repository_v1.rs:185-193): which blobs go in
@@ -1738,6 +1769,7 @@ static int plan_packs(mcdc_ctx *ctx, const uint8_t key[32], const uint64_t *lens
       hdr.push_back(0xff);
     }
   }
+  SAVE_T("plan headers");
   // SecureStorage::encode of every header (zstd on host threads, sealing on the GPU)
   size_t enc_cap = hdr.size() + hdr.size() / 64 + 1024 * np + 64;
   std::vector<uint8_t> enc(enc_cap);
@@ -1753,6 +1785,7 @@ static int plan_packs(mcdc_ctx *ctx, const uint8_t key[32], const uint64_t *lens
     }
     if (rc) return rc;
   }
+  SAVE_T("plan encoded");
   P.meta.clear();
   P.moff.assign(np + 1, 0);
   P.body.assign(np, 0);
@@ -1781,6 +1814,7 @@ static void fill_pack_records(const PackPlan &P, const uint8_t *pid, mcdc_pack *
 }
 
 // ------------------------------------------------------------ save path --
+
 // The Archiver's save path for a run of files (processor.rs:138-205 +
 // Repository::save_blob, repository_v1.rs:155-195), composed from the stages
 // above: size gate, chunking (GPU), chunk IDs (GPU), dedup (GPU index),
@@ -1789,73 +1823,271 @@ static void fill_pack_records(const PackPlan &P, const uint8_t *pid, mcdc_pack *
 static constexpr uint64_t kMinChunkSize = 512 * 1024;  // global::defaults::MIN_CHUNK_SIZE (defaults.rs:35)
 
 // GPU encode (store->gpu_compress): the stored blobs of the device copy d are
-// compressed and sealed in HBM, the packs assembled there (each pack's body is
-// one contiguous run of encoded blobs: one device-to-device copy; its encoded
-// header and trailer come from the host), hashed there, and copied out once.
+// compressed and sealed in HBM straight into the packs' layout, hashed there,
+// and copied out pack by pack while the next blobs compress.
+//   * Groups of blobs (in storing order, each at least the compressor's batch
+//     of 32 KiB blocks, "zc_batch_blocks": both of its streams stay busy) go
+//     through mcdc_zstd_compress_device one after the other.  After a group, its
+//     blobs' encoded sizes are known (frame + kAeadOverhead), so the packer's
+//     flush rule (Packer::add_blob / flush, packer.rs:101-186,
+//     repository_v1.rs:185-193) places every blob of the group: a blob's pack
+//     starts where the packs before it end, and a pack's header follows its
+//     body.
+//   * Headers (generate_header: 37-byte entries padded to a multiple of 64)
+//     are SecureStorage-encoded with their zstd frame holding raw blocks
+//     (decode-equal: mapache's decoder reads any frame; ~10 % larger than
+//     level 3 on IDs, which are random bytes -- 0.1 % of the packs), so a
+//     header's encoded size follows from its entry count and the layout is
+//     fixed before anything is sealed.
+//   * The group's blobs and the headers of the packs it closes are sealed by
+//     aead_run into their places in sv_pack, the trailers (le32 of the
+//     encoded header's length) copied beside them; then the closed packs
+//     cross PCIe on stream3 while the next group compresses (the D2H was ~7
+//     ms after everything else for the kernel-tree stand-in).
+//   * The pack IDs (BLAKE3 of each pack) over sv_pack at the end.
+// A too small packs_out / packs capacity is found as the packs close: no
+// further copy is issued, the sizes are still computed, and MCDC_E_CAPACITY
+// returns with the totals.
+
 static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t *d, size_t n,
                            const std::vector<mcdc_blob> &sext, const std::vector<uint8_t> &sids,
                            const std::vector<uint8_t> &types, void *packs_out, size_t packs_out_cap,
                            size_t *packs_bytes, mcdc_pack *packs, size_t packs_cap, size_t *npacks) {
   const size_t m = sext.size();
+  const bool keyed = store->key != nullptr;
+  const uint64_t over = keyed ? kAeadOverhead : 0;
   std::vector<mcdc_chunk> sch(m);
-  for (size_t k = 0; k < m; ++k) sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
-  std::vector<mcdc_blob> fr(m);
-  size_t bound = 0, cbytes = 0;  // the raw-frame bound k_zc_nblocks reports, from the lengths
+  uint64_t in_total = 0, bound = 0;  // (bound: the raw frames k_zc_nblocks reports, from the lengths)
   for (size_t k = 0; k < m; ++k) {
+    sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
     const uint64_t len = sext[k].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
     bound += zs::kFrameHdr + zs::kBlockHdr * nb + len;
+    in_total += len;
   }
+  for (size_t k = 0; k < m; ++k)
+    if (sext[k].length + over + zs::kFrameHdr + 3 * (sext[k].length / kZcBlock + 1) > 0xffffffffull)
+      return fail(MCDC_E_INVALID, "blob %zu exceeds the header's u32 length", k);
+  // the packs' bound: every blob at its raw frame, every header entry (padding
+  // included: fewer than 64 per pack) raw-framed and sealed, the trailers
+  const uint64_t mps = std::max<uint64_t>(store->max_pack_size, 1);
+  const uint64_t np_max = (bound + over * m) / mps + 2;
+  const uint64_t pack_bound = bound + over * m + (m + 64 * np_max) * kHeaderEntry +
+                              np_max * (zs::kFrameHdr + over + 4 + 3 * ((m * kHeaderEntry) / (128 << 10) + 2));
+  // sv_comp: every group's frames, each followed by the framed headers of the
+  // packs it closes
+  const uint64_t comp_cap = pack_bound + 64;
   int rc = MCDC_OK;
-  // (buffers of their own: plan_packs' header encode reuses enc_in / enc_out)
-  if ((rc = ensure(ctx, ctx->sv_comp, std::max<size_t>(bound, 1))) ||
-      (rc = mcdc_zstd_compress_device(ctx, d, n, sch.data(), m, ctx->sv_comp.p, bound, &cbytes, fr.data())))
+  if ((rc = ensure(ctx, ctx->sv_comp, comp_cap)) || (rc = ensure(ctx, ctx->sv_pack, std::max<uint64_t>(pack_bound, 1))))
     return rc;
-  std::vector<uint64_t> eo(m + 1, 0);
-  const uint8_t *E = (const uint8_t *)ctx->sv_comp.p;  // encoded blob k = E[eo[k], eo[k + 1])
-  if (store->key) {
-    const size_t scap = cbytes + (size_t)kAeadOverhead * m;
-    if ((rc = ensure(ctx, ctx->sv_seal, scap)) ||
-        (rc = aead_run(ctx, 0, store->key, ctx->sv_comp.p, cbytes, fr.data(), m, store->nonces, ctx->sv_seal.p, scap,
-                       eo.data(), nullptr, nullptr, false)))  // (the pack plan's host work overlaps the seal)
-      return rc;
-    E = (const uint8_t *)ctx->sv_seal.p;
-  } else {  // frames are back to back from sv_comp
-    for (size_t k = 0; k < m; ++k) eo[k] = fr[k].offset;
-    eo[m] = cbytes;
+  uint8_t *C = (uint8_t *)ctx->sv_comp.p, *D = (uint8_t *)ctx->sv_pack.p;
+  std::vector<mcdc_blob> fr(m);   // frames, offsets from their group's start in C
+  std::vector<uint64_t> lens(m);  // encoded sizes
+  std::vector<uint64_t> place(m); // blob k at D + place[k]
+  // the packs: first blob of each (+ m), extents, header sizes
+  std::vector<size_t> first;
+  std::vector<mcdc_chunk> pk;
+  std::vector<uint64_t> meta;  // encoded header + 4
+  uint64_t at = 0, body = 0;   // the open pack's start in D, its body so far
+  bool open = false, overflow = false;
+  size_t pad_used = 0, copied = 0;  // padding entries drawn; packs handed to stream3
+  std::vector<uint8_t> hbuf;        // host: raw-framed headers of the packs closing in a group
+  std::vector<hipEvent_t> evs;
+  auto cleanup = [&]() {  // (every exit: nothing queued may still write the caller's buffer)
+    (void)hipStreamSynchronize(ctx->stream3);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+  };
+  // a header's raw zstd frame: frame header, then raw blocks of <= 128 KiB
+  auto frame_len = [](uint64_t hl) {
+    const uint64_t nb = hl ? (hl + (128 << 10) - 1) / (128 << 10) : 1;
+    return zs::kFrameHdr + zs::kBlockHdr * nb + hl;
+  };
+  // close pack [first.back(), e): its extent, header, its place in D
+  struct Closing {
+    size_t k;
+    uint64_t hpos, hlen;  // the header's frame at hbuf[hpos, + hlen)
+  };
+  std::vector<Closing> closing;
+  auto close_pack = [&](size_t e) -> int {
+    const size_t k = pk.size(), b0 = first.back(), cnt = e - b0;
+    const size_t pad = cnt % kHeaderMultiple ? kHeaderMultiple - cnt % kHeaderMultiple : 0;
+    if (pad_used + pad > store->npadding)
+      return fail(MCDC_E_INVALID, "the padding pool holds %zu entries, the headers need more", store->npadding);
+    if (keyed && k >= store->nheader_nonces)
+      return fail(MCDC_E_INVALID, "more packs than the %zu header nonces given", store->nheader_nonces);
+    const uint64_t hl = (cnt + pad) * kHeaderEntry, fl = frame_len(hl);
+    const uint64_t hpos = hbuf.size();
+    hbuf.resize(hpos + fl);
+    uint8_t *h = hbuf.data() + hpos;
+    zs::put_frame_header(h);
+    uint64_t o = zs::kFrameHdr, left = hl;
+    std::vector<uint8_t> hdr(hl);  // generate_header (packer.rs:113-150)
+    uint8_t *q = hdr.data();
+    for (size_t i = b0; i < e; ++i, q += kHeaderEntry) {
+      const uint32_t len = (uint32_t)lens[i];
+      std::memcpy(q, sids.data() + 32 * i, 32);
+      std::memcpy(q + 32, &len, 4);
+      q[36] = types[i];
+    }
+    for (size_t j = 0; j < pad; ++j, ++pad_used, q += kHeaderEntry) {
+      std::memcpy(q, store->padding + 36 * pad_used, 36);
+      q[36] = 0xff;
+    }
+    const uint8_t *src = hdr.data();
+    do {
+      const uint32_t bs = (uint32_t)std::min<uint64_t>(left, 128 << 10);
+      zs::put_block_header(h + o, left == bs, 0, bs);
+      std::memcpy(h + o + zs::kBlockHdr, src, bs);
+      o += zs::kBlockHdr + bs, src += bs, left -= bs;
+    } while (left);
+    const uint64_t enc = fl + over;
+    (void)e;
+    pk.push_back(mcdc_chunk{at, body + enc + 4, 0});
+    meta.push_back(enc + 4);
+    closing.push_back(Closing{k, hpos, fl});
+    at += body + enc + 4;
+    body = 0;
+    open = false;
+    return MCDC_OK;
+  };
+  hipStream_t st = ctx->stream, s3 = ctx->stream3;
+  const uint64_t group_blocks = ctx->knobs.save_group_blocks ? ctx->knobs.save_group_blocks : ctx->knobs.zc_batch;
+  uint64_t coff = 0;
+  size_t g0 = 0;
+  while (g0 < m) {  // the groups
+    size_t g1 = g0;
+    uint64_t gblk = 0;  // (a group of at least the compressor's batch in blocks: its two streams stay busy)
+    while (g1 < m && gblk < group_blocks) gblk += sext[g1].length ? (sext[g1++].length + kZcBlock - 1) / kZcBlock : (++g1, 1);
+    const size_t gm = g1 - g0;
+    size_t cbytes = 0;
+    if ((rc = mcdc_zstd_compress_device(ctx, d, n, sch.data() + g0, gm, C + coff, comp_cap - coff, &cbytes,
+                                        fr.data() + g0)))
+      return cleanup(), rc;
+    SAVE_T("group compressed");
+    // place the group's blobs; close the packs the flush rule closes
+    closing.clear();
+    hbuf.clear();
+    for (size_t i = g0; i < g1; ++i) {
+      lens[i] = fr[i].length + over;
+      if (!open) first.push_back(i), open = true;
+      place[i] = at + body;
+      body += lens[i];
+      if (body > mps && (rc = close_pack(i + 1))) return cleanup(), rc;
+    }
+    if (g1 == m && open && (rc = close_pack(m))) return cleanup(), rc;
+    // headers of the closing packs, framed on the host, to HBM after the group's frames
+    const uint64_t hin = coff + cbytes;
+    if (hin + hbuf.size() > comp_cap)  // (frames within their raw bound, headers within pack_bound's share)
+      return cleanup(), fail(MCDC_E_INTERNAL, "save path: header staging beyond the compressor buffer");
+    if ((rc = ensure_pinned(ctx, ctx->h_meta, ctx->h_meta_cap, hbuf.size() + 8 * closing.size() + 64)))
+      return cleanup(), rc;
+    uint8_t *hm = (uint8_t *)ctx->h_meta;
+    if (!hbuf.empty()) {
+      std::memcpy(hm, hbuf.data(), hbuf.size());
+      HIP_TRY(hipMemcpyAsync(C + hin, hm, hbuf.size(), hipMemcpyHostToDevice, st));
+    }
+    // trailers: le32(encoded header length) after each closing pack's header
+    uint8_t *tr = hm + hbuf.size();
+    for (size_t c = 0; c < closing.size(); ++c) {
+      const uint32_t el = (uint32_t)(meta[closing[c].k] - 4);
+      std::memcpy(tr + 4 * c, &el, 4);
+    }
+    if (keyed) {
+      std::vector<uint64_t> pl(gm + 1);
+      uint64_t end = 0;
+      for (size_t i = 0; i < gm; ++i) pl[i] = place[g0 + i], end = std::max(end, place[g0 + i] + lens[g0 + i]);
+      pl[gm] = end;
+      if ((rc = aead_run(ctx, 0, store->key, C + coff, cbytes, fr.data() + g0, gm, store->nonces + 12 * g0, D,
+                         ctx->sv_pack.cap, nullptr, nullptr, nullptr, false, pl.data())))
+        return cleanup(), rc;
+      if (!closing.empty()) {  // the headers: their frames sealed into place
+        std::vector<mcdc_blob> hx(closing.size());
+        std::vector<uint64_t> hp(closing.size() + 1);
+        std::vector<uint8_t> hn(12 * closing.size());
+        uint64_t hend = 0;
+        for (size_t c = 0; c < closing.size(); ++c) {
+          const size_t k = closing[c].k;
+          hx[c] = mcdc_blob{closing[c].hpos, closing[c].hlen};
+          hp[c] = pk[k].offset + pk[k].length - meta[k];
+          hend = std::max(hend, hp[c] + closing[c].hlen + over);
+          std::memcpy(hn.data() + 12 * c, store->header_nonces + 12 * k, 12);
+        }
+        hp[closing.size()] = hend;
+        if ((rc = aead_run(ctx, 0, store->key, C + hin, hbuf.size(), hx.data(), closing.size(), hn.data(), D,
+                           ctx->sv_pack.cap, nullptr, nullptr, nullptr, false, hp.data())))
+          return cleanup(), rc;
+      }
+    } else {  // frames as they are: the group's frames run by run of one pack, the headers
+      for (size_t i = g0; i < g1;) {
+        size_t e = i + 1;
+        while (e < g1 && place[e] == place[e - 1] + lens[e - 1]) ++e;
+        HIP_TRY(hipMemcpyAsync(D + place[i], C + coff + fr[i].offset, place[e - 1] + lens[e - 1] - place[i],
+                               hipMemcpyDeviceToDevice, st));
+        i = e;
+      }
+      for (const Closing &c : closing)
+        HIP_TRY(hipMemcpyAsync(D + pk[c.k].offset + pk[c.k].length - meta[c.k], C + hin + c.hpos, c.hlen,
+                               hipMemcpyDeviceToDevice, st));
+    }
+    for (size_t c = 0; c < closing.size(); ++c) {
+      const size_t k = closing[c].k;
+      HIP_TRY(hipMemcpyAsync(D + pk[k].offset + pk[k].length - 4, tr + 4 * c, 4, hipMemcpyHostToDevice, st));
+    }
+    // the closed packs to the host on stream3, after this group's work on st
+    if (!closing.empty()) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
+      evs.push_back(e);
+      HIP_TRY(hipEventRecord(e, st));
+      const size_t k1 = pk.size();
+      overflow |= k1 > packs_cap || (packs_out == nullptr) ||
+                  pk[k1 - 1].offset + pk[k1 - 1].length > packs_out_cap;
+      if (!overflow) {
+        HIP_TRY(hipStreamWaitEvent(s3, e, 0));
+        const uint64_t lo = pk[copied].offset, hi = pk[k1 - 1].offset + pk[k1 - 1].length;
+        HIP_TRY(hipMemcpyAsync((uint8_t *)packs_out + lo, D + lo, hi - lo, hipMemcpyDeviceToHost, s3));
+        copied = k1;
+      }
+    }
+    // the next group's frames after this group's frames and headers
+    coff = hin + hbuf.size();
+    g0 = g1;
   }
-  std::vector<uint64_t> lens(m);
-  for (size_t k = 0; k < m; ++k) lens[k] = eo[k + 1] - eo[k];
-  PackPlan P;
-  if ((rc = plan_packs(ctx, store->key, lens.data(), sids.data(), types.data(), m, store->max_pack_size,
-                       store->header_nonces, store->nheader_nonces, store->padding, store->npadding, P)))
-    return rc;
-  const size_t np = P.np();
+  // (the host buffers the queued copies read -- pl, hx, hp, hn, hbuf: H2D from
+  // pageable memory returns once the bytes are staged -- and h_meta, read by
+  // this group's copies: every group's copies finished before the next
+  // group's mcdc_zstd_compress_device returned, which synchronises st)
+  const size_t np = pk.size();
+  first.push_back(m);
   *npacks = np;
-  if (packs_bytes) *packs_bytes = P.total;
-  if (np > packs_cap || (np && !packs)) return fail(MCDC_E_CAPACITY, "%zu packs, capacity %zu", np, packs_cap);
-  if (P.total > packs_out_cap || (P.total && !packs_out))
-    return fail(MCDC_E_CAPACITY, "output capacity %zu < %zu bytes", packs_out_cap, P.total);
-  if (!np) return MCDC_OK;
-  if ((rc = ensure(ctx, ctx->sv_pack, P.total))) return rc;
-  uint8_t *D = (uint8_t *)ctx->sv_pack.p;
-  for (size_t k = 0; k < np; ++k) {  // body: blobs first[k] .. first[k+1]-1 are contiguous in E
-    const uint64_t b0 = eo[P.first[k]];
-    if (P.body[k])
-      HIP_TRY(hipMemcpyAsync(D + P.pk[k].offset, E + b0, P.body[k], hipMemcpyDeviceToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(D + P.pk[k].offset + P.body[k], P.meta.data() + P.moff[k], P.moff[k + 1] - P.moff[k],
-                           hipMemcpyHostToDevice, ctx->stream));
+  if (packs_bytes) *packs_bytes = at;
+  if (np > packs_cap || (np && !packs)) {
+    HIP_TRY(hipStreamSynchronize(s3));
+    HIP_TRY(hipStreamSynchronize(st));
+    return cleanup(), fail(MCDC_E_CAPACITY, "%zu packs, capacity %zu", np, packs_cap);
   }
-  // the packs cross PCIe on the second stream while their IDs are computed
-  // (both only read D; ~7 ms of D2H for the kernel-tree stand-in's packs)
-  HIP_TRY(hipEventRecord(ctx->ev_prep, ctx->stream));
-  HIP_TRY(hipStreamWaitEvent(ctx->stream2, ctx->ev_prep, 0));
-  HIP_TRY(hipMemcpyAsync(packs_out, D, P.total, hipMemcpyDeviceToHost, ctx->stream2));
+  if (overflow || at > packs_out_cap) {
+    HIP_TRY(hipStreamSynchronize(s3));
+    HIP_TRY(hipStreamSynchronize(st));
+    return cleanup(), fail(MCDC_E_CAPACITY, "output capacity %zu < %llu bytes", packs_out_cap,
+                           (unsigned long long)at);
+  }
+  SAVE_T("sealed enqueued");
   std::vector<uint8_t> pid(32 * np);
-  rc = mcdc_chunk_ids_device(ctx, D, P.total, P.pk.data(), np, pid.data());
-  HIP_TRY(hipStreamSynchronize(ctx->stream2));
+  rc = np ? mcdc_chunk_ids_device(ctx, D, at, pk.data(), np, pid.data()) : MCDC_OK;
+  HIP_TRY(hipStreamSynchronize(s3));
+  HIP_TRY(hipStreamSynchronize(st));
+  cleanup();
   if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  fill_pack_records(P, pid.data(), packs);
+  SAVE_T("packs out");
+  for (size_t k = 0; k < np; ++k) {
+    packs[k].offset = pk[k].offset;
+    packs[k].length = pk[k].length;
+    packs[k].nblobs = first[k + 1] - first[k];
+    packs[k].meta_size = meta[k];
+    std::memcpy(packs[k].id, pid.data() + 32 * k, 32);
+  }
   return MCDC_OK;
 }
 
@@ -1941,6 +2173,7 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   *npacks = 0;
   if (packs_bytes) *packs_bytes = 0;
   const double t0 = now_ms();
+  t_trace0 = t0;
   const bool host_in = data && !is_device_ptr(data);
   // the bytes in HBM (one copy of a host input)
   const uint8_t *d = (const uint8_t *)data;
@@ -1972,6 +2205,7 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
                                       bcnt.data(), &got)))
       return rc;
   }
+  SAVE_T("chunked");
   // every blob in processing order (file order, chunk order), offsets into d
   std::vector<mcdc_chunk> list;
   list.reserve(nfiles + cap);
@@ -1990,8 +2224,10 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   const size_t nb = list.size();
   *nblobs = nb;
   if (nb > blobs_cap || (nb && !ids)) return fail(MCDC_E_CAPACITY, "%zu blobs, capacity %zu", nb, blobs_cap);
+  SAVE_T("list");
   // ID::from_content of every blob (CalculateID of a small file is the same hash)
   if (nb && (rc = mcdc_chunk_ids_device(ctx, d, n, list.data(), nb, ids))) return rc;
+  SAVE_T("ids");
   // save_blob's dedup check (:173-180) -- the index changes here.  From here
   // on every failure, whatever returns it (capacity, nonces, a HIP call),
   // leaves through the one rollback below: the previous index buffer is
@@ -1999,6 +2235,7 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   std::vector<uint8_t> nw(std::max<size_t>(nb, 1));
   size_t m = 0;
   if (nb && (rc = mcdc_index_add(ctx, ix, ids, nb, nw.data(), nullptr, nullptr, &m))) return rc;
+  SAVE_T("index");
   auto rest = [&]() -> int {
     if (store->key && m > store->nnonces)
       return fail(MCDC_E_INVALID, "%zu new blobs need %zu nonces (%zu given)", m, m, store->nnonces);
@@ -2012,6 +2249,7 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
         sids.insert(sids.end(), ids + 32 * i, ids + 32 * i + 32);
       }
     const std::vector<uint8_t> types(std::max<size_t>(m, 1), 0);  // BlobType::Data (processor.rs:191)
+    SAVE_T("new list");
     if (store->gpu_compress && m)
       return save_encode_gpu(ctx, store, d, n, sext, sids, types, packs_out, packs_out_cap, packs_bytes, packs,
                              packs_cap, npacks);
@@ -2127,8 +2365,10 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   int k = 0, prev = -1;  // set of the batch, set of the batch before
   for (uint64_t c0 = 0; c0 < nchunks; k ^= two ? 1 : 0) {  // batches of whole chunks, <= mb blocks each
     uint64_t c1 = c0, nseg = 0, nsmall[4] = {0, 0, 0, 0};  // (chunks of one block per k_zc_small class)
+    uint64_t blongest = 0;  // (the batch's longest chunk in blocks: k_zc_far only above one segment)
     do {
       const uint64_t nbk = hfirst[c1 + 1] - hfirst[c1];
+      blongest = std::max(blongest, nbk);
       nseg += (nbk + kZcSegBlocks - 1) / kZcSegBlocks;
       if (hcls[c1] < 4) ++nsmall[hcls[c1]];
       ++c1;
@@ -2138,7 +2378,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
                     (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
                     (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
                     ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
-                    two ? ev[1 + k] : nullptr, longest > kZcSegBlocks, nseg, ctx->knobs.zc_small ? nsmall : nullptr);
+                    two ? ev[1 + k] : nullptr, blongest > kZcSegBlocks, nseg, ctx->knobs.zc_small ? nsmall : nullptr);
     if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
     prev = k;
     c0 = c1;

@@ -20,7 +20,8 @@
 //                 quad-coalesced loads transposed through LDS, the group's
 //                 subtree reduced on the fly (completed subtrees in registers);
 //                 a chunk of <= 16 leaves finishes its ID here (ROOT)
-//   k_b3_tree_wide one wave per chunk of more than 16 groups (nodes in LDS)
+//   k_b3_tree_wide one wave per chunk of more than 16 groups (the levels of more
+//                 than 512 nodes in HBM, the rest in LDS)
 //   k_b3_tree     one lane per chunk of 2-16 groups: level-by-level pairing of its
 //                 group nodes (the last node of an odd level moves up
 //                 unchanged — the same tree as the specification's stack rule)
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(256) void k_b3_owner(const DevChunk *chunks, const 
   const bool ok = i < n && gtotal(last) <= bound;
   if (ok) {  // chunks for the wave-parallel tree
     const uint64_t m = gtotal(goff[i + 1]) - gtotal(goff[i]);
-    if (m > kTreeLaneMax && m <= kTreeWaveMax) wide[atomicAdd(wide_cnt, 1u)] = (uint32_t)i;
+    if (m > kTreeLaneMax) wide[atomicAdd(wide_cnt, 1u)] = (uint32_t)i;
   }
   uint64_t a = 0, b = 0;
   uint32_t bin = 0, rank = 0;
@@ -455,15 +456,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
 }
 
-// One lane per chunk of more than one group: level-by-level pairing of its
+// One lane per chunk of 2 - kTreeLaneMax groups: level-by-level pairing of its
 // group nodes in place (nodes [goff[i], goff[i+1]) belong to this lane only).
 // Chunks of more than kTreeLaneMax groups (over 256 KiB: mapache's own
-// 512K/1M/8M chunks, up to 512 groups) are paired by a whole wave
-// (k_b3_tree_wide): per level, lanes take pairs, the nodes live in LDS, so a
-// 512-group chunk costs 13 wave-steps instead of 511 serial compressions on
-// one lane (the tree was 11 % of a 512K/1M/8M ID pass).  k_b3_owner lists
-// these chunks; persistent waves draw them from a counter.  Longer chunks (the
-// packer's ~16 MiB packs) keep the lane path.
+// 512K/1M/8M chunks, up to 512 groups, and the packer's ~16 MiB packs, whose
+// IDs are calculate_hash of the pack, src/utils/mod.rs:62-68) are paired by a
+// whole wave (k_b3_tree_wide): per level, lanes take pairs; the levels above
+// kTreeWaveMax nodes in place in HBM, the rest in LDS.  A 512-group chunk
+// costs 13 wave-steps instead of 511 serial compressions on one lane (the
+// tree was 11 % of a 512K/1M/8M ID pass); a 16 MiB pack ~20 instead of 1023
+// (1.6-1.8 ms per kernel-tree save call on the lane path, round 5).
+// k_b3_owner lists these chunks; persistent waves draw them from a counter.
 
 // order the wave's LDS accesses (fences keep the compiler from moving a
 // lane's write above another lane's read of the same node)
@@ -474,7 +477,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __global__ __launch_bounds__(64) void k_b3_tree_wide(const uint64_t *goff, uint64_t n, uint64_t bound,
-                                                     const uint32_t *nodes, uint8_t *ids, const uint32_t *wide,
+                                                     uint32_t *nodes, uint8_t *ids, const uint32_t *wide,
                                                      uint32_t *cnt) {
   __shared__ uint4 nd[2 * kTreeWaveMax];  // node j = nd[2 j], nd[2 j + 1] (16 KiB)
   const uint32_t lane = threadIdx.x;
@@ -491,9 +494,39 @@ __global__ __launch_bounds__(64) void k_b3_tree_wide(const uint64_t *goff, uint6
   while (k < total) {
     const uint64_t i = wide[k];
     const uint64_t g0 = gtotal(goff[i]);
-    uint32_t m = (uint32_t)(gtotal(goff[i + 1]) - g0);
-    const uint4 *src = reinterpret_cast<const uint4 *>(nodes + 8 * g0);
-    for (uint32_t t = lane; t < 2 * m; t += 64) nd[t] = src[t];
+    uint64_t mg = gtotal(goff[i + 1]) - g0;
+    uint4 *gn = reinterpret_cast<uint4 *>(nodes + 8 * g0);  // (this chunk's nodes: this wave's only)
+    // levels of more than kTreeWaveMax nodes in place in HBM: batch t0 reads
+    // nodes [2 t0, + 128) and writes [t0, + 64) -- each lane's store follows
+    // the wave's loads of the batch (its inputs), and later batches read above
+    // what earlier ones wrote; a level's stores are made visible to the next
+    // level's loads by the fence (the L1 is not coherent with them)
+    while (mg > kTreeWaveMax) {
+      const uint64_t pairs = mg / 2;
+      for (uint64_t t0 = 0; t0 < pairs; t0 += 64) {
+        const uint64_t t = t0 + lane;
+        uint32_t l[8], r[8], o[8];
+        if (t < pairs) {
+          const uint4 a = gn[4 * t], bb = gn[4 * t + 1], c = gn[4 * t + 2], d = gn[4 * t + 3];
+          l[0] = a.x; l[1] = a.y; l[2] = a.z; l[3] = a.w; l[4] = bb.x; l[5] = bb.y; l[6] = bb.z; l[7] = bb.w;
+          r[0] = c.x; r[1] = c.y; r[2] = c.z; r[3] = c.w; r[4] = d.x; r[5] = d.y; r[6] = d.z; r[7] = d.w;
+          parent(l, r, 0, o);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (t < pairs) {
+          gn[2 * t] = make_uint4(o[0], o[1], o[2], o[3]);
+          gn[2 * t + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (mg & 1) {  // the last node of an odd level moves up unchanged (it lies above every write)
+        if (lane < 2) gn[2 * pairs + lane] = gn[2 * (mg - 1) + lane];
+      }
+      mg = pairs + (mg & 1);
+      __threadfence();
+    }
+    uint32_t m = (uint32_t)mg;
+    for (uint32_t t = lane; t < 2 * m; t += 64) nd[t] = gn[t];
     wave_lds_sync();
     while (m > 1) {
       const uint32_t pairs = m / 2;
@@ -532,7 +565,7 @@ __global__ void k_b3_tree(const DevChunk *chunks, const uint64_t *goff, uint64_t
   if (i >= n || gtotal(goff[n]) > bound) return;
   uint64_t m = gtotal(goff[i + 1]) - gtotal(goff[i]);
   if (m < 2) return;  // finished by k_b3_leaves
-  if (m > kTreeLaneMax && m <= kTreeWaveMax) return;  // k_b3_tree_wide
+  if (m > kTreeLaneMax) return;  // k_b3_tree_wide
   uint32_t *nd = nodes + 8 * gtotal(goff[i]);
   uint32_t l[8], r[8], o[8];
   while (m > 1) {
@@ -585,7 +618,7 @@ void launch_b3_hash(const uint8_t *base, const DevChunk *chunks, uint64_t n, con
                      goff, (const uint32_t *)owner, n, group_bound, nodes, ids);
   // (at most as many waves as fit: 16 KiB of LDS each)
   hipLaunchKernelGGL(k_b3_tree_wide, dim3((unsigned)std::min<uint64_t>(n, 2048)), dim3(64), 0, stream, goff, n,
-                     group_bound, (const uint32_t *)nodes, ids, (const uint32_t *)wide, wcnt);
+                     group_bound, nodes, ids, (const uint32_t *)wide, wcnt);
   hipLaunchKernelGGL(k_b3_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, chunks, goff, n, group_bound,
                      nodes, ids);
 }

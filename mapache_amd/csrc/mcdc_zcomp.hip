@@ -754,6 +754,12 @@ __global__ __launch_bounds__(64 * W) void k_zc_small(const uint8_t *base, uint64
     for (uint32_t p = tid; p < L; p += NT) wc[p] = 0u;
     return;
   }
+#ifdef MCDC_ZC_TIMING  // (A/B: clocks per phase of thread 0, some workgroups, printed)
+  uint64_t tq[5], tq0 = __builtin_amdgcn_s_memtime();
+#define ZQ(k) (tq[k] = __builtin_amdgcn_s_memtime())
+#else
+#define ZQ(k) ((void)0)
+#endif
   // 1. the bytes (16-byte loads at chunk offsets: misaligned global loads;
   // the last 16 readable bytes realigned) and the histogram
   uint32_t *const hist = hts;  // (256 words, cleared with the tables below)
@@ -780,6 +786,7 @@ __global__ __launch_bounds__(64 * W) void k_zc_small(const uint8_t *base, uint64
         if ((b < 4 || whole) && 16 * k + b < L) atomicAdd(&hist[(w4[b >> 2] >> (8 * (b & 3))) & 0xFFu], 1u);
     }
   }
+  ZQ(0);
   // 2. entropy (wave 0; thread 0 keeps the answer): n log2 n - sum c log2 c
   // >= thr n, thr as k_zc_probe's
   tile_sync<NT>();
@@ -797,8 +804,10 @@ __global__ __launch_bounds__(64 * W) void k_zc_small(const uint8_t *base, uint64
     high = n >= 512 && (float)n * __log2f((float)n) - sc >= thr * (float)n;
   }
   tile_sync<NT>();
+  ZQ(1);
   for (uint32_t k = tid; k < ((1u << HS) + (1u << HL)) / 4; k += NT) reinterpret_cast<uint4 *>(hts)[k] = make_uint4(0, 0, 0, 0);
   tile_sync<NT>();
+  ZQ(2);
   // 3. the finder, NT positions per tile
   auto bytes16 = [&](uint32_t p) {  // chunk bytes p .. p + 15 from LDS (past L: anything)
     const uint32_t i = p >> 2, sh = p & 3;
@@ -828,6 +837,14 @@ __global__ __launch_bounds__(64 * W) void k_zc_small(const uint8_t *base, uint64
     if (vl) atomicMax(htl + hl, r | gl);
     tile_sync<NT>();  // every insert before the next tile's lookups
   }
+  ZQ(3);
+#ifdef MCDC_ZC_TIMING
+  if (tid == 0 && blockIdx.x % 397 == 0)
+    printf("ZCS W %u L %u tiles %u load %lu ent %lu clear %lu loop %lu per_tile %lu\n", W, L, (L + NT - 1) / NT,
+           (unsigned long)(tq[0] - tq0), (unsigned long)(tq[1] - tq[0]), (unsigned long)(tq[2] - tq[1]),
+           (unsigned long)(tq[3] - tq[2]), (unsigned long)((tq[3] - tq[2]) / ((L + NT - 1) / NT)));
+#endif
+#undef ZQ
   // 4. hopeless: high entropy, no repeat (the tables are free: hts[0] is the
   // workgroup's "any repeat")
   bool any = __ballot(rep) != 0;
@@ -931,13 +948,16 @@ __global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nb
 }
 
 #ifdef MCDC_ZC_TIMING  // (A/B: cycles per phase of one wave, some blocks, printed)
-#define ZT_DECL uint64_t zt_[6] = {0, 0, 0, 0, 0, 0}, zt0_ = __builtin_amdgcn_s_memtime(), zt1_ = 0
+#define ZT_DECL uint64_t zt_[6] = {0, 0, 0, 0, 0, 0}, zt0_ = __builtin_amdgcn_s_memtime(), zt1_ = 0; uint32_t ztn_[2] = {0, 0}
 #define ZT(k) (zt1_ = __builtin_amdgcn_s_memtime(), zt_[k] += zt1_ - zt0_, zt0_ = zt1_)
+#define ZTN(k) (++ztn_[k])
 #define ZT_PRINT(name, cond)                                                                                      \
   if ((cond) && lane_id() == 0)                                                                                  \
-  printf("ZCT %s blk %lu t0 %lu t1 %lu t2 %lu t3 %lu t4 %lu\n", name, (unsigned long)blockIdx.x,                   \
-         (unsigned long)zt_[0], (unsigned long)zt_[1], (unsigned long)zt_[2], (unsigned long)zt_[3], (unsigned long)zt_[4])
+  printf("ZCT %s blk %lu t0 %lu t1 %lu t2 %lu t3 %lu t4 %lu n0 %u n1 %u\n", name, (unsigned long)blockIdx.x,      \
+         (unsigned long)zt_[0], (unsigned long)zt_[1], (unsigned long)zt_[2], (unsigned long)zt_[3], (unsigned long)zt_[4], \
+         ztn_[0], ztn_[1])
 #else
+#define ZTN(k) ((void)0)
 #define ZT_DECL
 #define ZT(k) ((void)0)
 #define ZT_PRINT(name, cond)
@@ -995,7 +1015,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   __shared__ uint16_t ends[257], jp[256];
   __shared__ uint8_t mk[260], capl[256];
   __shared__ uint32_t offl[256], wbyt[64], mend[256], moff[256], llen[256];
-  __shared__ uint16_t xlist[256];
+  __shared__ uint16_t xlist[256], llist[256];
   if (blockIdx.x >= nblk) return;
   const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
@@ -1038,6 +1058,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   issue(0, nwd, nby);
   while (cur < end) {
     const uint32_t wb = cur & ~63u, s0 = cur - wb;
+    ZTN(0);
     ZT(4);
     wait_all(nwd, nby);
     uint32_t wd[4], by;
@@ -1125,6 +1146,57 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         ends[i] = (uint16_t)(m == kRunExt ? kEndLong : i + kMlCap + m);
       }
       lds_sync();
+      // Runs still matching after kRunExt more bytes: kRunLong more each, 8
+      // lanes per run (32 bytes a lane), every such run of the window at once
+      // -- one round of loads, where the chain walk below extended each long
+      // match on the chain by itself (a memory round trip per match: most of
+      // the parse's time on source code, whose repeated lines are such
+      // matches).  A run still matching after those stays long (the walk
+      // extends it).
+      uint32_t nl = 0;
+      for (uint32_t r0 = 0; r0 < nx; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        const bool lg = r < nx && ends[xlist[r]] == kEndLong;
+        const uint64_t bl = __ballot(lg);
+        if (lg) llist[nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u))] =
+            xlist[r];
+        nl += (uint32_t)__builtin_popcountll(bl);
+      }
+      if (nl) {
+        lds_sync();  // (the list, written by other lanes)
+        const uint32_t gq = lane >> 3, gj = lane & 7;
+        for (uint32_t r0 = 0; r0 < nl; r0 += 8) {
+          const uint32_t r = r0 + gq;
+          uint32_t m = 32, i = 0;
+          if (r < nl) {
+            i = llist[r];
+            const uint32_t off = offl[i], q = wb + i + kMlCap + kRunExt + 32 * gj;
+            uint4 x[2], y[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const uint64_t g = B.src + q + 16 * u;
+              x[u] = ld16c(base, g, nbytes);
+              y[u] = ld16c(base, g - off, nbytes);
+            }
+            m = 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const uint32_t qu = q + 16 * u;
+              const uint64_t g = B.src + qu;
+              const uint32_t mu =
+                  qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
+              m += m == 16 * (uint32_t)u ? mu : 0u;
+            }
+          }
+          // the run's first lane short of 32 bytes ends it
+          const uint64_t brk = __ballot(r < nl && m < 32);
+          const uint32_t gb = (uint32_t)(brk >> (8 * gq)) & 0xFFu;
+          const uint32_t jf = gb ? (uint32_t)__builtin_ctz(gb) : 0u;
+          const uint32_t mf = (uint32_t)__shfl((int)m, (int)(8 * gq + jf));
+          if (r < nl && gj == 0 && gb) ends[i] = (uint16_t)(i + kMlCap + kRunExt + 32 * jf + mf);
+        }
+        lds_sync();
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (ext[j]) en[j] = ends[64 * j + lane];
@@ -1194,6 +1266,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         if (lf == 0x7FFFFFFF && bl) lf = 64 * j + (int32_t)__builtin_ctzll(bl);
       }
       if (lf == 0x7FFFFFFF) break;
+      ZTN(1);
       const uint32_t L = (uint32_t)lf, pos = wb + L, off = offl[L];
       uint32_t mlt = kMlCap;
       for (;;) {

@@ -169,14 +169,17 @@ def test_many_tail_lengths_in_list_order(ctx):
 
 
 def test_large_chunks_tree_paths(ctx):
-    """Chunks of 17-512 groups (kTreeWaveMax, mcdc_blake3.hip) go to the
-    wave-parallel tree (k_b3_tree_wide), longer ones to the lane path:
-    256 KiB + 1 (17 groups), 1 MiB, 8 MiB - 16 KiB + 1 (512 groups, an odd
-    last group), 8 MiB (mapache's max, 512 groups: the wave path's limit),
-    8 MiB + 1 (513 groups: the first lane-path size), 16 MiB + 1 (a pack's
-    size), 24 MiB and 40 MiB + 3 (the lane path), at odd offsets."""
+    """Chunks of more than 16 groups go to the wave-parallel tree
+    (k_b3_tree_wide, mcdc_blake3.hip): up to kTreeWaveMax = 512 nodes in LDS,
+    the levels above that in place in HBM first.  256 KiB + 1 (17 groups),
+    1 MiB, 8 MiB - 16 KiB + 1 (512 groups, an odd last group), 8 MiB
+    (mapache's max, 512 groups: all in LDS), 8 MiB + 1 (513 groups: one HBM
+    level, an odd one), 16 MiB + 1 (a pack's size: 1025 groups), 16 MiB (1024,
+    even levels), 24 MiB, 40 MiB + 3 and 64 MiB + 16 KiB + 5 (3-4 HBM levels,
+    odd counts), at odd offsets; the IDs equal the specification's tree
+    (the pack ID is calculate_hash of the pack, src/utils/mod.rs:62-68)."""
     lens = [(256 << 10) + 1, 1 << 20, (8 << 20) - (16 << 10) + 1, 8 << 20, (8 << 20) + 1, (16 << 20) + 1,
-            24 << 20, (40 << 20) + 3]
+            16 << 20, 24 << 20, (40 << 20) + 3, (64 << 20) + (16 << 10) + 5]
     pairs, pos = [], 5
     for n_ in lens:
         pairs.append((pos, n_))

@@ -21,6 +21,9 @@ rng = np.random.default_rng(9)
 nonces = rng.integers(0, 256, (nfiles + n // (512 << 10) + 64, 12), dtype=np.uint8)
 hn, pad = rng.integers(0, 256, (4096, 12), dtype=np.uint8), rng.integers(0, 256, (4096 * 63, 36), dtype=np.uint8)
 with _lib.Context(0, 2 << 30) as ctx:
+    for kv in os.environ.get("ZC_OPTS", "").split(","):  # (A/B: "save_group_blocks=16384,zc_small=0")
+        if kv:
+            ctx.set_option(kv.split("=")[0], int(kv.split("=")[1]))
     dp = ctx.device_alloc(n + 16)
     ctx.h2d(dp, data)
     ob = ctx.pinned_bytes(int(n * 1.01) + 4096 * nfiles + (1 << 16))

@@ -25,8 +25,11 @@ p = _lib.params(524288, 1048576, 8388608, 1) if len(sys.argv) > 4 and sys.argv[4
 ctx_cap = n + (1 << 20)
 ctx = _lib.Context(0, ctx_cap)
 ZC_BATCH = int(os.environ.get("ZC_BATCH", "0"))  # (A/B: the compressor's batch, "zc_batch_blocks")
+ZC_OPTS = [(k, int(v)) for k, v in (kv.split("=") for kv in os.environ.get("ZC_OPTS", "").split(",") if kv)]
 if ZC_BATCH:
-    ctx.set_option("zc_batch_blocks", ZC_BATCH)
+    ZC_OPTS.append(("zc_batch_blocks", ZC_BATCH))
+for k_, v_ in ZC_OPTS:  # (A/B: "zc_two=0,zc_small=0", mcdc_ctx_set_option)
+    ctx.set_option(k_, v_)
 res = {}
 n_arg = n
 for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text", "records", "binary", "far")):
@@ -40,8 +43,8 @@ for kind in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "text",
             ctx.close()
             ctx_cap = n + (1 << 20)
             ctx = _lib.Context(0, ctx_cap)
-            if ZC_BATCH:
-                ctx.set_option("zc_batch_blocks", ZC_BATCH)
+            for k_, v_ in ZC_OPTS:
+                ctx.set_option(k_, v_)
     dp = ctx.device_alloc(n)
     if tree is not None:
         ctx.h2d(dp, tree[0])
