@@ -131,14 +131,18 @@ def pad_library_fills(lib: str, asm_dir: str, rows) -> int:
     return len(done)
 
 
-def build_lib(force: bool = False, ab: bool = False) -> str:
-    out = os.path.join(HERE, "libmcdc_ab.so" if ab else "libmcdc.so")
+def build_lib(force: bool = False, ab: bool = False, defines=(), out: str | None = None) -> str:
+    """libmcdc.so (ab: libmcdc_ab.so; defines/out: a variant for on-box A/B
+    runs, tools/build_variants.py), through the same device-code guard and
+    descriptor padding as the product: an unpadded variant once left a
+    library kernel at an exact VGPR fill."""
+    out = out or os.path.join(HERE, "libmcdc_ab.so" if ab else "libmcdc.so")
     deps = [os.path.join(HERE, d) for d in LIB_DEPS]
     if force or _stale(out, deps):
         tmp = out + ".tmp"
         with tempfile.TemporaryDirectory() as td:  # -save-temps: device assembly + code objects for the guard
-            flags = [HIPCC, *CXXFLAGS, *(["-DMCDC_AB_KNOBS"] if ab else []), "-save-temps", "-fPIC",
-                     f"-I{os.path.join(ROOT, 'include')}"]
+            flags = [HIPCC, *CXXFLAGS, *(["-DMCDC_AB_KNOBS"] if ab else []), *[f"-D{d}" for d in defines],
+                     "-save-temps", "-fPIC", f"-I{os.path.join(ROOT, 'include')}"]
             procs, objs = [], []
             for src in LIB_SRCS:  # one translation unit per process, in parallel
                 o = os.path.join(td, os.path.basename(src).replace(".hip", ".o"))

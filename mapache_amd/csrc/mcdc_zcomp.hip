@@ -1015,7 +1015,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   __shared__ uint16_t ends[257], jp[256];
   __shared__ uint8_t mk[260], capl[256];
   __shared__ uint32_t offl[256], wbyt[64], mend[256], moff[256], llen[256];
-  __shared__ uint16_t xlist[256], llist[256];
+  __shared__ uint16_t xlist[256];
   if (blockIdx.x >= nblk) return;
   const uint64_t bi = porder[blockIdx.x];  // (the longest blocks first, k_zc_segorder)
   const uint32_t lane = lane_id();
@@ -1146,57 +1146,6 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
         ends[i] = (uint16_t)(m == kRunExt ? kEndLong : i + kMlCap + m);
       }
       lds_sync();
-      // Runs still matching after kRunExt more bytes: kRunLong more each, 8
-      // lanes per run (32 bytes a lane), every such run of the window at once
-      // -- one round of loads, where the chain walk below extended each long
-      // match on the chain by itself (a memory round trip per match: most of
-      // the parse's time on source code, whose repeated lines are such
-      // matches).  A run still matching after those stays long (the walk
-      // extends it).
-      uint32_t nl = 0;
-      for (uint32_t r0 = 0; r0 < nx; r0 += 64) {
-        const uint32_t r = r0 + lane;
-        const bool lg = r < nx && ends[xlist[r]] == kEndLong;
-        const uint64_t bl = __ballot(lg);
-        if (lg) llist[nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u))] =
-            xlist[r];
-        nl += (uint32_t)__builtin_popcountll(bl);
-      }
-      if (nl) {
-        lds_sync();  // (the list, written by other lanes)
-        const uint32_t gq = lane >> 3, gj = lane & 7;
-        for (uint32_t r0 = 0; r0 < nl; r0 += 8) {
-          const uint32_t r = r0 + gq;
-          uint32_t m = 32, i = 0;
-          if (r < nl) {
-            i = llist[r];
-            const uint32_t off = offl[i], q = wb + i + kMlCap + kRunExt + 32 * gj;
-            uint4 x[2], y[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const uint64_t g = B.src + q + 16 * u;
-              x[u] = ld16c(base, g, nbytes);
-              y[u] = ld16c(base, g - off, nbytes);
-            }
-            m = 0;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const uint32_t qu = q + 16 * u;
-              const uint64_t g = B.src + qu;
-              const uint32_t mu =
-                  qu < end ? min(prefix16(fix16(x[u], g, nbytes), fix16(y[u], g - off, nbytes)), end - qu) : 0u;
-              m += m == 16 * (uint32_t)u ? mu : 0u;
-            }
-          }
-          // the run's first lane short of 32 bytes ends it
-          const uint64_t brk = __ballot(r < nl && m < 32);
-          const uint32_t gb = (uint32_t)(brk >> (8 * gq)) & 0xFFu;
-          const uint32_t jf = gb ? (uint32_t)__builtin_ctz(gb) : 0u;
-          const uint32_t mf = (uint32_t)__shfl((int)m, (int)(8 * gq + jf));
-          if (r < nl && gj == 0 && gb) ends[i] = (uint16_t)(i + kMlCap + kRunExt + 32 * jf + mf);
-        }
-        lds_sync();
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (ext[j]) en[j] = ends[64 * j + lane];

@@ -3,7 +3,6 @@
 them where gpurun sends them).
 usage: python tools/build_variants.py name:DEF=1,DEF2=0 ..."""
 import os
-import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
 
@@ -14,10 +13,10 @@ from mapache_amd import build as B  # noqa: E402
 def one(spec):
     name, _, defs = spec.partition(":")
     out = os.path.join(B.ROOT, OUTDIR, name + ".so")
-    cmd = [B.HIPCC, *B.CXXFLAGS, *[f"-D{d}" for d in defs.split(",") if d], "-fPIC", "-shared",
-           f"-I{os.path.join(B.ROOT, 'include')}", "-o", out, *[os.path.join(B.HERE, x) for x in B.LIB_SRCS]]
-    subprocess.run(cmd, check=True, cwd=B.ROOT)
-    return out
+    # (the product's build: the device-code guard and the library descriptors'
+    # padding apply to variants too -- a plain hipcc build left a rocPRIM
+    # kernel at an exact VGPR fill)
+    return B.build_lib(force=True, defines=[d for d in defs.split(",") if d], out=out)
 
 
 OUTDIR = os.environ.get("MCDC_AB_DIR", "ablib")  # (abship/: variants sent to the GPU box)
