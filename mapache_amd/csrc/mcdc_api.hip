@@ -1703,6 +1703,68 @@ int mcdc_decode_blobs(mcdc_ctx *ctx, const uint8_t key[32], const void *h_in, si
   return MCDC_OK;
 }
 
+// The GPU save path's seal of n blobs of d_in (extents ext, host, relative to
+// d_in; nonces: 12 B each) into d_out at host-given places, enqueued on
+// `st` with no host wait: the output and tile offsets (k_aead_sizes' rule)
+// computed on the host, the records staged from pinned memory `stage` (at
+// least seal_stage_bytes(n), untouched until `st` has run the copies), the
+// context's AEAD workspace reused in stream order (ensured beforehand for
+// the largest call: ensure() would wait for every stream).
+static size_t seal_stage_bytes(size_t n) { return n * (16 + 12) + 2 * (n + 1) * 8 + 64; }
+static uint64_t seal_tiles(uint64_t len) {  // (k_aead_sizes, seal: tiles of a blob of len bytes)
+  const uint64_t T = len + kAeadOverhead;
+  const uint64_t ct = ((T - 1) / 16 + 2 + kAeadTileBlocks - 1) / kAeadTileBlocks;
+  const uint64_t nblk = (len + 15) / 16, rows = (nblk + 63) / 64;
+  uint64_t pt = (rows + kAeadRows - 1) / kAeadRows;
+  if (pt > 1 && rows - kAeadRows * (pt - 1) < kAeadRows / 2) --pt;
+  return ct > pt ? ct : pt;
+}
+static int seal_workspace(mcdc_ctx *ctx, size_t n, uint64_t ntiles) {
+  int rc;
+  if ((rc = ensure(ctx, ctx->ae_ext, n * 16)) || (rc = ensure(ctx, ctx->ae_nonce, n * kAeadNonce)) ||
+      (rc = ensure(ctx, ctx->ae_ooff, (n + 1) * 8)) || (rc = ensure(ctx, ctx->ae_toff, (n + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->ae_rec, n * sizeof(AeadRec))) || (rc = ensure(ctx, ctx->ae_keys, n * sizeof(AeadKeys))) ||
+      (rc = ensure(ctx, ctx->ae_owner, ntiles * 4)) || (rc = ensure(ctx, ctx->ae_tsum, ntiles * 16)) ||
+      (rc = ensure(ctx, ctx->err, 32)))
+    return rc;
+  return MCDC_OK;
+}
+static int seal_placed(mcdc_ctx *ctx, hipStream_t st, const uint8_t *key, const uint8_t *d_in, const mcdc_blob *ext,
+                       size_t n, const uint8_t *nonces, uint8_t *d_out, const uint64_t *place, uint8_t *stage) {
+  if (n == 0) return MCDC_OK;
+  uint64_t *sx = reinterpret_cast<uint64_t *>(stage);  // ext pairs, then ooff, toff; nonces after
+  uint64_t *so = sx + 2 * n, *stt = so + n + 1;
+  uint8_t *sn = reinterpret_cast<uint8_t *>(stt + n + 1);
+  uint64_t nt = 0;
+  for (size_t i = 0; i < n; ++i) {
+    sx[2 * i] = ext[i].offset;
+    sx[2 * i + 1] = ext[i].length;
+    so[i] = place[i];
+    stt[i] = nt;
+    nt += seal_tiles(ext[i].length);
+  }
+  so[n] = place[n];
+  stt[n] = nt;
+  std::memcpy(sn, nonces, n * kAeadNonce);
+  if (nt >= (1ull << 32)) return fail(MCDC_E_TOOBIG, "input too large (%llu tiles)", (unsigned long long)nt);
+  if (ctx->ae_owner.cap < nt * 4 || ctx->ae_tsum.cap < nt * 16 || ctx->ae_ext.cap < n * 16 ||
+      ctx->ae_rec.cap < n * sizeof(AeadRec) || ctx->ae_keys.cap < n * sizeof(AeadKeys))
+    return fail(MCDC_E_INTERNAL, "save path: seal workspace not reserved");
+  HIP_TRY(hipMemcpyAsync(ctx->ae_ext.p, sx, n * 16, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->ae_ooff.p, so, (n + 1) * 8, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->ae_toff.p, stt, (n + 1) * 8, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->ae_nonce.p, sn, n * kAeadNonce, hipMemcpyHostToDevice, st));
+  AeadMaster mk;
+  aead_expand_key256(key, mk.rk);
+  launch_aead_seal(mk, d_in, (const uint64_t *)ctx->ae_ext.p, (const uint32_t *)ctx->ae_nonce.p, n, d_out,
+                   (const uint64_t *)ctx->ae_ooff.p, (const uint64_t *)ctx->ae_toff.p, nt, (AeadRec *)ctx->ae_rec.p,
+                   (AeadKeys *)ctx->ae_keys.p, (uint32_t *)ctx->ae_owner.p, (uint4 *)ctx->ae_tsum.p,
+                   (uint32_t *)ctx->err.p + 4, ctx->num_cus, st);
+  std::memset(mk.rk, 0, sizeof mk.rk);
+  HIP_TRY(hipGetLastError());
+  return MCDC_OK;
+}
+
 #ifdef MCDC_SAVE_TRACE  // (A/B builds only: host time of the save path's stages, to stderr)
 #define SAVE_T(name) fprintf(stderr, "SAVE %-14s %8.3f ms\n", name, now_ms() - t_trace0)
 #else
@@ -1857,12 +1919,11 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   const bool keyed = store->key != nullptr;
   const uint64_t over = keyed ? kAeadOverhead : 0;
   std::vector<mcdc_chunk> sch(m);
-  uint64_t in_total = 0, bound = 0;  // (bound: the raw frames k_zc_nblocks reports, from the lengths)
+  uint64_t bound = 0;  // (the raw frames k_zc_nblocks reports, from the lengths)
   for (size_t k = 0; k < m; ++k) {
     sch[k] = mcdc_chunk{sext[k].offset, sext[k].length, 0};
     const uint64_t len = sext[k].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
     bound += zs::kFrameHdr + zs::kBlockHdr * nb + len;
-    in_total += len;
   }
   for (size_t k = 0; k < m; ++k)
     if (sext[k].length + over + zs::kFrameHdr + 3 * (sext[k].length / kZcBlock + 1) > 0xffffffffull)
@@ -1952,18 +2013,65 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   };
   hipStream_t st = ctx->stream, s3 = ctx->stream3;
   const uint64_t group_blocks = ctx->knobs.save_group_blocks ? ctx->knobs.save_group_blocks : ctx->knobs.zc_batch;
-  uint64_t coff = 0;
-  size_t g0 = 0;
-  while (g0 < m) {  // the groups
+  // the groups, and what their seals need at most: the AEAD workspace is
+  // reserved here (ensure() would wait for every stream mid-pipeline), the
+  // seals' records and the headers staged in one pinned buffer, a region per
+  // group (nothing the queued copies read is overwritten within the call)
+  std::vector<size_t> gstart;
+  size_t gmax = 0;
+  uint64_t tmax = 0;
+  for (size_t g0 = 0; g0 < m;) {
     size_t g1 = g0;
-    uint64_t gblk = 0;  // (a group of at least the compressor's batch in blocks: its two streams stay busy)
-    while (g1 < m && gblk < group_blocks) gblk += sext[g1].length ? (sext[g1++].length + kZcBlock - 1) / kZcBlock : (++g1, 1);
-    const size_t gm = g1 - g0;
+    uint64_t gblk = 0, gt = 0;  // (a group of at least the compressor's batch in blocks: its two streams stay busy)
+    while (g1 < m && gblk < group_blocks) {
+      const uint64_t len = sext[g1].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
+      gblk += nb;
+      gt += seal_tiles(zs::kFrameHdr + zs::kBlockHdr * nb + len);  // (the raw frame: the longest encoding)
+      ++g1;
+    }
+    gstart.push_back(g0);
+    gmax = std::max(gmax, g1 - g0);
+    tmax = std::max(tmax, gt);
+    g0 = g1;
+  }
+  gstart.push_back(m);
+  const size_t G = gstart.size() - 1;
+  const uint64_t hdr_bound = pack_bound - bound - over * m;  // (the headers' and trailers' share)
+  const uint64_t hmax = np_max + 1;                           // (headers per seal, at most)
+  uint64_t htiles = 0;
+  {
+    const uint64_t per = (hdr_bound + hmax - 1) / hmax;
+    htiles = hmax * seal_tiles(per + 1) + seal_tiles(hdr_bound);
+  }
+  const size_t stage_bytes = seal_stage_bytes(m) + G * (seal_stage_bytes(hmax) + 256) + hdr_bound + 8 * hmax + 4096;
+  if ((keyed && (rc = seal_workspace(ctx, std::max<size_t>(gmax, hmax), std::max(tmax, htiles)))) ||
+      (rc = ensure_pinned(ctx, ctx->h_meta, ctx->h_meta_cap, stage_bytes)))
+    return cleanup(), rc;
+  uint8_t *const hstage = (uint8_t *)ctx->h_meta;
+  size_t hcur = 0;
+  auto take = [&](size_t bytes) {  // a region of the pinned staging, 64-byte aligned
+    uint8_t *p = hstage + hcur;
+    hcur += (bytes + 63) / 64 * 64;
+    return hcur <= stage_bytes ? p : nullptr;
+  };
+  hipEvent_t ev_comp = nullptr, ev_s3 = nullptr;
+  if (hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ev_s3, hipEventDisableTiming) != hipSuccess)
+    return (ev_comp ? (void)hipEventDestroy(ev_comp) : (void)0), cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
+  evs.push_back(ev_comp);
+  evs.push_back(ev_s3);
+  uint64_t coff = 0;
+  for (size_t g = 0; g < G; ++g) {  // compress a group; its seals, headers and closed packs on stream3
+    const size_t g0 = gstart[g], g1 = gstart[g + 1], gm = g1 - g0;
     size_t cbytes = 0;
     if ((rc = mcdc_zstd_compress_device(ctx, d, n, sch.data() + g0, gm, C + coff, comp_cap - coff, &cbytes,
                                         fr.data() + g0)))
       return cleanup(), rc;
     SAVE_T("group compressed");
+    // (the group's frames are complete: mcdc_zstd_compress_device synchronised
+    // its streams; stream3 is ordered after them by an event all the same)
+    HIP_TRY(hipEventRecord(ev_comp, st));
+    HIP_TRY(hipStreamWaitEvent(s3, ev_comp, 0));
     // place the group's blobs; close the packs the flush rule closes
     closing.clear();
     hbuf.clear();
@@ -1979,16 +2087,14 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     const uint64_t hin = coff + cbytes;
     if (hin + hbuf.size() > comp_cap)  // (frames within their raw bound, headers within pack_bound's share)
       return cleanup(), fail(MCDC_E_INTERNAL, "save path: header staging beyond the compressor buffer");
-    if ((rc = ensure_pinned(ctx, ctx->h_meta, ctx->h_meta_cap, hbuf.size() + 8 * closing.size() + 64)))
-      return cleanup(), rc;
-    uint8_t *hm = (uint8_t *)ctx->h_meta;
-    if (!hbuf.empty()) {
+    uint8_t *hm = hbuf.empty() ? nullptr : take(hbuf.size()), *tr = closing.empty() ? nullptr : take(4 * closing.size());
+    if ((!hbuf.empty() && !hm) || (!closing.empty() && !tr))
+      return cleanup(), fail(MCDC_E_INTERNAL, "save path: header staging full");
+    if (hm) {
       std::memcpy(hm, hbuf.data(), hbuf.size());
-      HIP_TRY(hipMemcpyAsync(C + hin, hm, hbuf.size(), hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(C + hin, hm, hbuf.size(), hipMemcpyHostToDevice, s3));
     }
-    // trailers: le32(encoded header length) after each closing pack's header
-    uint8_t *tr = hm + hbuf.size();
-    for (size_t c = 0; c < closing.size(); ++c) {
+    for (size_t c = 0; c < closing.size(); ++c) {  // trailers: le32(encoded header length)
       const uint32_t el = (uint32_t)(meta[closing[c].k] - 4);
       std::memcpy(tr + 4 * c, &el, 4);
     }
@@ -1997,8 +2103,10 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
       uint64_t end = 0;
       for (size_t i = 0; i < gm; ++i) pl[i] = place[g0 + i], end = std::max(end, place[g0 + i] + lens[g0 + i]);
       pl[gm] = end;
-      if ((rc = aead_run(ctx, 0, store->key, C + coff, cbytes, fr.data() + g0, gm, store->nonces + 12 * g0, D,
-                         ctx->sv_pack.cap, nullptr, nullptr, nullptr, false, pl.data())))
+      uint8_t *sst = take(seal_stage_bytes(gm));
+      if (!sst) return cleanup(), fail(MCDC_E_INTERNAL, "save path: seal staging full");
+      if ((rc = seal_placed(ctx, s3, store->key, C + coff, fr.data() + g0, gm, store->nonces + 12 * g0, D, pl.data(),
+                            sst)))
         return cleanup(), rc;
       if (!closing.empty()) {  // the headers: their frames sealed into place
         std::vector<mcdc_blob> hx(closing.size());
@@ -2013,8 +2121,9 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
           std::memcpy(hn.data() + 12 * c, store->header_nonces + 12 * k, 12);
         }
         hp[closing.size()] = hend;
-        if ((rc = aead_run(ctx, 0, store->key, C + hin, hbuf.size(), hx.data(), closing.size(), hn.data(), D,
-                           ctx->sv_pack.cap, nullptr, nullptr, nullptr, false, hp.data())))
+        uint8_t *hst = take(seal_stage_bytes(closing.size()));
+        if (!hst) return cleanup(), fail(MCDC_E_INTERNAL, "save path: seal staging full");
+        if ((rc = seal_placed(ctx, s3, store->key, C + hin, hx.data(), closing.size(), hn.data(), D, hp.data(), hst)))
           return cleanup(), rc;
       }
     } else {  // frames as they are: the group's frames run by run of one pack, the headers
@@ -2022,29 +2131,23 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
         size_t e = i + 1;
         while (e < g1 && place[e] == place[e - 1] + lens[e - 1]) ++e;
         HIP_TRY(hipMemcpyAsync(D + place[i], C + coff + fr[i].offset, place[e - 1] + lens[e - 1] - place[i],
-                               hipMemcpyDeviceToDevice, st));
+                               hipMemcpyDeviceToDevice, s3));
         i = e;
       }
       for (const Closing &c : closing)
         HIP_TRY(hipMemcpyAsync(D + pk[c.k].offset + pk[c.k].length - meta[c.k], C + hin + c.hpos, c.hlen,
-                               hipMemcpyDeviceToDevice, st));
+                               hipMemcpyDeviceToDevice, s3));
     }
     for (size_t c = 0; c < closing.size(); ++c) {
       const size_t k = closing[c].k;
-      HIP_TRY(hipMemcpyAsync(D + pk[k].offset + pk[k].length - 4, tr + 4 * c, 4, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(D + pk[k].offset + pk[k].length - 4, tr + 4 * c, 4, hipMemcpyHostToDevice, s3));
     }
-    // the closed packs to the host on stream3, after this group's work on st
+    // the closed packs to the host, behind their seals on stream3
     if (!closing.empty()) {
-      hipEvent_t e = nullptr;
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-        return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
-      evs.push_back(e);
-      HIP_TRY(hipEventRecord(e, st));
       const size_t k1 = pk.size();
       overflow |= k1 > packs_cap || (packs_out == nullptr) ||
                   pk[k1 - 1].offset + pk[k1 - 1].length > packs_out_cap;
       if (!overflow) {
-        HIP_TRY(hipStreamWaitEvent(s3, e, 0));
         const uint64_t lo = pk[copied].offset, hi = pk[k1 - 1].offset + pk[k1 - 1].length;
         HIP_TRY(hipMemcpyAsync((uint8_t *)packs_out + lo, D + lo, hi - lo, hipMemcpyDeviceToHost, s3));
         copied = k1;
@@ -2052,12 +2155,10 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     }
     // the next group's frames after this group's frames and headers
     coff = hin + hbuf.size();
-    g0 = g1;
   }
-  // (the host buffers the queued copies read -- pl, hx, hp, hn, hbuf: H2D from
-  // pageable memory returns once the bytes are staged -- and h_meta, read by
-  // this group's copies: every group's copies finished before the next
-  // group's mcdc_zstd_compress_device returned, which synchronises st)
+  // the pack IDs (on st) after the last seals and copies into D (stream3)
+  HIP_TRY(hipEventRecord(ev_s3, s3));
+  HIP_TRY(hipStreamWaitEvent(st, ev_s3, 0));
   const size_t np = pk.size();
   first.push_back(m);
   *npacks = np;
