@@ -455,11 +455,14 @@ int mcdc_device_free(struct mcdc_ctx *ctx, void *d_ptr);
  * second HIP runtime, e.g. torch's, in the libmcdc process). */
 int mcdc_ctx_synchronize(struct mcdc_ctx *ctx);
 /* Per-context settings for tests and tuning (not reference interface):
- *   "zc_batch_blocks"        blocks per GPU compressor batch (default 32768,
- *                            1 GiB; two streams take half each), >= 8
+ *   "zc_batch_blocks"        blocks per GPU compressor batch (default 16384,
+ *                            512 MiB; two streams take half each; ~5 bytes
+ *                            of scratch per byte of a batch), >= 8
  *   "zc_two"                 0: compressor batches on one stream
  *   "save_group_blocks"      GPU save path: 32 KiB blocks per compression
- *                            group (0, the default: "zc_batch_blocks"); the
+ *                            group (0, the default: "zc_batch_blocks" or
+ *                            32768, the larger: a group ends with a host
+ *                            wait, fewer groups wait less); the
  *                            packs a group closes are copied out while the
  *                            next group compresses
  *   "zc_small"               0: chunks of one block (<= 32 KiB) through the

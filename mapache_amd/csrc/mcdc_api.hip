@@ -237,8 +237,8 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_blocks, zc_stage, zc_seqs, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words, zc_recs,
-      zc_blocks2, zc_stage2, zc_seqs2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_recs2;  // (the second batch set)
+      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_blocks, zc_stage, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words,
+      zc_blocks2, zc_stage2, zc_piece2, zc_poff2, zc_tmp2, zc_words2;  // (the second batch set)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -1049,10 +1049,10 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_cls, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs,
-                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_recs,
-                    &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_seqs2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
-                    &ctx->zc_words2, &ctx->zc_recs2};
+                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_cls, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage,
+                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words,
+                    &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
+                    &ctx->zc_words2};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1888,7 +1888,8 @@ static constexpr uint64_t kMinChunkSize = 512 * 1024;  // global::defaults::MIN_
 // compressed and sealed in HBM straight into the packs' layout, hashed there,
 // and copied out pack by pack while the next blobs compress.
 //   * Groups of blobs (in storing order, each at least the compressor's batch
-//     of 32 KiB blocks, "zc_batch_blocks": both of its streams stay busy) go
+//     of 32 KiB blocks, "zc_batch_blocks", and 1 GiB of blocks: both of its
+//     streams stay busy, few host waits) go
 //     through mcdc_zstd_compress_device one after the other.  After a group, its
 //     blobs' encoded sizes are known (frame + kAeadOverhead), so the packer's
 //     flush rule (Packer::add_blob / flush, packer.rs:101-186,
@@ -2012,7 +2013,10 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     return MCDC_OK;
   };
   hipStream_t st = ctx->stream, s3 = ctx->stream3;
-  const uint64_t group_blocks = ctx->knobs.save_group_blocks ? ctx->knobs.save_group_blocks : ctx->knobs.zc_batch;
+  // (a group's compression ends with a host wait: groups of at least 1 GiB of
+  // blocks keep those few; tools/tree_probe.py, 16384 -> 32768: -9 %)
+  const uint64_t group_blocks =
+      ctx->knobs.save_group_blocks ? ctx->knobs.save_group_blocks : std::max<uint64_t>(ctx->knobs.zc_batch, 32768);
   // the groups, and what their seals need at most: the AEAD workspace is
   // reserved here (ensure() would wait for every stream mid-pipeline), the
   // seals' records and the headers staged in one pinned buffer, a region per
@@ -2434,17 +2438,14 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   const uint64_t mb = two ? zb / 2 : std::max(std::min<uint64_t>(total_blocks, zb), longest);
   tmpb = std::max(tmpb, zc_tmp_bytes(mb));
   struct Set {
-    DevBuf *blocks, *stage, *seqs, *piece, *poff, *tmp, *words, *recs;
-  } sets[2] = {{&ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_seqs, &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_tmp,
-                &ctx->zc_words, &ctx->zc_recs},
-               {&ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_seqs2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
-                &ctx->zc_words2, &ctx->zc_recs2}};
+    DevBuf *blocks, *stage, *piece, *poff, *tmp, *words;
+  } sets[2] = {{&ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_tmp, &ctx->zc_words},
+               {&ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2, &ctx->zc_words2}};
   for (int k = 0; k < (two ? 2 : 1); ++k) {
     const Set &z = sets[k];
     if ((rc = ensure(ctx, *z.tmp, tmpb)) || (rc = ensure(ctx, *z.blocks, mb * sizeof(ZcBlock))) ||
-        (rc = ensure(ctx, *z.stage, mb * kZcSlot)) || (rc = ensure(ctx, *z.seqs, mb * kZcSeqCap * 8)) ||
-        (rc = ensure(ctx, *z.piece, (mb + 1) * 8)) || (rc = ensure(ctx, *z.poff, (mb + 1) * 8)) ||
-        (rc = ensure(ctx, *z.words, (mb * kZcBlock + 1024) * 4)) || (rc = ensure(ctx, *z.recs, mb * kZcSeqCap * 8)))
+        (rc = ensure(ctx, *z.stage, mb * kZcSlot + kZcStagePad)) || (rc = ensure(ctx, *z.piece, (mb + 1) * 8)) ||
+        (rc = ensure(ctx, *z.poff, (mb + 1) * 8)) || (rc = ensure(ctx, *z.words, (mb * kZcBlock + 1024) * 4)))
       return rc;
   }
   // [0] setup done on st; [1 + k] set k's last final copy
@@ -2476,8 +2477,7 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
     } while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb);
     const Set &z = sets[k];
     launch_zc_batch((const uint8_t *)d_data, n, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
-                    (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint64_t *)z.seqs->p, (uint32_t *)z.words->p,
-                    (uint64_t *)z.recs->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
+                    (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint32_t *)z.words->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
                     ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
                     two ? ev[1 + k] : nullptr, blongest > kZcSegBlocks, nseg, ctx->knobs.zc_small ? nsmall : nullptr);
     if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
@@ -2523,8 +2523,8 @@ int mcdc_zstd_compress_scratch(mcdc_ctx *ctx, const mcdc_chunk *chunks, size_t n
   // (every buffer as ensure() allocates it, headroom included; the call's
   // own buffers as mcdc_zstd_compress_device requests them)
   const uint64_t tmpb = std::max(zc_tmp_bytes(nchunks), zc_tmp_bytes(mb));
-  const uint64_t set = ensure_bytes(tmpb) + ensure_bytes(mb * sizeof(ZcBlock)) + ensure_bytes(mb * kZcSlot) +
-                       2 * ensure_bytes(mb * kZcSeqCap * 8) + 2 * ensure_bytes((mb + 1) * 8) +
+  const uint64_t set = ensure_bytes(tmpb) + ensure_bytes(mb * sizeof(ZcBlock)) +
+                       ensure_bytes(mb * kZcSlot + kZcStagePad) + 2 * ensure_bytes((mb + 1) * 8) +
                        ensure_bytes((mb * kZcBlock + 1024) * 4);
   const uint64_t call = ensure_bytes(nchunks * sizeof(mcdc_chunk)) + 2 * ensure_bytes((nchunks + 1) * 8) +
                         ensure_bytes(nchunks + 1) +

@@ -161,10 +161,10 @@ struct Knobs {
   int lane_seg_chunks = 4;// MCDC_LANE_SEG_CHUNKS: expected chunks per segment on the lane walk
   bool zc_huf = true;      // MCDC_ZC_HUF: Huffman / RLE literals in the GPU zstd compressor
   bool zc_two = true;      // MCDC_ZC_TWO: compressor batches alternate between two streams
-  uint64_t save_group_blocks = 0;  // GPU save path: blocks per compression group (0: zc_batch)
+  uint64_t save_group_blocks = 0;  // GPU save path: blocks per compression group (0: max(zc_batch, 32768))
   bool zc_small = true;    // chunks of one block through k_zc_small (0: k_zc_probe / k_zc_find, the A/B)
   // set by mcdc_ctx_set_option only (no environment variable):
-  uint64_t zc_batch = 32768;           // "zc_batch_blocks": blocks per compressor batch (two streams: half each)
+  uint64_t zc_batch = 16384;           // "zc_batch_blocks": blocks per compressor batch (two streams: half each)
   bool test_fail_after_index = false;  // "test_fail_after_index": mcdc_save_files fails after its index
                                        // add (test hook: the rollback path, tests/test_gpu_save.py)
   // A/B builds only

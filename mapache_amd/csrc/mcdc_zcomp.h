@@ -12,6 +12,7 @@ namespace mcdc {
 constexpr uint64_t kZcBlock = 32768;               // zstd block: 32 KiB of one chunk
 constexpr uint32_t kZcSeqCap = kZcBlock / 4;       // sequences per block: every match is >= 4 bytes
 constexpr uint64_t kZcSlot = kZcBlock + 64;        // staging bytes per block
+constexpr uint64_t kZcStagePad = 16384;            // staging bytes after a batch's last slot (k_zc_chain's prefetch)
 constexpr uint32_t kZcSegBlocks = 8;               // blocks of a chunk one match-finder workgroup covers
 constexpr uint32_t kZcPrime = 65536;               // bytes before a segment the finder re-inserts
 
@@ -26,8 +27,8 @@ constexpr uint32_t kZcRaw = 1u;
 constexpr uint32_t kZcSegRaw = 2u;  // (on a segment's first record) every block of the segment is kZcRaw
 // Far matches (k_zc_probe / k_zc_far): per block record kZcFarSlots table
 // entries (a segment of kZcSegBlocks records owns kZcSegBlocks x kZcFarSlots
-// slots) and kZcBlock / 1024 anchor ballots, carved from the batch's `recs`
-// scratch (free until k_zc_chain).
+// slots) and kZcBlock / 1024 anchor ballots, carved from the batch's staging
+// slots (free until k_zc_parse).
 constexpr uint32_t kZcFarSlots = 512;
 constexpr uint32_t kZcFarBallots = (uint32_t)(kZcBlock / 1024);
 
@@ -39,17 +40,18 @@ size_t zc_tmp_bytes(uint64_t n);
 void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint64_t *first,
                        uint32_t *err, uint64_t *bound, uint8_t *cls, void *tmp, size_t tmp_bytes, hipStream_t st);
 // Scratch per batch of nblk blocks (bytes), all device memory of the context:
-//   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot, seqs nblk x kZcSeqCap
-//   x 8, state records nblk x kZcSeqCap x 8, match words (nblk x kZcBlock +
-//   1024) x 4 (9 x the batch's input in all: 4.5 GiB for a batch set of
-//   16384 blocks), piece / poff (nblk + 1) x 8.  A batch holds whole chunks,
-//   at most the context's "zc_batch_blocks" (32768: two sets of 16384 on two
-//   streams) unless one chunk is longer (1 GiB: 7 x 2^18 words).
+//   blocks nblk x sizeof(ZcBlock), stage nblk x kZcSlot + kZcStagePad (also
+//   the far tables until k_zc_parse, and the sequence codes), match words
+//   (nblk x kZcBlock + 1024) x 4 (also the sequences, k_zc_huff's section,
+//   the FSE tables and the state records after k_zc_parse), piece / poff
+//   (nblk + 1) x 8: ~5 x the batch's input in all, 2.5 GiB for a batch set of
+//   16384 blocks.  A batch holds whole chunks, at most the context's
+//   "zc_batch_blocks" (two sets of half that on two streams) unless one
+//   chunk is longer (1 GiB: 7 x 2^18 words).
 // one batch: the chunks [c0, c1), blocks [b0, b0 + nblk)
 void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
-                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
-                     uint32_t *words, uint64_t *recs,
-                     const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
+                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage,
+                     uint32_t *words, const zs::ZTables &T, uint64_t *piece, uint64_t *poff, uint64_t *obase, uint8_t *out,
                      uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf = true,
                      hipEvent_t final_after = nullptr, hipEvent_t final_done = nullptr, bool far = true,
                      uint64_t nseg = 0, const uint64_t *nsmall = nullptr);

@@ -103,6 +103,18 @@ constexpr uint32_t kPrime = kZcPrime;         // bytes before a segment re-inser
 // Match words: length (<= kMlCap) << 24 | offset; bit 31 marks a verified
 // kMlCap match of the finder's own (readers take the length as (w >> 24) & 31)
 constexpr uint32_t kZcLocalCap = 1u << 31;
+// A block's kZcBlock words are its only per-block scratch besides the staging
+// slot: the match words until k_zc_parse, which writes the block's sequences
+// over them as it goes (sequence i, 8 bytes at 8 i, is written in the window
+// of a position >= 4 i, after that window's words were read, and every word
+// read later lies at 4 x a later position: never overtaken); the upper half
+// then holds k_zc_huff's section under assembly, after it k_zc_plan's tables
+// and k_zc_chain's state records (kZcHalf: the half's first word).
+constexpr uint32_t kZcHalf = (uint32_t)kZcBlock / 2;
+__device__ __forceinline__ uint64_t *blk_seqs(uint32_t *words, uint64_t bi) {
+  return reinterpret_cast<uint64_t *>(words + bi * kZcBlock);
+}
+static_assert(kZcSeqCap * 8 <= kZcHalf * 4, "sequences in the lower half of the block's words");
 // The parse's run ends (ends[]): kEndNext = take the next position's,
 // kEndLong = still matching kRunExt bytes after kMlCap (the wave extends it)
 constexpr uint32_t kRunExt = 32, kEndNext = 0xFFFFu, kEndLong = 0xFFFEu;
@@ -1009,8 +1021,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return (uint32_t)lane
 // sequence's offset, literal length > 0: rep[0] is always the previous
 // offset when only that code is used) after the block's first sequence.
 __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t nbytes, ZcBlock *blocks, uint64_t nblk,
-                                                 const uint32_t *words, uint8_t *stage, uint64_t *seqs,
-                                                 const uint32_t *porder) {
+                                                 uint32_t *words, uint8_t *stage, const uint32_t *porder) {
   __shared__ uint16_t J[6][257];
   __shared__ uint16_t ends[257], jp[256];
   __shared__ uint8_t mk[260], capl[256];
@@ -1028,7 +1039,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   const uint8_t *p0 = base + B.src;
   const uint32_t *w = words + bi * kZcBlock;
   uint8_t *lit = stage + bi * kZcSlot + zs::kLitHdr;
-  uint64_t *sq = seqs + bi * kZcSeqCap;
+  uint64_t *sq = blk_seqs(words, bi);  // (over the words already read: see kZcHalf)
   uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0, last_off = 0;  // (last_off 0: no sequence yet)
   if (lane == 0) {
     for (int k = 0; k < 6; ++k) J[k][256] = 256;
@@ -1480,7 +1491,7 @@ __device__ void huf_build_wave(const uint32_t (&c)[4], const uint32_t (&r)[4], u
 //            the last literal first), a lane per piece: its bit count, a
 //            wave scan for its offset, then its bits packed in a register
 //            and stored a word at a time into the block's match-word
-//            scratch (free after k_zc_parse; words shared with a
+//            scratch's upper half (the sequences fill at most the lower; words shared with a
 //            neighbouring piece OR-ed in)
 //   store    header, tree, jump table; the section copied to the slot
 // (LDS ~9 KiB per wave: 16 waves per CU; the section itself stays in HBM.)
@@ -1628,7 +1639,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
   if (one && csize >= 1024) return;  // (one stream: 10-bit sizes)
   const uint32_t hdr = lit_hdr_size(n, csize, one);
-  uint32_t *sw = scratch + bi * kZcBlock;  // the section under assembly (words)
+  uint32_t *sw = scratch + bi * kZcBlock + kZcHalf;  // the section under assembly (the words' upper half)
   const uint32_t nq = (total + 3) / 4 + 1;
   for (uint32_t k = lane; k < nq; k += 64) sw[k] = 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (same wave: agent scope would write back the L2)
@@ -1818,7 +1829,9 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
 //                sequences, LDS atomics), seq_plan on lane 0 (per symbol type
 //                the block's own FSE_Compressed_Mode table or the predefined
 //                one), the own tables built by the wave; plan and tables to
-//                the block's match-word scratch (free after k_zc_huff)
+//                the upper half of the block's match-word scratch (free
+//                after k_zc_huff), the codes to the staging slot after the
+//                raw literals (free until k_zc_encode)
 //   k_zc_chain   ONE LANE PER STATE MACHINE, 9 blocks x 3 types per wave:
 //                the wave's 27 tables in LDS, each lane walks its block's
 //                sequences from the last to the first, per sequence the state
@@ -1832,24 +1845,36 @@ __device__ void fse_build_wave(const int16_t *norm, uint32_t tl, FseCTL &ct, uin
 //                partial last word carried; then the final states, the end
 //                mark and the header (count, modes, descriptions)
 // The block stays raw when the compressed block is not smaller.
-struct ZcSeqTab {    // (in the block's match-word scratch)
+struct ZcSeqTab {    // (in the upper half of the block's match-word scratch)
   FseCTL t[3];       // LL, OF, ML: own or predefined
   uint32_t fin[3];   // final states (k_zc_chain)
   uint32_t sbits[3]; // state bits of each machine's sequences (k_zc_chain)
   uint32_t xbits;    // extra bits of the block's sequences (k_zc_plan)
   SeqPlan P;
 };
-static_assert(sizeof(ZcSeqTab) <= kZcBlock * 4, "sequence tables exceed the block's scratch");
 __device__ __forceinline__ ZcSeqTab *seq_tab(uint32_t *words, uint64_t bi) {
-  return reinterpret_cast<ZcSeqTab *>(words + bi * kZcBlock);
+  return reinterpret_cast<ZcSeqTab *>(words + bi * kZcBlock + kZcHalf);
 }
-// After the tables: per symbol type the sequences' codes, one byte each, the
-// last sequence first (k_zc_chain's walking order), + 8 bytes of slack.
+// After the tables: k_zc_chain's state records, three arrays of kZcSeqCap
+// 16-bit words (LL, OF, ML), by sequence.
 constexpr uint32_t kSeqTabBytes = (sizeof(ZcSeqTab) + 15) / 16 * 16;
-static_assert(kSeqTabBytes + 3 * (kZcSeqCap + 8) <= kZcBlock * 4, "sequence codes exceed the block's scratch");
-__device__ __forceinline__ uint8_t *seq_codes(uint32_t *words, uint64_t bi, uint32_t k) {
-  return reinterpret_cast<uint8_t *>(words + bi * kZcBlock) + kSeqTabBytes + k * (kZcSeqCap + 8);
+static_assert(kSeqTabBytes + 3 * kZcSeqCap * 2 + 256 <= kZcHalf * 4, "tables and state records exceed the upper half");
+__device__ __forceinline__ uint16_t *blk_recs(uint32_t *words, uint64_t bi) {
+  return reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(seq_tab(words, bi)) + kSeqTabBytes);
 }
+// Per symbol type the sequences' codes, one byte each, the last sequence
+// first (k_zc_chain's walking order), + 8 bytes of slack, in the staging slot
+// after the raw literals (16-byte aligned): every sequence covers a match of
+// at least 4 bytes, so nlit + 4 nseq <= len and the three arrays fit in the
+// slot; k_zc_huff's section is shorter than the raw literals it replaces, and
+// k_zc_encode writes over the codes only after k_zc_chain read them.
+// (k_zc_chain's prefetches read up to kZcCodeOver bytes past a block's codes:
+// the staging buffer carries that much more, kZcStagePad.)
+__device__ __forceinline__ uint8_t *seq_codes(uint8_t *stage, uint64_t bi, uint32_t nlit, uint32_t nseq, uint32_t k) {
+  return stage + bi * kZcSlot + ((kLitHdr + nlit + 15) & ~15u) + k * (nseq + 8);
+}
+static_assert(kLitHdr + 15 + 3 * 8 + kZcBlock <= kZcSlot, "codes fit the staging slot (nlit + 3 nseq <= len)");
+static_assert(kZcSeqCap + 64 <= kZcStagePad, "staging pad covers k_zc_chain's reads past the codes");
 
 // Float sum over the wave's 64 lanes (DPP, as wave_incl_sum), the total in every lane.
 __device__ __forceinline__ float wave_sum_f(float v) {
@@ -1919,7 +1944,7 @@ __device__ void seq_plan_wave(uint32_t (*cnt)[53], uint32_t nseq, SeqPlan &P, ui
   }
 }
 
-__global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t nblk, const uint64_t *seqs,
+__global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
                                                 uint32_t *words, ZTables T, const uint32_t *porder) {
   __shared__ FseCTL tb[3];
   __shared__ SeqPlan P;
@@ -1930,11 +1955,12 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   if (ns == 0) return;
-  const uint64_t *sq = seqs + bi * kZcSeqCap;
+  const uint64_t *sq = blk_seqs(words, bi);
   ZT_DECL;
   for (uint32_t k = lane; k < 3 * 53; k += 64) (&hist[0][0])[k] = 0;
   __syncthreads();
-  uint8_t *cd0 = seq_codes(words, bi, 0), *cd1 = seq_codes(words, bi, 1), *cd2 = seq_codes(words, bi, 2);
+  uint8_t *cd0 = seq_codes(stage, bi, B.nlit, ns, 0), *cd1 = seq_codes(stage, bi, B.nlit, ns, 1),
+          *cd2 = seq_codes(stage, bi, B.nlit, ns, 2);
   uint32_t xb = 0;  // extra bits
   // (64 sequences per step, the next step's requested meanwhile outside the
   // compiler's wait counting: see ald16s)
@@ -2008,7 +2034,7 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
 // them their codes, one byte per sequence, in walking order.
 constexpr uint32_t kChainBlocks = 9;
 constexpr uint32_t kChainSplit = 64;  // blocks with at least this many sequences: two lanes per state machine
-__global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t nblk, uint64_t *recs,
+__global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
                                                  uint32_t *words) {
   __shared__ FseCTL tb[3 * kChainBlocks];
   const uint32_t lane = lane_id();
@@ -2043,15 +2069,15 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   const uint32_t j = min(jk / 3, kChainBlocks - 1), k = jk % 3;
   const uint64_t b = g0 + j;
   const bool act = lane < 6 * kChainBlocks && b < nblk;
-  const uint32_t ns = act ? blocks[b].nseq : 0u;
+  const uint32_t ns = act ? blocks[b].nseq : 0u, nl = blocks[act ? b : 0].nlit;
   const bool split = ns >= kChainSplit;
   const uint32_t h = split ? ns / 2 : ns;                       // half 0: codes [1, h), half 1: [h, ns)
   const uint32_t m_lo = half ? h : 1u, m_hi = half ? (split ? ns : h) : h;
   const uint32_t nsl = m_hi > m_lo ? m_hi - m_lo : 0u;
   const FseCTL &ct = tb[3 * j + k];
   // type k's state records, one 16-bit word per sequence (sequence order)
-  uint16_t *rec = reinterpret_cast<uint16_t *>(recs + (act ? b : 0) * kZcSeqCap) + k * kZcSeqCap;
-  const uint8_t *cd = seq_codes(words, act ? b : 0, k);  // codes in walking order: cd[m] = sequence ns - 1 - m
+  uint16_t *rec = blk_recs(words, act ? b : 0) + k * kZcSeqCap;
+  const uint8_t *cd = seq_codes(stage, act ? b : 0, nl, act ? ns : blocks[0].nseq, k);  // cd[m] = sequence ns - 1 - m
   const uint8_t *cdl = cd + m_lo;
   // 16 sequences per batch: codes of batch t in a register quad, of batch
   // t + 1 in flight (a load outside the compiler's wait counting, waited
@@ -2159,8 +2185,7 @@ __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint64_t lo, 
 }
 
 __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                  const uint64_t *seqs, const uint64_t *recs, uint32_t *words,
-                                                  uint64_t *piece) {
+                                                  uint32_t *words, uint64_t *piece) {
   MCDC_VGPR_PAD(40);  // (not an exact fill)
   constexpr uint32_t kWbWords = 512 + 64 * 96 / 32 + 8;  // 512 words + a batch's bits + slack
   __shared__ uint32_t wb[kWbWords];
@@ -2170,9 +2195,9 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   if (bi >= nblk) return;
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
-  const uint64_t *sq = seqs + bi * kZcSeqCap;
+  const uint64_t *sq = blk_seqs(words, bi);
   // the state records: three arrays of kZcSeqCap 16-bit words (LL, OF, ML), by sequence
-  const uint16_t *rec = reinterpret_cast<const uint16_t *>(recs + bi * kZcSeqCap);
+  const uint16_t *rec = blk_recs(words, bi);
   uint8_t *st = stage + bi * kZcSlot;
   uint32_t csize = 0;
   if (ns || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
@@ -2373,8 +2398,8 @@ void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint
 }
 
 void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
-                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage, uint64_t *seqs,
-                     uint32_t *words, uint64_t *recs, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
+                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage,
+                     uint32_t *words, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
                      hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg, const uint64_t *nsmall) {
@@ -2386,8 +2411,9 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
   // finder's segment order and the parse's block order)
   uint32_t *order = reinterpret_cast<uint32_t *>(piece), *porder = order + nblk;
   hipLaunchKernelGGL(k_zc_segorder, dim3(1), dim3(1024), 0, st, blocks, nblk, order, porder);
-  // (the far tables and ballots live in recs, free until k_zc_chain)
-  uint32_t *ftab = reinterpret_cast<uint32_t *>(recs);
+  // (the far tables and ballots live in the staging slots, free until k_zc_parse)
+  static_assert(kZcFarSlots * 4 + kZcFarBallots * 8 <= kZcSlot, "far tables in the staging slots");
+  uint32_t *ftab = reinterpret_cast<uint32_t *>(stage);
   uint64_t *fbits = reinterpret_cast<uint64_t *>(ftab + nblk * kZcFarSlots);
   // the probe over the segments of longer chunks (the front of the order),
   // the small chunks (one block) by k_zc_small per size class (then the
@@ -2427,15 +2453,15 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
     hipLaunchKernelGGL(k_zc_far, gfar, dim3(256), 0, st, base, nbytes, blocks, nblk, ftab, fbits, words, false);
   if (nwork) {
     hipLaunchKernelGGL(k_zc_parse, dim3((unsigned)nwork), dim3(64), 0, st, base, nbytes, blocks, nblk, words, stage,
-                       seqs, porder);
+                       porder);
     if (huf)
       hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nwork), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words,
                          porder);
-    hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nwork), dim3(64), 0, st, blocks, nblk, seqs, words, T, porder);
+    hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nwork), dim3(64), 0, st, blocks, nblk, stage, words, T, porder);
   }
   hipLaunchKernelGGL(k_zc_chain, dim3((unsigned)((nblk + kChainBlocks - 1) / kChainBlocks)), dim3(64), 0, st, blocks,
-                     nblk, recs, words);
-  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, seqs, recs, words, piece);
+                     nblk, stage, words);
+  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, words, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);
   if (final_after) (void)hipStreamWaitEvent(st, final_after, 0);

@@ -392,9 +392,12 @@ def test_scratch_query(ctx):
     small = np.zeros(3, dtype=_lib.CHUNK_DTYPE)
     small["length"] = [100_000, 65_536, 1]
     s = ctx.zstd_compress_scratch(small)
-    assert 9 * 6 * 32768 < s < 16 * 6 * 32768 + (1 << 20)  # (6 blocks: ~9-10 bytes of scratch per byte)
+    assert 4.5 * 6 * 32768 < s < 8 * 6 * 32768 + (1 << 20)  # (6 blocks: ~5 bytes of scratch per byte + pads)
     big = np.zeros(40_000, dtype=_lib.CHUNK_DTYPE)
     big["length"] = 65_536
     b = ctx.zstd_compress_scratch(big)
-    assert 9 * 32768 * 32768 < b < 11 * 32768 * 32768  # (two sets of 16384 blocks: the default batch)
+    # (two sets of 8192 blocks, the default batch of 16384: ~5 bytes per byte of
+    # scratch, the sequences, tables and state records aliased into the match
+    # words; at most 3 GiB for a worker context)
+    assert 4.5 * 16384 * 32768 < b <= 3 << 30
     assert ctx.zstd_compress_scratch(big[:0]) == 0
