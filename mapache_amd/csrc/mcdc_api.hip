@@ -222,7 +222,8 @@ struct mcdc_ctx {
   size_t max_bytes = 0;
   hipStream_t stream = nullptr;   // scan (and input copies)
   hipStream_t stream2 = nullptr;  // chain resolution, overlapping the scan's later parts
-  hipStream_t stream3 = nullptr;  // the GPU save path's pack copies to the host, beside the compressor
+  hipStream_t stream3 = nullptr;  // the GPU save path's seals and pack assembly, beside the compressor
+  hipStream_t stream4 = nullptr;  // the GPU save path's pack copies to the host, beside the seals
   hipEvent_t ev_start = nullptr, ev_scan = nullptr, ev_end = nullptr, ev_h2d0 = nullptr,
              ev_h2d1 = nullptr;
   hipEvent_t ev_part[kMaxParts] = {};
@@ -237,8 +238,9 @@ struct mcdc_ctx {
       link_seg, link_idx, link_pos, file_flags, seg_true, entry_idx, seg_count, seg_off, out, err,
       scan_tmp, seg_incl, irr, tile_ctr, b3_chunks, b3_gcnt, b3_goff, b3_owner, b3_nodes, b3_ids, b3_tmp, b3_hist, enc_in, enc_out, zf_sz, zf_off, zf_tmp, zf_ext,
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
-      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_blocks, zc_stage, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words,
-      zc_blocks2, zc_stage2, zc_piece2, zc_poff2, zc_tmp2, zc_words2;  // (the second batch set)
+      sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_wcnt, zc_wfirst, zc_blocks, zc_stage, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words,
+      zc_extra, zc_blocks2, zc_stage2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_extra2,  // (the second batch set)
+      sv_zch, sv_zpre, sv_zext;  // (the GPU save path's compressor input: all blobs, prefixes, frame extents)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -294,6 +296,7 @@ int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream3));
+    HIP_TRY(hipStreamSynchronize(ctx->stream4));
     HIP_TRY(hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -314,6 +317,7 @@ int ensure_stage(mcdc_ctx *ctx, size_t bytes) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream3));
+    HIP_TRY(hipStreamSynchronize(ctx->stream4));
     HIP_TRY(hipHostFree(ctx->h_stage));
     ctx->h_stage = nullptr;
     ctx->h_stage_cap = 0;
@@ -334,6 +338,7 @@ int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream3));
+    HIP_TRY(hipStreamSynchronize(ctx->stream4));
     HIP_TRY(hipHostFree(ctx->h_tab));
     ctx->h_tab = nullptr;
     ctx->h_tab_cap = 0;
@@ -354,6 +359,7 @@ int ensure_fcnt(mcdc_ctx *ctx, size_t n) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream3));
+    HIP_TRY(hipStreamSynchronize(ctx->stream4));
     HIP_TRY(hipHostFree(ctx->h_fcnt));
     ctx->h_fcnt = nullptr;
     ctx->h_fcnt_cap = 0;
@@ -376,6 +382,7 @@ int ensure_pinned(mcdc_ctx *ctx, void *&p, size_t &cap, size_t bytes) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream2));
     HIP_TRY(hipStreamSynchronize(ctx->stream3));
+    HIP_TRY(hipStreamSynchronize(ctx->stream4));
     HIP_TRY(hipHostFree(p));
     p = nullptr;
     cap = 0;
@@ -998,7 +1005,8 @@ int mcdc_ctx_create(int device, size_t max_bytes, mcdc_ctx **out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream4, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(MCDC_E_DEVICE, "hipStreamCreate failed"));
   hipEvent_t *evs[] = {&ctx->ev_start, &ctx->ev_scan, &ctx->ev_end, &ctx->ev_h2d0, &ctx->ev_h2d1};
   for (hipEvent_t *e : evs)
@@ -1032,6 +1040,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
+  if (ctx->stream4) (void)hipStreamSynchronize(ctx->stream4);
   if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_fcnt) (void)hipHostFree(ctx->h_fcnt);
@@ -1049,10 +1058,10 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zf_off, &ctx->zf_tmp, &ctx->zf_ext,
                     &ctx->ae_ext, &ctx->ae_nonce, &ctx->ae_olen, &ctx->ae_tcnt, &ctx->ae_ooff, &ctx->ae_toff,
                     &ctx->ae_tmp, &ctx->ae_rec, &ctx->ae_keys, &ctx->ae_owner, &ctx->ae_tsum, &ctx->ae_status,
-                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_cls, &ctx->zc_first, &ctx->zc_blocks, &ctx->zc_stage,
-                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words,
+                    &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_cls, &ctx->zc_first, &ctx->zc_wcnt, &ctx->zc_wfirst, &ctx->zc_blocks, &ctx->zc_stage,
+                    &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_extra,
                     &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
-                    &ctx->zc_words2};
+                    &ctx->zc_words2, &ctx->zc_extra2, &ctx->sv_zch, &ctx->sv_zpre, &ctx->sv_zext};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -1070,6 +1079,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
+  if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
   delete ctx;
 }
 
@@ -1307,6 +1317,7 @@ int mcdc_ctx_synchronize(mcdc_ctx *ctx) {
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream2));
   HIP_TRY(hipStreamSynchronize(ctx->stream3));
+  HIP_TRY(hipStreamSynchronize(ctx->stream4));
   HIP_TRY(hipStreamSynchronize(nullptr));
   return MCDC_OK;
 }
@@ -1877,6 +1888,132 @@ static void fill_pack_records(const PackPlan &P, const uint8_t *pid, mcdc_pack *
 
 // ------------------------------------------------------------ save path --
 
+// ---------------------------------------------------- zstd compression --
+// The compressor's batches: whole chunks, in order, each within `cap_w` words
+// (zc_span, ~ its input bytes) and `cap_b` blocks unless one chunk is
+// longer.  Two scratch sets on two streams (batches alternate) when the list
+// takes more than one set of "zc_batch_blocks" / 2 x 32 KiB of words; one
+// set of up to the whole batch otherwise.  first / wfirst: the chunks'
+// block and word prefixes (n + 1 entries, relative: only differences count).
+struct ZcBatches {
+  std::vector<size_t> cut;  // batch k: chunks [cut[k], cut[k + 1])
+  uint64_t mw = 0, mb = 0;  // the largest batch's words and blocks (the scratch sets' sizes)
+  bool two = false;
+};
+static ZcBatches zc_batches(const uint64_t *first, const uint64_t *wfirst, size_t n, const Knobs &kn) {
+  ZcBatches r;
+  uint64_t longest_w = 0, longest_b = 0;
+  for (size_t i = 0; i < n; ++i) {
+    longest_w = std::max(longest_w, wfirst[i + 1] - wfirst[i]);
+    longest_b = std::max(longest_b, first[i + 1] - first[i]);
+  }
+  const uint64_t zb = kn.zc_batch, set_w = std::min<uint64_t>(zb / 2 * kZcBlock, 1ull << 31);
+  const uint64_t total_w = wfirst[n] - wfirst[0], total_b = first[n] - first[0];
+  r.two = kn.zc_two && total_w > set_w && longest_w <= set_w;
+  // (blocks: twice the words' full blocks, so that a set of shorter blocks
+  // -- small files -- still holds the words' worth of input)
+  const uint64_t cap_w = r.two ? set_w : std::max(std::min<uint64_t>(total_w, 2 * set_w), longest_w);
+  const uint64_t cap_b = r.two ? zb : std::max(std::min<uint64_t>(total_b, 2 * zb), longest_b);
+  for (size_t c0 = 0; c0 < n;) {
+    size_t c1 = c0 + 1;
+    while (c1 < n && wfirst[c1 + 1] - wfirst[c0] <= cap_w && first[c1 + 1] - first[c0] <= cap_b) ++c1;
+    r.cut.push_back(c0);
+    r.mw = std::max(r.mw, wfirst[c1] - wfirst[c0]);
+    r.mb = std::max(r.mb, first[c1] - first[c0]);
+    c0 = c1;
+  }
+  r.cut.push_back(n);
+  return r;
+}
+// A scratch set's buffers for batches of up to mw words and mb blocks.
+static uint64_t zc_set_words_bytes(uint64_t mw) { return (mw + 1024) * 4; }
+static uint64_t zc_set_stage_bytes(uint64_t mw, uint64_t mb) { return mw + 64 * mb + kZcStagePad; }
+
+// The scratch sets for batches of up to mw words and mb blocks (set 1 only
+// with two streams); set 0's tmp also holds the call's own scans (tmpb).
+static int zc_ensure_sets(mcdc_ctx *ctx, uint64_t mw, uint64_t mb, bool two, size_t tmpb) {
+  DevBuf *const sets[2][7] = {{&ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_tmp,
+                               &ctx->zc_words, &ctx->zc_extra},
+                              {&ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
+                               &ctx->zc_words2, &ctx->zc_extra2}};
+  const size_t bytes[7] = {mb * sizeof(ZcBlock), zc_set_stage_bytes(mw, mb), (mb + 1) * 8, (mb + 1) * 8,
+                           std::max(tmpb, zc_tmp_bytes(mb)), zc_set_words_bytes(mw), mb * kZcExtra};
+  for (int k = 0; k < (two ? 2 : 1); ++k)
+    for (int b = 0; b < 7; ++b) {
+      const int rc = ensure(ctx, *sets[k][b], bytes[b]);
+      if (rc) return rc;
+    }
+  return MCDC_OK;
+}
+
+// One compression call's batches enqueued on the context's streams, no host
+// wait: chunks [0, nchunks) of dch with their block / word prefixes (first /
+// wfirst on the device, hfirst / hwfirst on the host, same base) and the
+// k_zc_small classes hcls; frames back to back from d_out (the running offset
+// in misc[2], reset here), extents to ext.  The sets must hold zbt's batches
+// (zc_ensure_sets); on return ctx->stream is ordered after every batch.
+static int zc_enqueue(mcdc_ctx *ctx, const uint8_t *d_data, size_t n, const DevChunk *dch, const uint64_t *first,
+                      const uint64_t *wfirst, const uint64_t *hfirst, const uint64_t *hwfirst, const uint8_t *hcls,
+                      const ZcBatches &zbt, uint8_t *d_out, uint64_t *ext, uint64_t *misc) {
+  static const zs::ZTables T = zs::build_tables();
+  hipStream_t st = ctx->stream;
+  const bool two = zbt.two;
+  const size_t tmpb = ctx->zc_tmp.cap;
+  const size_t tmpb2 = ctx->zc_tmp2.cap;
+  struct Set {
+    DevBuf *blocks, *stage, *piece, *poff, *tmp, *words, *extra;
+    size_t tmpb;
+  } sets[2] = {{&ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_tmp, &ctx->zc_words,
+                &ctx->zc_extra, tmpb},
+               {&ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2, &ctx->zc_words2,
+                &ctx->zc_extra2, tmpb2}};
+  HIP_TRY(hipMemsetAsync(misc + 2, 0, 8, st));
+  // [0] setup done on st; [1 + k] set k's last final copy
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  auto destroy = [&]() {
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (auto &e : ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return e = nullptr, destroy(), fail(MCDC_E_DEVICE, "event creation failed");
+  hipStream_t ss[2] = {st, ctx->stream2};
+  if (two) {
+    const int rc = hipEventRecord(ev[0], st) == hipSuccess && hipStreamWaitEvent(ss[1], ev[0], 0) == hipSuccess
+                       ? MCDC_OK
+                       : fail(MCDC_E_DEVICE, "stream ordering failed");
+    if (rc) return destroy(), rc;
+  }
+  int k = 0, prev = -1;  // set of the batch, set of the batch before
+  for (size_t bt = 0; bt + 1 < zbt.cut.size(); ++bt, k ^= two ? 1 : 0) {
+    const size_t c0 = zbt.cut[bt], c1 = zbt.cut[bt + 1];
+    uint64_t nseg = 0, nsmall[4] = {0, 0, 0, 0};  // (chunks of one block per k_zc_small class)
+    uint64_t blongest = 0;  // (the batch's longest chunk in blocks: k_zc_far only above one segment)
+    for (size_t c = c0; c < c1; ++c) {
+      const uint64_t nbk = hfirst[c + 1] - hfirst[c];
+      blongest = std::max(blongest, nbk);
+      nseg += (nbk + kZcSegBlocks - 1) / kZcSegBlocks;
+      if (hcls[c] < 4) ++nsmall[hcls[c]];
+    }
+    const uint64_t nblk = hfirst[c1] - hfirst[c0];
+    const Set &z = sets[k];
+    if (nblk > zbt.mb || hwfirst[c1] - hwfirst[c0] > zbt.mw || z.words->cap < zc_set_words_bytes(hwfirst[c1] - hwfirst[c0]) ||
+        z.extra->cap < nblk * kZcExtra || z.stage->cap < zc_set_stage_bytes(hwfirst[c1] - hwfirst[c0], nblk))
+      return destroy(), fail(MCDC_E_INTERNAL, "compressor batch beyond its scratch set");
+    launch_zc_batch(d_data, n, dch, first, wfirst, c0, c1, hfirst[c0], nblk, (ZcBlock *)z.blocks->p,
+                    (uint8_t *)z.stage->p, (uint32_t *)z.words->p, (uint8_t *)z.extra->p, T, (uint64_t *)z.piece->p,
+                    (uint64_t *)z.poff->p, misc + 2, d_out, ext, z.tmp->p, z.tmpb, ss[k], ctx->knobs.zc_huf,
+                    two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr, two ? ev[1 + k] : nullptr,
+                    blongest > kZcSegBlocks, nseg, ctx->knobs.zc_small ? nsmall : nullptr);
+    if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
+    prev = k;
+  }
+  if (two && prev == 1 && hipStreamWaitEvent(st, ev[2], 0) != hipSuccess)
+    return destroy(), fail(MCDC_E_DEVICE, "stream ordering failed");
+  destroy();
+  return MCDC_OK;
+}
+
 // The Archiver's save path for a run of files (processor.rs:138-205 +
 // Repository::save_blob, repository_v1.rs:155-195), composed from the stages
 // above: size gate, chunking (GPU), chunk IDs (GPU), dedup (GPU index),
@@ -1887,10 +2024,11 @@ static constexpr uint64_t kMinChunkSize = 512 * 1024;  // global::defaults::MIN_
 // GPU encode (store->gpu_compress): the stored blobs of the device copy d are
 // compressed and sealed in HBM straight into the packs' layout, hashed there,
 // and copied out pack by pack while the next blobs compress.
-//   * Groups of blobs (in storing order, each at least the compressor's batch
-//     of 32 KiB blocks, "zc_batch_blocks", and 1 GiB of blocks: both of its
-//     streams stay busy, few host waits) go
-//     through mcdc_zstd_compress_device one after the other.  After a group, its
+//   * Groups of blobs (in storing order, 1 GiB of 32 KiB blocks or the
+//     compressor's batch, the larger; the last ones halving) are compressed
+//     by zc_enqueue one after the other on the compressor's streams, every
+//     input uploaded once, so the next group's batches queue before the host
+//     waits for a group: no gap between groups.  After a group, its
 //     blobs' encoded sizes are known (frame + kAeadOverhead), so the packer's
 //     flush rule (Packer::add_blob / flush, packer.rs:101-186,
 //     repository_v1.rs:185-193) places every blob of the group: a blob's pack
@@ -1955,6 +2093,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   std::vector<uint8_t> hbuf;        // host: raw-framed headers of the packs closing in a group
   std::vector<hipEvent_t> evs;
   auto cleanup = [&]() {  // (every exit: nothing queued may still write the caller's buffer)
+    (void)hipStreamSynchronize(ctx->stream4);
     (void)hipStreamSynchronize(ctx->stream3);
     (void)hipStreamSynchronize(ctx->stream);
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -2012,11 +2151,16 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     open = false;
     return MCDC_OK;
   };
-  hipStream_t st = ctx->stream, s3 = ctx->stream3;
-  // (a group's compression ends with a host wait: groups of at least 1 GiB of
-  // blocks keep those few; tools/tree_probe.py, 16384 -> 32768: -9 %)
+  hipStream_t st = ctx->stream, s3 = ctx->stream3, s4 = ctx->stream4;
+  // Groups of at least 1 GiB of blocks, the last ones halving: a group's
+  // seals and pack copies (stream3, about half its compression time) hide
+  // behind the next group's compression, and only the last, small group's
+  // are left after the compressor finishes.
   const uint64_t group_blocks =
       ctx->knobs.save_group_blocks ? ctx->knobs.save_group_blocks : std::max<uint64_t>(ctx->knobs.zc_batch, 32768);
+  constexpr uint64_t kTailBlocks = 8192;  // (the halving stops here: a seal call has ~0.3 ms of fixed latency)
+  uint64_t left = 0;
+  for (size_t k = 0; k < m; ++k) left += sext[k].length ? (sext[k].length + kZcBlock - 1) / kZcBlock : 1;
   // the groups, and what their seals need at most: the AEAD workspace is
   // reserved here (ensure() would wait for every stream mid-pipeline), the
   // seals' records and the headers staged in one pinned buffer, a region per
@@ -2026,8 +2170,11 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   uint64_t tmax = 0;
   for (size_t g0 = 0; g0 < m;) {
     size_t g1 = g0;
-    uint64_t gblk = 0, gt = 0;  // (a group of at least the compressor's batch in blocks: its two streams stay busy)
-    while (g1 < m && gblk < group_blocks) {
+    uint64_t gblk = 0, gt = 0;
+    const uint64_t target = left > 2 * group_blocks ? group_blocks
+                            : left > 2 * kTailBlocks ? std::max<uint64_t>(left / 2, kTailBlocks)
+                                                     : left;
+    while (g1 < m && gblk < target) {
       const uint64_t len = sext[g1].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
       gblk += nb;
       gt += seal_tiles(zs::kFrameHdr + zs::kBlockHdr * nb + len);  // (the raw frame: the longest encoding)
@@ -2036,6 +2183,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     gstart.push_back(g0);
     gmax = std::max(gmax, g1 - g0);
     tmax = std::max(tmax, gt);
+    left -= std::min(left, gblk);
     g0 = g1;
   }
   gstart.push_back(m);
@@ -2047,8 +2195,9 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     const uint64_t per = (hdr_bound + hmax - 1) / hmax;
     htiles = hmax * seal_tiles(per + 1) + seal_tiles(hdr_bound);
   }
-  const size_t stage_bytes = seal_stage_bytes(m) + G * (seal_stage_bytes(hmax) + 256) + hdr_bound + 8 * hmax + 4096;
-  if ((keyed && (rc = seal_workspace(ctx, std::max<size_t>(gmax, hmax), std::max(tmax, htiles)))) ||
+  const size_t stage_bytes =
+      seal_stage_bytes(m) + G * (seal_stage_bytes(hmax) + 256) + hdr_bound + 8 * hmax + 16 * m + 4096;
+  if ((keyed && (rc = seal_workspace(ctx, gmax + hmax, tmax + htiles))) ||
       (rc = ensure_pinned(ctx, ctx->h_meta, ctx->h_meta_cap, stage_bytes)))
     return cleanup(), rc;
   uint8_t *const hstage = (uint8_t *)ctx->h_meta;
@@ -2058,24 +2207,76 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     hcur += (bytes + 63) / 64 * 64;
     return hcur <= stage_bytes ? p : nullptr;
   };
-  hipEvent_t ev_comp = nullptr, ev_s3 = nullptr;
-  if (hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ev_s3, hipEventDisableTiming) != hipSuccess)
-    return (ev_comp ? (void)hipEventDestroy(ev_comp) : (void)0), cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
-  evs.push_back(ev_comp);
+  // The compressor's input for every group, uploaded once (no upload or host
+  // wait between groups): the blobs, their block / word prefixes and classes
+  // on the host and in HBM, each group's batches, the scratch sets for the
+  // largest; group g's frames at C + cstart[g] (its raw bound reserved), the
+  // headers after all of them (at C + bound).
+  std::vector<uint64_t> zpre(2 * (m + 1), 0);
+  std::vector<uint8_t> zcls(m);
+  uint64_t *const zfirst = zpre.data(), *const zwfirst = zpre.data() + m + 1;
+  for (size_t k = 0; k < m; ++k) {
+    const uint64_t len = sext[k].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
+    zfirst[k + 1] = zfirst[k] + nb;
+    zwfirst[k + 1] = zwfirst[k] + zc_span(len);
+    zcls[k] = nb == 1 ? (uint8_t)zc_small_class(len) : (uint8_t)4;
+  }
+  std::vector<ZcBatches> zbs(G);
+  std::vector<uint64_t> cstart(G + 1, 0);
+  uint64_t zmw = 0, zmb = 0;
+  bool ztwo = false;
+  for (size_t g = 0; g < G; ++g) {
+    const size_t g0 = gstart[g], g1 = gstart[g + 1];
+    zbs[g] = zc_batches(zfirst + g0, zwfirst + g0, g1 - g0, ctx->knobs);
+    zmw = std::max(zmw, zbs[g].mw), zmb = std::max(zmb, zbs[g].mb), ztwo |= zbs[g].two;
+    uint64_t gb = 0;
+    for (size_t k = g0; k < g1; ++k)
+      gb += zs::kFrameHdr + zs::kBlockHdr * (zfirst[k + 1] - zfirst[k]) + sext[k].length;
+    cstart[g + 1] = cstart[g] + gb;
+  }
+  if ((rc = stage_arg(ctx, ctx->sv_zch, sch.data(), m * sizeof(mcdc_chunk))) ||
+      (rc = stage_arg(ctx, ctx->sv_zpre, zpre.data(), zpre.size() * 8)) || (rc = ensure(ctx, ctx->sv_zext, 16 * m)) ||
+      (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = zc_ensure_sets(ctx, zmw, zmb, ztwo, 0)))
+    return cleanup(), rc;
+  HIP_TRY(hipStreamSynchronize(st));  // (the uploads read pageable host memory)
+  const DevChunk *zch = (const DevChunk *)ctx->sv_zch.p;
+  const uint64_t *dzfirst = (const uint64_t *)ctx->sv_zpre.p, *dzwfirst = dzfirst + m + 1;
+  uint64_t *const zext = (uint64_t *)ctx->sv_zext.p, *const zmisc = (uint64_t *)ctx->zc_misc.p;
+  uint64_t *const hext = (uint64_t *)take(16 * m);
+  if (!hext) return cleanup(), fail(MCDC_E_INTERNAL, "save path: frame staging full");
+  std::vector<hipEvent_t> evg(G, nullptr);  // group g's frames and extents complete (on st)
+  hipEvent_t ev_s3 = nullptr, ev_cp = nullptr;
+  for (auto &e : evg) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return e = nullptr, cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
+    evs.push_back(e);
+  }
+  if (hipEventCreateWithFlags(&ev_s3, hipEventDisableTiming) != hipSuccess)
+    return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
   evs.push_back(ev_s3);
-  uint64_t coff = 0;
+  if (hipEventCreateWithFlags(&ev_cp, hipEventDisableTiming) != hipSuccess)
+    return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
+  evs.push_back(ev_cp);
+  auto enqueue = [&](size_t g) -> int {  // group g's compression, then its extents to the host
+    const size_t g0 = gstart[g], gm = gstart[g + 1] - g0;
+    int r = zc_enqueue(ctx, d, n, zch + g0, dzfirst + g0, dzwfirst + g0, zfirst + g0, zwfirst + g0, zcls.data() + g0,
+                       zbs[g], C + cstart[g], zext + 2 * g0, zmisc);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(hext + 2 * g0, zext + 2 * g0, 16 * gm, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(evg[g], st));
+    return MCDC_OK;
+  };
+  uint64_t hoff = 0;  // the headers' running offset after the frames (C + bound)
+  if (G && (rc = enqueue(0))) return cleanup(), rc;
   for (size_t g = 0; g < G; ++g) {  // compress a group; its seals, headers and closed packs on stream3
     const size_t g0 = gstart[g], g1 = gstart[g + 1], gm = g1 - g0;
-    size_t cbytes = 0;
-    if ((rc = mcdc_zstd_compress_device(ctx, d, n, sch.data() + g0, gm, C + coff, comp_cap - coff, &cbytes,
-                                        fr.data() + g0)))
-      return cleanup(), rc;
+    // the next group's batches queue behind this one's on the compressor's
+    // streams before the host waits: no gap between groups
+    if (g + 1 < G && (rc = enqueue(g + 1))) return cleanup(), rc;
+    HIP_TRY(hipEventSynchronize(evg[g]));
+    for (size_t i = g0; i < g1; ++i) fr[i] = mcdc_blob{hext[2 * i], hext[2 * i + 1]};
     SAVE_T("group compressed");
-    // (the group's frames are complete: mcdc_zstd_compress_device synchronised
-    // its streams; stream3 is ordered after them by an event all the same)
-    HIP_TRY(hipEventRecord(ev_comp, st));
-    HIP_TRY(hipStreamWaitEvent(s3, ev_comp, 0));
+    HIP_TRY(hipStreamWaitEvent(s3, evg[g], 0));
     // place the group's blobs; close the packs the flush rule closes
     closing.clear();
     hbuf.clear();
@@ -2087,8 +2288,8 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
       if (body > mps && (rc = close_pack(i + 1))) return cleanup(), rc;
     }
     if (g1 == m && open && (rc = close_pack(m))) return cleanup(), rc;
-    // headers of the closing packs, framed on the host, to HBM after the group's frames
-    const uint64_t hin = coff + cbytes;
+    // headers of the closing packs, framed on the host, to HBM after every group's frames
+    const uint64_t hin = bound + hoff;
     if (hin + hbuf.size() > comp_cap)  // (frames within their raw bound, headers within pack_bound's share)
       return cleanup(), fail(MCDC_E_INTERNAL, "save path: header staging beyond the compressor buffer");
     uint8_t *hm = hbuf.empty() ? nullptr : take(hbuf.size()), *tr = closing.empty() ? nullptr : take(4 * closing.size());
@@ -2102,39 +2303,35 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
       const uint32_t el = (uint32_t)(meta[closing[c].k] - 4);
       std::memcpy(tr + 4 * c, &el, 4);
     }
-    if (keyed) {
-      std::vector<uint64_t> pl(gm + 1);
+    if (keyed) {  // the group's blobs and the closing packs' headers: one seal into their places
+      const size_t nc = closing.size(), ns = gm + nc;
+      std::vector<mcdc_blob> sx(ns);
+      std::vector<uint64_t> pl(ns + 1);
+      std::vector<uint8_t> sn(12 * ns);
       uint64_t end = 0;
-      for (size_t i = 0; i < gm; ++i) pl[i] = place[g0 + i], end = std::max(end, place[g0 + i] + lens[g0 + i]);
-      pl[gm] = end;
-      uint8_t *sst = take(seal_stage_bytes(gm));
-      if (!sst) return cleanup(), fail(MCDC_E_INTERNAL, "save path: seal staging full");
-      if ((rc = seal_placed(ctx, s3, store->key, C + coff, fr.data() + g0, gm, store->nonces + 12 * g0, D, pl.data(),
-                            sst)))
-        return cleanup(), rc;
-      if (!closing.empty()) {  // the headers: their frames sealed into place
-        std::vector<mcdc_blob> hx(closing.size());
-        std::vector<uint64_t> hp(closing.size() + 1);
-        std::vector<uint8_t> hn(12 * closing.size());
-        uint64_t hend = 0;
-        for (size_t c = 0; c < closing.size(); ++c) {
-          const size_t k = closing[c].k;
-          hx[c] = mcdc_blob{closing[c].hpos, closing[c].hlen};
-          hp[c] = pk[k].offset + pk[k].length - meta[k];
-          hend = std::max(hend, hp[c] + closing[c].hlen + over);
-          std::memcpy(hn.data() + 12 * c, store->header_nonces + 12 * k, 12);
-        }
-        hp[closing.size()] = hend;
-        uint8_t *hst = take(seal_stage_bytes(closing.size()));
-        if (!hst) return cleanup(), fail(MCDC_E_INTERNAL, "save path: seal staging full");
-        if ((rc = seal_placed(ctx, s3, store->key, C + hin, hx.data(), closing.size(), hn.data(), D, hp.data(), hst)))
-          return cleanup(), rc;
+      for (size_t i = 0; i < gm; ++i) {
+        sx[i] = fr[g0 + i];
+        pl[i] = place[g0 + i];
+        end = std::max(end, place[g0 + i] + lens[g0 + i]);
       }
+      std::memcpy(sn.data(), store->nonces + 12 * g0, 12 * gm);
+      for (size_t c = 0; c < nc; ++c) {  // (header frames at C + hin: offsets from the group's frames)
+        const size_t k = closing[c].k;
+        sx[gm + c] = mcdc_blob{hin - cstart[g] + closing[c].hpos, closing[c].hlen};
+        pl[gm + c] = pk[k].offset + pk[k].length - meta[k];
+        end = std::max(end, pl[gm + c] + closing[c].hlen + over);
+        std::memcpy(sn.data() + 12 * (gm + c), store->header_nonces + 12 * k, 12);
+      }
+      pl[ns] = end;
+      uint8_t *sst = take(seal_stage_bytes(ns));
+      if (!sst) return cleanup(), fail(MCDC_E_INTERNAL, "save path: seal staging full");
+      if ((rc = seal_placed(ctx, s3, store->key, C + cstart[g], sx.data(), ns, sn.data(), D, pl.data(), sst)))
+        return cleanup(), rc;
     } else {  // frames as they are: the group's frames run by run of one pack, the headers
       for (size_t i = g0; i < g1;) {
         size_t e = i + 1;
         while (e < g1 && place[e] == place[e - 1] + lens[e - 1]) ++e;
-        HIP_TRY(hipMemcpyAsync(D + place[i], C + coff + fr[i].offset, place[e - 1] + lens[e - 1] - place[i],
+        HIP_TRY(hipMemcpyAsync(D + place[i], C + cstart[g] + fr[i].offset, place[e - 1] + lens[e - 1] - place[i],
                                hipMemcpyDeviceToDevice, s3));
         i = e;
       }
@@ -2146,21 +2343,24 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
       const size_t k = closing[c].k;
       HIP_TRY(hipMemcpyAsync(D + pk[k].offset + pk[k].length - 4, tr + 4 * c, 4, hipMemcpyHostToDevice, s3));
     }
-    // the closed packs to the host, behind their seals on stream3
+    // the closed packs to the host on stream4, behind their seals and
+    // trailers (stream3): the next group's seals do not wait for the copy
     if (!closing.empty()) {
       const size_t k1 = pk.size();
       overflow |= k1 > packs_cap || (packs_out == nullptr) ||
                   pk[k1 - 1].offset + pk[k1 - 1].length > packs_out_cap;
       if (!overflow) {
         const uint64_t lo = pk[copied].offset, hi = pk[k1 - 1].offset + pk[k1 - 1].length;
-        HIP_TRY(hipMemcpyAsync((uint8_t *)packs_out + lo, D + lo, hi - lo, hipMemcpyDeviceToHost, s3));
+        HIP_TRY(hipEventRecord(ev_cp, s3));
+        HIP_TRY(hipStreamWaitEvent(s4, ev_cp, 0));
+        HIP_TRY(hipMemcpyAsync((uint8_t *)packs_out + lo, D + lo, hi - lo, hipMemcpyDeviceToHost, s4));
         copied = k1;
       }
     }
-    // the next group's frames after this group's frames and headers
-    coff = hin + hbuf.size();
+    hoff += hbuf.size();
   }
-  // the pack IDs (on st) after the last seals and copies into D (stream3)
+  // the pack IDs (on st) after the last seals and copies into D (stream3),
+  // beside the last packs' copy to the host (stream4)
   HIP_TRY(hipEventRecord(ev_s3, s3));
   HIP_TRY(hipStreamWaitEvent(st, ev_s3, 0));
   const size_t np = pk.size();
@@ -2181,6 +2381,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   SAVE_T("sealed enqueued");
   std::vector<uint8_t> pid(32 * np);
   rc = np ? mcdc_chunk_ids_device(ctx, D, at, pk.data(), np, pid.data()) : MCDC_OK;
+  HIP_TRY(hipStreamSynchronize(s4));
   HIP_TRY(hipStreamSynchronize(s3));
   HIP_TRY(hipStreamSynchronize(st));
   cleanup();
@@ -2392,28 +2593,29 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
   if (out_bytes) *out_bytes = 0;
   if (nchunks == 0) return MCDC_OK;
   if (nchunks >= (1ull << 31)) return fail(MCDC_E_TOOBIG, "too many chunks (%zu)", nchunks);
-  static const zs::ZTables T = zs::build_tables();
   const double t0 = now_ms();
   hipStream_t st = ctx->stream;
   size_t tmpb = zc_tmp_bytes(nchunks);
   if ((rc = stage_arg(ctx, ctx->b3_chunks, chunks, nchunks * sizeof(mcdc_chunk))) ||
       (rc = ensure(ctx, ctx->zc_cnt, (nchunks + 1) * 8)) || (rc = ensure(ctx, ctx->zc_first, (nchunks + 1) * 8)) ||
       (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = ensure(ctx, ctx->zc_tmp, tmpb)) ||
-      (rc = ensure(ctx, ctx->zc_cls, nchunks + 1)))
+      (rc = ensure(ctx, ctx->zc_cls, nchunks + 1)) || (rc = ensure(ctx, ctx->zc_wcnt, (nchunks + 1) * 8)) ||
+      (rc = ensure(ctx, ctx->zc_wfirst, (nchunks + 1) * 8)))
     return rc;
   uint64_t *misc = (uint64_t *)ctx->zc_misc.p;  // [0] err, [1] raw bound, [2] output base
   HIP_TRY(hipMemsetAsync(misc, 0, 32, st));
   HIP_TRY(hipEventRecord(ctx->ev_start, st));
   const DevChunk *dch = (const DevChunk *)ctx->b3_chunks.p;
-  uint64_t *first = (uint64_t *)ctx->zc_first.p;
-  launch_zc_nblocks(dch, nchunks, n, (uint64_t *)ctx->zc_cnt.p, first, (uint32_t *)misc, misc + 1,
-                    (uint8_t *)ctx->zc_cls.p, ctx->zc_tmp.p, tmpb, st);
+  uint64_t *first = (uint64_t *)ctx->zc_first.p, *wfirst = (uint64_t *)ctx->zc_wfirst.p;
+  launch_zc_nblocks(dch, nchunks, n, (uint64_t *)ctx->zc_cnt.p, first, (uint64_t *)ctx->zc_wcnt.p, wfirst,
+                    (uint32_t *)misc, misc + 1, (uint8_t *)ctx->zc_cls.p, ctx->zc_tmp.p, tmpb, st);
   HIP_TRY(hipGetLastError());
-  std::vector<uint64_t> hfirst(nchunks + 1);
+  std::vector<uint64_t> hfirst(nchunks + 1), hwfirst(nchunks + 1);
   std::vector<uint8_t> hcls(nchunks);  // (the k_zc_small class of each chunk: the list may be device memory)
   uint64_t hm[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(hm, misc, 16, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hfirst.data(), first, (nchunks + 1) * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hwfirst.data(), wfirst, (nchunks + 1) * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(hcls.data(), ctx->zc_cls.p, nchunks, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (hm[0]) return fail(MCDC_E_INVALID, "a chunk lies outside the %zu-byte buffer or is 2 GiB or longer", n);
@@ -2426,67 +2628,11 @@ int mcdc_zstd_compress_device(mcdc_ctx *ctx, const void *d_data, size_t n, const
     if ((rc = ensure(ctx, ctx->zf_ext, nchunks * 16))) return rc;
     ext = (uint64_t *)ctx->zf_ext.p;
   }
-  const uint64_t total_blocks = hfirst[nchunks];
-  uint64_t longest = 0;  // a batch holds whole chunks
-  for (size_t i = 0; i < nchunks; ++i) longest = std::max<uint64_t>(longest, hfirst[i + 1] - hfirst[i]);
-  // Batches alternate between two scratch sets on the context's two streams,
-  // so one batch's kernels run into the other's tails; only the final copies
-  // (output offsets carried from batch to batch) are ordered across streams.
-  // One set when a single batch of zc_batch / 2 blocks holds everything.
-  const uint64_t zb = ctx->knobs.zc_batch;
-  const bool two = ctx->knobs.zc_two && total_blocks > zb / 2 && longest <= zb / 2;
-  const uint64_t mb = two ? zb / 2 : std::max(std::min<uint64_t>(total_blocks, zb), longest);
-  tmpb = std::max(tmpb, zc_tmp_bytes(mb));
-  struct Set {
-    DevBuf *blocks, *stage, *piece, *poff, *tmp, *words;
-  } sets[2] = {{&ctx->zc_blocks, &ctx->zc_stage, &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_tmp, &ctx->zc_words},
-               {&ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2, &ctx->zc_words2}};
-  for (int k = 0; k < (two ? 2 : 1); ++k) {
-    const Set &z = sets[k];
-    if ((rc = ensure(ctx, *z.tmp, tmpb)) || (rc = ensure(ctx, *z.blocks, mb * sizeof(ZcBlock))) ||
-        (rc = ensure(ctx, *z.stage, mb * kZcSlot + kZcStagePad)) || (rc = ensure(ctx, *z.piece, (mb + 1) * 8)) ||
-        (rc = ensure(ctx, *z.poff, (mb + 1) * 8)) || (rc = ensure(ctx, *z.words, (mb * kZcBlock + 1024) * 4)))
-      return rc;
-  }
-  // [0] setup done on st; [1 + k] set k's last final copy
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  auto destroy = [&]() {
-    for (auto &e : ev)
-      if (e) (void)hipEventDestroy(e);
-  };
-  for (auto &e : ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-      return e = nullptr, destroy(), fail(MCDC_E_DEVICE, "event creation failed");
-  hipStream_t ss[2] = {st, ctx->stream2};
-  if (two) {
-    rc = hipEventRecord(ev[0], st) == hipSuccess && hipStreamWaitEvent(ss[1], ev[0], 0) == hipSuccess
-             ? MCDC_OK
-             : fail(MCDC_E_DEVICE, "stream ordering failed");
-    if (rc) return destroy(), rc;
-  }
-  int k = 0, prev = -1;  // set of the batch, set of the batch before
-  for (uint64_t c0 = 0; c0 < nchunks; k ^= two ? 1 : 0) {  // batches of whole chunks, <= mb blocks each
-    uint64_t c1 = c0, nseg = 0, nsmall[4] = {0, 0, 0, 0};  // (chunks of one block per k_zc_small class)
-    uint64_t blongest = 0;  // (the batch's longest chunk in blocks: k_zc_far only above one segment)
-    do {
-      const uint64_t nbk = hfirst[c1 + 1] - hfirst[c1];
-      blongest = std::max(blongest, nbk);
-      nseg += (nbk + kZcSegBlocks - 1) / kZcSegBlocks;
-      if (hcls[c1] < 4) ++nsmall[hcls[c1]];
-      ++c1;
-    } while (c1 < nchunks && hfirst[c1 + 1] - hfirst[c0] <= mb);
-    const Set &z = sets[k];
-    launch_zc_batch((const uint8_t *)d_data, n, dch, first, c0, c1, hfirst[c0], hfirst[c1] - hfirst[c0],
-                    (ZcBlock *)z.blocks->p, (uint8_t *)z.stage->p, (uint32_t *)z.words->p, T, (uint64_t *)z.piece->p, (uint64_t *)z.poff->p, misc + 2, (uint8_t *)d_out,
-                    ext, z.tmp->p, tmpb, ss[k], ctx->knobs.zc_huf, two && prev >= 0 && prev != k ? ev[1 + prev] : nullptr,
-                    two ? ev[1 + k] : nullptr, blongest > kZcSegBlocks, nseg, ctx->knobs.zc_small ? nsmall : nullptr);
-    if (hipGetLastError() != hipSuccess) return destroy(), fail(MCDC_E_DEVICE, "compress launch failed");
-    prev = k;
-    c0 = c1;
-  }
-  if (two && prev == 1 && hipStreamWaitEvent(st, ev[2], 0) != hipSuccess)
-    return destroy(), fail(MCDC_E_DEVICE, "stream ordering failed");
-  destroy();
+  const ZcBatches zbt = zc_batches(hfirst.data(), hwfirst.data(), nchunks, ctx->knobs);
+  if ((rc = zc_ensure_sets(ctx, zbt.mw, zbt.mb, zbt.two, tmpb)) ||
+      (rc = zc_enqueue(ctx, (const uint8_t *)d_data, n, dch, first, wfirst, hfirst.data(), hwfirst.data(), hcls.data(),
+                       zbt, (uint8_t *)d_out, ext, misc)))
+    return rc;
   HIP_TRY(hipEventRecord(ctx->ev_end, st));
   uint64_t total = 0;
   HIP_TRY(hipMemcpyAsync(&total, misc + 2, 8, hipMemcpyDeviceToHost, st));
@@ -2510,23 +2656,23 @@ int mcdc_zstd_compress_scratch(mcdc_ctx *ctx, const mcdc_chunk *chunks, size_t n
   if (is_device_ptr(chunks)) return fail(MCDC_E_INVALID, "chunks must be host memory");
   *bytes = 0;
   if (nchunks == 0) return MCDC_OK;
-  uint64_t total_blocks = 0, longest = 0;
+  std::vector<uint64_t> first(nchunks + 1, 0), wfirst(nchunks + 1, 0);
   for (size_t i = 0; i < nchunks; ++i) {
-    const uint64_t nb = chunks[i].length ? (chunks[i].length + kZcBlock - 1) / kZcBlock : 1;
-    total_blocks += nb;
-    longest = std::max(longest, nb);
+    const uint64_t len = chunks[i].length, nb = len ? (len + kZcBlock - 1) / kZcBlock : 1;
+    first[i + 1] = first[i] + nb;
+    wfirst[i + 1] = wfirst[i] + zc_span(len);
   }
   // as mcdc_zstd_compress_device sizes its batch sets
-  const uint64_t zb = ctx->knobs.zc_batch;
-  const bool two = ctx->knobs.zc_two && total_blocks > zb / 2 && longest <= zb / 2;
-  const uint64_t mb = two ? zb / 2 : std::max(std::min<uint64_t>(total_blocks, zb), longest);
+  const ZcBatches zbt = zc_batches(first.data(), wfirst.data(), nchunks, ctx->knobs);
+  const bool two = zbt.two;
+  const uint64_t mw = zbt.mw, mb = zbt.mb;
   // (every buffer as ensure() allocates it, headroom included; the call's
   // own buffers as mcdc_zstd_compress_device requests them)
   const uint64_t tmpb = std::max(zc_tmp_bytes(nchunks), zc_tmp_bytes(mb));
   const uint64_t set = ensure_bytes(tmpb) + ensure_bytes(mb * sizeof(ZcBlock)) +
-                       ensure_bytes(mb * kZcSlot + kZcStagePad) + 2 * ensure_bytes((mb + 1) * 8) +
-                       ensure_bytes((mb * kZcBlock + 1024) * 4);
-  const uint64_t call = ensure_bytes(nchunks * sizeof(mcdc_chunk)) + 2 * ensure_bytes((nchunks + 1) * 8) +
+                       ensure_bytes(zc_set_stage_bytes(mw, mb)) + 2 * ensure_bytes((mb + 1) * 8) +
+                       ensure_bytes(zc_set_words_bytes(mw)) + ensure_bytes(mb * kZcExtra);
+  const uint64_t call = ensure_bytes(nchunks * sizeof(mcdc_chunk)) + 4 * ensure_bytes((nchunks + 1) * 8) +
                         ensure_bytes(nchunks + 1) +
                         ensure_bytes(32) + ensure_bytes(nchunks * 16);
   *bytes = (size_t)(set * (two ? 2 : 1) + call);

@@ -103,18 +103,32 @@ constexpr uint32_t kPrime = kZcPrime;         // bytes before a segment re-inser
 // Match words: length (<= kMlCap) << 24 | offset; bit 31 marks a verified
 // kMlCap match of the finder's own (readers take the length as (w >> 24) & 31)
 constexpr uint32_t kZcLocalCap = 1u << 31;
-// A block's kZcBlock words are its only per-block scratch besides the staging
-// slot: the match words until k_zc_parse, which writes the block's sequences
-// over them as it goes (sequence i, 8 bytes at 8 i, is written in the window
-// of a position >= 4 i, after that window's words were read, and every word
-// read later lies at 4 x a later position: never overtaken); the upper half
-// then holds k_zc_huff's section under assembly, after it k_zc_plan's tables
-// and k_zc_chain's state records (kZcHalf: the half's first word).
-constexpr uint32_t kZcHalf = (uint32_t)kZcBlock / 2;
-__device__ __forceinline__ uint64_t *blk_seqs(uint32_t *words, uint64_t bi) {
-  return reinterpret_cast<uint64_t *>(words + bi * kZcBlock);
+// Per-block scratch, packed by the blocks' lengths (mcdc_zcomp.h): block bi
+// of a batch owns words[B.w0, + zc_span(len)) -- a chunk's blocks are
+// consecutive, so its words are contiguous, position p of the chunk at
+// chunk base + p -- the staging slot stage[B.w0 + 64 bi, + span + 64) and
+// kZcExtra bytes of extra[].  The words are the match words until
+// k_zc_parse, which writes the block's sequences over them as it goes
+// (sequence i, 8 bytes at 8 i, is written in the window of a position >= 4 i,
+// after that window's words were read, and every word read later lies at 4 x
+// a later position: never overtaken); the upper half then holds k_zc_huff's
+// section under assembly, then k_zc_chain's state records (blocks of 512
+// words or more; shorter ones keep them in extra[]).
+__device__ __forceinline__ uint32_t blk_span(uint32_t len) { return (uint32_t)zc_span(len); }
+__device__ __forceinline__ uint64_t *blk_seqs(uint32_t *words, const ZcBlock &B) {
+  return reinterpret_cast<uint64_t *>(words + B.w0);
 }
-static_assert(kZcSeqCap * 8 <= kZcHalf * 4, "sequences in the lower half of the block's words");
+__device__ __forceinline__ uint32_t *blk_upper(uint32_t *words, const ZcBlock &B) {
+  return words + B.w0 + blk_span(B.len) / 2;
+}
+__device__ __forceinline__ uint8_t *blk_slot(uint8_t *stage, const ZcBlock &B, uint64_t bi) {
+  return stage + B.w0 + 64 * bi;
+}
+// (a chunk's position p: word chunk_words(...)[p]; B any of its blocks)
+__device__ __forceinline__ uint32_t *chunk_words(uint32_t *words, const ZcBlock &B) {
+  return words + (B.w0 - B.b * (uint32_t)kZcBlock);
+}
+static_assert(kZcBlock % 64 == 0, "a chunk's full blocks span whole 64-word steps: its words are contiguous");
 // The parse's run ends (ends[]): kEndNext = take the next position's,
 // kEndLong = still matching kRunExt bytes after kMlCap (the wave extends it)
 constexpr uint32_t kRunExt = 32, kEndNext = 0xFFFFu, kEndLong = 0xFFFEu;
@@ -159,8 +173,8 @@ __device__ __forceinline__ void tile_sync() {
   else wave_lds_order();
 }
 
-__global__ void k_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint32_t *err,
-                             uint64_t *bound, uint8_t *cls) {
+__global__ void k_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint64_t *wcnt,
+                             uint32_t *err, uint64_t *bound, uint8_t *cls) {
   MCDC_VGPR_PAD(12);  // (not an exact fill)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t raw = 0;
@@ -170,22 +184,25 @@ __global__ void k_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes
     if (!ok) atomicOr(err, 1u);
     const uint64_t nb = c.length ? (c.length + kZcBlock - 1) / kZcBlock : 1;
     cnt[i] = nb;
+    wcnt[i] = zc_span(c.length);  // (= the sum of its blocks' spans: full blocks span kZcBlock)
     cls[i] = nb == 1 ? (uint8_t)zc_small_class(c.length) : (uint8_t)4;
     raw = kFrameHdr + kBlockHdr * nb + c.length;
   } else if (i == n) {
     cnt[i] = 0;
+    wcnt[i] = 0;
   }
   for (int o = 32; o > 0; o >>= 1) raw += __shfl_down(raw, o);
   if (lane_id() == 0 && raw) atomicAdd(reinterpret_cast<unsigned long long *>(bound), (unsigned long long)raw);
 }
 
-__global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint64_t c0, uint64_t c1, uint64_t b0,
-                            ZcBlock *blocks) {
+__global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, const uint64_t *wfirst, uint64_t c0,
+                            uint64_t c1, uint64_t b0, ZcBlock *blocks) {
   MCDC_VGPR_PAD(16);  // (not an exact fill)
   const uint64_t c = c0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= c1) return;
   const DevChunk ch = chunks[c];
   const uint64_t f = first[c], nb = first[c + 1] - f;
+  const uint32_t w = (uint32_t)(wfirst[c] - wfirst[c0]);  // (the chunk's first word in the batch)
   for (uint64_t b = 0; b < nb; ++b) {
     ZcBlock z;
     z.src = ch.offset + b * kZcBlock;
@@ -194,6 +211,7 @@ __global__ void k_zc_blocks(const DevChunk *chunks, const uint64_t *first, uint6
     z.b = (uint32_t)b;
     z.nb = (uint32_t)nb;
     z.nlit = z.nseq = z.csize = z.lsize = z.flags = 0;
+    z.w0 = w + (uint32_t)b * (uint32_t)kZcBlock;
     blocks[f + b - b0] = z;
   }
 }
@@ -357,7 +375,7 @@ __global__ __launch_bounds__(NT) void k_zc_find_t(const uint8_t *base, uint64_t 
   const uint64_t cbytes = nbytes - csrc;  // (bytes readable from the chunk start)
   // the segment's words: the chunk's blocks are consecutive records, so
   // position p's word is wseg[p]; positions outside the segment keep nothing
-  uint32_t *wseg = words + (bi0 - B0.b) * kZcBlock;
+  uint32_t *wseg = chunk_words(words, B0);
   // (word stores: a 32-bit offset from the segment's first word; from the
   // chunk's, 4 p wraps for chunks of 1 GiB or more)
   uint32_t *const wseg0 = wseg + seg0;
@@ -761,7 +779,7 @@ __global__ __launch_bounds__(64 * W) void k_zc_small(const uint8_t *base, uint64
   if (B.nb != 1 || L > DMAX) return;  // (not this class: the host's counts disagree)
   const uint8_t *cb = base + B.src;
   const uint64_t cbytes = nbytes - B.src;
-  uint32_t *const wc = words + bi * kZcBlock;
+  uint32_t *const wc = words + B.w0;
   if (L < 16 || cbytes < 16) {  // (too short to match: every position a literal; flags stay 0)
     for (uint32_t p = tid; p < L; p += NT) wc[p] = 0u;
     return;
@@ -902,7 +920,7 @@ __global__ __launch_bounds__(256) void k_zc_far(const uint8_t *base, uint64_t nb
   const uint32_t clen = (B.nb - 1) * (uint32_t)kZcBlock + blocks[bi + (B.nb - 1 - B.b)].len;
   const uint8_t *cb = base + csrc;
   const uint64_t cbytes = nbytes - csrc;
-  uint32_t *wc = words + rec0 * kZcBlock;  // the chunk's words
+  uint32_t *wc = chunk_words(words, B);
   const uint32_t s = B.b / kZcSegBlocks;
   const uint32_t p = B.b * (uint32_t)kZcBlock + j * 1024 + 16 * lane;
   const uint32_t bend = min(clen, (B.b + 1) * (uint32_t)kZcBlock);
@@ -1037,9 +1055,10 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   }
   const uint32_t end = B.len;
   const uint8_t *p0 = base + B.src;
-  const uint32_t *w = words + bi * kZcBlock;
-  uint8_t *lit = stage + bi * kZcSlot + zs::kLitHdr;
-  uint64_t *sq = blk_seqs(words, bi);  // (over the words already read: see kZcHalf)
+  const uint32_t *w = words + (uint32_t)__builtin_amdgcn_readfirstlane((int)B.w0);  // (uniform: an SGPR base)
+  uint8_t *lit = blk_slot(stage, B, bi) + zs::kLitHdr;
+  uint64_t *sq = blk_seqs(words, B);  // (over the words already read: see blk_span)
+  const uint32_t wlast = blk_span(B.len) - 1;  // (the block's last word: reads past the end clamped)
   uint32_t nlit = 0, nseq = 0, lit0 = 0, cur = 0, last_off = 0;  // (last_off 0: no sequence yet)
   if (lane == 0) {
     for (int k = 0; k < 6; ++k) J[k][256] = 256;
@@ -1055,7 +1074,7 @@ __global__ __launch_bounds__(64) void k_zc_parse(const uint8_t *base, uint64_t n
   auto issue = [&](uint32_t wb, uint32_t *v, uint32_t &by) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t q = min(wb + 64 * j + lane, (uint32_t)kZcBlock - 1);
+      const uint32_t q = min(wb + 64 * j + lane, wlast);
       asm volatile("global_load_dword %0, %1, %2" : "=v"(v[j]) : "v"(4 * q), "s"(w) : "memory");
     }
     asm volatile("global_load_dword %0, %1, %2" : "=v"(by) : "v"(min(wb + 4 * lane, lim4)), "s"(p0) : "memory");
@@ -1517,7 +1536,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   // a block without sequences: all of it literals, read from the input (k_zc_parse staged nothing)
   const uint32_t n = B.nseq ? B.nlit : B.len;
   if (n < 32 || (B.flags & kZcRaw)) return;  // (lsize stays 0: raw literals; hopeless blocks stored raw)
-  uint8_t *st = stage + bi * kZcSlot;
+  uint8_t *st = blk_slot(stage, B, bi);
   const uint8_t *src = B.nseq ? st + kLitHdr : base + B.src;
   ZT_DECL;
   for (uint32_t k = lane; k < 4 * 256; k += 64) (&hist[0][0])[k] = 0;
@@ -1639,7 +1658,7 @@ __global__ __launch_bounds__(64) void k_zc_huff(const uint8_t *base, uint64_t nb
   const uint32_t csize = tree + (one ? 0 : 6) + ssz[0] + (one ? 0 : ssz[1] + ssz[2] + ssz[3]);
   if (one && csize >= 1024) return;  // (one stream: 10-bit sizes)
   const uint32_t hdr = lit_hdr_size(n, csize, one);
-  uint32_t *sw = scratch + bi * kZcBlock + kZcHalf;  // the section under assembly (the words' upper half)
+  uint32_t *sw = blk_upper(scratch, B);  // the section under assembly (the words' upper half)
   const uint32_t nq = (total + 3) / 4 + 1;
   for (uint32_t k = lane; k < nq; k += 64) sw[k] = 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (same wave: agent scope would write back the L2)
@@ -1852,28 +1871,33 @@ struct ZcSeqTab {    // (in the upper half of the block's match-word scratch)
   uint32_t xbits;    // extra bits of the block's sequences (k_zc_plan)
   SeqPlan P;
 };
-__device__ __forceinline__ ZcSeqTab *seq_tab(uint32_t *words, uint64_t bi) {
-  return reinterpret_cast<ZcSeqTab *>(words + bi * kZcBlock + kZcHalf);
+__device__ __forceinline__ ZcSeqTab *seq_tab(uint8_t *extra, uint64_t bi) {
+  return reinterpret_cast<ZcSeqTab *>(extra + bi * kZcExtra);
 }
-// After the tables: k_zc_chain's state records, three arrays of kZcSeqCap
-// 16-bit words (LL, OF, ML), by sequence.
+// k_zc_chain's state records: three arrays of rec_cap 16-bit words (LL, OF,
+// ML), by sequence (a block of len bytes has at most len / 4 sequences), in
+// the upper half of the block's words (k_zc_huff's section copied out by
+// then), or after the tables in extra[] for blocks under 512 words.
 constexpr uint32_t kSeqTabBytes = (sizeof(ZcSeqTab) + 15) / 16 * 16;
-static_assert(kSeqTabBytes + 3 * kZcSeqCap * 2 + 256 <= kZcHalf * 4, "tables and state records exceed the upper half");
-__device__ __forceinline__ uint16_t *blk_recs(uint32_t *words, uint64_t bi) {
-  return reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(seq_tab(words, bi)) + kSeqTabBytes);
+constexpr uint32_t kRecsUpper = 512;  // (span >= this: 1.5 span + the 128-byte reads past the end <= 2 span)
+static_assert(kSeqTabBytes + 3 * (kRecsUpper - 64) / 2 + 256 <= kZcExtra, "tables and short blocks' records in extra[]");
+__device__ __forceinline__ uint32_t rec_cap(const ZcBlock &B) { return blk_span(B.len) / 4; }
+__device__ __forceinline__ uint16_t *blk_recs(uint32_t *words, uint8_t *extra, const ZcBlock &B, uint64_t bi) {
+  return blk_span(B.len) >= kRecsUpper ? reinterpret_cast<uint16_t *>(blk_upper(words, B))
+                                       : reinterpret_cast<uint16_t *>(extra + bi * kZcExtra + kSeqTabBytes);
 }
 // Per symbol type the sequences' codes, one byte each, the last sequence
 // first (k_zc_chain's walking order), + 8 bytes of slack, in the staging slot
 // after the raw literals (16-byte aligned): every sequence covers a match of
 // at least 4 bytes, so nlit + 4 nseq <= len and the three arrays fit in the
-// slot; k_zc_huff's section is shorter than the raw literals it replaces, and
-// k_zc_encode writes over the codes only after k_zc_chain read them.
-// (k_zc_chain's prefetches read up to kZcCodeOver bytes past a block's codes:
-// the staging buffer carries that much more, kZcStagePad.)
-__device__ __forceinline__ uint8_t *seq_codes(uint8_t *stage, uint64_t bi, uint32_t nlit, uint32_t nseq, uint32_t k) {
-  return stage + bi * kZcSlot + ((kLitHdr + nlit + 15) & ~15u) + k * (nseq + 8);
+// slot (span + 64 bytes); k_zc_huff's section is shorter than the raw
+// literals it replaces, and k_zc_encode writes over the codes only after
+// k_zc_chain read them.  (k_zc_chain's prefetches read up to kZcSeqCap + 48
+// bytes past a block's codes: the staging buffer carries kZcStagePad more.)
+__device__ __forceinline__ uint8_t *seq_codes(uint8_t *stage, const ZcBlock &B, uint64_t bi, uint32_t k) {
+  return blk_slot(stage, B, bi) + ((kLitHdr + B.nlit + 15) & ~15u) + k * (B.nseq + 8);
 }
-static_assert(kLitHdr + 15 + 3 * 8 + kZcBlock <= kZcSlot, "codes fit the staging slot (nlit + 3 nseq <= len)");
+static_assert(kLitHdr + 15 + 3 * 8 <= 64, "codes fit the staging slot (nlit + 3 nseq <= len <= span)");
 static_assert(kZcSeqCap + 64 <= kZcStagePad, "staging pad covers k_zc_chain's reads past the codes");
 
 // Float sum over the wave's 64 lanes (DPP, as wave_incl_sum), the total in every lane.
@@ -1945,7 +1969,7 @@ __device__ void seq_plan_wave(uint32_t (*cnt)[53], uint32_t nseq, SeqPlan &P, ui
 }
 
 __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                uint32_t *words, ZTables T, const uint32_t *porder) {
+                                                uint32_t *words, uint8_t *extra, ZTables T, const uint32_t *porder) {
   __shared__ FseCTL tb[3];
   __shared__ SeqPlan P;
   __shared__ uint32_t hist[3][53], cum[54], seen[54];
@@ -1955,12 +1979,11 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
   if (ns == 0) return;
-  const uint64_t *sq = blk_seqs(words, bi);
+  const uint64_t *sq = blk_seqs(words, B);
   ZT_DECL;
   for (uint32_t k = lane; k < 3 * 53; k += 64) (&hist[0][0])[k] = 0;
   __syncthreads();
-  uint8_t *cd0 = seq_codes(stage, bi, B.nlit, ns, 0), *cd1 = seq_codes(stage, bi, B.nlit, ns, 1),
-          *cd2 = seq_codes(stage, bi, B.nlit, ns, 2);
+  uint8_t *cd0 = seq_codes(stage, B, bi, 0), *cd1 = seq_codes(stage, B, bi, 1), *cd2 = seq_codes(stage, B, bi, 2);
   uint32_t xb = 0;  // extra bits
   // (64 sequences per step, the next step's requested meanwhile outside the
   // compiler's wait counting: see ald16s)
@@ -2008,7 +2031,7 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
     }
     __syncthreads();
   }
-  ZcSeqTab *tab = seq_tab(words, bi);
+  ZcSeqTab *tab = seq_tab(extra, bi);
   xb = wave_sum(xb);
   if (lane == 0) tab->xbits = xb;
 #pragma unroll
@@ -2035,7 +2058,7 @@ __global__ __launch_bounds__(64) void k_zc_plan(const ZcBlock *blocks, uint64_t 
 constexpr uint32_t kChainBlocks = 9;
 constexpr uint32_t kChainSplit = 64;  // blocks with at least this many sequences: two lanes per state machine
 __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                 uint32_t *words) {
+                                                 uint32_t *words, uint8_t *extra) {
   __shared__ FseCTL tb[3 * kChainBlocks];
   const uint32_t lane = lane_id();
   const uint64_t g0 = (uint64_t)blockIdx.x * kChainBlocks;
@@ -2043,7 +2066,7 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   for (uint32_t j = 0; j < kChainBlocks && g0 + j < nblk; ++j) {
     const uint64_t b = g0 + j;
     if (blocks[b].nseq == 0) continue;
-    const ZcSeqTab *tab = seq_tab(words, b);
+    const ZcSeqTab *tab = seq_tab(extra, b);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       FseCTL &d = tb[3 * j + k];
@@ -2069,15 +2092,17 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
   const uint32_t j = min(jk / 3, kChainBlocks - 1), k = jk % 3;
   const uint64_t b = g0 + j;
   const bool act = lane < 6 * kChainBlocks && b < nblk;
-  const uint32_t ns = act ? blocks[b].nseq : 0u, nl = blocks[act ? b : 0].nlit;
+  const uint64_t bq = act ? b : 0;  // (inactive lanes: block 0's addresses, nothing stored)
+  const ZcBlock Bq = blocks[bq];
+  const uint32_t ns = act ? Bq.nseq : 0u;
   const bool split = ns >= kChainSplit;
   const uint32_t h = split ? ns / 2 : ns;                       // half 0: codes [1, h), half 1: [h, ns)
   const uint32_t m_lo = half ? h : 1u, m_hi = half ? (split ? ns : h) : h;
   const uint32_t nsl = m_hi > m_lo ? m_hi - m_lo : 0u;
   const FseCTL &ct = tb[3 * j + k];
   // type k's state records, one 16-bit word per sequence (sequence order)
-  uint16_t *rec = blk_recs(words, act ? b : 0) + k * kZcSeqCap;
-  const uint8_t *cd = seq_codes(stage, act ? b : 0, nl, act ? ns : blocks[0].nseq, k);  // cd[m] = sequence ns - 1 - m
+  uint16_t *rec = blk_recs(words, extra, Bq, bq) + k * rec_cap(Bq);
+  const uint8_t *cd = seq_codes(stage, Bq, bq, k);  // codes in walking order: cd[m] = sequence ns - 1 - m
   const uint8_t *cdl = cd + m_lo;
   // 16 sequences per batch: codes of batch t in a register quad, of batch
   // t + 1 in flight (a load outside the compiler's wait counting, waited
@@ -2163,8 +2188,8 @@ __global__ __launch_bounds__(64) void k_zc_chain(const ZcBlock *blocks, uint64_t
     if (st != sg) state = st;  // (never agreed: the true walk ran to the end)
   }
   if (act && ns && (half ? split : !split)) {  // the walk that ends at the block's last code
-    seq_tab(words, b)->fin[k] = state;
-    seq_tab(words, b)->sbits[k] = sbits + (half ? bits0 : 0u);
+    seq_tab(extra, b)->fin[k] = state;
+    seq_tab(extra, b)->sbits[k] = sbits + (half ? bits0 : 0u);
   }
   ZT(1);
   ZT_PRINT("chain", blockIdx.x % 97 == 0);
@@ -2185,7 +2210,7 @@ __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint64_t lo, 
 }
 
 __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk, uint8_t *stage,
-                                                  uint32_t *words, uint64_t *piece) {
+                                                  uint32_t *words, uint8_t *extra, uint64_t *piece) {
   MCDC_VGPR_PAD(40);  // (not an exact fill)
   constexpr uint32_t kWbWords = 512 + 64 * 96 / 32 + 8;  // 512 words + a batch's bits + slack
   __shared__ uint32_t wb[kWbWords];
@@ -2195,10 +2220,11 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
   if (bi >= nblk) return;
   const ZcBlock B = blocks[bi];
   const uint32_t ns = B.nseq;
-  const uint64_t *sq = blk_seqs(words, bi);
-  // the state records: three arrays of kZcSeqCap 16-bit words (LL, OF, ML), by sequence
-  const uint16_t *rec = blk_recs(words, bi);
-  uint8_t *st = stage + bi * kZcSlot;
+  const uint64_t *sq = blk_seqs(words, B);
+  // the state records: three arrays of rec_cap 16-bit words (LL, OF, ML), by sequence
+  const uint16_t *rec = blk_recs(words, extra, B, bi);
+  const uint32_t rcap = rec_cap(B);
+  uint8_t *st = blk_slot(stage, B, bi);
   uint32_t csize = 0;
   if (ns || B.lsize) {  // (no sequences but a Huffman / RLE section: a literals-only block)
     const uint32_t at = B.lsize ? B.lsize : kLitHdr + B.nlit;  // the literals section (k_zc_huff / raw)
@@ -2208,7 +2234,7 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
       csize = at + 1 < B.len ? at + 1 : 0;
     } else {
       ZT_DECL;
-      const ZcSeqTab *tab = seq_tab(words, bi);
+      const ZcSeqTab *tab = seq_tab(extra, bi);
       const uint32_t ndesc = tab->P.ndesc;
       // the section: header, then the bitstream from a 4-byte aligned word base
       const uint32_t cnt = ns < 128 ? 1u : ns < 0x7F00 ? 2u : 3u;
@@ -2255,8 +2281,8 @@ __global__ __launch_bounds__(64) void k_zc_encode(ZcBlock *blocks, uint64_t nblk
           const int32_t i = b1 - 1 - (int32_t)lane, ic = i >= 0 ? i : 0;
           asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(q) : "v"(sq + ic) : "memory");
           asm volatile("global_load_ushort %0, %1, off" : "=v"(r0) : "v"(rec + ic) : "memory");
-          asm volatile("global_load_ushort %0, %1, off" : "=v"(r1) : "v"(rec + kZcSeqCap + ic) : "memory");
-          asm volatile("global_load_ushort %0, %1, off" : "=v"(r2) : "v"(rec + 2 * kZcSeqCap + ic) : "memory");
+          asm volatile("global_load_ushort %0, %1, off" : "=v"(r1) : "v"(rec + rcap + ic) : "memory");
+          asm volatile("global_load_ushort %0, %1, off" : "=v"(r2) : "v"(rec + 2 * rcap + ic) : "memory");
         };
         auto batch = [&](int32_t b1, u32x2 &qv, uint32_t &r0, uint32_t &r1, uint32_t &r2) {
           const int32_t b0 = b1 > 64 ? b1 - 64 : 0;
@@ -2358,7 +2384,7 @@ __global__ __launch_bounds__(64) void k_zc_final(const uint8_t *base, const ZcBl
     d[lane] = (uint8_t)(h >> (8 * lane));
   }
   d += kBlockHdr;
-  const uint8_t *s = comp ? stage + bi * kZcSlot : base + B.src;
+  const uint8_t *s = comp ? blk_slot(const_cast<uint8_t *>(stage), B, bi) : base + B.src;
   // bytes up to the output's 16-byte grid, then aligned 16-byte stores fed by
   // misaligned 16-byte loads (gfx950 reads them as the bytes at the address,
   // tools/dbg/unaligned_probe.hip), the tail byte by byte
@@ -2390,30 +2416,33 @@ size_t zc_tmp_bytes(uint64_t n) {
 }
 
 void launch_zc_nblocks(const DevChunk *chunks, uint64_t n, uint64_t nbytes, uint64_t *cnt, uint64_t *first,
-                       uint32_t *err, uint64_t *bound, uint8_t *cls, void *tmp, size_t tmp_bytes, hipStream_t st) {
+                       uint64_t *wcnt, uint64_t *wfirst, uint32_t *err, uint64_t *bound, uint8_t *cls, void *tmp,
+                       size_t tmp_bytes, hipStream_t st) {
   hipLaunchKernelGGL(k_zc_nblocks, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, chunks, n, nbytes, cnt,
-                     err, bound, cls);
+                     wcnt, err, bound, cls);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, cnt, first, (int)n + 1, st);
+  b = tmp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, wcnt, wfirst, (int)n + 1, st);
 }
 
-void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first, uint64_t c0,
-                     uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks, uint8_t *stage,
-                     uint32_t *words, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
+void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunks, const uint64_t *first,
+                     const uint64_t *wfirst, uint64_t c0, uint64_t c1, uint64_t b0, uint64_t nblk, ZcBlock *blocks,
+                     uint8_t *stage, uint32_t *words, uint8_t *extra, const zs::ZTables &T, uint64_t *piece, uint64_t *poff,
                      uint64_t *obase,
                      uint8_t *out, uint64_t *ext, void *tmp, size_t tmp_bytes, hipStream_t st, bool huf,
                      hipEvent_t final_after, hipEvent_t final_done, bool far, uint64_t nseg, const uint64_t *nsmall) {
   if (nblk == 0) return;
   if (nseg == 0 || nseg > nblk) nseg = nblk, nsmall = nullptr;  // (every segment's first record is in order[0, nseg))
-  hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, c0, c1,
-                     b0, blocks);
+  hipLaunchKernelGGL(k_zc_blocks, dim3((unsigned)((c1 - c0 + 255) / 256)), dim3(256), 0, st, chunks, first, wfirst,
+                     c0, c1, b0, blocks);
   // (piece, nblk + 1 words of 8 bytes, is free until k_zc_encode: the
   // finder's segment order and the parse's block order)
   uint32_t *order = reinterpret_cast<uint32_t *>(piece), *porder = order + nblk;
   hipLaunchKernelGGL(k_zc_segorder, dim3(1), dim3(1024), 0, st, blocks, nblk, order, porder);
-  // (the far tables and ballots live in the staging slots, free until k_zc_parse)
-  static_assert(kZcFarSlots * 4 + kZcFarBallots * 8 <= kZcSlot, "far tables in the staging slots");
-  uint32_t *ftab = reinterpret_cast<uint32_t *>(stage);
+  // (the far tables and ballots live in extra[], free until k_zc_plan)
+  static_assert(kZcFarSlots * 4 + kZcFarBallots * 8 <= kZcExtra, "far tables in extra[]");
+  uint32_t *ftab = reinterpret_cast<uint32_t *>(extra);
   uint64_t *fbits = reinterpret_cast<uint64_t *>(ftab + nblk * kZcFarSlots);
   // the probe over the segments of longer chunks (the front of the order),
   // the small chunks (one block) by k_zc_small per size class (then the
@@ -2457,11 +2486,11 @@ void launch_zc_batch(const uint8_t *base, uint64_t nbytes, const DevChunk *chunk
     if (huf)
       hipLaunchKernelGGL(k_zc_huff, dim3((unsigned)nwork), dim3(64), 0, st, base, nbytes, blocks, nblk, stage, words,
                          porder);
-    hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nwork), dim3(64), 0, st, blocks, nblk, stage, words, T, porder);
+    hipLaunchKernelGGL(k_zc_plan, dim3((unsigned)nwork), dim3(64), 0, st, blocks, nblk, stage, words, extra, T, porder);
   }
   hipLaunchKernelGGL(k_zc_chain, dim3((unsigned)((nblk + kChainBlocks - 1) / kChainBlocks)), dim3(64), 0, st, blocks,
-                     nblk, stage, words);
-  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, words, piece);
+                     nblk, stage, words, extra);
+  hipLaunchKernelGGL(k_zc_encode, dim3((unsigned)nblk), dim3(64), 0, st, blocks, nblk, stage, words, extra, piece);
   size_t b = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, b, piece, poff, (int)nblk + 1, st);
   if (final_after) (void)hipStreamWaitEvent(st, final_after, 0);

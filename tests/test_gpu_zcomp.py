@@ -392,12 +392,57 @@ def test_scratch_query(ctx):
     small = np.zeros(3, dtype=_lib.CHUNK_DTYPE)
     small["length"] = [100_000, 65_536, 1]
     s = ctx.zstd_compress_scratch(small)
-    assert 4.5 * 6 * 32768 < s < 8 * 6 * 32768 + (1 << 20)  # (6 blocks: ~5 bytes of scratch per byte + pads)
+    # (~5 bytes of scratch per byte of the chunks, rounded to 64, + 6 KiB per block + pads)
+    assert 5 * 165_632 < s < 8 * 165_632 + (1 << 20)
     big = np.zeros(40_000, dtype=_lib.CHUNK_DTYPE)
     big["length"] = 65_536
     b = ctx.zstd_compress_scratch(big)
-    # (two sets of 8192 blocks, the default batch of 16384: ~5 bytes per byte of
-    # scratch, the sequences, tables and state records aliased into the match
-    # words; at most 3 GiB for a worker context)
+    # (two sets of 256 MiB of words, the default batch of 16384 x 32 KiB: ~5
+    # bytes per byte of scratch -- the sequences and state records written over
+    # the match words, the codes in the staging slots -- + 6 KiB per block; at
+    # most 3 GiB for a worker context)
     assert 4.5 * 16384 * 32768 < b <= 3 << 30
     assert ctx.zstd_compress_scratch(big[:0]) == 0
+
+
+@pytest.mark.parametrize("kind", ["full", "small"])
+def test_scratch_matches_allocation(kind):
+    """ADVICE (r5): mcdc_zstd_compress_scratch is what a compress call
+    allocates -- device free memory (hipMemGetInfo) before and after the first
+    call on a fresh context, within allocation granularity.  full: 64 KiB
+    chunks (two sets of full blocks); small: 2-20 KiB chunks (one-block
+    chunks, their scratch packed by length)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def free_bytes():
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        assert hip.hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
+        return f.value
+
+    n = 768 << 20
+    if kind == "full":
+        lens = np.full(n // 65536, 65536, np.uint64)
+    else:
+        lens = np.random.default_rng(5).integers(2048, 20480, n // 11264).astype(np.uint64)
+    ch = np.zeros(lens.size, _lib.CHUNK_DTYPE)
+    ch["length"] = lens
+    ch["offset"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    n = int(lens.sum())
+    c = _lib.Context(0, 1 << 20)
+    try:
+        dp = c.device_alloc(n)
+        c.fill_random(dp, n, 7)
+        cap = _lib.Context.zstd_compress_bound(ch["length"]) + 64
+        d_out = c.device_alloc(cap)
+        s = c.zstd_compress_scratch(ch)
+        f0 = free_bytes()
+        c.zstd_compress(dp, n, ch, d_out, cap)
+        used = f0 - free_bytes()
+        assert abs(used - s) <= 0.02 * s + (32 << 20), (used, s)
+        if kind == "full":
+            assert s <= 3 << 30
+        for x in (d_out, dp):
+            c.device_free(x)
+    finally:
+        c.close()
