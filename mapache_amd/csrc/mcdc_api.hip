@@ -1911,7 +1911,10 @@ static ZcBatches zc_batches(const uint64_t *first, const uint64_t *wfirst, size_
   const uint64_t total_w = wfirst[n] - wfirst[0], total_b = first[n] - first[0];
   r.two = kn.zc_two && total_w > set_w && longest_w <= set_w;
   // (blocks: twice the words' full blocks, so that a set of shorter blocks
-  // -- small files -- still holds the words' worth of input)
+  // -- small files -- still holds the words' worth of input.  Two half
+  // batches for a call of one set or less, on the two streams, measured no
+  // faster: tools/tree_probe.py 29.8-31.1 vs 29.6-31.1 ms, 256 MiB of text
+  // 59.6 vs 60.7 GiB/s, the same box)
   const uint64_t cap_w = r.two ? set_w : std::max(std::min<uint64_t>(total_w, 2 * set_w), longest_w);
   const uint64_t cap_b = r.two ? zb : std::max(std::min<uint64_t>(total_b, 2 * zb), longest_b);
   for (size_t c0 = 0; c0 < n;) {
@@ -2165,6 +2168,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   // reserved here (ensure() would wait for every stream mid-pipeline), the
   // seals' records and the headers staged in one pinned buffer, a region per
   // group (nothing the queued copies read is overwritten within the call)
+  SAVE_T("gpu: buffers");
   std::vector<size_t> gstart;
   size_t gmax = 0;
   uint64_t tmax = 0;
@@ -2200,6 +2204,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   if ((keyed && (rc = seal_workspace(ctx, gmax + hmax, tmax + htiles))) ||
       (rc = ensure_pinned(ctx, ctx->h_meta, ctx->h_meta_cap, stage_bytes)))
     return cleanup(), rc;
+  SAVE_T("gpu: groups");
   uint8_t *const hstage = (uint8_t *)ctx->h_meta;
   size_t hcur = 0;
   auto take = [&](size_t bytes) {  // a region of the pinned staging, 64-byte aligned
@@ -2234,11 +2239,13 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
       gb += zs::kFrameHdr + zs::kBlockHdr * (zfirst[k + 1] - zfirst[k]) + sext[k].length;
     cstart[g + 1] = cstart[g] + gb;
   }
+  SAVE_T("gpu: batches");
   if ((rc = stage_arg(ctx, ctx->sv_zch, sch.data(), m * sizeof(mcdc_chunk))) ||
       (rc = stage_arg(ctx, ctx->sv_zpre, zpre.data(), zpre.size() * 8)) || (rc = ensure(ctx, ctx->sv_zext, 16 * m)) ||
       (rc = ensure(ctx, ctx->zc_misc, 32)) || (rc = zc_ensure_sets(ctx, zmw, zmb, ztwo, 0)))
     return cleanup(), rc;
   HIP_TRY(hipStreamSynchronize(st));  // (the uploads read pageable host memory)
+  SAVE_T("gpu: uploads");
   const DevChunk *zch = (const DevChunk *)ctx->sv_zch.p;
   const uint64_t *dzfirst = (const uint64_t *)ctx->sv_zpre.p, *dzwfirst = dzfirst + m + 1;
   uint64_t *const zext = (uint64_t *)ctx->sv_zext.p, *const zmisc = (uint64_t *)ctx->zc_misc.p;
@@ -2545,14 +2552,12 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   auto rest = [&]() -> int {
     if (store->key && m > store->nnonces)
       return fail(MCDC_E_INVALID, "%zu new blobs need %zu nonces (%zu given)", m, m, store->nnonces);
-    std::vector<mcdc_blob> sext;
-    std::vector<uint8_t> sids;
-    sext.reserve(m);
-    sids.reserve(32 * m);
-    for (size_t i = 0; i < nb; ++i)
+    std::vector<mcdc_blob> sext(m);
+    std::vector<uint8_t> sids(32 * m);
+    for (size_t i = 0, k = 0; i < nb; ++i)
       if (nw[i]) {
-        sext.push_back(mcdc_blob{list[i].offset, list[i].length});
-        sids.insert(sids.end(), ids + 32 * i, ids + 32 * i + 32);
+        sext[k] = mcdc_blob{list[i].offset, list[i].length};
+        std::memcpy(sids.data() + 32 * k++, ids + 32 * i, 32);
       }
     const std::vector<uint8_t> types(std::max<size_t>(m, 1), 0);  // BlobType::Data (processor.rs:191)
     SAVE_T("new list");

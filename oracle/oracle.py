@@ -19,6 +19,7 @@ import hashlib
 import math
 import os
 import subprocess
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -622,15 +623,22 @@ class Zstd:
         z.ZSTD_freeCCtx(c)
         return out.raw[:ob.pos]
 
+    _tls = threading.local()
+
     def decompress(self, frame: bytes, size: int) -> bytes:
         z = self.z
         d = z.ZSTD_createDCtx()
         z.ZSTD_DCtx_setParameter(d, 100, 20)  # window_log_max 20 (storage.rs:90)
-        out = self.ct.create_string_buffer(max(size, 1))
-        r = z.ZSTD_decompressDCtx(d, out, len(out), frame, len(frame))
+        # (one output buffer per thread, reused: a fresh zero-filled buffer of
+        # the size hint per frame, under the GIL, cost a 72 000-blob decode
+        # minutes; only the r decoded bytes are copied out)
+        out = getattr(Zstd._tls, "buf", None)
+        if out is None or len(out) < max(size, 1):
+            out = Zstd._tls.buf = self.ct.create_string_buffer(max(size, 1))
+        r = z.ZSTD_decompressDCtx(d, out, max(size, 1), frame, len(frame))
         z.ZSTD_freeDCtx(d)
         assert not z.ZSTD_isError(r), "not a zstd frame within a 2^20 window"
-        return out.raw[:r]
+        return self.ct.string_at(out, r)
 
 
 # ------------------------------------------------- SecureStorage + Packer --
