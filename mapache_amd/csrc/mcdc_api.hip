@@ -282,6 +282,14 @@ struct mcdc_ctx {
 
 namespace {
 
+double now_ms();
+#ifdef MCDC_SAVE_TRACE  // (A/B builds only: host time of the save path's stages, to stderr)
+#define SAVE_T(name) fprintf(stderr, "SAVE %-14s %8.3f ms\n", name, now_ms() - t_trace0)
+#else
+#define SAVE_T(name) ((void)0)
+#endif
+static double t_trace0 = 0;
+
 // The bytes ensure() allocates for a request (headroom against regrowth):
 // mcdc_zstd_compress_scratch reports the same.
 size_t ensure_bytes(size_t bytes) {
@@ -302,6 +310,9 @@ int ensure(mcdc_ctx *ctx, DevBuf &b, size_t bytes) {
     b.cap = 0;
   }
   const size_t alloc = ensure_bytes(bytes);
+#ifdef MCDC_SAVE_TRACE
+  fprintf(stderr, "ENSURE %p %zu -> %zu\n", (void *)&b, b.cap, alloc);
+#endif
   if (hipMalloc(&b.p, alloc) != hipSuccess) {
     b.p = nullptr;
     (void)hipGetLastError();
@@ -322,6 +333,7 @@ int ensure_stage(mcdc_ctx *ctx, size_t bytes) {
     ctx->h_stage = nullptr;
     ctx->h_stage_cap = 0;
   }
+  SAVE_T("pinned alloc");
   if (hipHostMalloc(&ctx->h_stage, bytes, hipHostMallocDefault) != hipSuccess) {
     ctx->h_stage = nullptr;
     (void)hipGetLastError();
@@ -344,6 +356,7 @@ int ensure_tab(mcdc_ctx *ctx, size_t bytes) {
     ctx->h_tab_cap = 0;
   }
   const size_t alloc = (bytes + bytes / 4 + 4095) / 4096 * 4096;
+  SAVE_T("pinned alloc");
   if (hipHostMalloc(&ctx->h_tab, alloc, hipHostMallocDefault) != hipSuccess) {
     ctx->h_tab = nullptr;
     (void)hipGetLastError();
@@ -365,6 +378,7 @@ int ensure_fcnt(mcdc_ctx *ctx, size_t n) {
     ctx->h_fcnt_cap = 0;
   }
   const size_t alloc = (n + n / 4 + 511) / 512 * 512;
+  SAVE_T("pinned alloc");
   if (hipHostMalloc((void **)&ctx->h_fcnt, alloc * 8, hipHostMallocDefault) != hipSuccess) {
     ctx->h_fcnt = nullptr;
     (void)hipGetLastError();
@@ -388,6 +402,7 @@ int ensure_pinned(mcdc_ctx *ctx, void *&p, size_t &cap, size_t bytes) {
     cap = 0;
   }
   const size_t alloc = (bytes + bytes / 8 + 4095) / 4096 * 4096;
+  SAVE_T("pinned alloc");
   if (hipHostMalloc(&p, alloc, hipHostMallocDefault) != hipSuccess) {
     p = nullptr;
     (void)hipGetLastError();
@@ -438,6 +453,7 @@ double now_ms() {
 int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, uint64_t n_al,
                  const uint64_t *fstart, const uint64_t *fend, size_t nfiles, mcdc_chunk *out,
                  size_t cap, size_t *counts, size_t *n_out, const std::function<int()> &after_scan = {}) {
+  SAVE_T("pipe: start");
   uint64_t ms = 0, ml = 0;
   int rc = check_params(params, &ms, &ml);
   if (rc) return rc;
@@ -477,6 +493,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const size_t rb_cap = ctx->run_bits.cap;
   if ((rc = ensure(ctx, ctx->run_bits, nbitw * 16 + 64))) return rc;
   if (ctx->run_bits.cap != rb_cap) ctx->bits_zero = DevBuf{};  // (reallocated: the zeroed words are gone)
+  SAVE_T("pipe: ensured");
   if ((rc = ensure(ctx, ctx->err, 32))) return rc;  // (zeroed by the first scan launch)
   Work W{};
   W.base = base;
@@ -519,6 +536,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipGetLastError());
     if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));  // (the group walk's stream waits for it)
   }
+  SAVE_T("pipe: scan queued");
   if (after_scan && (rc = after_scan())) return rc;
 
   // ---- plan segments (host; reused when the layout repeats) ----
@@ -709,6 +727,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     // uploads out of the pinned stage are waited for first: a call that
     // failed after enqueuing them returned without synchronising)
     if (ctx->tab_inflight) {
+      SAVE_T("pipe: wait tab");
       HIP_TRY(hipEventSynchronize(ctx->ev_tab));
       ctx->tab_inflight = false;
     }
@@ -780,9 +799,11 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipGetLastError());
   }
 
+  SAVE_T("pipe: finish queued");
   // ---- results: one synchronisation in the common case ----
   const double t_d2h0 = now_ms();
   HIP_TRY(hipStreamSynchronize(rs));
+  SAVE_T("pipe: synced");
   const uint64_t total = ((volatile uint64_t *)ctx->h_res)[0];
   const uint32_t err = (uint32_t)((volatile uint64_t *)ctx->h_res)[1];
   const uint64_t nfallback = ((volatile uint64_t *)ctx->h_res)[2];
@@ -1776,12 +1797,6 @@ static int seal_placed(mcdc_ctx *ctx, hipStream_t st, const uint8_t *key, const 
   return MCDC_OK;
 }
 
-#ifdef MCDC_SAVE_TRACE  // (A/B builds only: host time of the save path's stages, to stderr)
-#define SAVE_T(name) fprintf(stderr, "SAVE %-14s %8.3f ms\n", name, now_ms() - t_trace0)
-#else
-#define SAVE_T(name) ((void)0)
-#endif
-static double t_trace0 = 0;
 
 // ------------------------------------------------------------ pack plan --
 // Packer::add_blob / flush over a run of encoded blob lengths
