@@ -450,7 +450,15 @@ def kernel_tree(ctx, nfiles: int, steps: int) -> dict:
                 with ctx.index_create() as ix:
                     return ctx.save_files(p512, ix, dp, offs, lens, key, nonces, hn, pad, n=n,
                                           gpu_compress=mode == "gpu_compress", out_buf=ob, split=False)
-            dt, (ids, fb, new, packed, packs) = _timed(call, steps, 1)
+            calls = []
+
+            def timed_call():
+                t0 = time.perf_counter()
+                r = call()
+                calls.append(time.perf_counter() - t0)
+                return r
+            dt, (ids, fb, new, packed, packs) = _timed(timed_call, steps, 1)
+            calls = calls[1:]  # (the warm-up call out)
             t = ctx.timing()
             distinct = len({x.tobytes() for x in ids})
             body = packed[int(packs[0]["offset"]):int(packs[0]["offset"] + packs[0]["length"])].tobytes()
@@ -458,6 +466,8 @@ def kernel_tree(ctx, nfiles: int, steps: int) -> dict:
             okd = all(O.blake3(np.frombuffer(O.storage_decode(body[o:o + ln], key, 16 << 20), np.uint8)) == b
                       for b, _, o, ln in hdr[:64])
             out[mode] = {"ms": round(dt * 1e3, 1), "gib_s": round(n / dt / GIB, 2), "files_per_s": round(nfiles / dt, 1),
+                         "ms_calls": [round(x * 1e3, 1) for x in calls],
+                         "ms_median": round(float(np.median(calls)) * 1e3, 1),
                          "blobs": int(new.size), "stored": int(new.sum()), "distinct_ids": distinct,
                          "packs": int(len(packs)), "packed_bytes": int(packed.size), "ratio": round(n / packed.size, 3),
                          "device_ms": round(t.get("device_ms", 0.0), 2), "decode_probe_ok": bool(okd and
@@ -465,7 +475,9 @@ def kernel_tree(ctx, nfiles: int, steps: int) -> dict:
     finally:
         ctx.device_free(dp)
     out["note"] = ("mcdc_save_files from device memory at 512K/1M/8M (gate 512 KiB), key, fresh index per call, "
-                   "packs D2H into a reused pinned buffer; decode probe: the first pack's first 64 blobs decoded "
+                   "packs D2H into a reused pinned buffer; ms: the mean of the timed calls (ms_calls: each; in this "
+                   "process an occasional call waits 12-30 ms with its first kernels queued and the GPU idle, "
+                   "DESIGN.md 0e item 2); decode probe: the first pack's first 64 blobs decoded "
                    "and BLAKE3-checked, stored == distinct IDs; full parity: tests/test_gpu_configs3.py")
     out["data"] = "synthetic kernel-tree stand-in (tests/corpora.kernel_tree)"
     return out
@@ -1220,7 +1232,7 @@ def main() -> int:
         for key, fn in (("batch_files", lambda: batch_files(ctx, p, a.batch_files, 8 << 20, 3, cpu_files, threads)
                          if a.batch_files > 0 else None),
                         ("small_files", lambda: small_files(ctx, p, a.small_files, 5) if a.small_files > 0 else None),
-                        ("kernel_tree", lambda: kernel_tree(ctx, a.kernel_tree, 3) if a.kernel_tree > 0 else None)):
+                        ("kernel_tree", lambda: kernel_tree(ctx, a.kernel_tree, 5) if a.kernel_tree > 0 else None)):
             try:
                 result[key] = fn()
             except Exception as ex:  # reported, never silently dropped

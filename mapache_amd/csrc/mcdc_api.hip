@@ -522,17 +522,21 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
                       ctx->bits_zero.cap == zero_bytes;
   ctx->bits_zero = DevBuf{};
   const bool lane_early = early && use_lane_walk(params, kn);
+  if (!zeroed) SAVE_T("pipe: cold");
   if (early) {
     // (the scan's start and end events are recorded by its dispatch: an event
     // record between two kernels delays the second by ~5 us, kernel traces
     // of tools/small_probe.py)
+#ifndef MCDC_COLD_EVENT  // (A/B: 1 = the start event recorded before the cold path's memset, as in round 5)
+#define MCDC_COLD_EVENT 0
+#endif
     if (!zeroed) {
-      HIP_TRY(hipEventRecord(ctx->ev_start, st));
+      if (MCDC_COLD_EVENT) HIP_TRY(hipEventRecord(ctx->ev_start, st));
       HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
     }
     const int pc = kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus);
     launch_scan(W, P, ctx->num_cus, st, 0, n_al > 0 ? (n_al / kRun) / (64 / pc) : 0, n_al > 0, pc, kn.scan_cold,
-                zeroed ? ctx->ev_start : nullptr, ctx->ev_scan);
+                zeroed || !MCDC_COLD_EVENT ? ctx->ev_start : nullptr, ctx->ev_scan);
     HIP_TRY(hipGetLastError());
     if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));  // (the group walk's stream waits for it)
   }

@@ -1,6 +1,7 @@
 """The configs[3] kernel-tree stand-in through mcdc_save_files (P512, gate,
 key, GPU compression), a few calls, for a kernel trace of what bounds it
-(tools only).  Usage: python tools/tree_probe.py [files] [calls] [host]"""
+(tools only).  Usage: python tools/tree_probe.py [files] [calls] [modes: gpu | host | host,gpu]
+(TREE_FREE_HSAVE=1: release the context's pinned host staging between the modes)"""
 import os
 import sys
 import time
@@ -13,7 +14,7 @@ from tests import corpora  # noqa: E402
 
 nfiles = int(sys.argv[1]) if len(sys.argv) > 1 else 80000
 calls = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-gpu = not (len(sys.argv) > 3 and sys.argv[3] == "host")
+modes = (sys.argv[3] if len(sys.argv) > 3 else "gpu").split(",")
 data, offs, lens, dup = corpora.kernel_tree(nfiles)
 n = int(data.size)
 p = _lib.params(512 << 10, 1 << 20, 8 << 20, 1)
@@ -27,11 +28,12 @@ with _lib.Context(0, 2 << 30) as ctx:
     dp = ctx.device_alloc(n + 16)
     ctx.h2d(dp, data)
     ob = ctx.pinned_bytes(int(n * 1.01) + 4096 * nfiles + (1 << 16))
-    for c in range(calls):
-        t0 = time.perf_counter()
-        with ctx.index_create() as ix:
-            ids, fb, new, packed, packs = ctx.save_files(p, ix, dp, offs, lens, bytes(range(32)), nonces, hn, pad, n=n,
-                                                     gpu_compress=gpu, out_buf=ob, split=False)
-        dt = time.perf_counter() - t0
-        print(f"call {c}: {dt * 1e3:.1f} ms  {n / dt / 2**30:.2f} GiB/s  stored {int(new.sum())}  packed {packed.size}",
-              flush=True)
+    for mode in modes:
+        for c in range(calls):
+            t0 = time.perf_counter()
+            with ctx.index_create() as ix:
+                ids, fb, new, packed, packs = ctx.save_files(p, ix, dp, offs, lens, bytes(range(32)), nonces, hn, pad,
+                                                         n=n, gpu_compress=mode == "gpu", out_buf=ob, split=False)
+            dt = time.perf_counter() - t0
+            print(f"{mode} call {c}: {dt * 1e3:.1f} ms  {n / dt / 2**30:.2f} GiB/s  stored {int(new.sum())}  "
+                  f"packed {packed.size}", flush=True)
