@@ -240,7 +240,8 @@ struct mcdc_ctx {
       ae_ext, ae_nonce, ae_olen, ae_tcnt, ae_ooff, ae_toff, ae_tmp, ae_rec, ae_keys, ae_owner, ae_tsum, ae_status,
       sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_wcnt, zc_wfirst, zc_blocks, zc_stage, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words,
       zc_extra, zc_blocks2, zc_stage2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_extra2,  // (the second batch set)
-      sv_zch, sv_zpre, sv_zext;  // (the GPU save path's compressor input: all blobs, prefixes, frame extents)
+      sv_zch, sv_zpre, sv_zext,  // (the GPU save path's compressor input: all blobs, prefixes, frame extents)
+      rl_ent, run_list;  // (the list-mode scan: its range entries and run list)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -276,6 +277,10 @@ struct mcdc_ctx {
   size_t h_encb_cap = 0;
   void *h_meta = nullptr;      // pinned: the GPU save path's encoded pack headers (their H2D source)
   size_t h_meta_cap = 0;
+  void *h_rl = nullptr;        // pinned: the list-mode scan's range entries (their H2D source)
+  size_t h_rl_cap = 0;
+  int list_state = 0;          // run list of the plan's layout: 0 none, 1 built (run_list), 2 not worth it
+  uint64_t list_n = 0, list_nal = 0, list_min = 0;  // its runs, the arena length and min_size it was built for
   uint64_t *d_res = nullptr;  // its device alias
   mcdc_timing timing{};
 };
@@ -445,6 +450,69 @@ double now_ms() {
       .count();
 }
 
+// The list-mode scan's run list for a layout (run_pipeline): per file longer
+// than min_size the full runs holding [start + min_size, end) -- every run a
+// chunk window of the file reads (lane_next, group_next, forced_run and
+// run_first_hit read runs at or after a chunk start + min_size of the file;
+// the restart positions before it are re-hashed from bytes) -- merged while
+// the files ascend (files that do not: no list), as entries of <= 64 runs, the
+// list expanded by k_run_list on stream2.  Kept (list_state 1) when it skips
+// at least 20 % of the runs (MCDC_RUN_LIST=2: always).
+int build_run_list(mcdc_ctx *ctx, const mcdc_params *params, uint64_t n_al, const uint64_t *fstart,
+                   const uint64_t *fend, size_t nfiles) {
+  const Knobs &kn = ctx->knobs;
+  const uint64_t nfull = n_al / kRun, mn = params->min_size;
+  ctx->list_state = 2;
+  uint32_t *e = nullptr;
+  int rc = MCDC_OK;
+  uint64_t tot = 0, k = 0;
+  // two passes: the runs it would list (the decision), then the entries
+  auto pass = [&](bool write) -> bool {
+    uint64_t c0 = 0, c1 = 0;
+    tot = k = 0;
+    auto flush = [&]() {
+      if (!write) {
+        tot += c1 - c0;
+        return;
+      }
+      for (uint64_t r = c0; r < c1; r += 64, ++k) {
+        e[2 * k] = (uint32_t)r;
+        e[2 * k + 1] = (uint32_t)tot;
+        tot += std::min<uint64_t>(64, c1 - r);
+      }
+    };
+    for (size_t i = 0; i < nfiles; ++i) {
+      if (fend[i] - fstart[i] <= mn) continue;  // (one chunk, hash 0: nothing of it is hashed)
+      const uint64_t r0 = (fstart[i] + mn) / kRun, r1 = std::min<uint64_t>((fend[i] + kRun - 1) / kRun, nfull);
+      if (r0 >= r1) continue;
+      if (r0 < c0) return false;  // (files not ascending: the flat scan)
+      if (r0 <= c1 && c1 > c0) {
+        c1 = std::max(c1, r1);
+      } else {
+        flush();
+        c0 = r0;
+        c1 = r1;
+      }
+    }
+    flush();
+    return true;
+  };
+  if (!pass(false) || tot >= (1ull << 32) || !(kn.run_list == 2 || (nfull >= 2048 && tot * 5 <= nfull * 4)))
+    return MCDC_OK;
+  if ((rc = ensure_pinned(ctx, ctx->h_rl, ctx->h_rl_cap, (nfiles + tot / 64 + 2) * 8))) return rc;
+  e = (uint32_t *)ctx->h_rl;
+  pass(true);
+  if ((rc = ensure(ctx, ctx->rl_ent, k * 8)) || (rc = ensure(ctx, ctx->run_list, (tot + 64) * 4))) return rc;
+  if (k) HIP_TRY(hipMemcpyAsync(ctx->rl_ent.p, ctx->h_rl, k * 8, hipMemcpyHostToDevice, ctx->stream2));
+  launch_run_list((const uint32_t *)ctx->rl_ent.p, k, tot, (uint32_t *)ctx->run_list.p, nullptr, 0, ctx->stream2);
+  HIP_TRY(hipGetLastError());
+  ctx->list_state = 1;
+  ctx->list_n = tot;
+  ctx->list_nal = n_al;
+  ctx->list_min = mn;
+  return MCDC_OK;
+}
+
 // Core: files are [fstart[i], fend[i]) in an arena at `base` (16-aligned),
 // arena length n_al (multiple of 16, all reads stay below it).
 // after_scan (optional) runs once the scan is enqueued, before fstart /
@@ -523,22 +591,47 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   ctx->bits_zero = DevBuf{};
   const bool lane_early = early && use_lane_walk(params, kn);
   if (!zeroed) SAVE_T("pipe: cold");
-  if (early) {
+  // List-mode scan: cut_gear hashes a chunk from min_size on (v2020), so a
+  // file's first min_size bytes, less the 48-byte window warm-up, are read by
+  // no chunk window -- every byte of a file up to min_size long: half the
+  // bytes of the configs[3] stand-in.  The run list (build_run_list) depends
+  // only on the layout, like the segment plan, and is kept with it: a call
+  // whose layout repeats the previous call's builds it (on the host, while its
+  // scan runs) and the calls after it scan through it, speculatively -- the
+  // layout is compared with the plan's while the scan runs, and a call whose
+  // layout turns out different re-scans flat (one wasted list scan; a
+  // workload whose layouts change never builds a list, so never speculates).
+  const bool spec_list = early && ctx->list_state == 1 && ctx->list_nal == n_al && ctx->list_min == params->min_size &&
+                         (kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus)) == 2;
+  auto scan_flat = [&](bool cold) -> int {
     // (the scan's start and end events are recorded by its dispatch: an event
     // record between two kernels delays the second by ~5 us, kernel traces
     // of tools/small_probe.py)
 #ifndef MCDC_COLD_EVENT  // (A/B: 1 = the start event recorded before the cold path's memset, as in round 5)
 #define MCDC_COLD_EVENT 0
 #endif
-    if (!zeroed) {
+    if (cold) {
       if (MCDC_COLD_EVENT) HIP_TRY(hipEventRecord(ctx->ev_start, st));
       HIP_TRY(hipMemsetAsync(W.run_bits + 2 * bw0, 0, zero_bytes, st));
     }
     const int pc = kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus);
     launch_scan(W, P, ctx->num_cus, st, 0, n_al > 0 ? (n_al / kRun) / (64 / pc) : 0, n_al > 0, pc, kn.scan_cold,
-                zeroed || !MCDC_COLD_EVENT ? ctx->ev_start : nullptr, ctx->ev_scan);
+                !cold || !MCDC_COLD_EVENT ? ctx->ev_start : nullptr, ctx->ev_scan);
     HIP_TRY(hipGetLastError());
     if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));  // (the group walk's stream waits for it)
+    return MCDC_OK;
+  };
+  if (spec_list) {  // (the bitmap words and the tile counter zeroed, then the listed runs and the partial last run)
+    launch_run_list(nullptr, 0, 0, nullptr, W.run_bits, 2 * nbitw + 1, st, ctx->ev_start);
+    W.run_list = (const uint32_t *)ctx->run_list.p;
+    W.list_n = ctx->list_n;
+    launch_scan(W, P, ctx->num_cus, st, 0, (ctx->list_n + 31) / 32, true, 2, false, nullptr, ctx->ev_scan);
+    HIP_TRY(hipGetLastError());
+    W.run_list = nullptr;  // (the resolution kernels take W by value: the scan's fields only)
+    W.list_n = 0;
+    if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));
+  } else if (early) {
+    if ((rc = scan_flat(!zeroed))) return rc;
   }
   SAVE_T("pipe: scan queued");
   if (after_scan && (rc = after_scan())) return rc;
@@ -583,6 +676,17 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     }
   }
   const uint32_t nsegs = (uint32_t)ctx->h_segs.size();
+  // the run list follows the plan: a new layout drops it; a speculative list
+  // scan of another layout's runs is replaced by the flat scan (same stream:
+  // every kernel after it reads the flat scan's run data)
+  if (!same_plan) ctx->list_state = 0;
+  if (spec_list && !same_plan && (rc = scan_flat(true))) return rc;
+  bool list_built = false;
+  if (early && same_plan && ctx->list_state == 0 && kn.run_list && n_al >= kRun &&
+      (kn.scan_pieces ? kn.scan_pieces : scan_pieces(n_al / kRun, ctx->num_cus)) == 2) {
+    if ((rc = build_run_list(ctx, params, n_al, fstart, fend, nfiles))) return rc;
+    list_built = ctx->list_state == 1;
+  }
 
   // ---- workspace ----
   const void *tabs_before[3] = {ctx->segs.p, ctx->files.p, ctx->node_off.p};
@@ -807,6 +911,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   // ---- results: one synchronisation in the common case ----
   const double t_d2h0 = now_ms();
   HIP_TRY(hipStreamSynchronize(rs));
+  if (list_built && rs != st2) HIP_TRY(hipStreamSynchronize(st2));  // (the run list's build, long done)
   SAVE_T("pipe: synced");
   const uint64_t total = ((volatile uint64_t *)ctx->h_res)[0];
   const uint32_t err = (uint32_t)((volatile uint64_t *)ctx->h_res)[1];
@@ -1073,6 +1178,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_zarena) (void)hipHostFree(ctx->h_zarena);
   if (ctx->h_encb) (void)hipHostFree(ctx->h_encb);
   if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
+  if (ctx->h_rl) (void)hipHostFree(ctx->h_rl);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
@@ -1086,7 +1192,8 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->sv_in, &ctx->sv_pack, &ctx->sv_comp, &ctx->sv_seal, &ctx->sv_ext, &ctx->zc_cnt, &ctx->zc_cls, &ctx->zc_first, &ctx->zc_wcnt, &ctx->zc_wfirst, &ctx->zc_blocks, &ctx->zc_stage,
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_extra,
                     &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
-                    &ctx->zc_words2, &ctx->zc_extra2, &ctx->sv_zch, &ctx->sv_zpre, &ctx->sv_zext};
+                    &ctx->zc_words2, &ctx->zc_extra2, &ctx->sv_zch, &ctx->sv_zpre, &ctx->sv_zext, &ctx->rl_ent,
+                    &ctx->run_list};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);

@@ -141,6 +141,8 @@ struct Work {
   uint32_t *punt_link;   // (k_link_list), count err[5]
   uint32_t ncu;          // compute units (persistent grids)
   uint64_t *lb_status;   // k_incr_lookback tile status words (lane walk: zeroed per call), ticket err[6]
+  const uint32_t *run_list;  // list-mode scan (or nullptr): the full runs a chunk window can reach, ascending
+  uint64_t list_n;           // (k_run_list builds it; k_scan_q<.., LIST> scans only those)
 };
 
 // Tuning switches of a context, read from the environment once, when the
@@ -159,6 +161,8 @@ struct Knobs {
   int pinned_direct = 1;  // MCDC_PINNED_DIRECT: k_emit writes pinned host output directly
   int lane_walk = 1;      // MCDC_LANE_WALK: 0 group walk only, 1 lane walk when max <= 64 runs, 2 always
   int lane_seg_chunks = 4;// MCDC_LANE_SEG_CHUNKS: expected chunks per segment on the lane walk
+  int run_list = 1;       // MCDC_RUN_LIST: list-mode scan of batch calls (0 off, 1 when it skips >= 20 % of
+                          // the runs, 2 whenever the layout allows it: tests)
   bool zc_huf = true;      // MCDC_ZC_HUF: Huffman / RLE literals in the GPU zstd compressor
   bool zc_two = true;      // MCDC_ZC_TWO: compressor batches alternate between two streams
   uint64_t save_group_blocks = 0;  // GPU save path: blocks per compression group (0: max(zc_batch, 32768))
@@ -205,5 +209,10 @@ size_t scan_tmp_bytes(uint32_t nsegs);
 void launch_finish(const Work &w, uint64_t *res, hipStream_t stream, hipEvent_t ev_done = nullptr,
                    uint64_t *zero = nullptr, uint32_t zwords = 0);
 void launch_file_counts(const Work &w, uint64_t *dst, hipStream_t stream);  // chunks per file -> dst
+// the list-mode scan's run list from nent {first run, list index} entries
+// (each <= 64 runs, the last ending at list_n), the candidate-bitmap words and
+// the tile counter zeroed (words [0, nwords)); ev0: recorded at its start
+void launch_run_list(const uint32_t *ent, uint64_t nent, uint64_t list_n, uint32_t *list, uint64_t *words,
+                     uint64_t nwords, hipStream_t stream, hipEvent_t ev0 = nullptr);
 
 }  // namespace mcdc

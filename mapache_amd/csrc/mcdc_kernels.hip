@@ -394,18 +394,20 @@ static_assert(kQBlkDw == 4 || kQBlkDw == 8, "16- or 32-byte prefilter blocks");
 // Drain the wave's queue: lane i re-walks entry i's block exactly.
 // PC pieces per run: lane l hashes bytes [l*SUB, (l+1)*SUB) of the tile, part
 // l % PC of run run0 + l / PC; offsets and counters are per run.
-template <int RUN, int PC>
+template <int RUN, int PC, bool LIST = false>
 __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t lo, const uint8_t *base,
                                                   uint32_t *run_ent, uint64_t ms16, uint64_t ml16, uint32_t cap,
                                                   const char *pad, uint32_t *lcnt, uint32_t qn, uint64_t run0,
-                                                  uint32_t lane) {
+                                                  uint32_t lane, const uint32_t *lst = nullptr, uint32_t lim = 0) {
   constexpr int SUB = RUN / PC;
   if (lane < qn) {
     const char *slot = pad + lane * kQPad + 64;
     uint64_t x = *reinterpret_cast<const uint64_t *>(slot);
     const uint32_t meta = *reinterpret_cast<const uint32_t *>(slot + 8);
     const uint32_t pl = meta >> 16, rl = pl / PC, off = (pl % PC) * SUB + (meta & 0xffffu);
-    const uint64_t run = run0 + rl;
+    const uint64_t run = LIST ? (uint64_t)lst[min(rl, lim)] : run0 + rl;  // (list mode: the tile's rl-th listed run)
+    // (list mode: lanes past the list's end re-scan its last run; only its own lanes store)
+    const uint32_t kcap = LIST && rl > lim ? 0u : cap;
     uint32_t *ent = run_ent + run * (uint64_t)cap;
     uint32_t wd[kQBlkDw];
 #pragma unroll
@@ -419,7 +421,7 @@ __device__ __attribute__((noinline)) void q_drain(const uint64_t *tab, uint32_t 
       const uint32_t s_ = (x & ms16) == 0, l_ = (x & ml16) == 0;
       if (s_ | l_) {
         const uint32_t k = atomicAdd(&lcnt[rl], 1u);
-        if (k < cap) ent[k] = (off + i) | (s_ << 31) | (l_ << 30);
+        if (k < kcap) ent[k] = (off + i) | (s_ << 31) | (l_ << 30);
         if (s_) atomicMin(&lcnt[64 + rl], off + i);   // first S / first L of the run (summary)
         if (l_) atomicMin(&lcnt[128 + rl], off + i);
       }
@@ -435,6 +437,8 @@ struct QScan {  // per-wave state of k_scan_q
   uint32_t *lcnt;
   const uint8_t *base;
   uint32_t *run_ent;
+  const uint32_t *lst;  // list mode: the tile's runs (W.run_list + RPT t), lim = valid entries - 1
+  uint32_t lim;
 };
 
 // 64 bytes (16 dwords) of one run: lookups one dword ahead of the chain;
@@ -443,7 +447,7 @@ struct QScan {  // per-wave state of k_scan_q
 // ND dwords (16: one 64-byte group; 12: the re-walked first 48 bytes of a
 // cold-started piece).  skip3: the first 48 positions of a cold-started piece
 // hold incomplete windows; their blocks are not tested here (see k_scan_q).
-template <int RUN, int PC, int ND = 16>
+template <int RUN, int PC, int ND = 16, bool LIST = false>
 __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint64_t &h, uint32_t off,
                                         uint32_t &qn, uint64_t run0, bool skip3 = false) {
   uint64_t g[2][4];
@@ -465,7 +469,8 @@ __device__ __forceinline__ void scan64q(const QScan &q, const uint32_t *w, uint6
       if (__builtin_expect(m != 0, 0)) {
         const uint32_t n = (uint32_t)__popcll(m);
         if (qn + n > 64) {
-          q_drain<RUN, PC>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, q.lane);
+          q_drain<RUN, PC, LIST>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, q.lane,
+                                 q.lst, q.lim);
           qn = 0;
         }
         if (acc == 0) {
@@ -509,9 +514,19 @@ __device__ __forceinline__ void store_run_bits(uint64_t *bits, uint64_t run0, ui
 // the end of the tile from the previous lane's final hash (the state after
 // the previous piece), so the previous piece's last line is fetched once.
 // Lane 0 still warms up from memory (the previous tile is another wave's).
-template <int RUN, int PC, bool CW>
+//
+// LIST (run-list mode, small-file calls): tile t is the RPT runs
+// W.run_list[RPT t, + RPT) instead of the contiguous runs RPT t.. -- the runs
+// some chunk window can reach (a file's first min_size - 64 bytes never are:
+// cut_gear starts hashing at min_size, v2020), so the bytes of every file
+// below min_size and every file's head are not scanned.  Each lane warms up
+// from the 48 bytes before its piece (pieces of consecutive list entries need
+// not be adjacent); the runs' bitmap bits are set with atomics (words zeroed
+// by k_run_list); the arena's partial last run is the tail (scan_run_coop).
+template <int RUN, int PC, bool CW, bool LIST = false>
 __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_t tile0, uint64_t tile1,
                                                    int do_tail) {
+  static_assert(!LIST || (PC == 2 && !CW), "list mode: two warm pieces per run");
   // + one 8-byte slot per wave: lane 0's warm-up hash waits there for the
   // tile-end re-walk (CW) instead of holding two VGPRs across the tile
   __shared__ __attribute__((aligned(16))) uint64_t smem[(kSTab + 16 * kQWaveBytes) / 8 + 16];
@@ -520,6 +535,8 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
   QScan q;
+  q.lst = nullptr;
+  q.lim = 0;
   q.tab = smem;
   q.lo = (lane & 31) << 3;
   q.lane = lane;
@@ -545,7 +562,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   constexpr int SUB = RUN / PC, RPT = 64 / PC;  // bytes per lane piece, runs per tile
   const uint64_t nfull = W.n_al / RUN;
   const uint64_t ntiles_full = nfull / RPT;
-  if (tile1 > ntiles_full) tile1 = ntiles_full;
+  if (!LIST && tile1 > ntiles_full) tile1 = ntiles_full;
   constexpr int G = SUB / 64;
   static_assert(G % 2 == 0, "even group count");
   const uint32_t qi = lane >> 2, qj = lane & 3;
@@ -574,13 +591,22 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
   // (a 1.3 GB call: scan 0.80 -> ~0.4 ms).
   if (do_tail) {  // one wave per run, the last waves first (in a static round they have the fewest tiles)
     const uint64_t nruns = (W.n_al + RUN - 1) / RUN;
-    for (uint64_t run = ntiles_full * RPT + (nwaves - 1 - wid); run < nruns; run += nwaves)
+    for (uint64_t run = (LIST ? nfull : ntiles_full * RPT) + (nwaves - 1 - wid); run < nruns; run += nwaves)
       scan_run_coop(q.tab, q.lo, W, P, run, lane);
   }
   uint64_t t = dyn && !W.first_static ? grab() : tile0 + wid;
   while (t < tile1) {
     const uint64_t t_next = dyn ? grab() : t + nwaves;
-    const uint64_t run0 = t * RPT, piece = t * 64 + lane;
+    const uint64_t run0 = t * RPT;
+    uint64_t piece = t * 64 + lane;
+    uint64_t ra = 0, rb = 0;  // list mode: this lane quad's two runs (pieces 4 qi .. 4 qi + 3), byte offsets
+    if constexpr (LIST) {
+      q.lst = W.run_list + run0;
+      q.lim = (uint32_t)min<uint64_t>(RPT, W.list_n - run0) - 1;
+      piece = (uint64_t)q.lst[min(lane / PC, q.lim)] * PC + lane % PC;
+      ra = (uint64_t)q.lst[min(2 * qi, q.lim)] * RUN + 16 * qj;
+      rb = (uint64_t)q.lst[min(2 * qi + 1, q.lim)] * RUN + 16 * qj;
+    }
     uint64_t h = 0, hw = 0;
     if (piece > 0 && (!CW || lane == 0)) {  // warm-up: the 48 bytes before the piece complete every window
       const uint4 *p = reinterpret_cast<const uint4 *>(W.base + piece * (uint64_t)SUB);
@@ -594,7 +620,9 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     uint4 f0, f1, f2;  // CW: the piece's first 48 bytes
     uint32_t qn = 0;  // wave-uniform queue length
     const uint8_t *tb = W.base + run0 * (uint64_t)RUN;  // wave-uniform tile base (SGPR)
-#define MCDC_LDQ(k, gg) (*reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * SUB + 64 * (gg))))
+#define MCDC_LDQ(k, gg)                                                                                     \
+  (LIST ? *reinterpret_cast<const uint4 *>(W.base + ((k) < 2 ? ra : rb) + ((k) & 1) * SUB + 64 * (gg))       \
+        : *reinterpret_cast<const uint4 *>(tb + (uint64_t)(uint32_t)(o0 + (k) * SUB + 64 * (gg))))
     uint4 a0 = MCDC_LDQ(0, 0), a1 = MCDC_LDQ(1, 0), a2 = MCDC_LDQ(2, 0), a3 = MCDC_LDQ(3, 0);
     uint4 b0 = MCDC_LDQ(0, 1), b1 = MCDC_LDQ(1, 1), b2 = MCDC_LDQ(2, 1), b3 = MCDC_LDQ(3, 1);
 #pragma unroll 1
@@ -611,7 +639,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
         if (CW && g == 0) { f0 = c0; f1 = c1; f2 = c2; }
-        scan64q<RUN, PC>(q, w, h, 64u * g, qn, run0, CW && g == 0);
+        scan64q<RUN, PC, 16, LIST>(q, w, h, 64u * g, qn, run0, CW && g == 0);
       }
       {
         *reinterpret_cast<uint4 *>(wr) = b0;
@@ -631,7 +659,7 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
         a2 = MCDC_LDQ(2, ga); b2 = MCDC_LDQ(2, gb); a3 = MCDC_LDQ(3, ga); b3 = MCDC_LDQ(3, gb);
         const uint32_t w[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        scan64q<RUN, PC>(q, w, h, 64u * (g + 1), qn, run0);
+        scan64q<RUN, PC, 16, LIST>(q, w, h, 64u * (g + 1), qn, run0);
       }
     }
 #undef MCDC_LDQ
@@ -641,11 +669,25 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
       const uint32_t w[12] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, f2.x, f2.y, f2.z, f2.w};
       scan64q<RUN, PC, 12>(q, w, hp, 0u, qn, run0);
     }
-    if (qn) q_drain<RUN, PC>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane);
+    if (qn)
+      q_drain<RUN, PC, LIST>(q.tab, q.lo, q.base, q.run_ent, q.ms16, q.ml16, q.cap, q.pad, q.lcnt, qn, run0, lane,
+                             q.lst, q.lim);
     const uint32_t cnt = q.lcnt[lane], fs = q.lcnt[64 + lane], fl = q.lcnt[128 + lane];
     q.lcnt[lane] = 0;
     q.lcnt[64 + lane] = 0xffffffffu;
     q.lcnt[128 + lane] = 0xffffffffu;
+    if constexpr (LIST) {  // (entries past the list's end repeat its last run: written once, by its own lane)
+      if (lane <= q.lim) {
+        const uint64_t run = q.lst[lane];
+        W.run_cnt[run] = cnt > q.cap ? kRunOverflow : (uint8_t)cnt;
+        W.run_sum[run] = run_summary(cnt, fs, fl);
+        uint32_t *b32 = reinterpret_cast<uint32_t *>(W.run_bits) + 4 * (run >> 6) + ((run >> 5) & 1);
+        if (fs != 0xffffffffu) atomicOr(b32, 1u << (run & 31));
+        if (fl != 0xffffffffu) atomicOr(b32 + 2, 1u << (run & 31));
+      }
+      t = t_next;
+      continue;
+    }
     const bool mine = PC == 1 || lane < RPT;
     if (mine) {
       const uint64_t run = run0 + lane;
@@ -658,6 +700,29 @@ __global__ __launch_bounds__(1024, 4) void k_scan_q(Work W, DevParams P, uint64_
     }
     t = t_next;
   }
+}
+
+// The list-mode scan's run list: entry i = {first run, list index} of up to 64
+// consecutive runs (the host merges and splits the files' ranges), written
+// one thread per entry; the same grid zeroes the candidate-bitmap words and
+// the tile counter after them (the scan sets the listed runs' bits with atomics).
+__global__ void k_run_list(const uint2 *ent, uint64_t nent, uint64_t list_n, uint32_t *list, uint64_t *words,
+                           uint64_t nwords) {
+  MCDC_VGPR_PAD(16);  // (not an exact fill)
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nent) {  // (nent = 0: the zeroing only)
+    const uint2 e = ent[i];
+    const uint64_t p1 = i + 1 < nent ? ent[i + 1].y : list_n;
+    for (uint64_t j = e.y; j < p1; ++j) list[j] = e.x + (uint32_t)(j - e.y);
+  }
+  for (uint64_t k = i; k < nwords; k += (uint64_t)gridDim.x * blockDim.x) words[k] = 0;
+}
+
+void launch_run_list(const uint32_t *ent, uint64_t nent, uint64_t list_n, uint32_t *list, uint64_t *words,
+                     uint64_t nwords, hipStream_t stream, hipEvent_t ev0) {
+  const uint64_t n = std::max<uint64_t>(std::max(nent, std::min<uint64_t>(nwords, 65536)), 1);
+  hipExtLaunchKernelGGL(k_run_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ev0, nullptr, 0,
+                        reinterpret_cast<const uint2 *>(ent), nent, list_n, list, words, nwords);
 }
 
 // Product configuration: quad-coalesced scan, 16 waves (one 1024-thread
@@ -678,7 +743,9 @@ void launch_scan(const Work &w, const DevParams &p, int num_cus, hipStream_t str
   }
   const int t = tail ? 1 : 0;
   const dim3 gr((unsigned)blocks), bl(1024);
-  if (cold && pieces != 1) {  // (one piece: the saved bytes would spill, 128 VGPRs)
+  if (w.run_list) {  // list mode (tile1: the list's tiles of 32 runs; tail: the partial last run)
+    hipExtLaunchKernelGGL((k_scan_q<kRun, 2, false, true>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
+  } else if (cold && pieces != 1) {  // (one piece: the saved bytes would spill, 128 VGPRs)
     if (pieces == 4) hipExtLaunchKernelGGL((k_scan_q<kRun, 4, true>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
     else hipExtLaunchKernelGGL((k_scan_q<kRun, 2, true>), gr, bl, 0, stream, ev0, ev1, 0, w, p, tile0, tile1, t);
   } else {
@@ -2161,6 +2228,7 @@ Knobs read_knobs() {
   k.pinned_direct = env("MCDC_PINNED_DIRECT", k.pinned_direct) != 0;
   k.lane_walk = std::min(std::max(env("MCDC_LANE_WALK", k.lane_walk), 0), 2);
   k.lane_seg_chunks = std::max(env("MCDC_LANE_SEG_CHUNKS", k.lane_seg_chunks), 1);
+  k.run_list = std::min(std::max(env("MCDC_RUN_LIST", k.run_list), 0), 2);
   k.zc_huf = env("MCDC_ZC_HUF", k.zc_huf ? 1 : 0) != 0;
   k.zc_two = env("MCDC_ZC_TWO", k.zc_two ? 1 : 0) != 0;
 #ifdef MCDC_AB_KNOBS

@@ -590,3 +590,103 @@ def test_pageable_staging_sizes(ctx):
     r, rc = O.chunk_files(O.Params(*p), files, threads=8)
     assert (gc == rc).all()
     _same(g, r)
+
+
+def _arena_files(rng, sizes, gaps):
+    """Host bytes of files laid out in one arena with the given gaps before
+    each; returns (arena bytes, offsets, lengths, per-file arrays)."""
+    parts, offs, at = [], [], 0
+    files = []
+    for i, (s, g) in enumerate(zip(sizes, gaps)):
+        if g:
+            parts.append(rng.integers(0, 256, int(g), dtype=np.uint8))
+            at += int(g)
+        d = O.random_bytes(int(s), SEED + 7919 * i + int(s))
+        files.append(d)
+        parts.append(d)
+        offs.append(at)
+        at += int(s)
+    arena = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return arena, np.array(offs, np.uint64), np.array([int(s) for s in sizes], np.uint64), files
+
+
+def _batch_device_calls(ctx, p, arena, offs, lens, calls):
+    """`calls` calls of mcdc_chunk_batch_device on one uploaded arena."""
+    dp = ctx.device_alloc(arena.size + 16)
+    try:
+        ctx.h2d(dp, arena)
+        return [ctx.chunk_batch_device(_lib.params(*p), dp, offs, lens) for _ in range(calls)]
+    finally:
+        ctx.device_free(dp)
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_run_list_scan(knob_ctx, mode):
+    """The list-mode scan (MCDC_RUN_LIST=2: whenever the files ascend; 0: the
+    flat scan) of device batches: only the runs some chunk window reaches (a
+    file's first min_size bytes are never hashed by cut_gear) are scanned,
+    through a run list built on a call whose layout repeats the previous one
+    and used by the calls after it.  Every layout three times (flat, flat +
+    list built, list scan) against the oracle, file by file: sizes around
+    min_size and its window warm-up, files crossing run edges, gaps, a partial
+    last run, every file at most min_size (a list of no runs), tiny parameters
+    whose files share runs (ranges merged), a dense-byte file (overflowed
+    runs), descending offsets (no list), mapache's 512K/1M/8M (group walk);
+    then a layout change of the same span after a list was built (the
+    speculative list scan replaced by the flat scan)."""
+    ctx = knob_ctx(MCDC_RUN_LIST=mode)
+    rng = np.random.default_rng(77 + mode)
+
+    def check(p, arena, offs, lens, files, calls=3):
+        r, rc = O.chunk_files(O.Params(*p), files, threads=4)
+        for g, gc in _batch_device_calls(ctx, p, arena, offs, lens, calls):
+            assert (gc == rc).all()
+            _same(g, r)
+
+    for p in [PARAMS[0], PARAMS[2], PARAMS[1], PARAMS[3], PARAMS[4]]:
+        mn = p[0]
+        edge = [mn - 1, mn, mn + 1, mn + 47, mn + 48, mn + 64, mn + 4096, 2 * mn + 5, 3 * p[2] + 11]
+        layouts = [
+            (edge * 3, [0] * len(edge) * 3),
+            (list(rng.integers(1, 4 * mn + 2, 300)), list(rng.integers(0, 9000, 300) * (rng.random(300) < 0.3))),
+            ([min(mn, 50000)] * 40, [0] * 40),  # every file <= min_size: nothing listed
+            ([int(x) for x in np.minimum(np.exp(rng.normal(np.log(max(mn // 2, 64)), 1.2, 500)).astype(np.int64) + 1,
+                                         40 * mn)], [0] * 500),
+        ]
+        for sizes, gaps in layouts:
+            arena, offs, lens, files = _arena_files(rng, sizes, gaps)
+            check(p, arena, offs, lens, files)
+    # a dense-byte file among random ones (runs whose entry lists overflow)
+    p = PARAMS[2]
+    b = _find_dense_byte(p)
+    if b is not None:
+        files = [O.random_bytes(3000, 5), np.full(700_000, b, np.uint8), O.random_bytes(1 << 20, 6)]
+        check(p, np.concatenate(files), np.array([0, 3000, 703000], np.uint64),
+              np.array([f.size for f in files], np.uint64), files)
+    # descending offsets (no list), then the same files ascending
+    p = PARAMS[0]
+    sizes = [int(x) for x in rng.integers(1, 200_000, 64)]
+    arena, offs, lens, files = _arena_files(rng, sizes, [0] * 64)
+    for order in (np.arange(64)[::-1], np.arange(64)):
+        check(p, arena, offs[order], lens[order], [files[i] for i in order])
+    # a list built for layout A, then layout B of the same span (one boundary
+    # moved): B's first call scans A's runs speculatively and re-scans flat
+    sizes = [int(x) for x in rng.integers(20_000, 120_000, 400)]
+    arena, offs, lens, files = _arena_files(rng, sizes, [0] * 400)
+    lens_b = lens.copy()
+    lens_b[10] -= np.uint64(30_000)
+    lens_b[11] += np.uint64(30_000)
+    offs_b = offs.copy()
+    offs_b[11] -= np.uint64(30_000)
+    files_b = [arena[int(o):int(o) + int(n)] for o, n in zip(offs_b, lens_b)]
+    ra, rca = O.chunk_files(O.Params(*p), files, threads=4)
+    rb, rcb = O.chunk_files(O.Params(*p), files_b, threads=4)
+    dp = ctx.device_alloc(arena.size + 16)
+    try:
+        ctx.h2d(dp, arena)
+        for o, n, r, rc in [(offs, lens, ra, rca)] * 3 + [(offs_b, lens_b, rb, rcb)] * 3 + [(offs, lens, ra, rca)]:
+            g, gc = ctx.chunk_batch_device(_lib.params(*p), dp, o, n)
+            assert (gc == rc).all()
+            _same(g, r)
+    finally:
+        ctx.device_free(dp)
