@@ -375,13 +375,23 @@ def small_files(ctx, p, nfiles: int, steps: int) -> dict:
     sizes = np.minimum(np.exp(rng.normal(np.log(8192), 1.2, nfiles)).astype(np.uint64) + 1, 64 << 20)
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
     n = int(sizes.sum())
-    arena = ctx.device_alloc(n + 16)
+    arena = ctx.device_alloc(n + 64)
     cap = int(sum(int(s) // (p.min_size - 1) + 2 for s in sizes))
     d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
     try:
         ctx.fill_random(arena, n, SEED ^ 0x5F)
+        # every call a new layout (offsets alternately +0 / +16 bytes): the
+        # segment plan and the scan's run list rebuilt per call (timed first;
+        # the repeated layout below is the line's number)
+        fresh = []
+        for c in range(steps + 2):
+            t0 = time.perf_counter()
+            ctx.chunk_batch_device_to_device(p, arena, offs + np.uint64(16 * (c % 2)), sizes, d_out, cap)
+            fresh.append(time.perf_counter() - t0)
+        fresh_ms = float(np.median(fresh[2:])) * 1e3
+        # (two warm-up calls: the first plans the layout, the second builds its run list)
         dt, (total, counts) = _timed(lambda: ctx.chunk_batch_device_to_device(p, arena, offs, sizes, d_out, cap),
-                                     steps, 1)
+                                     steps, 2)
         from oracle import oracle as O
         chunks = ctx.d2h_chunks(d_out, total)
         host = O.random_bytes(n, SEED ^ 0x5F)
@@ -391,6 +401,10 @@ def small_files(ctx, p, nfiles: int, steps: int) -> dict:
         return {"files": nfiles, "bytes": n, "median_file_bytes": int(np.median(sizes)),
                 "ms_per_step": round(dt * 1e3, 3), "gib_s": round(n / dt / GIB, 2),
                 "files_per_s": round(nfiles / dt, 1), "chunks": int(total), "parity_ok": bool(ok),
+                "fresh_layout_ms": round(fresh_ms, 3), "fresh_layout_gib_s": round(n / (fresh_ms * 1e-3) / GIB, 2),
+                "note": "ms_per_step: the same layout every call (the segment plan and the list-mode scan's run "
+                        "list kept from the previous call, DESIGN.md §5 'List-mode scan'); fresh_layout_ms: a new "
+                        "layout every call (median)",
                 "data": "synthetic log-normal size mix (median 8 KiB), uniform-random bytes"}
     finally:
         ctx.device_free(d_out)
@@ -431,7 +445,7 @@ def kernel_tree(ctx, nfiles: int, steps: int) -> dict:
         d_out = ctx.device_alloc(cap * _lib.CHUNK_DTYPE.itemsize)
         try:
             dt, (total, counts) = _timed(lambda: ctx.chunk_batch_device_to_device(p16, dp, offs, lens, d_out, cap),
-                                         steps, 1)
+                                         steps, 2)  # (as small_files: plan, then run list)
             g = ctx.d2h_chunks(d_out, total)
             pick = np.arange(0, nfiles, 997)
             ends = np.cumsum(counts)

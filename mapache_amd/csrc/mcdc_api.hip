@@ -241,7 +241,8 @@ struct mcdc_ctx {
       sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_wcnt, zc_wfirst, zc_blocks, zc_stage, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words,
       zc_extra, zc_blocks2, zc_stage2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_extra2,  // (the second batch set)
       sv_zch, sv_zpre, sv_zext,  // (the GPU save path's compressor input: all blobs, prefixes, frame extents)
-      rl_ent, run_list;  // (the list-mode scan: its range entries and run list)
+      rl_ent, run_list,  // (the list-mode scan: its range entries and run list)
+      plan_in, plan_tmp;  // (the GPU plan's extents and block sums)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
   // may still be in flight, ev_h2d0/1 mark its completion)
   void *h_stage = nullptr;
@@ -257,7 +258,10 @@ struct mcdc_ctx {
   // Plan cache: the segment tables depend only on the file ranges and the
   // parameters (never on the bytes), so a call with the same layout as the
   // previous one reuses the uploaded tables.
-  std::vector<uint64_t> plan_key;
+  uint64_t plan_n = 0, plan_z = 0, plan_min = 0;  // (the plan's key: these and the files' extents, in h_files
+                                                  // or, planned on the GPU, staged in h_tab)
+  bool plan_gpu = false;
+  uint64_t plan_nsegs = 0, plan_nodes = 0;
   bool plan_valid = false;
   std::vector<uint64_t> bx_fs, bx_fe;
   DevBuf bits_zero;          // run_bits words [bits_zero_at * 2, + cap bytes) zeroed after the last call
@@ -450,6 +454,21 @@ double now_ms() {
       .count();
 }
 
+// x / d for one divisor d and many x < 2^53 (the plan's segment and node
+// counts): a double-precision estimate corrected to the exact quotient.
+struct FastDiv {
+  uint64_t d;
+  double inv;
+  explicit FastDiv(uint64_t dv) : d(dv), inv(1.0 / (double)dv) {}
+  uint64_t div(uint64_t x) const {
+    if (x >= (1ull << 52)) return x / d;
+    uint64_t q = (uint64_t)((double)x * inv);
+    if (q * d > x) --q;
+    else if ((q + 1) * d <= x) ++q;
+    return q;
+  }
+};
+
 // The list-mode scan's run list for a layout (run_pipeline): per file longer
 // than min_size the full runs holding [start + min_size, end) -- every run a
 // chunk window of the file reads (lane_next, group_next, forced_run and
@@ -635,47 +654,81 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   }
   SAVE_T("pipe: scan queued");
   if (after_scan && (rc = after_scan())) return rc;
+  SAVE_T("pipe: ranges");
 
   // ---- plan segments (host; reused when the layout repeats) ----
-  uint64_t total_bytes = 0, out_bound = 0;
-  for (size_t i = 0; i < nfiles; ++i) {
-    const uint64_t len = fend[i] - fstart[i];
-    total_bytes += len;
-    out_bound += len / (params->min_size - 1) + 2;
+  // (no division per file: the output bound from the total -- it bounds the
+  // per-file sum -- and the plan's quotients by FastDiv; the plan key is the
+  // kept file table itself.  80 000 files: ~0.3 ms of 64-bit divisions before)
+  uint64_t total_bytes = 0;
+  for (size_t i = 0; i < nfiles; ++i) total_bytes += fend[i] - fstart[i];
+  const uint64_t out_bound = total_bytes / (params->min_size - 1) + 2 * (uint64_t)nfiles + 1;
+  bool same_plan = ctx->plan_valid && ctx->plan_n == nfiles && ctx->plan_z == Z && ctx->plan_min == params->min_size;
+  if (same_plan && ctx->plan_gpu) {  // (the key: the extents staged for the GPU plan, starts then ends)
+    const uint64_t *ks = (const uint64_t *)ctx->h_tab, *ke = ks + nfiles;
+    for (size_t i = 0; same_plan && i < nfiles; ++i) same_plan = ks[i] == fstart[i] && ke[i] == fend[i];
+  } else {
+    for (size_t i = 0; same_plan && i < nfiles; ++i)
+      same_plan = ctx->h_files[i].start == fstart[i] && ctx->h_files[i].end == fend[i];
   }
-  bool same_plan = ctx->plan_valid && ctx->plan_key.size() == 2 * nfiles + 2 &&
-                   ctx->plan_key[0] == Z && ctx->plan_key[1] == params->min_size;
-  for (size_t i = 0; same_plan && i < nfiles; ++i)
-    same_plan = ctx->plan_key[2 + 2 * i] == fstart[i] && ctx->plan_key[3 + 2 * i] == fend[i];
   if (!same_plan) {
     ctx->plan_valid = false;
-    ctx->plan_key.assign(2 * nfiles + 2, 0);
-    ctx->plan_key[0] = Z;
-    ctx->plan_key[1] = params->min_size;
-    ctx->h_files.resize(nfiles);
+    ctx->plan_n = nfiles;
+    ctx->plan_z = Z;
+    ctx->plan_min = params->min_size;
+    const FastDiv dz(Z), dm(params->min_size - 1);
+    const uint64_t ncap_full = dm.div(Z) + 2;  // (a whole segment's node capacity)
+    // A single-part call of many files plans on the GPU (launch_plan, after
+    // the extents' upload below): here only the totals the workspace needs,
+    // and the extents staged (pinned) as the upload's source and the key.
+    ctx->plan_gpu = early && nfiles >= 2048;
+    ctx->h_files.clear();
     ctx->h_segs.clear();
     ctx->h_node_off.clear();
-    ctx->h_node_off.push_back(0);
-    for (size_t i = 0; i < nfiles; ++i) {
-      ctx->plan_key[2 + 2 * i] = fstart[i];
-      ctx->plan_key[3 + 2 * i] = fend[i];
-      const uint64_t len = fend[i] - fstart[i];
-      const uint32_t nseg = (uint32_t)((len + Z - 1) / Z);
-      File F{fstart[i], fend[i], (uint32_t)ctx->h_segs.size(), nseg};
-      ctx->h_files[i] = F;
-      for (uint32_t k = 0; k < nseg; ++k) {
-        Seg S;
-        S.start = fstart[i] + (uint64_t)k * Z;
-        S.end = std::min<uint64_t>(S.start + Z, fend[i]);
-        S.file = (uint32_t)i;
-        S.flags = (k == 0 ? kSegFirst : 0) | (k + 1 == nseg ? kSegLast : 0);
-        ctx->h_segs.push_back(S);
-        const uint64_t ncap = (S.end - S.start) / (params->min_size - 1) + 2;
-        ctx->h_node_off.push_back(ctx->h_node_off.back() + ncap);
+    if (ctx->plan_gpu) {
+      if (ctx->tab_inflight) {  // (the previous upload out of the stage)
+        HIP_TRY(hipEventSynchronize(ctx->ev_tab));
+        ctx->tab_inflight = false;
       }
+      if ((rc = ensure_tab(ctx, 16 * nfiles))) return rc;
+      uint64_t *ks = (uint64_t *)ctx->h_tab, *ke = ks + nfiles;
+      uint64_t ns = 0, nodes = 0;
+      for (size_t i = 0; i < nfiles; ++i) {  // (one pass: staged and counted)
+        const uint64_t a = fstart[i], e = fend[i], len = e - a, k = dz.div(len + Z - 1);
+        ks[i] = a;
+        ke[i] = e;
+        ns += k;
+        nodes += k ? (k - 1) * ncap_full + dm.div(len - (k - 1) * Z) + 2 : 0;
+      }
+      ctx->plan_nsegs = ns;
+      ctx->plan_nodes = nodes;
+    } else {
+      ctx->h_files.resize(nfiles);
+      ctx->h_segs.reserve(nfiles + total_bytes / Z + 1);
+      ctx->h_node_off.reserve(nfiles + total_bytes / Z + 2);
+      ctx->h_node_off.push_back(0);
+      uint64_t noff = 0;
+      for (size_t i = 0; i < nfiles; ++i) {
+        const uint64_t fs0 = fstart[i], fe0 = fend[i], len = fe0 - fs0;
+        const uint32_t nseg = (uint32_t)dz.div(len + Z - 1);
+        ctx->h_files[i] = File{fs0, fe0, (uint32_t)ctx->h_segs.size(), nseg};
+        for (uint32_t k = 0; k < nseg; ++k) {
+          Seg S;
+          S.start = fs0 + (uint64_t)k * Z;
+          S.end = k + 1 < nseg ? S.start + Z : fe0;
+          S.file = (uint32_t)i;
+          S.flags = (k == 0 ? kSegFirst : 0) | (k + 1 == nseg ? kSegLast : 0);
+          ctx->h_segs.push_back(S);
+          noff += k + 1 < nseg ? ncap_full : dm.div(S.end - S.start) + 2;
+          ctx->h_node_off.push_back(noff);
+        }
+      }
+      ctx->plan_nsegs = ctx->h_segs.size();
+      ctx->plan_nodes = noff;
     }
   }
-  const uint32_t nsegs = (uint32_t)ctx->h_segs.size();
+  const uint32_t nsegs = (uint32_t)ctx->plan_nsegs;
+  SAVE_T(same_plan ? "pipe: plan same" : "pipe: planned");
   // the run list follows the plan: a new layout drops it; a speculative list
   // scan of another layout's runs is replaced by the flat scan (same stream:
   // every kernel after it reads the flat scan's run data)
@@ -692,8 +745,8 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const void *tabs_before[3] = {ctx->segs.p, ctx->files.p, ctx->node_off.p};
   if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
   if ((rc = ensure(ctx, ctx->files, nfiles * sizeof(File)))) return rc;
-  if ((rc = ensure(ctx, ctx->nodes, ctx->h_node_off.back() * sizeof(uint64_t)))) return rc;
-  if ((rc = ensure(ctx, ctx->node_off, ctx->h_node_off.size() * sizeof(uint64_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->nodes, ctx->plan_nodes * sizeof(uint64_t)))) return rc;
+  if ((rc = ensure(ctx, ctx->node_off, (nsegs + 1) * sizeof(uint64_t)))) return rc;
   if (tabs_before[0] != ctx->segs.p || tabs_before[1] != ctx->files.p || tabs_before[2] != ctx->node_off.p)
     ctx->plan_valid = false;  // reallocated: the uploaded tables are gone
   if ((rc = ensure(ctx, ctx->node_cnt, nsegs * 4))) return rc;
@@ -826,7 +879,19 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipEventRecord(ctx->ev_scan, st));
   }
   bool uploaded = false;
-  if (!ctx->plan_valid) {  // tables -> pinned stage -> one async copy each
+  if (!ctx->plan_valid && ctx->plan_gpu) {  // the extents (staged at planning) -> the plan kernels on stream2
+    uploaded = true;
+    if ((rc = ensure(ctx, ctx->plan_in, 16 * nfiles)) || (rc = ensure(ctx, ctx->plan_tmp, 16 * (nfiles / 256 + 1))))
+      return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->plan_in.p, ctx->h_tab, 16 * nfiles, hipMemcpyHostToDevice, st2));
+    HIP_TRY(hipEventRecord(ctx->ev_tab, st2));
+    ctx->tab_inflight = true;
+    launch_plan((const uint64_t *)ctx->plan_in.p, nfiles, Z, params->min_size - 1, (uint64_t *)ctx->plan_tmp.p,
+                (File *)ctx->files.p, (Seg *)ctx->segs.p, (uint64_t *)ctx->node_off.p, st2);
+    HIP_TRY(hipGetLastError());
+    ctx->plan_valid = true;
+    SAVE_T("pipe: plan queued");
+  } else if (!ctx->plan_valid) {  // tables -> pinned stage -> one async copy each
     uploaded = true;
     const size_t b_segs = nsegs * sizeof(Seg), b_files = nfiles * sizeof(File),
                  b_noff = ctx->h_node_off.size() * 8;
@@ -844,6 +909,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     if (b_segs) std::memcpy(tbuf, ctx->h_segs.data(), b_segs);
     if (b_files) std::memcpy(tbuf + o_files, ctx->h_files.data(), b_files);
     std::memcpy(tbuf + o_noff, ctx->h_node_off.data(), b_noff);
+    SAVE_T("pipe: staged");
     if (b_segs) HIP_TRY(hipMemcpyAsync(ctx->segs.p, tbuf, b_segs, hipMemcpyHostToDevice, st2));
     if (b_files) HIP_TRY(hipMemcpyAsync(ctx->files.p, tbuf + o_files, b_files, hipMemcpyHostToDevice, st2));
     HIP_TRY(hipMemcpyAsync(ctx->node_off.p, tbuf + o_noff, b_noff, hipMemcpyHostToDevice, st2));
@@ -1193,7 +1259,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_extra,
                     &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
                     &ctx->zc_words2, &ctx->zc_extra2, &ctx->sv_zch, &ctx->sv_zpre, &ctx->sv_zext, &ctx->rl_ent,
-                    &ctx->run_list};
+                    &ctx->run_list, &ctx->plan_in, &ctx->plan_tmp};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);

@@ -212,6 +212,11 @@ void launch_file_counts(const Work &w, uint64_t *dst, hipStream_t stream);  // c
 // the list-mode scan's run list from nent {first run, list index} entries
 // (each <= 64 runs, the last ending at list_n), the candidate-bitmap words and
 // the tile counter zeroed (words [0, nwords)); ev0: recorded at its start
+// the segment plan of n files (fse: their starts, then their ends) on the
+// GPU: files[n], segs, node_off (as run_pipeline's host plan); bsum: 2 words
+// per 256 files
+void launch_plan(const uint64_t *fse, uint64_t n, uint64_t Z, uint64_t ms1, uint64_t *bsum, File *files, Seg *segs,
+                 uint64_t *node_off, hipStream_t stream);
 void launch_run_list(const uint32_t *ent, uint64_t nent, uint64_t list_n, uint32_t *list, uint64_t *words,
                      uint64_t nwords, hipStream_t stream, hipEvent_t ev0 = nullptr);
 

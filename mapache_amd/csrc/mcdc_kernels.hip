@@ -725,6 +725,106 @@ void launch_run_list(const uint32_t *ent, uint64_t nent, uint64_t list_n, uint32
                         reinterpret_cast<const uint2 *>(ent), nent, list_n, list, words, nwords);
 }
 
+// The segment plan of a batch on the GPU (run_pipeline, a new layout of many
+// files): from the files' arena extents fs[i], fe[i], per file nseg =
+// ceil(len / Z) segments of Z bytes (the last shorter), each with room for
+// len / (min_size - 1) + 2 chain nodes, as the host plan builds them.  Two
+// kernels: per-block sums of the segment and node counts, then per file its
+// prefix (the sums of the blocks before its own, then a block scan) and its
+// File, Seg and node_off records (node_off[first + nseg] too: the next file's
+// first entry, or node_off[nsegs]).
+__device__ __forceinline__ void plan_counts(uint64_t len, uint64_t Z, uint64_t ms1, uint64_t &nseg, uint64_t &nodes) {
+  nseg = (len + Z - 1) / Z;
+  nodes = nseg ? (nseg - 1) * (Z / ms1 + 2) + (len - (nseg - 1) * Z) / ms1 + 2 : 0;
+}
+
+__device__ __forceinline__ void block_sum2(uint64_t &a, uint64_t &b, uint64_t *sh) {  // (256 threads; a, b -> totals)
+  const uint32_t t = threadIdx.x;
+  sh[t] = a;
+  sh[256 + t] = b;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      sh[t] += sh[t + o];
+      sh[256 + t] += sh[256 + t + o];
+    }
+    __syncthreads();
+  }
+  a = sh[0];
+  b = sh[256];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_plan_count(const uint64_t *fs, const uint64_t *fe, uint64_t n, uint64_t Z,
+                                                     uint64_t ms1, uint64_t *bsum) {
+  __shared__ uint64_t sh[512];
+  MCDC_VGPR_PAD(16);  // (not an exact fill)
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t ns = 0, nd = 0;
+  if (i < n) plan_counts(fe[i] - fs[i], Z, ms1, ns, nd);
+  block_sum2(ns, nd, sh);
+  if (threadIdx.x == 0) {
+    bsum[2 * blockIdx.x] = ns;
+    bsum[2 * blockIdx.x + 1] = nd;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_plan_write(const uint64_t *fs, const uint64_t *fe, uint64_t n, uint64_t Z,
+                                                     uint64_t ms1, const uint64_t *bsum, File *files, Seg *segs,
+                                                     uint64_t *node_off) {
+  __shared__ uint64_t sh[512];
+  MCDC_VGPR_PAD(24);  // (not an exact fill)
+  const uint32_t t = threadIdx.x;
+  // the blocks before this one
+  uint64_t bs = 0, bn = 0;
+  for (uint32_t b = t; b < blockIdx.x; b += 256) {
+    bs += bsum[2 * b];
+    bn += bsum[2 * b + 1];
+  }
+  block_sum2(bs, bn, sh);
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+  uint64_t ns = 0, nd = 0, a = 0, e = 0;
+  if (i < n) {
+    a = fs[i];
+    e = fe[i];
+    plan_counts(e - a, Z, ms1, ns, nd);
+  }
+  // inclusive block scan of (ns, nd), Hillis-Steele
+  sh[t] = ns;
+  sh[256 + t] = nd;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {
+    const uint64_t xs = t >= o ? sh[t - o] : 0, xn = t >= o ? sh[256 + t - o] : 0;
+    __syncthreads();
+    sh[t] += xs;
+    sh[256 + t] += xn;
+    __syncthreads();
+  }
+  if (i >= n) return;
+  const uint64_t first = bs + sh[t] - ns, node0 = bn + sh[256 + t] - nd;
+  files[i] = File{a, e, (uint32_t)first, (uint32_t)ns};
+  const uint64_t full = Z / ms1 + 2;
+  for (uint64_t k = 0; k < ns; ++k) {
+    Seg S;
+    S.start = a + k * Z;
+    S.end = k + 1 < ns ? S.start + Z : e;
+    S.file = (uint32_t)i;
+    S.flags = (k == 0 ? kSegFirst : 0u) | (k + 1 == ns ? kSegLast : 0u);
+    segs[first + k] = S;
+    node_off[first + k] = node0 + k * full;
+  }
+  node_off[first + ns] = node0 + nd;
+}
+
+void launch_plan(const uint64_t *fse, uint64_t n, uint64_t Z, uint64_t ms1, uint64_t *bsum, File *files, Seg *segs,
+                 uint64_t *node_off, hipStream_t stream) {
+  if (n == 0) return;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_plan_count, dim3(blocks), dim3(256), 0, stream, fse, fse + n, n, Z, ms1, bsum);
+  hipLaunchKernelGGL(k_plan_write, dim3(blocks), dim3(256), 0, stream, fse, fse + n, n, Z, ms1, bsum, files, segs,
+                     node_off);
+}
+
 // Product configuration: quad-coalesced scan, 16 waves (one 1024-thread
 // block) per CU; tools/scanbench.hip keeps the lane-strided k_scan_t variants
 // for comparison.

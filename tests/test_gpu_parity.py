@@ -690,3 +690,35 @@ def test_run_list_scan(knob_ctx, mode):
             _same(g, r)
     finally:
         ctx.device_free(dp)
+
+
+@pytest.mark.parametrize("p", [PARAMS[0], PARAMS[1], PARAMS[2], PARAMS[3]], ids=lambda p: "/".join(map(str, p)))
+def test_gpu_plan_many_files(ctx, p):
+    """A single-part batch of >= 2048 files is planned on the GPU (k_plan_count
+    / k_plan_write: files, segments, node offsets from the uploaded extents):
+    empty files, files of exactly k segments and one byte either side,
+    multi-segment files, gaps; a new layout every call (offsets shifted by 16
+    bytes) and the same layout again (the kept plan), against the oracle."""
+    z = _segment_bytes(p)
+    rng = np.random.default_rng(4242)
+    special = [0, 1, p[0], p[0] + 1, z - 1, z, z + 1, 2 * z, 2 * z + 1, 3 * z - 1]
+    sizes = [int(x) for x in rng.integers(0, 3 * p[0] + 5, 2600)]
+    for k, s in enumerate(special * 12):
+        sizes[(k * 211) % len(sizes)] = s
+    gaps = [int(g) * (k % 7 == 0) for k, g in enumerate(rng.integers(1, 5000, len(sizes)))]
+    arena, offs, lens, files = _arena_files(rng, sizes, gaps)
+    arena = np.concatenate([arena, np.zeros(64, np.uint8)])
+    shifted = [np.concatenate([arena[int(o) + 16:int(o) + 16 + int(n)]]) for o, n in zip(offs, lens)]
+    r0, rc0 = O.chunk_files(O.Params(*p), files, threads=4)
+    r1, rc1 = O.chunk_files(O.Params(*p), shifted, threads=4)
+    dp = ctx.device_alloc(arena.size + 16)
+    try:
+        ctx.h2d(dp, arena)
+        for c in range(6):  # new, new, new, new, same, same
+            sh = 16 * (c % 2) if c < 4 else 0
+            g, gc = ctx.chunk_batch_device(_lib.params(*p), dp, offs + np.uint64(sh), lens)
+            r, rc = (r1, rc1) if sh else (r0, rc0)
+            assert (gc == rc).all()
+            _same(g, r)
+    finally:
+        ctx.device_free(dp)
