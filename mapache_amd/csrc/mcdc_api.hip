@@ -58,6 +58,8 @@ int fail(int code, const char *fmt, ...) {
   } while (0)
 
 constexpr uint32_t MINIMUM_MIN = 64, MINIMUM_MAX = 1048576;
+
+
 constexpr uint32_t AVERAGE_MIN = 256, AVERAGE_MAX = 4194304;
 constexpr uint32_t MAXIMUM_MIN = 1024, MAXIMUM_MAX = 16777216;
 
@@ -241,6 +243,7 @@ struct mcdc_ctx {
       sv_in, sv_pack, sv_comp, sv_seal, sv_ext, zc_cnt, zc_cls, zc_first, zc_wcnt, zc_wfirst, zc_blocks, zc_stage, zc_piece, zc_poff, zc_misc, zc_tmp, zc_words,
       zc_extra, zc_blocks2, zc_stage2, zc_piece2, zc_poff2, zc_tmp2, zc_words2, zc_extra2,  // (the second batch set)
       sv_zch, sv_zpre, sv_zext,  // (the GPU save path's compressor input: all blobs, prefixes, frame extents)
+      sv_ids,  // (the save path's blob IDs in HBM)
       rl_ent, run_list,  // (the list-mode scan: its range entries and run list)
       plan_in, plan_tmp;  // (the GPU plan's extents and block sums)
   // pinned host staging (two slabs; stage_busy: an async copy out of slab k
@@ -281,6 +284,8 @@ struct mcdc_ctx {
   size_t h_encb_cap = 0;
   void *h_meta = nullptr;      // pinned: the GPU save path's encoded pack headers (their H2D source)
   size_t h_meta_cap = 0;
+  void *h_list = nullptr;      // pinned: mcdc_save_files' blob list (the IDs' upload source)
+  size_t h_list_cap = 0;
   void *h_rl = nullptr;        // pinned: the list-mode scan's range entries (their H2D source)
   size_t h_rl_cap = 0;
   int list_state = 0;          // run list of the plan's layout: 0 none, 1 built (run_list), 2 not worth it
@@ -608,7 +613,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const bool zeroed = ctx->bits_zero.p == ctx->run_bits.p && ctx->bits_zero_at == bw0 &&
                       ctx->bits_zero.cap == zero_bytes;
   ctx->bits_zero = DevBuf{};
-  const bool lane_early = early && use_lane_walk(params, kn);
   if (!zeroed) SAVE_T("pipe: cold");
   // List-mode scan: cut_gear hashes a chunk from min_size on (v2020), so a
   // file's first min_size bytes, less the 48-byte window warm-up, are read by
@@ -637,7 +641,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     launch_scan(W, P, ctx->num_cus, st, 0, n_al > 0 ? (n_al / kRun) / (64 / pc) : 0, n_al > 0, pc, kn.scan_cold,
                 !cold || !MCDC_COLD_EVENT ? ctx->ev_start : nullptr, ctx->ev_scan);
     HIP_TRY(hipGetLastError());
-    if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));  // (the group walk's stream waits for it)
     return MCDC_OK;
   };
   if (spec_list) {  // (the bitmap words and the tile counter zeroed, then the listed runs and the partial last run)
@@ -648,7 +651,6 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     HIP_TRY(hipGetLastError());
     W.run_list = nullptr;  // (the resolution kernels take W by value: the scan's fields only)
     W.list_n = 0;
-    if (!lane_early) HIP_TRY(hipEventRecord(ctx->ev_part[0], st));
   } else if (early) {
     if ((rc = scan_flat(!zeroed))) return rc;
   }
@@ -920,33 +922,35 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
   const bool want_counts = counts && nfiles;
   if (want_counts && (rc = ensure_fcnt(ctx, nfiles))) return rc;
   const bool lane_all = lane && K == 1;
+  // A single-part call resolves on the scan's own stream (either walk): its
+  // kernels follow the scan at a same-queue kernel boundary instead of a
+  // cross-queue event (~13 us measured), and wait for stream2 only for this
+  // call's table uploads / plan; the staged pipeline resolves part i on
+  // stream2 behind the scan's part-i event, overlapping the later parts.
+  hipStream_t rs = K == 1 ? st : st2;
   if (lane_all && n_al == 0) HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st));  // (no scan launch to clear them)
-  if (!lane_all) {  // (the lane walk's first kernels reset these: k_scan_q, k_spec_lane)
-    if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, st2));
-    HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, st2));
-    HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, st2));
-    HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, st2));
+  if (!lane_all) {  // (the lane walk's first kernels reset these: k_scan_q, k_spec_lane; the scan only clears err)
+    if (nfiles) HIP_TRY(hipMemsetAsync(ctx->file_flags.p, 0, nfiles * 4, rs));
+    HIP_TRY(hipMemsetAsync(ctx->err.p, 0, 32, rs));
+    HIP_TRY(hipMemsetAsync((uint64_t *)ctx->seg_count.p + nsegs, 0, 8, rs));
+    HIP_TRY(hipMemsetAsync(ctx->seg_off.p, 0, 8, rs));
   }
-  // The lane walk runs on the scan's own stream: it follows the scan at a
-  // same-queue kernel boundary instead of a cross-queue event (~13 us
-  // measured), and waits for stream2 only for this call's table uploads.
-  hipStream_t rs = lane_all ? st : st2;
+  if (K == 1 && uploaded) {
+    HIP_TRY(hipEventRecord(ctx->ev_prep, st2));
+    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prep, 0));
+  }
   if (lane_all) {
-    if (uploaded) {
-      HIP_TRY(hipEventRecord(ctx->ev_prep, st2));
-      HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prep, 0));
-    }
     launch_resolve_lane(W, P, (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st,
                         want_counts ? ctx->d_fcnt : nullptr);
     HIP_TRY(hipGetLastError());
   }
   for (int i = 0; i < (lane_all ? 0 : K); ++i) {
-    HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[i], 0));
+    if (K > 1) HIP_TRY(hipStreamWaitEvent(st2, ctx->ev_part[i], 0));
     const uint32_t a_s = i ? spec_hi[i - 1] : 0, a_l = i ? link_hi[i - 1] : 0;
-    launch_spec(W, P, kn, a_s, spec_hi[i], st2);
+    launch_spec(W, P, kn, a_s, spec_hi[i], rs);
     // parts before the last: link_hi assumes <= kContMax continuation steps
-    launch_link(W, P, kn, a_l, link_hi[i], i == K - 1 ? ~0ull : (uint64_t)kContMax, st2);
-    launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, st2);
+    launch_link(W, P, kn, a_l, link_hi[i], i == K - 1 ? ~0ull : (uint64_t)kContMax, rs);
+    launch_emit_incremental(W, P, a_l, link_hi[i], (uint64_t *)ctx->seg_incl.p, ctx->scan_tmp.p, tmpb, rs);
     HIP_TRY(hipGetLastError());
   }
   if (want_counts && !(lane_all && nsegs)) launch_file_counts(W, ctx->d_fcnt, rs);  // (else by the emit)
@@ -1245,6 +1249,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
   if (ctx->h_encb) (void)hipHostFree(ctx->h_encb);
   if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
   if (ctx->h_rl) (void)hipHostFree(ctx->h_rl);
+  if (ctx->h_list) (void)hipHostFree(ctx->h_list);
   DevBuf *bufs[] = {&ctx->arena, &ctx->run_cnt, &ctx->run_sum, &ctx->run_ent, &ctx->run_bits, &ctx->punt, &ctx->segs, &ctx->files, &ctx->nodes,
                     &ctx->node_off, &ctx->node_cnt, &ctx->seg_exit, &ctx->cont, &ctx->cont_cnt, &ctx->cont_rep,
                     &ctx->cont_ent, &ctx->long_list,
@@ -1259,7 +1264,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
                     &ctx->zc_piece, &ctx->zc_poff, &ctx->zc_misc, &ctx->zc_tmp, &ctx->zc_words, &ctx->zc_extra,
                     &ctx->zc_blocks2, &ctx->zc_stage2, &ctx->zc_piece2, &ctx->zc_poff2, &ctx->zc_tmp2,
                     &ctx->zc_words2, &ctx->zc_extra2, &ctx->sv_zch, &ctx->sv_zpre, &ctx->sv_zext, &ctx->rl_ent,
-                    &ctx->run_list, &ctx->plan_in, &ctx->plan_tmp};
+                    &ctx->run_list, &ctx->plan_in, &ctx->plan_tmp, &ctx->sv_ids};
   for (DevBuf *b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (ctx->d_gear) (void)hipFree(ctx->d_gear);
@@ -2711,27 +2716,34 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
       return rc;
   }
   SAVE_T("chunked");
-  // every blob in processing order (file order, chunk order), offsets into d
-  std::vector<mcdc_chunk> list;
-  list.reserve(nfiles + cap);
-  size_t bi = 0, at = 0;
+  // every blob in processing order (file order, chunk order), offsets into d,
+  // in the context's pinned list (the IDs' kernels read it by one DMA)
+  if ((rc = ensure_pinned(ctx, ctx->h_list, ctx->h_list_cap, (nfiles + cap + 1) * sizeof(mcdc_chunk)))) return rc;
+  mcdc_chunk *const list = (mcdc_chunk *)ctx->h_list;
+  size_t bi = 0, at = 0, nb = 0;
   for (size_t f = 0; f < nfiles; ++f) {
-    file_blobs[f] = list.size();
+    file_blobs[f] = nb;
     if (bi < big.size() && big[bi] == f) {
       for (size_t j = 0; j < bcnt[bi]; ++j, ++at)
-        list.push_back(mcdc_chunk{files[f].offset + bch[at].offset, bch[at].length, bch[at].hash});
+        list[nb++] = mcdc_chunk{files[f].offset + bch[at].offset, bch[at].length, bch[at].hash};
       ++bi;
     } else {
-      list.push_back(mcdc_chunk{files[f].offset, files[f].length, 0});
+      list[nb++] = mcdc_chunk{files[f].offset, files[f].length, 0};
     }
   }
-  if (nfiles) file_blobs[nfiles] = list.size();
-  const size_t nb = list.size();
+  if (nfiles) file_blobs[nfiles] = nb;
   *nblobs = nb;
   if (nb > blobs_cap || (nb && !ids)) return fail(MCDC_E_CAPACITY, "%zu blobs, capacity %zu", nb, blobs_cap);
   SAVE_T("list");
-  // ID::from_content of every blob (CalculateID of a small file is the same hash)
-  if (nb && (rc = mcdc_chunk_ids_device(ctx, d, n, list.data(), nb, ids))) return rc;
+  // ID::from_content of every blob (CalculateID of a small file is the same
+  // hash), into HBM: the index reads them there, the caller's array gets one
+  // copy (queued before the index's kernels, complete when they are)
+  if (nb) {
+    if ((rc = ensure(ctx, ctx->sv_ids, nb * 32)) || (rc = mcdc_chunk_ids_device(ctx, d, n, list, nb,
+                                                                                  (uint8_t *)ctx->sv_ids.p)))
+      return rc;
+    HIP_TRY(hipMemcpyAsync(ids, ctx->sv_ids.p, nb * 32, hipMemcpyDeviceToHost, ctx->stream));
+  }
   SAVE_T("ids");
   // save_blob's dedup check (:173-180) -- the index changes here.  From here
   // on every failure, whatever returns it (capacity, nonces, a HIP call),
@@ -2739,7 +2751,8 @@ int mcdc_save_files(mcdc_ctx *ctx, const mcdc_params *params, mcdc_index *ix, co
   // intact until the next add, so the index is exactly as before the call.
   std::vector<uint8_t> nw(std::max<size_t>(nb, 1));
   size_t m = 0;
-  if (nb && (rc = mcdc_index_add(ctx, ix, ids, nb, nw.data(), nullptr, nullptr, &m))) return rc;
+  if (nb && (rc = mcdc_index_add(ctx, ix, (const uint8_t *)ctx->sv_ids.p, nb, nw.data(), nullptr, nullptr, &m)))
+    return rc;
   SAVE_T("index");
   auto rest = [&]() -> int {
     if (store->key && m > store->nnonces)
