@@ -284,6 +284,8 @@ struct mcdc_ctx {
   size_t h_encb_cap = 0;
   void *h_meta = nullptr;      // pinned: the GPU save path's encoded pack headers (their H2D source)
   size_t h_meta_cap = 0;
+  std::vector<hipEvent_t> ev_pool;  // timing-free events the compressor and the save path take per call (kept)
+  std::mutex ev_pool_mu;
   void *h_list = nullptr;      // pinned: mcdc_save_files' blob list (the IDs' upload source)
   size_t h_list_cap = 0;
   void *h_rl = nullptr;        // pinned: the list-mode scan's range entries (their H2D source)
@@ -1275,6 +1277,7 @@ void mcdc_ctx_destroy(mcdc_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ev_part)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->ev_tab) (void)hipEventDestroy(ctx->ev_tab);
   if (ctx->ev_prep) (void)hipEventDestroy(ctx->ev_prep);
   if (ctx->ev_copy0) (void)hipEventDestroy(ctx->ev_copy0);
@@ -2152,6 +2155,27 @@ static int zc_ensure_sets(mcdc_ctx *ctx, uint64_t mw, uint64_t mb, bool two, siz
 // k_zc_small classes hcls; frames back to back from d_out (the running offset
 // in misc[2], reset here), extents to ext.  The sets must hold zbt's batches
 // (zc_ensure_sets); on return ctx->stream is ordered after every batch.
+// Timing-free events of a call (compressor batches, save-path groups) from the
+// context's pool, returned at the call's end: created once per context, not
+// per call (a call used ~18; a later record supersedes any earlier one a
+// stream wait already captured).
+static hipError_t take_event(mcdc_ctx *ctx, hipEvent_t *e) {
+  {
+    std::lock_guard<std::mutex> g(ctx->ev_pool_mu);
+    if (!ctx->ev_pool.empty()) {
+      *e = ctx->ev_pool.back();
+      ctx->ev_pool.pop_back();
+      return hipSuccess;
+    }
+  }
+  return hipEventCreateWithFlags(e, hipEventDisableTiming);
+}
+static void give_event(mcdc_ctx *ctx, hipEvent_t e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> g(ctx->ev_pool_mu);
+  ctx->ev_pool.push_back(e);
+}
+
 static int zc_enqueue(mcdc_ctx *ctx, const uint8_t *d_data, size_t n, const DevChunk *dch, const uint64_t *first,
                       const uint64_t *wfirst, const uint64_t *hfirst, const uint64_t *hwfirst, const uint8_t *hcls,
                       const ZcBatches &zbt, uint8_t *d_out, uint64_t *ext, uint64_t *misc) {
@@ -2171,11 +2195,10 @@ static int zc_enqueue(mcdc_ctx *ctx, const uint8_t *d_data, size_t n, const DevC
   // [0] setup done on st; [1 + k] set k's last final copy
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   auto destroy = [&]() {
-    for (auto &e : ev)
-      if (e) (void)hipEventDestroy(e);
+    for (auto &e : ev) give_event(ctx, e);
   };
   for (auto &e : ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+    if (take_event(ctx, &e) != hipSuccess)
       return e = nullptr, destroy(), fail(MCDC_E_DEVICE, "event creation failed");
   hipStream_t ss[2] = {st, ctx->stream2};
   if (two) {
@@ -2296,7 +2319,7 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
     (void)hipStreamSynchronize(ctx->stream4);
     (void)hipStreamSynchronize(ctx->stream3);
     (void)hipStreamSynchronize(ctx->stream);
-    for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+    for (hipEvent_t e : evs) give_event(ctx, e);
   };
   // a header's raw zstd frame: frame header, then raw blocks of <= 128 KiB
   auto frame_len = [](uint64_t hl) {
@@ -2451,15 +2474,13 @@ static int save_encode_gpu(mcdc_ctx *ctx, const mcdc_store *store, const uint8_t
   std::vector<hipEvent_t> evg(G, nullptr);  // group g's frames and extents complete (on st)
   hipEvent_t ev_s3 = nullptr, ev_cp = nullptr;
   for (auto &e : evg) {
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+    if (take_event(ctx, &e) != hipSuccess)
       return e = nullptr, cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
     evs.push_back(e);
   }
-  if (hipEventCreateWithFlags(&ev_s3, hipEventDisableTiming) != hipSuccess)
-    return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
+  if (take_event(ctx, &ev_s3) != hipSuccess) return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
   evs.push_back(ev_s3);
-  if (hipEventCreateWithFlags(&ev_cp, hipEventDisableTiming) != hipSuccess)
-    return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
+  if (take_event(ctx, &ev_cp) != hipSuccess) return cleanup(), fail(MCDC_E_DEVICE, "event creation failed");
   evs.push_back(ev_cp);
   auto enqueue = [&](size_t g) -> int {  // group g's compression, then its extents to the host
     const size_t g0 = gstart[g], gm = gstart[g + 1] - g0;
