@@ -696,17 +696,22 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
       }
       if ((rc = ensure_tab(ctx, 16 * nfiles))) return rc;
       uint64_t *ks = (uint64_t *)ctx->h_tab, *ke = ks + nfiles;
-      uint64_t ns = 0, nodes = 0;
+      uint64_t ns = 0, nodes = 0, kmax = 0;
       for (size_t i = 0; i < nfiles; ++i) {  // (one pass: staged and counted)
         const uint64_t a = fstart[i], e = fend[i], len = e - a, k = dz.div(len + Z - 1);
         ks[i] = a;
         ke[i] = e;
         ns += k;
+        kmax = std::max(kmax, k);
         nodes += k ? (k - 1) * ncap_full + dm.div(len - (k - 1) * Z) + 2 : 0;
       }
       ctx->plan_nsegs = ns;
       ctx->plan_nodes = nodes;
-    } else {
+      // (k_plan_write writes a file's segments on one lane: a batch holding a
+      // file of thousands of segments is planned on the host)
+      if (kmax > 1024) ctx->plan_gpu = false;
+    }
+    if (!ctx->plan_gpu) {
       ctx->h_files.resize(nfiles);
       ctx->h_segs.reserve(nfiles + total_bytes / Z + 1);
       ctx->h_node_off.reserve(nfiles + total_bytes / Z + 2);

@@ -722,3 +722,31 @@ def test_gpu_plan_many_files(ctx, p):
             _same(g, r)
     finally:
         ctx.device_free(dp)
+
+
+def test_gpu_plan_falls_back_for_huge_files(ctx):
+    """A batch of >= 2048 files holding a file of more than 1024 segments is
+    planned on the host (k_plan_write writes a file's segments on one lane):
+    same boundaries as the oracle, then the same batch without that file
+    (planned on the GPU)."""
+    p = PARAMS[2]
+    z = _segment_bytes(p)
+    rng = np.random.default_rng(99)
+    sizes = [int(x) for x in rng.integers(0, 3000, 2100)]
+    sizes[777] = 1100 * z + 5
+    arena, offs, lens, files = _arena_files(rng, sizes, [0] * len(sizes))
+    r, rc = O.chunk_files(O.Params(*p), files, threads=4)
+    keep = [i for i in range(len(sizes)) if i != 777]
+    r2, rc2 = O.chunk_files(O.Params(*p), [files[i] for i in keep], threads=4)
+    dp = ctx.device_alloc(arena.size + 16)
+    try:
+        ctx.h2d(dp, arena)
+        for _ in range(2):
+            g, gc = ctx.chunk_batch_device(_lib.params(*p), dp, offs, lens)
+            assert (gc == rc).all()
+            _same(g, r)
+            g, gc = ctx.chunk_batch_device(_lib.params(*p), dp, offs[keep], lens[keep])
+            assert (gc == rc2).all()
+            _same(g, r2)
+    finally:
+        ctx.device_free(dp)
