@@ -675,6 +675,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     for (size_t i = 0; same_plan && i < nfiles; ++i)
       same_plan = ctx->h_files[i].start == fstart[i] && ctx->h_files[i].end == fend[i];
   }
+  SAVE_T("pipe: compared");
   if (!same_plan) {
     ctx->plan_valid = false;
     ctx->plan_n = nfiles;
@@ -696,17 +697,20 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
       }
       if ((rc = ensure_tab(ctx, 16 * nfiles))) return rc;
       uint64_t *ks = (uint64_t *)ctx->h_tab, *ke = ks + nfiles;
-      uint64_t ns = 0, nodes = 0, kmax = 0;
-      for (size_t i = 0; i < nfiles; ++i) {  // (one pass: staged and counted)
-        const uint64_t a = fstart[i], e = fend[i], len = e - a, k = dz.div(len + Z - 1);
+      uint64_t ns = 0, kmax = 0;
+      for (size_t i = 0; i < nfiles; ++i) {  // (one pass: staged and counted; a division only past one segment)
+        const uint64_t a = fstart[i], e = fend[i], len = e - a;
+        const uint64_t k = len == 0 ? 0 : len <= Z ? 1 : dz.div(len + Z - 1);
         ks[i] = a;
         ke[i] = e;
         ns += k;
         kmax = std::max(kmax, k);
-        nodes += k ? (k - 1) * ncap_full + dm.div(len - (k - 1) * Z) + 2 : 0;
       }
       ctx->plan_nsegs = ns;
-      ctx->plan_nodes = nodes;
+      // (the node buffer's size: a bound of the per-segment capacities'
+      // sum, floor(len / (min_size - 1)) + 2 each, which k_plan_write lays out)
+      ctx->plan_nodes = total_bytes / (params->min_size - 1) + 2 * ns + 1;
+      SAVE_T("pipe: staged extents");
       // (k_plan_write writes a file's segments on one lane: a batch holding a
       // file of thousands of segments is planned on the host)
       if (kmax > 1024) ctx->plan_gpu = false;
@@ -750,6 +754,7 @@ int run_pipeline(mcdc_ctx *ctx, const mcdc_params *params, const uint8_t *base, 
     list_built = ctx->list_state == 1;
   }
 
+  SAVE_T("pipe: list checked");
   // ---- workspace ----
   const void *tabs_before[3] = {ctx->segs.p, ctx->files.p, ctx->node_off.p};
   if ((rc = ensure(ctx, ctx->segs, nsegs * sizeof(Seg)))) return rc;
